@@ -1,0 +1,87 @@
+/*
+ * siddhi_ir.h -- the versioned plan IR shared by the host planner
+ * (siddhi_amd/planner.py), libsiddhi_hip (siddhi_amd/csrc) and the CPU
+ * oracle (oracle/).  Constants only: every consumer has its own decoder.
+ *
+ * A plan is a little-endian array of int32 words:
+ *
+ *   magic 'SHDP', version, kind (1 = STATE, 2 = SINGLE)
+ *   n_streams, { n_attrs, type[n_attrs] } * n_streams      (plan-local streams)
+ *   n_consts,  { lo, hi } * n_consts                         (64-bit bit patterns)
+ *   n_exprs,   { n_instr, { op, a, b, c } * n_instr } * n_exprs
+ *   partition: n_keys, { stream, expr } * n_keys             (n_keys = 0: unpartitioned)
+ *   STATE:  state_type, within_lo, within_hi, n_states, node tree (prefix order)
+ *   SINGLE: stream, n_handlers, { FILTER expr | WINDOW kind p_lo p_hi } * n_handlers
+ *   selector: current_on, expired_on, n_aggs { kind, arg_expr, arg_type } ,
+ *             n_group { expr }, having_expr, n_out { type, expr }
+ *
+ * Node tree (StateInputStreamParser.parse, C/util/parser/StateInputStreamParser.java:148-408):
+ *   NODE_STREAM  state_id stream absent waiting_lo waiting_hi n_filters expr*
+ *   NODE_NEXT    <a> <b>
+ *   NODE_EVERY   <inner>
+ *   NODE_LOGICAL type(0 and, 1 or) <stream1> <stream2>
+ *   NODE_COUNT   min max <stream>
+ */
+#ifndef SIDDHI_IR_H
+#define SIDDHI_IR_H
+
+#define SHD_IR_MAGIC 0x50444853 /* 'SHDP' */
+#define SHD_IR_VERSION 1
+
+enum shd_kind { SHD_KIND_STATE = 1, SHD_KIND_SINGLE = 2 };
+
+/* Attribute types (io.siddhi.query.api.definition.Attribute.Type). STRING is
+ * a host dictionary id (u32); BOOL is a byte. */
+enum shd_type {
+  SHD_T_STRING = 0,
+  SHD_T_INT = 1,
+  SHD_T_LONG = 2,
+  SHD_T_FLOAT = 3,
+  SHD_T_DOUBLE = 4,
+  SHD_T_BOOL = 5
+};
+
+/* Expression bytecode: fixed 4-word instructions {op, a, b, c} over a value
+ * stack of (64-bit payload, null flag). Semantics follow
+ * C/executor/{condition,math}/ (see oracle/oracle.cpp for the restatement). */
+enum shd_op {
+  SHD_OP_END = 0,
+  SHD_OP_CONST = 1,   /* a = const index, b = type                         */
+  SHD_OP_NULL = 2,    /* b = type                                          */
+  SHD_OP_LOAD = 3,    /* a = state, b = chain index, c = attr | type << 16  */
+  SHD_OP_EVNULL = 4,  /* a = state, b = chain index : stream event is null  */
+  SHD_OP_CVT = 5,     /* a = from type, b = to type (Number.xValue())       */
+  SHD_OP_ADD = 6,     /* a = type                                          */
+  SHD_OP_SUB = 7,
+  SHD_OP_MUL = 8,
+  SHD_OP_DIV = 9,     /* divisor 0 -> null                                 */
+  SHD_OP_MOD = 10,    /* divisor 0 -> null                                 */
+  SHD_OP_EQ = 11,     /* a = operand type; null operand -> false           */
+  SHD_OP_NE = 12,
+  SHD_OP_GT = 13,
+  SHD_OP_GE = 14,
+  SHD_OP_LT = 15,
+  SHD_OP_LE = 16,
+  SHD_OP_AND = 17,    /* null -> false                                     */
+  SHD_OP_OR = 18,
+  SHD_OP_NOT = 19,    /* NOT(null) -> true                                 */
+  SHD_OP_ISNULL = 20,
+  SHD_OP_AGG = 21,    /* a = aggregator index (selector only)              */
+  SHD_OP_TS = 22      /* a = state, b = chain index : event timestamp      */
+};
+
+/* Chain indices (SiddhiConstants.CURRENT / LAST, C/util/SiddhiConstants.java:89-92). */
+#define SHD_IDX_CURRENT (-1)
+#define SHD_IDX_LAST (-2)
+
+enum shd_node { SHD_NODE_STREAM = 1, SHD_NODE_NEXT = 2, SHD_NODE_EVERY = 3,
+                SHD_NODE_LOGICAL = 4, SHD_NODE_COUNT = 5 };
+
+enum shd_handler { SHD_H_FILTER = 1, SHD_H_WINDOW = 2 };
+enum shd_window { SHD_W_LENGTH = 1, SHD_W_TIME = 2 };
+enum shd_agg { SHD_AGG_SUM = 1, SHD_AGG_AVG = 2, SHD_AGG_COUNT = 3 };
+
+/* Output / input event types (ComplexEvent.Type). */
+enum shd_evtype { SHD_EV_CURRENT = 0, SHD_EV_EXPIRED = 1, SHD_EV_TIMER = 2, SHD_EV_RESET = 3 };
+
+#endif

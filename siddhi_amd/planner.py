@@ -1,0 +1,602 @@
+"""Planner: query AST -> typed plan IR (include/siddhi_ir.h).
+
+Restates the reference planning rules the hot path depends on:
+
+* state ids in parse order, logical element 2 before element 1
+  (C/util/parser/StateInputStreamParser.java:148-408),
+* variable resolution incl. the `[last]` rule inside a state's own filter
+  (C/util/parser/ExpressionParser.java:1254-1439, :1262-1263, :1378-1385),
+  default chain index CURRENT for filters (SingleInputStreamParser.java:185-188)
+  and 0 for the selector (SelectorParser.java:215-218),
+* arithmetic result type = widest of DOUBLE > FLOAT > LONG > INT
+  (ExpressionParser.java:1488-1506),
+* compare promotion per executor class (C/executor/condition/compare/*):
+  relational ops use Java binary promotion; == / != on (Float, Long) or
+  (Long, Float) compare as double,
+* aggregator return types (SumAttributeAggregatorExecutor.java:84-134: INT/LONG
+  -> LONG, FLOAT/DOUBLE -> DOUBLE; avg -> DOUBLE; count -> LONG).
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import query_compiler as qc
+
+# ---- IR constants (mirror include/siddhi_ir.h) -----------------------------
+MAGIC, VERSION = 0x50444853, 1
+KIND_STATE, KIND_SINGLE = 1, 2
+T_STRING, T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL = 0, 1, 2, 3, 4, 5
+TYPE_CODE = {"string": T_STRING, "int": T_INT, "long": T_LONG, "float": T_FLOAT,
+             "double": T_DOUBLE, "bool": T_BOOL}
+TYPE_NAME = {v: k for k, v in TYPE_CODE.items()}
+(OP_END, OP_CONST, OP_NULL, OP_LOAD, OP_EVNULL, OP_CVT, OP_ADD, OP_SUB, OP_MUL,
+ OP_DIV, OP_MOD, OP_EQ, OP_NE, OP_GT, OP_GE, OP_LT, OP_LE, OP_AND, OP_OR, OP_NOT,
+ OP_ISNULL, OP_AGG, OP_TS) = range(23)
+IDX_CURRENT, IDX_LAST = -1, -2
+NODE_STREAM, NODE_NEXT, NODE_EVERY, NODE_LOGICAL, NODE_COUNT = 1, 2, 3, 4, 5
+H_FILTER, H_WINDOW = 1, 2
+W_LENGTH, W_TIME = 1, 2
+AGG_SUM, AGG_AVG, AGG_COUNT = 1, 2, 3
+UNKNOWN_STATE = -1
+NUMERIC_RANK = {T_INT: 0, T_LONG: 1, T_FLOAT: 2, T_DOUBLE: 3}
+ARITH_OPS = {"+": OP_ADD, "-": OP_SUB, "*": OP_MUL, "/": OP_DIV, "%": OP_MOD}
+CMP_OPS = {"==": OP_EQ, "!=": OP_NE, ">": OP_GT, ">=": OP_GE, "<": OP_LT, "<=": OP_LE}
+
+
+class SiddhiAppCreationException(Exception):
+    """Mirrors io.siddhi.core.exception.SiddhiAppCreationException."""
+
+
+class SiddhiAppValidationException(SiddhiAppCreationException):
+    """Mirrors io.siddhi.query.api.exception.SiddhiAppValidationException."""
+
+
+class UnsupportedPlanException(SiddhiAppCreationException):
+    """The plan is valid SiddhiQL but outside the MI355X hot path (SHD_E_UNSUPPORTED)."""
+
+
+# ---- string dictionary -----------------------------------------------------
+class StringDictionary:
+    """Host dictionary: string -> u32 id. Only equality is used on strings in
+    the hot path (SURVEY.md §7 'Dictionary-encoding strings')."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+        self.strings: List[str] = []
+
+    def id(self, s: str) -> int:
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.strings)
+            self.ids[s] = i
+            self.strings.append(s)
+        return i
+
+    def lookup(self, i: int) -> str:
+        return self.strings[i]
+
+
+# ---- plan model --------------------------------------------------------------
+@dataclass
+class Meta:
+    ref: Optional[str]
+    stream: str
+    attrs: List[Tuple[str, int]]      # (name, type code)
+    multi: bool = False
+
+    def attr(self, name):
+        for i, (n, t) in enumerate(self.attrs):
+            if n == name:
+                return i, t
+        return None
+
+
+@dataclass
+class Plan:
+    kind: int
+    query_name: Optional[str]
+    streams: List[str]                          # plan stream index -> app stream id
+    stream_types: List[List[int]]
+    consts: List[int] = field(default_factory=list)
+    exprs: List[List[Tuple[int, int, int, int]]] = field(default_factory=list)
+    partition_keys: List[Tuple[int, int]] = field(default_factory=list)   # (stream, expr)
+    # state
+    state_type: int = 0
+    within: int = -1
+    n_states: int = 0
+    tree: List[int] = field(default_factory=list)
+    # single
+    single_stream: int = 0
+    handlers: List[Tuple] = field(default_factory=list)
+    # selector
+    current_on: bool = True
+    expired_on: bool = False
+    aggs: List[Tuple[int, int, int]] = field(default_factory=list)        # (kind, expr, arg type)
+    group_by: List[int] = field(default_factory=list)
+    having: int = -1
+    outputs: List[Tuple[str, int, int]] = field(default_factory=list)     # (name, type, expr)
+    target: str = ""
+    # descriptive (host/runtime only)
+    states: List[Meta] = field(default_factory=list)
+    shape: Dict = field(default_factory=dict)
+
+    # -- serialization
+    def to_words(self) -> List[int]:
+        w = [MAGIC, VERSION, self.kind, len(self.streams)]
+        for types in self.stream_types:
+            w.append(len(types))
+            w.extend(types)
+        w.append(len(self.consts))
+        for c in self.consts:
+            c &= (1 << 64) - 1
+            w.append(_s32(c & 0xFFFFFFFF))
+            w.append(_s32(c >> 32))
+        w.append(len(self.exprs))
+        for e in self.exprs:
+            w.append(len(e))
+            for ins in e:
+                w.extend(ins)
+        w.append(len(self.partition_keys))
+        for s, e in self.partition_keys:
+            w.extend([s, e])
+        if self.kind == KIND_STATE:
+            w.extend([self.state_type, *_split64(self.within), self.n_states])
+            w.extend(self.tree)
+        else:
+            w.extend([self.single_stream, len(self.handlers)])
+            for h in self.handlers:
+                if h[0] == H_FILTER:
+                    w.extend([H_FILTER, h[1]])
+                else:
+                    w.extend([H_WINDOW, h[1], *_split64(h[2])])
+        w.extend([int(self.current_on), int(self.expired_on), len(self.aggs)])
+        for a in self.aggs:
+            w.extend(a)
+        w.append(len(self.group_by))
+        w.extend(self.group_by)
+        w.append(self.having)
+        w.append(len(self.outputs))
+        for _, t, e in self.outputs:
+            w.extend([t, e])
+        return w
+
+    def to_bytes(self) -> bytes:
+        words = self.to_words()
+        return struct.pack("<%di" % len(words), *words)
+
+
+def _s32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= (1 << 31) else x
+
+
+def _split64(v):
+    v &= (1 << 64) - 1
+    return _s32(v & 0xFFFFFFFF), _s32(v >> 32)
+
+
+def const_bits(type_code: int, value) -> int:
+    """64-bit payload of a value of the given type (see include/siddhi_ir.h)."""
+    if type_code in (T_INT, T_LONG):
+        return int(value) & ((1 << 64) - 1)
+    if type_code == T_FLOAT:
+        return struct.unpack("<I", struct.pack("<f", float(value)))[0]
+    if type_code == T_DOUBLE:
+        return struct.unpack("<Q", struct.pack("<d", float(value)))[0]
+    if type_code == T_BOOL:
+        return 1 if value else 0
+    if type_code == T_STRING:
+        return int(value)
+    raise ValueError(type_code)
+
+
+# ---- expression compiler -------------------------------------------------------
+class ExprCompiler:
+    def __init__(self, plan: Plan, dictionary: StringDictionary, metas: List[Meta],
+                 state_query: bool):
+        self.plan = plan
+        self.dict = dictionary
+        self.metas = metas
+        self.state_query = state_query
+        self.agg_allowed = False
+
+    def compile(self, expr, current_state: int, default_index: int, want_bool=False,
+                allow_agg=False) -> Tuple[int, int]:
+        """Returns (expr id, result type)."""
+        code: List[Tuple[int, int, int, int]] = []
+        self.agg_allowed = allow_agg
+        t = self._emit(expr, code, current_state, default_index)
+        if want_bool and t != T_BOOL:
+            raise SiddhiAppValidationException("condition must be of type BOOL but found %s" % TYPE_NAME.get(t))
+        self.plan.exprs.append(code)
+        return len(self.plan.exprs) - 1, t
+
+    def _const(self, t, v):
+        bits = const_bits(t, v)
+        try:
+            idx = self.plan.consts.index(bits)
+        except ValueError:
+            self.plan.consts.append(bits)
+            idx = len(self.plan.consts) - 1
+        return idx
+
+    def _emit(self, e, code, cs, di) -> int:
+        if isinstance(e, qc.Const):
+            if e.type == "null":
+                code.append((OP_NULL, 0, T_DOUBLE, 0))
+                return T_DOUBLE
+            t = TYPE_CODE[e.type]
+            v = self.dict.id(e.value) if t == T_STRING else e.value
+            code.append((OP_CONST, self._const(t, v), t, 0))
+            return t
+        if isinstance(e, qc.Var):
+            if self.state_query and e.stream is not None and e.attr is not None and \
+                    self._is_stream_ref_only(e):
+                pass
+            return self._emit_var(e, code, cs, di)
+        if isinstance(e, qc.IsNull):
+            inner = e.expr
+            if isinstance(inner, qc.StreamRef) or (isinstance(inner, qc.Var) and inner.stream is None
+                                                   and self._ref_state(inner.attr) is not None
+                                                   and not self._attr_exists(inner.attr, cs)):
+                ref = inner.stream if isinstance(inner, qc.StreamRef) else inner.attr
+                idx = inner.index if isinstance(inner, qc.StreamRef) else None
+                st = self._ref_state(ref)
+                if st is None:
+                    raise SiddhiAppValidationException("stream reference %s not found" % ref)
+                ci = di if idx is None else (idx + 1 if idx <= qc.LAST else idx)
+                code.append((OP_EVNULL, st, ci, 0))
+                return T_BOOL
+            self._emit(inner, code, cs, di)
+            code.append((OP_ISNULL, 0, 0, 0))
+            return T_BOOL
+        if isinstance(e, qc.Not):
+            t = self._emit(e.expr, code, cs, di)
+            if t != T_BOOL:
+                raise SiddhiAppValidationException("not requires a BOOL operand")
+            code.append((OP_NOT, 0, 0, 0))
+            return T_BOOL
+        if isinstance(e, qc.BinOp):
+            if e.op in ("and", "or"):
+                lt = self._emit(e.left, code, cs, di)
+                rt = self._emit(e.right, code, cs, di)
+                if lt != T_BOOL or rt != T_BOOL:
+                    raise SiddhiAppValidationException("%s requires BOOL operands" % e.op)
+                code.append((OP_AND if e.op == "and" else OP_OR, 0, 0, 0))
+                return T_BOOL
+            if e.op in ARITH_OPS:
+                lcode, rcode = [], []
+                lt = self._emit(e.left, lcode, cs, di)
+                rt = self._emit(e.right, rcode, cs, di)
+                if lt not in NUMERIC_RANK or rt not in NUMERIC_RANK:
+                    raise SiddhiAppValidationException("arithmetic on non-numeric operands")
+                rtype = max(lt, rt, key=lambda x: NUMERIC_RANK[x])
+                code.extend(lcode)
+                if lt != rtype:
+                    code.append((OP_CVT, lt, rtype, 0))
+                code.extend(rcode)
+                if rt != rtype:
+                    code.append((OP_CVT, rt, rtype, 0))
+                code.append((ARITH_OPS[e.op], rtype, 0, 0))
+                return rtype
+            if e.op in CMP_OPS:
+                lcode, rcode = [], []
+                lt = self._emit(e.left, lcode, cs, di)
+                rt = self._emit(e.right, rcode, cs, di)
+                ct = compare_type(e.op, lt, rt)
+                code.extend(lcode)
+                if lt != ct:
+                    code.append((OP_CVT, lt, ct, 0))
+                code.extend(rcode)
+                if rt != ct:
+                    code.append((OP_CVT, rt, ct, 0))
+                code.append((CMP_OPS[e.op], ct, 0, 0))
+                return T_BOOL
+            raise SiddhiAppValidationException("unknown operator %s" % e.op)
+        if isinstance(e, qc.Func):
+            name = e.name.lower()
+            if e.namespace is None and name in ("sum", "avg", "count"):
+                if not self.agg_allowed:
+                    raise SiddhiAppValidationException("aggregator %s not allowed here" % name)
+                if name == "count":
+                    arg, at = -1, -1
+                    if e.args:
+                        # count(attr) counts events regardless of nulls
+                        arg, at = ExprCompiler(self.plan, self.dict, self.metas, self.state_query) \
+                            .compile(e.args[0], cs, di)
+                    self.plan.aggs.append((AGG_COUNT, arg, at))
+                    rt = T_LONG
+                else:
+                    if len(e.args) != 1:
+                        raise SiddhiAppValidationException("%s needs exactly one parameter" % name)
+                    sub = ExprCompiler(self.plan, self.dict, self.metas, self.state_query)
+                    arg, at = sub.compile(e.args[0], cs, di)
+                    if at not in NUMERIC_RANK:
+                        raise SiddhiAppValidationException("%s not supported for %s" % (name, TYPE_NAME.get(at)))
+                    self.plan.aggs.append((AGG_SUM if name == "sum" else AGG_AVG, arg, at))
+                    rt = (T_LONG if at in (T_INT, T_LONG) else T_DOUBLE) if name == "sum" else T_DOUBLE
+                code.append((OP_AGG, len(self.plan.aggs) - 1, 0, 0))
+                return rt
+            if e.namespace is None and name == "eventtimestamp" and not e.args:
+                code.append((OP_TS, 0, IDX_CURRENT, 0))
+                return T_LONG
+            raise UnsupportedPlanException("function %s is outside the hot path" % e.name)
+        raise SiddhiAppValidationException("unsupported expression %r" % (e,))
+
+    def _is_stream_ref_only(self, e):
+        return False
+
+    def _ref_state(self, ref):
+        for i, m in enumerate(self.metas):
+            if m.ref == ref or (m.ref is None and m.stream == ref):
+                return i
+        return None
+
+    def _attr_exists(self, attr, cs):
+        if cs >= 0:
+            return self.metas[cs].attr(attr) is not None
+        return any(m.attr(attr) is not None for m in self.metas)
+
+    def _emit_var(self, v: qc.Var, code, cs, di) -> int:
+        """ExpressionParser.parseVariable (C/util/parser/ExpressionParser.java:1254-1439)."""
+        if v.index is not None:
+            ci = v.index + 1 if v.index <= qc.LAST else v.index
+        else:
+            ci = di
+        if not self.state_query:
+            m = self.metas[0]
+            if v.stream is not None and v.stream != m.stream and v.stream != m.ref:
+                raise SiddhiAppValidationException("Id '%s' not defined within the current scope" % v.stream)
+            found = m.attr(v.attr)
+            if found is None:
+                raise SiddhiAppValidationException("No matching stream reference found for attribute '%s'" % v.attr)
+            code.append((OP_LOAD, 0, IDX_CURRENT, found[0] | (found[1] << 16)))
+            return found[1]
+        state, typ, attr = None, None, None
+        if v.stream is None:
+            if cs == UNKNOWN_STATE:
+                for i, m in enumerate(self.metas):
+                    f = m.attr(v.attr)
+                    if f is not None:
+                        if state is not None:
+                            raise SiddhiAppValidationException(
+                                "Input streams contain attribute with same name '%s'" % v.attr)
+                        state, (attr, typ) = i, f
+            else:
+                f = self.metas[cs].attr(v.attr)
+                if f is None:
+                    raise SiddhiAppValidationException("attribute '%s' not found in state %d" % (v.attr, cs))
+                state, (attr, typ) = cs, f
+        else:
+            for i, m in enumerate(self.metas):
+                if m.ref is None:
+                    if m.stream == v.stream:
+                        f = m.attr(v.attr)
+                        if f is None:
+                            raise SiddhiAppValidationException("attribute %s not in %s" % (v.attr, m.stream))
+                        state, (attr, typ) = i, f
+                        break
+                elif m.ref == v.stream:
+                    f = m.attr(v.attr)
+                    if f is None:
+                        raise SiddhiAppValidationException("attribute %s not in %s" % (v.attr, m.stream))
+                    state, (attr, typ) = i, f
+                    if cs > -1 and self.metas[cs].ref is not None and v.index is not None \
+                            and v.index <= qc.LAST and v.stream == self.metas[cs].ref:
+                        ci = v.index
+                    elif cs == UNKNOWN_STATE and v.index is None and m.multi:
+                        raise UnsupportedPlanException(
+                            "multi-value selection of count state '%s' without index" % v.stream)
+                    break
+        if state is None:
+            if v.stream is None:
+                raise SiddhiAppValidationException(
+                    "No matching stream reference found for attribute '%s'" % v.attr)
+            raise SiddhiAppValidationException(
+                "Stream with reference '%s' not found for attribute '%s'" % (v.stream, v.attr))
+        code.append((OP_LOAD, state, ci, attr | (typ << 16)))
+        return typ
+
+
+def compare_type(op, lt, rt) -> int:
+    """Operand type each compare executor class compares in
+    (C/executor/condition/compare/*/*CompareConditionExpressionExecutor*.java)."""
+    if lt == T_STRING or rt == T_STRING:
+        if lt == rt == T_STRING and op in ("==", "!="):
+            return T_STRING
+        raise SiddhiAppValidationException("string comparison %s not supported" % op)
+    if lt == T_BOOL or rt == T_BOOL:
+        if lt == rt == T_BOOL and op in ("==", "!="):
+            return T_BOOL
+        raise SiddhiAppValidationException("bool comparison %s not supported" % op)
+    if op in ("==", "!=") and {lt, rt} == {T_FLOAT, T_LONG}:
+        return T_DOUBLE
+    return max(lt, rt, key=lambda x: NUMERIC_RANK[x])
+
+
+# ---- query planning -------------------------------------------------------------
+@dataclass
+class QueryPlan:
+    plan: Plan
+    ir: bytes
+    input_streams: List[str]
+    output_names: List[str]
+    output_types: List[int]
+    target: str
+    name: Optional[str]
+    partitioned: bool
+    receiver_kind: Dict[str, str]        # stream -> 'single' | 'multi' (state queries)
+
+
+def _stream_meta(app: qc.SiddhiApp, sid: str, ref=None, extra_streams=None) -> Meta:
+    sd = app.streams.get(sid) or (extra_streams or {}).get(sid)
+    if sd is None:
+        raise SiddhiAppValidationException("Stream '%s' is not defined" % sid)
+    return Meta(ref, sid, [(n, TYPE_CODE[t]) for n, t in sd.attrs])
+
+
+def plan_query(app: qc.SiddhiApp, q: qc.Query, dictionary: StringDictionary,
+               partition: Optional[qc.Partition] = None, extra_streams=None) -> QueryPlan:
+    inp = q.input
+    if q.inner_target or getattr(inp, "inner", False) or _uses_inner_stream(inp):
+        raise UnsupportedPlanException("partition-inner streams (#stream) are outside the hot path")
+    if isinstance(inp, qc.StateInput):
+        return _plan_state(app, q, dictionary, partition, extra_streams)
+    if isinstance(inp, qc.SingleInput):
+        return _plan_single(app, q, dictionary, partition, extra_streams)
+    raise UnsupportedPlanException("input kind %s is outside the hot path" % type(inp).__name__)
+
+
+def _plan_partition(plan: Plan, comp_factory, partition, streams: List[str], app, dictionary,
+                    extra_streams):
+    if partition is None:
+        return
+    for kexpr, sid in partition.with_:
+        if sid not in streams:
+            continue
+        si = streams.index(sid)
+        m = _stream_meta(app, sid, None, extra_streams)
+        ec = ExprCompiler(plan, dictionary, [m], state_query=False)
+        eid, t = ec.compile(kexpr, 0, IDX_CURRENT)
+        plan.partition_keys.append((si, eid))
+    missing = [s for s in streams if s not in [sid for _, sid in partition.with_]]
+    if missing:
+        raise UnsupportedPlanException("partition without a key for streams %s (broadcast) is outside the hot path"
+                                       % missing)
+
+
+def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta], state_query: bool):
+    sel = q.selector
+    plan.current_on = q.event_type in ("current", "all")
+    plan.expired_on = q.event_type in ("expired", "all")
+    names, types = [], []
+    if sel.select_all:
+        if state_query:
+            attrs = []
+            for st, m in enumerate(metas):
+                for (n, t) in m.attrs:
+                    attrs.append(qc.OutAttr(qc.Var(n, m.ref or m.stream, None), n))
+        else:
+            attrs = [qc.OutAttr(qc.Var(n), n) for n, _ in metas[0].attrs]
+    else:
+        attrs = sel.attrs
+    cs = UNKNOWN_STATE if state_query else 0
+    for oa in attrs:
+        eid, t = ec.compile(oa.expr, cs, 0, allow_agg=True)
+        plan.outputs.append((oa.name, t, eid))
+        names.append(oa.name)
+        types.append(t)
+    for g in sel.group_by:
+        eid, _ = ec.compile(g, cs, 0)
+        plan.group_by.append(eid)
+    if sel.having is not None:
+        raise UnsupportedPlanException("having is outside the round-1 hot path")
+    return names, types
+
+
+def _plan_state(app, q, dictionary, partition, extra_streams) -> QueryPlan:
+    si: qc.StateInput = q.input
+    streams: List[str] = []
+    counts: Dict[str, int] = {}
+    metas: List[Meta] = []
+    plan = Plan(KIND_STATE, q.name, streams, [])
+    plan.state_type = 0 if si.kind == "pattern" else 1
+    plan.within = si.within_ms if si.within_ms is not None else -1
+    ec = ExprCompiler(plan, dictionary, metas, state_query=True)
+
+    def stream_idx(sid):
+        if sid not in streams:
+            streams.append(sid)
+            plan.stream_types.append([t for _, t in _stream_meta(app, sid, None, extra_streams).attrs])
+        counts[sid] = counts.get(sid, 0) + 1
+        return streams.index(sid)
+
+    def walk(el, multi=False):
+        if isinstance(el, qc.StreamSE):
+            sidx = stream_idx(el.stream)
+            m = _stream_meta(app, el.stream, el.ref, extra_streams)
+            m.multi = multi
+            metas.append(m)
+            state_id = len(metas) - 1
+            fids = []
+            for f in el.filters:
+                eid, _ = ec.compile(f, state_id, IDX_CURRENT, want_bool=True)
+                fids.append(eid)
+            wait = el.waiting_ms if el.waiting_ms is not None else -1
+            if el.absent and el.waiting_ms is None:
+                raise UnsupportedPlanException("absent state without 'for' time")
+            return [NODE_STREAM, state_id, sidx, int(el.absent), *_split64(wait), len(fids), *fids]
+        if isinstance(el, qc.NextSE):
+            a = walk(el.a)
+            b = walk(el.b)
+            return [NODE_NEXT] + a + b
+        if isinstance(el, qc.EverySE):
+            return [NODE_EVERY] + walk(el.inner)
+        if isinstance(el, qc.LogicalSE):
+            b = walk(el.b)       # element 2 first (StateInputStreamParser.java:349-361)
+            a = walk(el.a)
+            return [NODE_LOGICAL, 0 if el.kind == "and" else 1] + a + b
+        if isinstance(el, qc.CountSE):
+            inner = walk(el.stream, multi=True)
+            return [NODE_COUNT, el.min, el.max] + inner
+        raise UnsupportedPlanException("state element %r" % (el,))
+
+    plan.tree = walk(si.element)
+    plan.n_states = len(metas)
+    plan.states = metas
+    names, types = _plan_selector(plan, q, ec, metas, True)
+    if plan.aggs or plan.group_by:
+        raise UnsupportedPlanException("aggregation over pattern output is outside the round-1 hot path")
+    _plan_partition(plan, None, partition, streams, app, dictionary, extra_streams)
+    plan.target = q.target
+    plan.shape = classify_state_shape(plan, si)
+    recv = {s: ("multi" if counts[s] > 1 else "single") for s in streams}
+    return QueryPlan(plan, plan.to_bytes(), list(streams), names, types, q.target, q.name,
+                     partition is not None, recv)
+
+
+def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
+    si: qc.SingleInput = q.input
+    m = _stream_meta(app, si.stream, si.ref, extra_streams)
+    plan = Plan(KIND_SINGLE, q.name, [si.stream], [[t for _, t in m.attrs]])
+    ec = ExprCompiler(plan, dictionary, [m], state_query=False)
+    n_windows = 0
+    for h in si.handlers:
+        if isinstance(h, qc.Filter):
+            eid, _ = ec.compile(h.expr, 0, IDX_CURRENT, want_bool=True)
+            plan.handlers.append((H_FILTER, eid))
+        else:
+            n_windows += 1
+            if n_windows > 1:
+                raise SiddhiAppValidationException("only one window per stream")
+            if h.name not in ("length", "time"):
+                raise UnsupportedPlanException("window %s is outside the round-1 hot path" % h.name)
+            if len(h.params) != 1 or not isinstance(h.params[0], qc.Const) or \
+                    h.params[0].type not in ("int", "long"):
+                raise SiddhiAppValidationException("%s window needs one constant int/long parameter" % h.name)
+            plan.handlers.append((H_WINDOW, W_LENGTH if h.name == "length" else W_TIME,
+                                  int(h.params[0].value)))
+    names, types = _plan_selector(plan, q, ec, [m], False)
+    _plan_partition(plan, None, partition, [si.stream], app, dictionary, extra_streams)
+    plan.target = q.target
+    plan.shape = {"kind": "single", "window": next((h[1] for h in plan.handlers if h[0] == H_WINDOW), 0)}
+    return QueryPlan(plan, plan.to_bytes(), [si.stream], names, types, q.target, q.name,
+                     partition is not None, {si.stream: "single"})
+
+
+def _uses_inner_stream(inp) -> bool:
+    return False
+
+
+def classify_state_shape(plan: Plan, si: qc.StateInput) -> Dict:
+    """Shape facts the device planner uses to pick kernels (e.g. the 2-state
+    `every e1 -> e2 within W` fast path)."""
+    el = si.element
+    shape = {"kind": "state", "type": si.kind}
+    if si.kind == "pattern" and isinstance(el, qc.NextSE) and isinstance(el.a, qc.EverySE) \
+            and isinstance(el.a.inner, qc.StreamSE) and isinstance(el.b, qc.StreamSE) \
+            and not el.a.inner.absent and not el.b.absent:
+        shape["every_a_then_b"] = True
+    return shape

@@ -1,0 +1,409 @@
+"""Host-side mirror of the reference API for the hot path.
+
+SiddhiManager / SiddhiAppRuntime / InputHandler / QueryCallback / StreamCallback
+with the reference's names, argument meaning and error behaviour
+(C/SiddhiManager.java:84-96, C/SiddhiAppRuntimeImpl.java:260-269,414-415,
+C/stream/input/InputHandler.java:50-95, C/query/output/callback/QueryCallback.java:61-106,
+C/stream/output/StreamCallback.java:93-129).
+
+Every query is executed by a query engine.  The product engine is
+`siddhi_amd.hip_engine.HipQueryEngine` (libsiddhi_hip, MI355X); there is no CPU
+fallback: if the HIP library cannot be loaded the runtime raises.  Tests may
+pass another engine factory (the CPU oracle) explicitly as a checker.
+
+Junction semantics (C/stream/StreamJunction.java:146-272): synchronous fan-out
+to subscribed queries in definition order; query outputs are delivered to the
+target stream's junction within the same call.  Time (playback,
+C/util/timestamp/TimestampGeneratorImpl.java:58-76): every InputHandler.send
+advances the app clock to the last event's timestamp and fires every query's
+due timers before the events are routed.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import planner as pl
+from . import query_compiler as qc
+
+CURRENT, EXPIRED = 0, 1
+
+
+class Event:
+    """io.siddhi.core.event.Event"""
+
+    __slots__ = ("timestamp", "data", "is_expired")
+
+    def __init__(self, timestamp: int = -1, data=None, is_expired: bool = False):
+        self.timestamp = int(timestamp)
+        self.data = list(data) if data is not None else []
+        self.is_expired = is_expired
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def getData(self, i=None):
+        return self.data if i is None else self.data[i]
+
+    def isExpired(self):
+        return self.is_expired
+
+    def __repr__(self):
+        return "Event{timestamp=%d, data=%r, isExpired=%s}" % (self.timestamp, self.data, self.is_expired)
+
+
+class QueryCallback:
+    """io.siddhi.core.query.output.callback.QueryCallback"""
+
+    def receive(self, timestamp, inEvents, removeEvents):  # noqa: N802,N803
+        raise NotImplementedError
+
+
+class StreamCallback:
+    """io.siddhi.core.stream.output.StreamCallback"""
+
+    def receive(self, events):
+        raise NotImplementedError
+
+
+class _FnQueryCallback(QueryCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, timestamp, inEvents, removeEvents):
+        self.fn(timestamp, inEvents, removeEvents)
+
+
+class _FnStreamCallback(StreamCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, events):
+        self.fn(events)
+
+
+# ---------------------------------------------------------------- columns
+_NP = {pl.T_STRING: np.uint32, pl.T_INT: np.int32, pl.T_LONG: np.int64, pl.T_FLOAT: np.float32,
+       pl.T_DOUBLE: np.float64, pl.T_BOOL: np.uint8}
+
+
+class ColumnBatch:
+    """Columnar micro-batch of one stream (SoA), the unit handed to engines."""
+
+    def __init__(self, ts: np.ndarray, cols: List[np.ndarray], nulls: List[Optional[np.ndarray]],
+                 call_offsets: Optional[np.ndarray] = None):
+        self.ts = ts
+        self.cols = cols
+        self.nulls = nulls
+        self.n = len(ts)
+        self.call_offsets = call_offsets if call_offsets is not None else np.array([0, self.n], np.int64)
+
+
+def _java_value(v, t, dictionary):
+    if v is None:
+        return None
+    if t == pl.T_STRING:
+        return dictionary.id(str(v))
+    if t == pl.T_BOOL:
+        return 1 if v else 0
+    if t == pl.T_INT:
+        iv = int(v)
+        return ((iv + 2 ** 31) % 2 ** 32) - 2 ** 31
+    if t == pl.T_LONG:
+        return int(v)
+    return float(v)
+
+
+def rows_to_batch(types: List[int], events: List[Event], dictionary) -> ColumnBatch:
+    n = len(events)
+    ts = np.fromiter((e.timestamp for e in events), np.int64, n)
+    cols, nulls = [], []
+    for a, t in enumerate(types):
+        raw = [_java_value(e.data[a] if a < len(e.data) else None, t, dictionary) for e in events]
+        nm = np.fromiter((x is None for x in raw), np.uint8, n)
+        col = np.array([0 if x is None else x for x in raw], dtype=_NP[t])
+        cols.append(col)
+        nulls.append(nm if nm.any() else None)
+    return ColumnBatch(ts, cols, nulls)
+
+
+def decode_value(bits: int, t: int, dictionary):
+    bits = int(bits) & ((1 << 64) - 1)
+    if t == pl.T_STRING:
+        return dictionary.lookup(bits)
+    if t == pl.T_INT:
+        v = bits & 0xFFFFFFFF
+        return v - (1 << 32) if v >= (1 << 31) else v
+    if t == pl.T_LONG:
+        return bits - (1 << 64) if bits >= (1 << 63) else bits
+    if t == pl.T_FLOAT:
+        return float(np.array([bits & 0xFFFFFFFF], np.uint32).view(np.float32)[0])
+    if t == pl.T_DOUBLE:
+        return float(np.array([bits], np.uint64).view(np.float64)[0])
+    if t == pl.T_BOOL:
+        return bool(bits)
+    raise ValueError(t)
+
+
+class OutputChunk:
+    """One callback invocation worth of output rows (ComplexEventChunk)."""
+
+    __slots__ = ("types", "ts", "values", "nulls")
+
+    def __init__(self, types, ts, values, nulls):
+        self.types = types      # np.int32 [n] CURRENT / EXPIRED
+        self.ts = ts            # np.int64 [n]
+        self.values = values    # np.uint64 [n, n_out] bit patterns
+        self.nulls = nulls      # np.uint8 [n, n_out]
+
+
+def split_chunks(chunk_ids, types, ts, vals, nulls) -> List[OutputChunk]:
+    out = []
+    n = len(chunk_ids)
+    if n == 0:
+        return out
+    starts = np.flatnonzero(np.r_[True, chunk_ids[1:] != chunk_ids[:-1]])
+    ends = np.r_[starts[1:], n]
+    for s, e in zip(starts, ends):
+        out.append(OutputChunk(types[s:e], ts[s:e], vals[s:e], nulls[s:e]))
+    return out
+
+
+# ---------------------------------------------------------------- runtime
+class _QueryRuntime:
+    def __init__(self, qp: pl.QueryPlan, engine, name):
+        self.qp = qp
+        self.engine = engine
+        self.name = name
+        self.callbacks: List[QueryCallback] = []
+
+
+class InputHandler:
+    """io.siddhi.core.stream.input.InputHandler (C/stream/input/InputHandler.java:50-95)."""
+
+    def __init__(self, runtime: "SiddhiAppRuntime", stream_id: str):
+        self._rt = runtime
+        self.stream_id = stream_id
+
+    def getStreamId(self):
+        return self.stream_id
+
+    def send(self, *args):
+        """send(Object[] data) | send(long ts, Object[] data) | send(Event) | send(Event[])."""
+        if len(args) == 2:
+            evs = [Event(args[0], args[1])]
+        elif len(args) == 1:
+            a = args[0]
+            if isinstance(a, Event):
+                evs = [a]
+            elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
+                evs = list(a)
+            elif isinstance(a, (list, tuple)) and not a:
+                return
+            else:
+                evs = [Event(self._rt._wall_clock(), a)]
+        else:
+            raise TypeError("send(data) | send(ts, data) | send(Event) | send(Event[])")
+        self._rt._send(self.stream_id, evs)
+
+    def send_batch(self, batch: ColumnBatch):
+        """Columnar fast path: one pre-built SoA batch (call boundaries in batch.call_offsets)."""
+        self._rt._send_columns(self.stream_id, batch)
+
+
+class SiddhiAppRuntime:
+    """io.siddhi.core.SiddhiAppRuntime"""
+
+    def __init__(self, app: qc.SiddhiApp, engine_factory: Callable, app_text: str):
+        self.app = app
+        self.app_text = app_text
+        self.dictionary = pl.StringDictionary()
+        self.name = None
+        ann = app.annotation("app:name")
+        if ann is not None and ann.elements:
+            self.name = ann.elements[0][1]
+        self.playback = app.annotation("app:playback") is not None
+        self.stream_types: Dict[str, List[int]] = {
+            s: [pl.TYPE_CODE[t] for _, t in sd.attrs] for s, sd in app.streams.items()}
+        self.queries: List[_QueryRuntime] = []
+        self.stream_callbacks: Dict[str, List[StreamCallback]] = {}
+        self.subscribers: Dict[str, List[tuple]] = {}
+        self.started = False
+        self._last_wall = 0
+        extra = {}
+        anon = 0
+        for item in app.execution_order:
+            part = item if isinstance(item, qc.Partition) else None
+            qs = item.queries if part else [item]
+            for q in qs:
+                # output stream definitions are inferred (QueryParser: OutputStream definition)
+                qp = pl.plan_query(app, q, self.dictionary, part, extra)
+                if q.target not in app.streams and q.target not in extra:
+                    extra[q.target] = qc.StreamDef(q.target, [(n, pl.TYPE_NAME[t]) for n, t in
+                                                              zip(qp.output_names, qp.output_types)])
+                    self.stream_types[q.target] = list(qp.output_types)
+                name = q.name or "query_%d" % anon
+                anon += 1
+                engine = engine_factory(qp, self.dictionary)
+                qr = _QueryRuntime(qp, engine, name)
+                self.queries.append(qr)
+                for si, sid in enumerate(qp.input_streams):
+                    self.subscribers.setdefault(sid, []).append((qr, si))
+
+    # -- public API
+    def getName(self):
+        return self.name
+
+    def addCallback(self, name: str, callback):
+        if callable(callback) and not isinstance(callback, (QueryCallback, StreamCallback)):
+            raise TypeError("callback must be a QueryCallback or StreamCallback")
+        if isinstance(callback, QueryCallback):
+            for q in self.queries:
+                if q.name == name:
+                    q.callbacks.append(callback)
+                    return
+            raise pl.SiddhiAppCreationException("No query with name '%s' exists" % name)
+        if isinstance(callback, StreamCallback):
+            if name not in self.stream_types:
+                raise pl.SiddhiAppCreationException("Stream with stream ID '%s' has not been defined" % name)
+            self.stream_callbacks.setdefault(name, []).append(callback)
+            return
+        raise TypeError("unknown callback type")
+
+    def getInputHandler(self, stream_id: str) -> InputHandler:
+        if stream_id not in self.stream_types:
+            raise pl.SiddhiAppCreationException("Stream with stream ID %s has not been defined" % stream_id)
+        return InputHandler(self, stream_id)
+
+    def start(self):
+        self.started = True
+
+    def shutdown(self):
+        for q in self.queries:
+            close = getattr(q.engine, "close", None)
+            if close:
+                close()
+        self.queries = []
+        self.started = False
+
+    # -- internals
+    def _wall_clock(self):
+        t = int(time.time() * 1000)
+        self._last_wall = max(self._last_wall, t)
+        return self._last_wall
+
+    def _send(self, stream_id, events: List[Event]):
+        if not self.started:
+            raise RuntimeError("Siddhi app '%s' is not running, cannot send events" % self.name)
+        batch = rows_to_batch(self.stream_types[stream_id], events, self.dictionary)
+        self._send_columns(stream_id, batch)
+
+    def _send_columns(self, stream_id, batch: ColumnBatch):
+        if batch.n == 0:
+            return
+        offs = batch.call_offsets
+        if len(offs) > 2:
+            # several InputHandler calls in one batch: time advances per call
+            for c in range(len(offs) - 1):
+                s, e = int(offs[c]), int(offs[c + 1])
+                sub = ColumnBatch(batch.ts[s:e], [x[s:e] for x in batch.cols],
+                                  [None if x is None else x[s:e] for x in batch.nulls])
+                self._send_columns(stream_id, sub)
+            return
+        # setCurrentTimestamp(last ts): every query's due timers first
+        t = int(batch.ts[-1])
+        for q in self.queries:
+            self._deliver(q, q.engine.set_time(t))
+        self._junction(stream_id, batch)
+
+    def _junction(self, stream_id, batch: ColumnBatch):
+        cbs = self.stream_callbacks.get(stream_id)
+        if cbs:
+            evs = self._batch_events(stream_id, batch)
+            for cb in cbs:
+                cb.receive(evs)
+        for q, si in self.subscribers.get(stream_id, []):
+            self._deliver(q, q.engine.push(si, batch))
+
+    def _batch_events(self, stream_id, batch):
+        types = self.stream_types[stream_id]
+        evs = []
+        for i in range(batch.n):
+            data = []
+            for a, t in enumerate(types):
+                if batch.nulls[a] is not None and batch.nulls[a][i]:
+                    data.append(None)
+                else:
+                    v = batch.cols[a][i]
+                    data.append(self.dictionary.lookup(int(v)) if t == pl.T_STRING else
+                                bool(v) if t == pl.T_BOOL else v.item())
+            evs.append(Event(int(batch.ts[i]), data))
+        return evs
+
+    def _deliver(self, q: _QueryRuntime, chunks: List[OutputChunk]):
+        if not chunks:
+            return
+        types = q.qp.output_types
+        for ch in chunks:
+            evs = []
+            for i in range(len(ch.ts)):
+                data = [None if ch.nulls[i, k] else decode_value(ch.values[i, k], t, self.dictionary)
+                        for k, t in enumerate(types)]
+                evs.append(Event(int(ch.ts[i]), data, int(ch.types[i]) == EXPIRED))
+            # QueryCallback.receiveStreamEvent (QueryCallback.java:61-91)
+            if q.callbacks:
+                cur = [e for e in evs if not e.is_expired] or None
+                rem = [e for e in evs if e.is_expired] or None
+                ts = evs[-1].timestamp
+                for cb in q.callbacks:
+                    cb.receive(ts, cur, rem)
+            # InsertIntoStreamCallback: EXPIRED -> CURRENT, into the target junction
+            target = q.qp.target
+            if target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target)):
+                cols, nulls = [], []
+                for k, t in enumerate(types):
+                    col = np.array([ch.values[i, k] for i in range(len(ch.ts))], np.uint64)
+                    cols.append(_bits_to_col(col, t))
+                    nm = ch.nulls[:, k].astype(np.uint8)
+                    nulls.append(nm if nm.any() else None)
+                out = ColumnBatch(np.asarray(ch.ts, np.int64), cols, nulls)
+                self._junction(target, out)
+
+
+def _bits_to_col(bits: np.ndarray, t: int) -> np.ndarray:
+    if t == pl.T_INT:
+        return (bits & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    if t == pl.T_LONG:
+        return bits.view(np.int64)
+    if t == pl.T_FLOAT:
+        return (bits & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
+    if t == pl.T_DOUBLE:
+        return bits.view(np.float64)
+    if t == pl.T_BOOL:
+        return bits.astype(np.uint8)
+    return bits.astype(np.uint32)
+
+
+class SiddhiManager:
+    """io.siddhi.core.SiddhiManager (C/SiddhiManager.java:84-96)."""
+
+    def __init__(self, engine_factory: Optional[Callable] = None):
+        self._engine_factory = engine_factory
+        self._runtimes: List[SiddhiAppRuntime] = []
+
+    def createSiddhiAppRuntime(self, app_text: str) -> SiddhiAppRuntime:
+        app = qc.parse(app_text)
+        factory = self._engine_factory
+        if factory is None:
+            from .hip_engine import HipQueryEngine   # product path: MI355X only
+            factory = HipQueryEngine
+        rt = SiddhiAppRuntime(app, factory, app_text)
+        self._runtimes.append(rt)
+        return rt
+
+    def shutdown(self):
+        for r in self._runtimes:
+            r.shutdown()
+        self._runtimes = []

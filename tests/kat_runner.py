@@ -1,0 +1,104 @@
+"""Runs a known-answer case (tests/golden/kat/*.json) through the host API
+(SiddhiManager -> SiddhiAppRuntime -> InputHandler -> callbacks) with a given
+query-engine factory, and checks the reference test's expectations.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+
+from siddhi_amd import runtime as rt
+
+KAT_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kat")
+
+
+def load_cases():
+    cases = []
+    for f in sorted(glob.glob(os.path.join(KAT_DIR, "*.json"))):
+        with open(f) as fp:
+            cases.extend(json.load(fp))
+    return cases
+
+
+def _py(v):
+    if isinstance(v, dict):
+        (k, x), = v.items()
+        if k == "float":
+            return ("f", float(np.float32(x)))
+        return ("n", x)
+    return ("v", v)
+
+
+def values_equal(expected, actual):
+    kind, e = _py(expected)
+    if e is None or actual is None:
+        return e is None and actual is None
+    if isinstance(e, str) or isinstance(actual, str) or isinstance(e, bool) or isinstance(actual, bool):
+        return e == actual
+    if kind == "f":
+        return float(np.float32(actual)) == e
+    return float(e) == float(actual) or (isinstance(e, int) and isinstance(actual, int) and e == actual)
+
+
+class Collector:
+    def __init__(self):
+        self.in_events = []
+        self.remove_events = []
+        self.chunks = []
+
+
+def run_case(case, engine_factory):
+    mgr = rt.SiddhiManager(engine_factory=engine_factory)
+    app = mgr.createSiddhiAppRuntime(case["app"])
+    col = Collector()
+    cb = case["callback"]
+    if cb["kind"] == "query":
+        class QC(rt.QueryCallback):
+            def receive(self, ts, inEvents, removeEvents):
+                col.chunks.append((inEvents or [], removeEvents or []))
+                if inEvents:
+                    col.in_events.extend(inEvents)
+                if removeEvents:
+                    col.remove_events.extend(removeEvents)
+        app.addCallback(cb["name"], QC())
+    else:
+        class SC(rt.StreamCallback):
+            def receive(self, events):
+                col.chunks.append((events, []))
+                col.in_events.extend(events)
+        app.addCallback(cb["name"], SC())
+    handlers = {}
+    app.start()
+    for s in case["sends"]:
+        h = handlers.get(s["stream"]) or app.getInputHandler(s["stream"])
+        handlers[s["stream"]] = h
+        data = [_py(v)[1] for v in s["data"]]
+        h.send(s["ts"], data)
+    app.shutdown()
+    return col
+
+
+def check_case(case, col):
+    errs = []
+    if case.get("expected_count") is not None and len(col.in_events) != case["expected_count"]:
+        errs.append("count %d != expected %d" % (len(col.in_events), case["expected_count"]))
+    if case.get("expected_remove_count") is not None and case["callback"]["kind"] == "query" \
+            and len(col.remove_events) != case["expected_remove_count"]:
+        errs.append("remove count %d != expected %d" % (len(col.remove_events), case["expected_remove_count"]))
+    for exp in case.get("expected_rows", []):
+        n = exp["n"]
+        if n == "all":
+            targets = col.in_events
+        elif n == "first_of_each":
+            targets = [c[0][0] for c in col.chunks if c[0]]
+        else:
+            if n - 1 >= len(col.in_events):
+                errs.append("missing event #%d" % n)
+                continue
+            targets = [col.in_events[n - 1]]
+        for ev in targets:
+            d = ev.getData()
+            if len(d) != len(exp["data"]) or not all(values_equal(e, a) for e, a in zip(exp["data"], d)):
+                errs.append("event %s: %r != expected %r" % (n, d, [_py(v)[1] for v in exp["data"]]))
+    return errs
