@@ -1,0 +1,243 @@
+"""Benchmark: partitioned 2-state pattern (config P3) on MI355X via libsiddhi_hip.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config P3|P3-dense|P1|W2-length|W2-time]
+
+Workload (BASELINE.json configs[2]): P1's query
+`every e1=StockStream[price>70] -> e2=StockStream[symbol==e1.symbol and
+price>e1.price*1.05] within 1 sec` inside `partition with (symbol of StockStream)`,
+synthetic seeded StockStream, 100M events per GPU over 10M keys per GPU,
+delta = 0.01 ms, InputHandler calls of 1024 events.
+
+One step = one pass of the hot path over the whole 100M-event stream from a
+freshly started query state, pushed as micro-batches (state carried between
+them); inputs are resident in HBM before the timed region.  Multi-GPU: one
+process per GPU, keys hash-sharded (each rank owns a disjoint 10M-key slice
+with its own 100M events: weak scaling, no data-path collective).  `value` =
+events of all ranks / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8 TB/s HBM3E peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="P3")
+    ap.add_argument("--events", type=int, default=0, help="override events per GPU")
+    ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
+    ap.add_argument("--batch", type=int, default=25_000_000, help="micro-batch size (events)")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
+    return ap.parse_args()
+
+
+def gen_device_columns(torch, n, keys, delta, seed_offset, key_base, dev):
+    from siddhi_amd import workloads as wl
+    sym = torch.empty(n, dtype=torch.int32, device=dev)
+    price = torch.empty(n, dtype=torch.float64, device=dev)
+    vol = torch.empty(n, dtype=torch.int64, device=dev)
+    ts = torch.empty(n, dtype=torch.int64, device=dev)
+    chunk = 5_000_000
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        s, p, v, t = wl.stock_stream(b - a, keys, delta, seed_offset=seed_offset, start=a)
+        sym[a:b] = torch.from_numpy((s.astype(np.int64) + key_base).astype(np.int32))
+        price[a:b] = torch.from_numpy(p)
+        vol[a:b] = torch.from_numpy(v)
+        ts[a:b] = torch.from_numpy(t)
+    return sym, price, vol, ts
+
+
+def alg_bytes_pattern(c, n):
+    """B_ev = 20 + 16*P + 24*f_new + 32*m per event."""
+    P = c["partial_scans"] / max(n, 1)
+    f_new = c["partials"] / max(n, 1)
+    m = c["matches"] / max(n, 1)
+    return (20 + 16 * P + 24 * f_new + 32 * m) * n, dict(P_bar=P, f_new=f_new, m_bar=m)
+
+
+def alg_bytes_window(c, n, n_out):
+    """B_ev = 20 (in) + 12 (re-read at expiry) + 36*o per event."""
+    o = c["matches"] / max(n, 1)
+    return (20 + 12 + 36 * o) * n, dict(o=o)
+
+
+def cpu_baseline(cfg_name, app, keys, delta, sample):
+    """CPU oracle (C++ restatement, 1 core) on the first `sample` events of the same stream."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_engine import OracleQueryEngine
+    from parity import compile_single_query, stock_batch
+    from siddhi_amd import workloads as wl
+    qp, _ = compile_single_query(app)
+    eng = OracleQueryEngine(qp, None)
+    s, p, v, t = wl.stock_stream(sample, keys, delta, seed_offset=0)
+    vals = np.stack([s.astype(np.uint64), p.view(np.uint64), v.view(np.uint64)], axis=1)
+    nul = np.zeros_like(vals, dtype=np.uint8)
+    offs = wl.call_offsets(sample)
+    lib = eng.lib
+    t0 = time.perf_counter()
+    for c in range(len(offs) - 1):
+        a, b = int(offs[c]), int(offs[c + 1])
+        vv = np.ascontiguousarray(vals[a:b])
+        nn = np.ascontiguousarray(nul[a:b])
+        tt = np.ascontiguousarray(t[a:b])
+        lib.orc_push(eng.h, 0, b - a, tt.ctypes.data, vv.ctypes.data, nn.ctypes.data, 1)
+        lib.orc_clear_rows(eng.h)
+    dt = time.perf_counter() - t0
+    eng.close()
+    return {"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the %s stream (%d keys, delta %g ms), C++ restatement of the "
+                      "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)}
+
+
+def main():
+    args = parse()
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(local)
+
+    from siddhi_amd import workloads as wl
+    from siddhi_amd import hip_engine as he
+    from siddhi_amd.planner import StringDictionary, plan_query
+    from siddhi_amd import query_compiler as qc
+
+    app, n_def, k_def, delta = wl.CONFIGS[args.config]
+    n = args.events or n_def
+    keys = args.keys or k_def
+    pattern = args.config.startswith("P")
+    qa = qc.parse(app)
+    item = qa.execution_order[0]
+    if isinstance(item, qc.Partition):
+        qp = plan_query(qa, item.queries[0], StringDictionary(), item)
+    else:
+        qp = plan_query(qa, item, StringDictionary())
+
+    # inputs resident in HBM before the timed region; rank r owns key slice r (pre-partitioned)
+    sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=rank * keys, dev=dev)
+    torch.cuda.synchronize()
+    he.context(local)
+    dq = he.DeviceQuery(qp.ir, device=local)
+    batch = min(args.batch, n)
+    cuts = list(range(0, n, batch)) + [n]
+    offs_all = wl.call_offsets(n)
+
+    def run_step(collect=None):
+        dq.reset()
+        tot = {}
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            # InputHandler calls of 1024 events inside the micro-batch
+            lo = np.searchsorted(offs_all, a)
+            hi = np.searchsorted(offs_all, b)
+            co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
+            cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
+            dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE,
+                        co.astype(np.int64), True)
+            dq.discard()
+            if collect is not None:
+                for k, v in dq.stage_times().items():
+                    tot[k] = tot.get(k, 0) + v
+        if collect is not None:
+            collect.append(tot)
+        return dq.counters()
+
+    for _ in range(args.warmup):
+        run_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    stage_runs = []
+    t0 = time.perf_counter()
+    counters = None
+    for _ in range(args.steps):
+        counters = run_step(stage_runs)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_events = n * world * args.steps
+    value = total_events / elapsed
+
+    # per-stage device times (HIP events on the query's stream), averaged per step
+    stages = {}
+    for r in stage_runs:
+        for k, v in r.items():
+            stages[k] = stages.get(k, 0) + v / len(stage_runs)
+    dominant = max(stages, key=stages.get) if stages else None
+    step_dev_ns = sum(stages.values())
+    if pattern:
+        bytes_step, derived = alg_bytes_pattern(counters, n)
+    else:
+        bytes_step, derived = alg_bytes_window(counters, n, len(qp.output_names))
+    launches = len(cuts) - 1
+    roof = None
+    if dominant:
+        # achieved: the path's algorithmic bytes per launch of the dominant kernel stage / its mean launch time
+        per_launch_bytes = bytes_step / launches
+        per_launch_s = stages[dominant] / launches * 1e-9
+        ach = per_launch_bytes / per_launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_stage": dominant,
+                "path_achieved": round(bytes_step / (step_dev_ns * 1e-9) / 1e9, 1),
+                "path_frac": round(bytes_step / (step_dev_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
+    matches_per_s = counters["matches"] * world * args.steps / elapsed
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample != 0:
+        sample = args.cpu_sample if args.cpu_sample > 0 else (2_000_000 if pattern else 1_000_000)
+        cpu = cpu_baseline(args.config, app, keys, delta, min(sample, n))
+
+    if rank == 0:
+        line = {
+            "metric": "events/sec ingested (partitioned pattern P3, %s)" % args.config,
+            "value": round(value, 1),
+            "unit": "events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
+            "config": {"workload": args.config, "events_per_gpu": n, "keys_per_gpu": keys, "delta_ms": delta,
+                       "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world},
+            "matches_per_s": round(matches_per_s, 1),
+            "counters": {k: counters[k] for k in ("events", "matches", "partials", "partial_scans", "carry")},
+            "derived": {k: round(v, 4) for k, v in derived.items()},
+            "stage_ms_per_step": {k: round(v / 1e6, 3) for k, v in stages.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    dq.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

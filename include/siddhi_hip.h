@@ -1,0 +1,124 @@
+/*
+ * siddhi_hip.h -- C-ABI of libsiddhi_hip, the MI355X (gfx950) implementation of
+ * Siddhi's pattern / sequence / sliding-window hot path.
+ *
+ * This is the drop-in boundary.  The reference has no FFI; each
+ * entry point replaces an in-JVM interface on the hot path:
+ *
+ *   shd_plan_load   <- QueryParser.parse / StateInputStreamParser.parseInputStream
+ *                      (modules/siddhi-core/src/main/java/io/siddhi/core/util/parser/
+ *                       QueryParser.java:94-283, StateInputStreamParser.java:76-146):
+ *                      the host planner hands over a compiled plan (include/siddhi_ir.h)
+ *                      instead of building Processor objects.
+ *   shd_push        <- StreamJunction.Receiver.receive(Event[])
+ *                      (C/stream/StreamJunction.java:443-456, reached from
+ *                       InputHandler.send(Event[]), C/stream/input/InputHandler.java:85-95)
+ *                      and PartitionStreamReceiver.receive(Event[])
+ *                      (C/partition/PartitionStreamReceiver.java:175-216).
+ *   shd_set_time    <- TimestampGeneratorImpl.setCurrentTimestamp -> Scheduler.onTimeChange
+ *                      (C/util/timestamp/TimestampGeneratorImpl.java:58-76,
+ *                       C/util/Scheduler.java:71-104), playback mode.
+ *   shd_poll        <- OutputRateLimiter.sendToCallBacks -> QueryCallback.receiveStreamEvent /
+ *                      InsertIntoStreamCallback.send
+ *                      (C/query/output/ratelimit/OutputRateLimiter.java:64-107).
+ *   shd_plan_free   <- QueryRuntime stop / SiddhiAppRuntime.shutdown.
+ *
+ * Conventions: every function returns an int status (0 = OK, < 0 = shd_status);
+ * no exception crosses the ABI; shd_last_error() returns a thread-local message.
+ * One shd_query is driven by one host thread at a time (the reference serialises
+ * a query with patternSyncObject + LockWrapper, MultiProcessStreamReceiver.java:97,
+ * QueryParser.java:155-215); different queries may be driven concurrently.
+ */
+#ifndef SIDDHI_HIP_H
+#define SIDDHI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shd_ctx shd_ctx;
+typedef struct shd_query shd_query;
+
+enum shd_status {
+  SHD_OK = 0,
+  SHD_E_INVALID_PLAN = -1, /* malformed IR                                      */
+  SHD_E_UNSUPPORTED = -2,  /* valid plan/data outside the device path           */
+  SHD_E_OOM = -3,          /* device allocation failed                          */
+  SHD_E_DEVICE = -4,       /* HIP runtime error / no device                     */
+  SHD_E_CAPACITY = -5,     /* a bounded table overflowed (never silently drops)  */
+  SHD_E_ARG = -6           /* bad argument                                      */
+};
+
+enum shd_mem { SHD_MEM_HOST = 0, SHD_MEM_DEVICE = 1 };
+
+/* One columnar micro-batch of ONE plan stream (the plan's stream index). */
+typedef struct shd_batch {
+  int32_t stream;               /* plan-local stream index                       */
+  int32_t mem;                  /* SHD_MEM_HOST or SHD_MEM_DEVICE (all pointers)  */
+  int64_t n;                    /* number of events                             */
+  const int64_t* ts;            /* [n] event timestamps (ms)                     */
+  int32_t ncols;                /* == number of attributes of the stream        */
+  const void* const* cols;      /* [ncols] typed columns: string=u32 dictionary id,
+                                   int=i32, long=i64, float=f32, double=f64, bool=u8 */
+  const uint8_t* const* nulls;  /* [ncols] NULL or [n] bytes, 1 = null; may be NULL */
+  int32_t ncalls;               /* InputHandler.send calls in this batch (>= 1)  */
+  const int64_t* call_offsets;  /* host array [ncalls+1]; NULL = one call        */
+  int32_t advance_time;         /* playback: set app time to each call's last ts */
+} shd_batch;
+
+/* Output rows of a query since the last poll, in reference order.  Rows with
+ * the same chunk id form one callback invocation (one ComplexEventChunk). */
+typedef struct shd_out {
+  int64_t n_rows;
+  int32_t n_cols;
+  const int64_t* chunk;         /* [n_rows]                                      */
+  const int32_t* type;          /* [n_rows] 0 = CURRENT, 1 = EXPIRED             */
+  const int64_t* ts;            /* [n_rows]                                      */
+  const uint64_t* values;       /* [n_rows * n_cols] 64-bit payloads (row-major)  */
+  const uint8_t* nulls;         /* [n_rows * n_cols]                             */
+} shd_out;
+
+typedef struct shd_counters {
+  int64_t events;               /* events ingested                               */
+  int64_t matches;              /* output rows produced                          */
+  int64_t partials;             /* partial matches created                       */
+  int64_t partial_scans;        /* (partial, event) pairs examined               */
+  int64_t bytes_touched;        /* algorithmic bytes             */
+  int64_t kernel_ns;            /* device time of the last push                  */
+  int64_t carry;                /* open partials / window items carried          */
+  int64_t reserved;
+} shd_counters;
+
+int shd_device_count(int* n);
+int shd_ctx_create(const int* device_ids, int n, shd_ctx** out);
+int shd_ctx_destroy(shd_ctx* ctx);
+
+int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out);
+int shd_plan_free(shd_query* q);
+/* Engine the plan runs on: 1 = pattern forward-scan, 2 = window/aggregate,
+ * 3 = filter/projection, 4 = generic per-key NFA. */
+int shd_plan_engine(shd_query* q, int* engine);
+
+int shd_set_time(shd_query* q, int64_t ts);
+int shd_push(shd_query* q, const shd_batch* batch);
+int shd_flush(shd_query* q);                  /* wait for queued device work      */
+int shd_poll(shd_query* q, shd_out* out);      /* buffers valid until next call    */
+int shd_discard_output(shd_query* q);          /* drop pending rows (benchmarks)   */
+int shd_reset(shd_query* q);                   /* back to freshly-started state   */
+int shd_get_counters(shd_query* q, shd_counters* c);
+/* Optional: the HIP stream (hipStream_t) a query launches on, for event timing. */
+int shd_query_stream(shd_query* q, void** stream);
+/* Profiling hook: per-stage device time of the last push, measured with HIP
+ * events on the query's stream around each kernel stage.  Writes up to `max`
+ * entries of ns[] and stage names (static strings) to names[]; *n = count. */
+int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int* n);
+
+const char* shd_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

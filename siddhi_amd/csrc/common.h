@@ -1,0 +1,164 @@
+// common.h -- shared host/device infrastructure for libsiddhi_hip (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_hip.h"
+#include "../../include/siddhi_ir.h"
+
+namespace shd {
+
+// ------------------------------------------------------------------ errors
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define SHD_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      throw ::shd::Error(e_ == hipErrorOutOfMemory ? SHD_E_OOM : SHD_E_DEVICE,        \
+                         std::string(#call) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+#define SHD_CHECK_LAUNCH() SHD_HIP(hipGetLastError())
+
+constexpr int kBlock = 256;
+constexpr int kMaxCols = 16;      // attributes per stream handled on device
+constexpr int kMaxStack = 16;     // expression stack depth
+constexpr int kMaxAggs = 8;
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int grid_for(int64_t n, int per_thread = 1, int cap = 256 * 64) {
+  int64_t g = ceil_div(n, (int64_t)kBlock * per_thread);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ------------------------------------------------------------------ device buffers
+// Grow-only device allocation owned by an engine (allocated outside launch
+// sequences so push() can be captured into a hipGraph later).
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  void reserve(size_t bytes) {
+    if (bytes <= cap) return;
+    release();
+    size_t b = bytes < 256 ? 256 : bytes;
+    b = (b + 255) & ~size_t(255);
+    SHD_HIP(hipMalloc(&p, b));
+    cap = b;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+  void reserve(size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    size_t b = bytes < 256 ? 256 : bytes;
+    SHD_HIP(hipHostMalloc(&p, b, hipHostMallocDefault));
+    cap = b;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ------------------------------------------------------------------ plan (host decode)
+struct Instr { int32_t op, a, b, c; };
+
+struct PNode {
+  int kind = 0;
+  int state_id = -1, stream = -1, absent = 0;
+  int64_t waiting = -1;
+  std::vector<int> filters;
+  int ltype = 0;
+  int min = 0, max = 0;
+  std::vector<PNode> kids;
+};
+
+struct Plan {
+  int kind = 0;
+  std::vector<std::vector<int>> stream_types;
+  std::vector<uint64_t> consts;
+  std::vector<std::vector<Instr>> exprs;
+  std::vector<std::pair<int, int>> part_keys;
+  int state_type = 0;
+  int64_t within = -1;
+  int n_states = 0;
+  PNode root;
+  int single_stream = 0;
+  struct Handler { int kind; int expr; int wkind; int64_t param; };
+  std::vector<Handler> handlers;
+  bool current_on = true, expired_on = false;
+  struct Agg { int kind, expr, type; };
+  std::vector<Agg> aggs;
+  std::vector<int> group_by;
+  int having = -1;
+  std::vector<std::pair<int, int>> outputs;  // (type, expr)
+};
+
+Plan decode_plan(const int32_t* w, int64_t n);
+int expr_result_type(const Plan& p, int expr, const std::vector<int>& agg_types);
+int expr_max_depth(const Plan& p, int expr);
+
+// Flattened device copy of all expressions of a plan.
+struct DevExprTable {
+  DevBuf ins;      // int4 per instruction
+  DevBuf consts;   // u64
+  std::vector<int> off, len;
+  void upload(const Plan& p);
+};
+
+// ------------------------------------------------------------------ columns
+// A set of typed device columns (one stream's batch, or a carry table).
+struct ColSet {
+  const void* col[kMaxCols];
+  const uint8_t* nul[kMaxCols];
+  int8_t type[kMaxCols];
+  int32_t ncols;
+  const int64_t* ts;
+};
+
+inline int type_size(int t) {
+  switch (t) {
+    case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: return 4;
+    case SHD_T_LONG: case SHD_T_DOUBLE: return 8;
+    case SHD_T_BOOL: return 1;
+  }
+  return 8;
+}
+
+// ------------------------------------------------------------------ primitives (primitives.hip)
+// Exclusive scan of u32 counts -> u32 offsets; returns nothing (total read from out[n-1]+in[n-1]).
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev,
+                        DevBuf& scratch, hipStream_t s);
+// Stable LSD radix sort of (key, value) pairs over key bits [0, bits).
+void radix_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                          int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& result_in_alt);
+void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, uint32_t* vals_alt,
+                          int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& result_in_alt);
+// Device-wide max of u64 keys (result to dev ptr).
+void reduce_max_u64(const uint64_t* in, int64_t n, uint64_t* out_dev, hipStream_t s);
+void fill_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s);
+
+}  // namespace shd

@@ -1,0 +1,296 @@
+// dev_expr.h -- per-lane interpreter for the filter / projection bytecode
+// (include/siddhi_ir.h), one expression evaluation per lane.
+//
+// Semantics restate the reference executors (paths under
+// modules/siddhi-core/src/main/java/io/siddhi/core/executor/):
+//   compare: condition/compare/CompareConditionExpressionExecutor.java:38-42 (null -> false)
+//            and the per-type subclasses (operands pre-converted by the planner)
+//   and/or/not/isnull: condition/{And,Or,Not,IsNull}ConditionExpressionExecutor.java
+//   + - * / %: math/*/*ExpressionExecutor{Int,Long,Float,Double}.java
+//            (null operand -> null; / and % by zero -> null; int wrap-around)
+// Compiled with -ffp-contract=off so float/double ops round exactly like Java.
+#pragma once
+#include "common.h"
+
+namespace shd {
+
+struct Val {
+  uint64_t b;
+  int null;
+};
+
+__device__ __forceinline__ int32_t v_i32(uint64_t b) { return (int32_t)(uint32_t)b; }
+__device__ __forceinline__ int64_t v_i64(uint64_t b) { return (int64_t)b; }
+__device__ __forceinline__ float v_f32(uint64_t b) { return __uint_as_float((uint32_t)b); }
+__device__ __forceinline__ double v_f64(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t p_i32(int32_t v) { return (uint64_t)(int64_t)v; }
+__device__ __forceinline__ uint64_t p_f32(float f) { return (uint64_t)__float_as_uint(f); }
+__device__ __forceinline__ uint64_t p_f64(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// Typed column element -> 64-bit payload.
+__device__ __forceinline__ Val col_load(const ColSet& cs, int64_t row, int attr) {
+  Val v;
+  const uint8_t* nm = cs.nul[attr];
+  if (nm && nm[row]) {
+    v.b = 0;
+    v.null = 1;
+    return v;
+  }
+  v.null = 0;
+  switch (cs.type[attr]) {
+    case SHD_T_STRING: v.b = ((const uint32_t*)cs.col[attr])[row]; break;
+    case SHD_T_INT: v.b = p_i32(((const int32_t*)cs.col[attr])[row]); break;
+    case SHD_T_LONG: v.b = (uint64_t)((const int64_t*)cs.col[attr])[row]; break;
+    case SHD_T_FLOAT: v.b = (uint64_t)((const uint32_t*)cs.col[attr])[row]; break;
+    case SHD_T_DOUBLE: v.b = ((const uint64_t*)cs.col[attr])[row]; break;
+    case SHD_T_BOOL: v.b = ((const uint8_t*)cs.col[attr])[row] ? 1 : 0; break;
+    default: v.b = 0; v.null = 1;
+  }
+  return v;
+}
+
+// Number.xValue() widening used by the planner's CVT ops.
+__device__ __forceinline__ uint64_t d_cvt(uint64_t b, int from, int to) {
+  if (from == to) return b;
+  double d = 0.0;
+  float f = 0.f;
+  int64_t l = 0;
+  switch (from) {
+    case SHD_T_INT: l = v_i32(b); d = (double)v_i32(b); f = (float)v_i32(b); break;
+    case SHD_T_LONG: l = v_i64(b); d = (double)v_i64(b); f = (float)v_i64(b); break;
+    case SHD_T_FLOAT: d = (double)v_f32(b); f = v_f32(b); l = (int64_t)v_f32(b); break;
+    case SHD_T_DOUBLE: d = v_f64(b); f = (float)v_f64(b); l = (int64_t)v_f64(b); break;
+  }
+  switch (to) {
+    case SHD_T_INT: return p_i32((int32_t)l);
+    case SHD_T_LONG: return (uint64_t)l;
+    case SHD_T_FLOAT: return p_f32(f);
+    case SHD_T_DOUBLE: return p_f64(d);
+  }
+  return b;
+}
+
+__device__ inline Val d_arith(int op, int t, Val l, Val r) {
+  Val o;
+  o.b = 0;
+  o.null = 1;
+  if (l.null || r.null) return o;
+  o.null = 0;
+  switch (t) {
+    case SHD_T_INT: {
+      int32_t a = v_i32(l.b), b = v_i32(r.b);
+      switch (op) {
+        case SHD_OP_ADD: o.b = p_i32((int32_t)((uint32_t)a + (uint32_t)b)); break;
+        case SHD_OP_SUB: o.b = p_i32((int32_t)((uint32_t)a - (uint32_t)b)); break;
+        case SHD_OP_MUL: o.b = p_i32((int32_t)((uint32_t)a * (uint32_t)b)); break;
+        case SHD_OP_DIV:
+          if (b == 0) o.null = 1;
+          else o.b = p_i32((a == INT32_MIN && b == -1) ? INT32_MIN : a / b);
+          break;
+        case SHD_OP_MOD:
+          if (b == 0) o.null = 1;
+          else o.b = p_i32(b == -1 ? 0 : a % b);
+          break;
+      }
+      break;
+    }
+    case SHD_T_LONG: {
+      int64_t a = v_i64(l.b), b = v_i64(r.b);
+      switch (op) {
+        case SHD_OP_ADD: o.b = (uint64_t)a + (uint64_t)b; break;
+        case SHD_OP_SUB: o.b = (uint64_t)a - (uint64_t)b; break;
+        case SHD_OP_MUL: o.b = (uint64_t)a * (uint64_t)b; break;
+        case SHD_OP_DIV:
+          if (b == 0) o.null = 1;
+          else o.b = (uint64_t)((a == INT64_MIN && b == -1) ? INT64_MIN : a / b);
+          break;
+        case SHD_OP_MOD:
+          if (b == 0) o.null = 1;
+          else o.b = (uint64_t)(b == -1 ? 0 : a % b);
+          break;
+      }
+      break;
+    }
+    case SHD_T_FLOAT: {
+      float a = v_f32(l.b), b = v_f32(r.b);
+      switch (op) {
+        case SHD_OP_ADD: o.b = p_f32(__fadd_rn(a, b)); break;
+        case SHD_OP_SUB: o.b = p_f32(__fsub_rn(a, b)); break;
+        case SHD_OP_MUL: o.b = p_f32(__fmul_rn(a, b)); break;
+        case SHD_OP_DIV:
+          if (b == 0.0f) o.null = 1;
+          else o.b = p_f32(__fdiv_rn(a, b));
+          break;
+        case SHD_OP_MOD:
+          if (b == 0.0f) o.null = 1;
+          else o.b = p_f32(fmodf(a, b));
+          break;
+      }
+      break;
+    }
+    case SHD_T_DOUBLE: {
+      double a = v_f64(l.b), b = v_f64(r.b);
+      switch (op) {
+        case SHD_OP_ADD: o.b = p_f64(__dadd_rn(a, b)); break;
+        case SHD_OP_SUB: o.b = p_f64(__dsub_rn(a, b)); break;
+        case SHD_OP_MUL: o.b = p_f64(__dmul_rn(a, b)); break;
+        case SHD_OP_DIV:
+          if (b == 0.0) o.null = 1;
+          else o.b = p_f64(__ddiv_rn(a, b));
+          break;
+        case SHD_OP_MOD:
+          if (b == 0.0) o.null = 1;
+          else o.b = p_f64(fmod(a, b));
+          break;
+      }
+      break;
+    }
+  }
+  return o;
+}
+
+__device__ inline bool d_compare(int op, int t, uint64_t l, uint64_t r) {
+  int c;  // -1 lt, 0 eq, 1 gt, 2 unordered / not-equal
+  switch (t) {
+    case SHD_T_STRING:
+    case SHD_T_BOOL:
+      c = (l == r) ? 0 : 2;
+      break;
+    case SHD_T_INT: {
+      int32_t a = v_i32(l), b = v_i32(r);
+      c = a < b ? -1 : (a > b ? 1 : 0);
+      break;
+    }
+    case SHD_T_LONG: {
+      int64_t a = v_i64(l), b = v_i64(r);
+      c = a < b ? -1 : (a > b ? 1 : 0);
+      break;
+    }
+    case SHD_T_FLOAT: {
+      float a = v_f32(l), b = v_f32(r);
+      c = (a < b) ? -1 : (a > b) ? 1 : (a == b) ? 0 : 2;
+      break;
+    }
+    default: {
+      double a = v_f64(l), b = v_f64(r);
+      c = (a < b) ? -1 : (a > b) ? 1 : (a == b) ? 0 : 2;
+      break;
+    }
+  }
+  switch (op) {
+    case SHD_OP_EQ: return c == 0;
+    case SHD_OP_NE: return c != 0;
+    case SHD_OP_GT: return c == 1;
+    case SHD_OP_GE: return c == 1 || c == 0;
+    case SHD_OP_LT: return c == -1;
+    case SHD_OP_LE: return c == -1 || c == 0;
+  }
+  return false;
+}
+
+// Evaluate one expression. Ctx provides:
+//   Val load(int state, int idx, int attr) const;  bool evnull(int state, int idx) const;
+//   int64_t ts(int state, int idx) const;          Val agg(int i) const;
+template <class Ctx>
+__device__ inline Val eval_expr(const int4* code, int len, const uint64_t* consts, const Ctx& cx) {
+  Val st[kMaxStack];
+  int sp = 0;
+  for (int k = 0; k < len; k++) {
+    int4 in = code[k];
+    switch (in.x) {
+      case SHD_OP_CONST: st[sp].b = consts[in.y]; st[sp].null = 0; sp++; break;
+      case SHD_OP_NULL: st[sp].b = 0; st[sp].null = 1; sp++; break;
+      case SHD_OP_LOAD: st[sp++] = cx.load(in.y, in.z, in.w & 0xFFFF); break;
+      case SHD_OP_EVNULL: st[sp].b = cx.evnull(in.y, in.z) ? 1 : 0; st[sp].null = 0; sp++; break;
+      case SHD_OP_TS: st[sp].b = (uint64_t)cx.ts(in.y, in.z); st[sp].null = 0; sp++; break;
+      case SHD_OP_CVT:
+        if (!st[sp - 1].null) st[sp - 1].b = d_cvt(st[sp - 1].b, in.y, in.z);
+        break;
+      case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD: {
+        Val r = st[--sp];
+        Val l = st[--sp];
+        st[sp++] = d_arith(in.x, in.y, l, r);
+        break;
+      }
+      case SHD_OP_EQ: case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE: {
+        Val r = st[--sp];
+        Val l = st[--sp];
+        st[sp].b = (!(l.null || r.null) && d_compare(in.x, in.y, l.b, r.b)) ? 1 : 0;
+        st[sp].null = 0;
+        sp++;
+        break;
+      }
+      case SHD_OP_AND: {
+        Val r = st[--sp];
+        Val l = st[--sp];
+        st[sp].b = ((!l.null && l.b) && (!r.null && r.b)) ? 1 : 0;
+        st[sp].null = 0;
+        sp++;
+        break;
+      }
+      case SHD_OP_OR: {
+        Val r = st[--sp];
+        Val l = st[--sp];
+        st[sp].b = ((!l.null && l.b) || (!r.null && r.b)) ? 1 : 0;
+        st[sp].null = 0;
+        sp++;
+        break;
+      }
+      case SHD_OP_NOT: {
+        Val x = st[--sp];
+        st[sp].b = (!x.null && x.b) ? 0 : 1;
+        st[sp].null = 0;
+        sp++;
+        break;
+      }
+      case SHD_OP_ISNULL: {
+        Val x = st[--sp];
+        st[sp].b = x.null ? 1 : 0;
+        st[sp].null = 0;
+        sp++;
+        break;
+      }
+      case SHD_OP_AGG: st[sp++] = cx.agg(in.y); break;
+      default: break;
+    }
+  }
+  if (sp == 0) {
+    Val z;
+    z.b = 0;
+    z.null = 1;
+    return z;
+  }
+  return st[sp - 1];
+}
+
+template <class Ctx>
+__device__ __forceinline__ bool eval_bool(const int4* code, int len, const uint64_t* consts, const Ctx& cx) {
+  Val v = eval_expr(code, len, consts, cx);
+  return !v.null && v.b;
+}
+
+// Expression handle passed to kernels (offset/length into the plan's table).
+struct DExpr {
+  int off;
+  int len;
+};
+
+struct DExprSet {
+  const int4* ins;
+  const uint64_t* consts;
+};
+
+// Conjunction of up to 4 filter expressions (FilterProcessor chain).
+struct DFilters {
+  DExpr f[4];
+  int n;
+};
+
+template <class Ctx>
+__device__ __forceinline__ bool eval_filters(const DExprSet& es, const DFilters& fs, const Ctx& cx) {
+  for (int i = 0; i < fs.n; i++)
+    if (!eval_bool(es.ins + fs.f[i].off, fs.f[i].len, es.consts, cx)) return false;
+  return true;
+}
+
+}  // namespace shd

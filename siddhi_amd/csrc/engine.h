@@ -1,0 +1,73 @@
+// engine.h -- query engines behind the C-ABI (one per loaded plan).
+#pragma once
+#include <memory>
+
+#include "common.h"
+#include "dev_expr.h"
+
+namespace shd {
+
+enum EngineKind { ENG_PATTERN = 1, ENG_WINDOW = 2, ENG_FILTER = 3, ENG_NFA = 4 };
+
+// Device output arena: rows accumulate across pushes until polled.
+struct OutputBuffer {
+  int ncols = 0;
+  int64_t count = 0, cap = 0;
+  DevBuf chunk, type, ts, vals, nulls;
+  void init(int nc) { ncols = nc; }
+  // Make room for `extra` more rows (copies existing rows on growth).
+  void ensure(int64_t extra, hipStream_t s);
+  int64_t* d_chunk() { return chunk.as<int64_t>(); }
+  int32_t* d_type() { return type.as<int32_t>(); }
+  int64_t* d_ts() { return ts.as<int64_t>(); }
+  uint64_t* d_vals() { return vals.as<uint64_t>(); }
+  uint8_t* d_nulls() { return nulls.as<uint8_t>(); }
+};
+
+// A batch staged on the device (columns either borrowed device pointers or
+// copies of host buffers).
+struct Staged {
+  int stream = 0;
+  int64_t n = 0;
+  ColSet cs{};
+  std::vector<int64_t> call_offsets;   // host, ncalls+1
+  bool advance_time = false;
+};
+
+struct Engine {
+  Plan plan;
+  DevExprTable ex;
+  hipStream_t stream = nullptr;
+  OutputBuffer out;
+  shd_counters counters{};
+  int64_t seq = 0;                         // global arrival index of the next event
+  int64_t now = INT64_MIN;                 // playback time (TimestampGeneratorImpl.lastEventTimestamp)
+  int64_t chunk_seq = 0;                   // next callback-chunk id
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // stage timing (profiling hook): events recorded around each kernel stage
+  static constexpr int kMaxStages = 16;
+  hipEvent_t sev[kMaxStages + 1] = {};
+  const char* stage_name[kMaxStages] = {};
+  int n_stages = 0;
+  int64_t stage_ns[kMaxStages] = {};
+  void stage_begin() { n_stages = 0; mark(nullptr); }
+  void mark(const char* name_of_finished_stage);
+  void stage_end();
+
+  virtual ~Engine();
+  virtual int kind() const = 0;
+  virtual void push(const Staged& b) = 0;
+  virtual void set_time(int64_t t) {
+    if (t >= now) now = t;
+  }
+  virtual void reset() = 0;
+
+  DExpr dexpr(int e) const { return DExpr{ex.off[e], ex.len[e]}; }
+  DExprSet dset() const { return DExprSet{ex.ins.as<int4>(), ex.consts.as<uint64_t>()}; }
+  DFilters dfilters(const std::vector<int>& ids) const;
+};
+
+std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);
+std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
+
+}  // namespace shd

@@ -1,0 +1,938 @@
+// engine_single.hip -- single-stream queries on the device:
+//   FILTER mode:  S[f]... select <expr> insert into   (+ optional `partition with`)
+//   AGG mode:     S[f]#window.length(L)|time(T) select k, sum/avg/count group by k  (config W2)
+//
+// Reference semantics (modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   query/processor/filter/FilterProcessor.java:47-60
+//   query/processor/stream/window/LengthWindowProcessor.java:105-142
+//   query/processor/stream/window/TimeWindowProcessor.java:132-169 (+ Scheduler TIMERs)
+//   query/selector/QuerySelector.java:161-205 (processNoGroupBy),
+//     :271-313 (processInBatchNoGroupBy), :315-373 (processInBatchGroupBy)
+//   query/selector/attribute/aggregator/{Sum,Avg,Count}AttributeAggregatorExecutor.java
+//   stream/input/InputHandler.java:85-89 (playback: now := last ts of the call)
+//
+// AGG mode turns a micro-batch into the reference's operation stream: for every
+// filtered event t, the window items that expire before it (FIFO order), then
+// its own add.  Expiry position of item x: length -> x + L; time -> first later
+// filtered event whose call time reaches ts_x + T, made FIFO-monotone with a
+// prefix max.  Operations are key-sorted (stable) and each group is folded
+// SEQUENTIALLY by one lane in operation order, so every double sum / avg is the
+// same IEEE result the reference computes (bit-exact, no reassociation).
+// Emission: one row per (call, group) with a CURRENT event, in first-seen
+// order, carrying the values after the group's last event of the call.
+#include <algorithm>
+
+#include "engine.h"
+
+namespace shd {
+
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kAddBit = 0x80000000u;
+constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
+
+struct RowCtx {
+  const ColSet* cs;
+  int64_t row;
+  const uint64_t* aggv;   // [nagg] payloads for OP_AGG (may be null)
+  const uint8_t* aggn;
+  __device__ __forceinline__ Val load(int, int idx, int attr) const {
+    (void)idx;
+    return col_load(*cs, row, attr);
+  }
+  __device__ __forceinline__ bool evnull(int, int) const { return false; }
+  __device__ __forceinline__ int64_t ts(int, int) const { return cs->ts[row]; }
+  __device__ __forceinline__ Val agg(int i) const {
+    Val v;
+    v.b = aggv ? aggv[i] : 0;
+    v.null = aggn ? aggn[i] : 1;
+    return v;
+  }
+};
+
+__device__ __forceinline__ uint64_t canon_key(Val v, int type) {
+  if (type == SHD_T_FLOAT) return p_f64((double)v_f32(v.b));
+  return v.b;
+}
+
+// ---------------------------------------------------------------- calls / time
+// call_of[i] for every event; call_last_ts[c]
+__global__ void k_call_of(const int64_t* offs, int ncalls, const int64_t* ts, int32_t* call_of, int64_t* last_ts) {
+  for (int c = blockIdx.x; c < ncalls; c += gridDim.x) {
+    int64_t a = offs[c], b = offs[c + 1];
+    for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) call_of[i] = c;
+    if (threadIdx.x == 0) last_ts[c] = b > a ? ts[b - 1] : INT64_MIN;
+  }
+}
+
+// now[c] = max(now_prev, last_ts[0..c])  (TimestampGeneratorImpl only moves forward)
+__global__ __launch_bounds__(kBlock) void k_call_now(const int64_t* last_ts, int ncalls, int64_t now_prev,
+                                                     int64_t* now) {
+  __shared__ int64_t carry;
+  __shared__ int64_t wmax[4];
+  if (threadIdx.x == 0) carry = now_prev;
+  __syncthreads();
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int base = 0; base < ncalls; base += kBlock) {
+    int c = base + threadIdx.x;
+    int64_t v = c < ncalls ? last_ts[c] : INT64_MIN;
+    for (int o = 1; o < 64; o <<= 1) {
+      int64_t t = __shfl_up(v, o, 64);
+      if (lane >= o) v = t > v ? t : v;
+    }
+    if (lane == 63) wmax[w] = v;
+    __syncthreads();
+    int64_t pre = carry;
+    for (int i = 0; i < w; i++) pre = wmax[i] > pre ? wmax[i] : pre;
+    int64_t r = v > pre ? v : pre;
+    if (c < ncalls) now[c] = r;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry = r;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- filter
+struct FilterArgs {
+  ColSet cs;
+  DExprSet es;
+  DFilters filters;
+  int partitioned;
+  DExpr key;
+  int key_col;
+  int key_type;
+};
+
+// flags: bit0 = passes filters, bit1 = has a (non-null) partition key
+__global__ __launch_bounds__(kBlock) void k_filter(FilterArgs a, int64_t n, uint8_t* flags, uint32_t* cnt,
+                                                   uint64_t* pkey) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    uint8_t f = 0;
+    bool keyed = true;
+    if (a.partitioned) {
+      Val kv = a.key_col >= 0 ? col_load(a.cs, i, a.key_col)
+                              : eval_expr(a.es.ins + a.key.off, a.key.len, a.es.consts, cx);
+      keyed = !kv.null;
+      pkey[i] = canon_key(kv, a.key_type);
+    }
+    if (keyed) {
+      f |= 2;
+      if (eval_filters(a.es, a.filters, cx)) f |= 1;
+    }
+    flags[i] = f;
+    cnt[i] = (f & 3) == 3 ? 1u : 0u;
+  }
+}
+
+// Partition runs (PartitionStreamReceiver.receive(Event[]) :189-214): a run
+// starts at the first keyed event of a call or where the key changes from the
+// previous keyed event.  run_start[i] in {0,1}; computed over keyed events.
+__global__ void k_run_starts(const uint8_t* flags, const uint64_t* pkey, const int32_t* call_of, int64_t n,
+                             uint32_t* start) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t s = 0;
+    if (flags[i] & 2) {
+      int64_t p = i - 1;
+      while (p >= 0 && call_of[p] == call_of[i] && !(flags[p] & 2)) p--;
+      s = (p < 0 || call_of[p] != call_of[i] || pkey[p] != pkey[i]) ? 1u : 0u;
+    }
+    start[i] = s;
+  }
+}
+
+struct ProjArgs {
+  ColSet cs;
+  DExprSet es;
+  DExpr outs[kMaxCols];
+  int nout;
+  int64_t row0;
+  int64_t chunk0;
+  int partitioned;
+};
+
+__global__ __launch_bounds__(kBlock) void k_project_rows(ProjArgs a, int64_t n, const uint32_t* cnt,
+                                                         const uint32_t* off, const int32_t* call_of,
+                                                         const uint32_t* run_excl, const uint32_t* run_start,
+                                                         int64_t* o_chunk, int32_t* o_type,
+                                                         int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!cnt[i]) continue;
+    int64_t row = a.row0 + off[i];
+    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    for (int c = 0; c < a.nout; c++) {
+      Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
+      o_vals[row * a.nout + c] = v.b;
+      o_nul[row * a.nout + c] = (uint8_t)v.null;
+    }
+    o_ts[row] = a.cs.ts[i];
+    o_type[row] = 0;
+    // run of event i = inclusive start count - 1
+    o_chunk[row] = a.chunk0 + (a.partitioned ? (int64_t)run_excl[i] + run_start[i] - 1 : (int64_t)call_of[i]);
+  }
+}
+
+// ---------------------------------------------------------------- aggregation
+struct ItemArgs {
+  ColSet cs;
+  DExprSet es;
+  int nagg;
+  DExpr agg_arg[kMaxAggs];
+  int has_arg[kMaxAggs];
+  int ngroup;
+  DExpr group;
+  int group_col;
+  int group_type;
+  int64_t C;
+};
+
+// New window items (one per filtered event), appended after the carried ones.
+__global__ __launch_bounds__(kBlock) void k_make_items(ItemArgs a, int64_t n, const uint32_t* cnt, const uint32_t* off,
+                                                       const int32_t* call_of, const int64_t* call_now,
+                                                       uint64_t* ikey, int64_t* its, uint64_t* iargv, uint8_t* iargn,
+                                                       int32_t* ievrow, int64_t* inow, int64_t cap,
+                                                       uint32_t* null_key_flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!cnt[i]) continue;
+    int64_t t = a.C + off[i];
+    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    uint64_t k = 0;
+    if (a.ngroup) {
+      Val kv = a.group_col >= 0 ? col_load(a.cs, i, a.group_col)
+                                : eval_expr(a.es.ins + a.group.off, a.group.len, a.es.consts, cx);
+      if (kv.null) atomicOr(null_key_flag, 1u);
+      k = kv.null ? 0 : canon_key(kv, a.group_type);
+    }
+    ikey[t] = k;
+    its[t] = a.cs.ts[i];
+    for (int g = 0; g < a.nagg; g++) {
+      Val v;
+      v.b = 0;
+      v.null = 1;
+      if (a.has_arg[g]) v = eval_expr(a.es.ins + a.agg_arg[g].off, a.agg_arg[g].len, a.es.consts, cx);
+      iargv[g * cap + t] = v.b;
+      iargn[g * cap + t] = (uint8_t)v.null;
+    }
+    ievrow[t] = (int32_t)i;
+    inow[t] = call_now[call_of[i]];
+  }
+}
+
+// Expiry position of every window item.
+__global__ void k_expiry(int wkind, int64_t wparam, int64_t C, int64_t total, const int64_t* its,
+                         const int64_t* inow, uint32_t* e) {
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t r = kInf;
+    if (wkind == SHD_W_LENGTH) {
+      int64_t t = x + wparam;
+      if (t < total) r = (uint32_t)t;
+    } else if (wkind == SHD_W_TIME) {
+      // TimeWindowProcessor: expire when ts_x - now + T <= 0, checked before each later add
+      int64_t lo = x + 1 > C ? x + 1 : C, hi = total;
+      int64_t target = its[x] + wparam;
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (inow[mid] >= target) hi = mid;
+        else lo = mid + 1;
+      }
+      if (lo < total) r = (uint32_t)lo;
+    }
+    e[x] = r;
+  }
+}
+
+// in-place inclusive prefix max over u32 (FIFO: an item cannot leave before its predecessor)
+__global__ __launch_bounds__(kBlock) void k_prefix_max_u32(uint32_t* e, int64_t n) {
+  __shared__ uint32_t carry;
+  __shared__ uint32_t wm[4];
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t base = 0; base < n; base += kBlock) {
+    int64_t i = base + threadIdx.x;
+    uint32_t v = i < n ? e[i] : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t t = __shfl_up(v, o, 64);
+      if (lane >= o) v = t > v ? t : v;
+    }
+    if (lane == 63) wm[w] = v;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (int k = 0; k < w; k++) pre = wm[k] > pre ? wm[k] : pre;
+    uint32_t r = v > pre ? v : pre;
+    if (i < n) e[i] = r;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry = r;
+    __syncthreads();
+  }
+}
+
+__global__ void k_count_expired(const uint32_t* e, int64_t n, unsigned long long* cnt) {
+  uint64_t c = 0;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
+    c += e[x] != kInf;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
+}
+
+// number of x with e[x] <= t (e is non-decreasing)
+__device__ __forceinline__ int64_t count_le(const uint32_t* e, int64_t n, uint32_t t) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (e[mid] <= t) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_make_ops(int64_t C, int64_t total, const uint32_t* e, const uint64_t* ikey, uint64_t* okey,
+                           uint32_t* oref) {
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
+    if (e[x] != kInf) {   // expire op of item x, before the add of item e[x]
+      int64_t idx = ((int64_t)e[x] - C) + x;
+      okey[idx] = ikey[x];
+      oref[idx] = (uint32_t)x;
+    }
+    if (x >= C) {         // add op of item x
+      int64_t idx = (x - C) + count_le(e, total, (uint32_t)x);
+      okey[idx] = ikey[x];
+      oref[idx] = (uint32_t)x | kAddBit;
+    }
+  }
+}
+
+__global__ void k_narrow(const uint64_t* in, uint32_t* out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)in[i];
+}
+
+__global__ void k_gather_u64(const uint64_t* src, const uint32_t* perm, uint64_t* dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[perm[i]];
+}
+
+__global__ void k_seg_heads(const uint32_t* skey, int64_t n, uint32_t* head) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    head[i] = (i == 0 || skey[i] != skey[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_head_list(const uint32_t* head, const uint32_t* hoff, int64_t n, uint32_t* hl) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (head[i]) hl[hoff[i]] = (uint32_t)i;
+}
+
+__device__ __forceinline__ int64_t java_d2l(double d) {
+  if (d != d) return 0;
+  if (d >= 9.2233720368547758e18) return INT64_MAX;
+  if (d <= -9.2233720368547758e18) return INT64_MIN;
+  return (int64_t)d;
+}
+
+struct FoldArgs {
+  int nagg;
+  int kind[kMaxAggs];
+  int type[kMaxAggs];
+  int64_t cap;               // item capacity (stride of per-agg item arrays)
+  // group state tables (dense by key), [nagg][nkeys]
+  double* dsum;
+  int64_t* lsum;
+  int64_t* cnt;
+  int64_t nkeys;
+};
+
+// One lane per group segment: the reference's sequential add/remove order.
+__global__ __launch_bounds__(kBlock) void k_fold(FoldArgs a, const uint32_t* heads, int64_t nheads, int64_t nops,
+                                                 const uint32_t* okey_sorted, const uint32_t* oref_sorted,
+                                                 const uint64_t* iargv, const uint8_t* iargn, const int32_t* ievrow,
+                                                 const int32_t* call_of, uint64_t* resv, uint8_t* resn,
+                                                 uint8_t* first, uint32_t* last_of) {
+  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nheads; h += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q0 = heads[h];
+    int64_t q1 = h + 1 < nheads ? (int64_t)heads[h + 1] : nops;
+    uint32_t key = okey_sorted[q0];
+    double d[kMaxAggs];
+    int64_t l[kMaxAggs], c[kMaxAggs];
+    for (int g = 0; g < a.nagg; g++) {
+      d[g] = a.dsum[g * a.nkeys + key];
+      l[g] = a.lsum[g * a.nkeys + key];
+      c[g] = a.cnt[g * a.nkeys + key];
+    }
+    int32_t cur_call = -1;
+    uint32_t t_first = 0, t_prev = 0;
+    for (int64_t q = q0; q < q1; q++) {
+      uint32_t ref = oref_sorted[q];
+      bool add = ref & kAddBit;
+      uint32_t t = ref & ~kAddBit;
+      for (int g = 0; g < a.nagg; g++) {
+        uint64_t xb = iargv[g * a.cap + t];
+        bool xn = iargn[g * a.cap + t];
+        uint64_t ob = 0;
+        bool on = true;
+        switch (a.kind[g]) {
+          case SHD_AGG_COUNT:
+            c[g] += add ? 1 : -1;
+            ob = (uint64_t)c[g];
+            on = false;
+            break;
+          case SHD_AGG_SUM:
+            if (a.type[g] == SHD_T_INT || a.type[g] == SHD_T_LONG) {
+              if (xn) {
+                if (c[g] != 0) { ob = (uint64_t)l[g]; on = false; }
+                break;
+              }
+              int64_t x = a.type[g] == SHD_T_INT ? (int64_t)v_i32(xb) : (int64_t)xb;
+              if (add) {
+                l[g] = (int64_t)((uint64_t)l[g] + (uint64_t)x);
+                c[g]++;
+                ob = (uint64_t)l[g];
+                on = false;
+              } else {
+                l[g] = java_d2l(__dsub_rn((double)l[g], (double)x));
+                c[g]--;
+                if (c[g] != 0) { ob = (uint64_t)l[g]; on = false; }
+              }
+            } else {
+              if (xn) {
+                if (a.type[g] == SHD_T_DOUBLE && c[g] != 0) { ob = p_f64(d[g]); on = false; }
+                break;
+              }
+              double x = a.type[g] == SHD_T_FLOAT ? (double)v_f32(xb) : v_f64(xb);
+              if (add) {
+                d[g] = __dadd_rn(d[g], x);
+                c[g]++;
+                ob = p_f64(d[g]);
+                on = false;
+              } else {
+                d[g] = __dsub_rn(d[g], x);
+                c[g]--;
+                if (c[g] != 0) { ob = p_f64(d[g]); on = false; }
+              }
+            }
+            break;
+          case SHD_AGG_AVG: {
+            if (xn) {
+              if (c[g] != 0) { ob = p_f64(__ddiv_rn(d[g], (double)c[g])); on = false; }
+              break;
+            }
+            double x;
+            switch (a.type[g]) {
+              case SHD_T_INT: x = (double)v_i32(xb); break;
+              case SHD_T_LONG: x = (double)(int64_t)xb; break;
+              case SHD_T_FLOAT: x = (double)v_f32(xb); break;
+              default: x = v_f64(xb);
+            }
+            if (add) { c[g]++; d[g] = __dadd_rn(d[g], x); }
+            else { c[g]--; d[g] = __dsub_rn(d[g], x); }
+            if (c[g] != 0) { ob = p_f64(__ddiv_rn(d[g], (double)c[g])); on = false; }
+            break;
+          }
+        }
+        if (add) {
+          resv[g * a.cap + t] = ob;
+          resn[g * a.cap + t] = (uint8_t)on;
+        }
+      }
+      if (add) {
+        int32_t call = call_of[ievrow[t]];
+        if (call != cur_call) {
+          if (cur_call >= 0) last_of[t_first] = t_prev;
+          first[t] = 1;
+          t_first = t;
+          cur_call = call;
+        }
+        t_prev = t;
+      }
+    }
+    if (cur_call >= 0) last_of[t_first] = t_prev;
+    for (int g = 0; g < a.nagg; g++) {
+      a.dsum[g * a.nkeys + key] = d[g];
+      a.lsum[g * a.nkeys + key] = l[g];
+      a.cnt[g * a.nkeys + key] = c[g];
+    }
+  }
+}
+
+__global__ void k_first_counts(const uint8_t* first, int64_t C, int64_t total, uint32_t* cnt) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total - C; t += (int64_t)gridDim.x * blockDim.x)
+    cnt[t] = first[C + t] ? 1u : 0u;
+}
+
+struct EmitArgs {
+  ColSet cs;
+  DExprSet es;
+  DExpr outs[kMaxCols];
+  int nout;
+  int nagg;
+  int64_t cap;
+  int64_t C;
+  int64_t row0;
+  int64_t chunk0;
+};
+
+__global__ __launch_bounds__(kBlock) void k_emit(EmitArgs a, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
+                                                 const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
+                                                 const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
+                                                 int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+  for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
+    if (!fcnt[t0]) continue;
+    int64_t tf = a.C + t0;
+    int64_t tl = last_of[tf];
+    int64_t ev = ievrow[tl];
+    uint64_t av[kMaxAggs];
+    uint8_t an[kMaxAggs];
+    for (int g = 0; g < a.nagg; g++) {
+      av[g] = resv[g * a.cap + tl];
+      an[g] = resn[g * a.cap + tl];
+    }
+    RowCtx cx{&a.cs, ev, av, an};
+    int64_t row = a.row0 + foff[t0];
+    for (int c = 0; c < a.nout; c++) {
+      Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
+      o_vals[row * a.nout + c] = v.b;
+      o_nul[row * a.nout + c] = (uint8_t)v.null;
+    }
+    o_ts[row] = a.cs.ts[ev];
+    o_type[row] = 0;
+    o_chunk[row] = a.chunk0 + call_of[ev];
+  }
+}
+
+int plain_load_attr(const Plan& p, int e) {
+  auto& code = p.exprs[e];
+  if (code.size() == 1 && code[0].op == SHD_OP_LOAD) return code[0].c & 0xFFFF;
+  return -1;
+}
+
+}  // namespace
+
+struct SingleEngine : Engine {
+  bool agg_mode = false;
+  std::vector<int> filters;
+  int wkind = 0;
+  int64_t wparam = 0;
+  bool partitioned = false;
+  int key_expr = -1, key_col = -1, key_type = 0;
+  int group_expr = -1, group_col = -1, group_type = 0;
+  std::vector<int> outs;
+  std::vector<int> types;
+  int nagg = 0;
+  // per-batch scratch
+  DevBuf d_offs, d_call_of, d_last_ts, d_now, d_flags, d_cnt, d_off, d_pkey, d_start, d_run, d_tot, d_scan, d_sort;
+  PinnedBuf h_tot;
+  // window items: carry [0, C) + new; double-buffered
+  int64_t C = 0;
+  int cur = 0;
+  DevBuf ikey[2], its[2], iargv[2], iargn[2];
+  int64_t icap[2] = {0, 0};
+  DevBuf ievrow, inow, e_exp, okey, oref, okey32, okey32_alt, oref_alt, heads, hoff, hlist, resv, resn, first,
+      last_of, fcnt, foff;
+  // group state (dense by key)
+  DevBuf g_dsum, g_lsum, g_cnt;
+  int64_t g_nkeys = 0;
+
+  int kind() const override { return agg_mode ? ENG_WINDOW : ENG_FILTER; }
+
+  void reset() override {
+    C = 0;
+    seq = 0;
+    now = INT64_MIN;
+    chunk_seq = 0;
+    out.count = 0;
+    counters = shd_counters{};
+    if (g_nkeys) {
+      SHD_HIP(hipMemset(g_dsum.p, 0, g_dsum.cap));
+      SHD_HIP(hipMemset(g_lsum.p, 0, g_lsum.cap));
+      SHD_HIP(hipMemset(g_cnt.p, 0, g_cnt.cap));
+    }
+  }
+
+  std::vector<int64_t> h_offs;   // lives until the next push (async H2D source)
+
+  void stage_calls(const Staged& b, int64_t& ncalls) {
+    h_offs = b.call_offsets;
+    if (h_offs.size() < 2) h_offs = {0, b.n};
+    std::vector<int64_t>& offs = h_offs;
+    ncalls = (int64_t)offs.size() - 1;
+    d_offs.reserve(offs.size() * 8);
+    SHD_HIP(hipMemcpyAsync(d_offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, stream));
+    d_call_of.reserve(b.n * 4);
+    d_last_ts.reserve(ncalls * 8);
+    d_now.reserve(ncalls * 8);
+    hipLaunchKernelGGL(k_call_of, dim3((unsigned)std::min<int64_t>(ncalls, 65535)), dim3(kBlock), 0, stream,
+                       (const int64_t*)d_offs.as<int64_t>(), (int)ncalls, b.cs.ts, d_call_of.as<int32_t>(),
+                       d_last_ts.as<int64_t>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_call_now, dim3(1), dim3(kBlock), 0, stream, (const int64_t*)d_last_ts.as<int64_t>(),
+                       (int)ncalls, now, d_now.as<int64_t>());
+    SHD_CHECK_LAUNCH();
+  }
+
+  void push(const Staged& b) override {
+    const int64_t n = b.n;
+    if (n <= 0) return;
+    hipStream_t s = stream;
+    SHD_HIP(hipEventRecord(ev0, s));
+    stage_begin();
+    int64_t ncalls = 0;
+    stage_calls(b, ncalls);
+    d_flags.reserve(n);
+    d_cnt.reserve(n * 4);
+    d_off.reserve(n * 4);
+    d_tot.reserve(64);
+    h_tot.reserve(64);
+    if (partitioned) d_pkey.reserve(n * 8);
+    FilterArgs fa{};
+    fa.cs = b.cs;
+    fa.es = dset();
+    fa.filters = dfilters(filters);
+    fa.partitioned = partitioned;
+    if (partitioned) {
+      fa.key = dexpr(key_expr);
+      fa.key_col = key_col;
+      fa.key_type = key_type;
+    }
+    hipLaunchKernelGGL(k_filter, dim3(grid_for(n)), dim3(kBlock), 0, s, fa, n, d_flags.as<uint8_t>(),
+                       d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
+    SHD_CHECK_LAUNCH();
+    uint32_t* d_m = (uint32_t*)d_tot.p;
+    scan_exclusive_u32(d_cnt.as<uint32_t>(), d_off.as<uint32_t>(), n, d_m, d_scan, s);
+    mark("filter");
+    if (!agg_mode) push_filter(b, ncalls, n);
+    else push_agg(b, ncalls, n);
+    SHD_HIP(hipEventRecord(ev1, s));
+    stage_end();
+    SHD_HIP(hipEventSynchronize(ev1));
+    float ms = 0.f;
+    SHD_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+    counters.kernel_ns = (int64_t)(ms * 1e6);
+    counters.events += n;
+    // TimestampGeneratorImpl: time moves to the last call's ts if later
+    if (b.advance_time || true) {
+      int64_t last = 0;
+      SHD_HIP(hipMemcpy(&last, d_now.as<int64_t>() + (ncalls - 1), 8, hipMemcpyDeviceToHost));
+      if (last > now) now = last;
+    }
+    seq += n;
+  }
+
+  void push_filter(const Staged& b, int64_t ncalls, int64_t n) {
+    hipStream_t s = stream;
+    uint32_t* d_m = (uint32_t*)d_tot.p;
+    uint32_t* d_r = d_m + 1;
+    if (partitioned) {
+      d_start.reserve(n * 4);
+      d_run.reserve(n * 4);
+      hipLaunchKernelGGL(k_run_starts, dim3(grid_for(n)), dim3(kBlock), 0, s, (const uint8_t*)d_flags.as<uint8_t>(),
+                         (const uint64_t*)d_pkey.as<uint64_t>(), (const int32_t*)d_call_of.as<int32_t>(), n,
+                         d_start.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      // run id of event i = (#starts up to and including i) - 1
+      scan_exclusive_u32(d_start.as<uint32_t>(), d_run.as<uint32_t>(), n, d_r, d_scan, s);
+    }
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    uint32_t m = h_tot.as<uint32_t>()[0];
+    uint32_t nruns = h_tot.as<uint32_t>()[1];
+    if (m > 0) {
+      out.ensure(m, s);
+      ProjArgs pa{};
+      pa.cs = b.cs;
+      pa.es = dset();
+      pa.nout = (int)outs.size();
+      for (size_t c = 0; c < outs.size(); c++) pa.outs[c] = dexpr(outs[c]);
+      pa.row0 = out.count;
+      // exclusive run ids: the run of event i is start-scan[i] (+0 if i is a start it is its own index)
+      pa.chunk0 = chunk_seq;
+      pa.partitioned = partitioned;
+      hipLaunchKernelGGL(k_project_rows, dim3(grid_for(n)), dim3(kBlock), 0, s, pa, n,
+                         (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
+                         (const int32_t*)d_call_of.as<int32_t>(), (const uint32_t*)d_run.as<uint32_t>(),
+                         (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+      SHD_CHECK_LAUNCH();
+      out.count += m;
+    }
+    chunk_seq += partitioned ? (int64_t)nruns : ncalls;
+    counters.matches += m;
+  }
+
+  void ensure_items(int slot, int64_t cap) {
+    if (icap[slot] >= cap) return;
+    int64_t nc = std::max<int64_t>(cap, 1024);
+    DevBuf k2, t2, v2, n2;
+    k2.reserve(nc * 8);
+    t2.reserve(nc * 8);
+    v2.reserve(std::max(nagg, 1) * nc * 8);
+    n2.reserve(std::max(nagg, 1) * nc);
+    std::swap(ikey[slot].p, k2.p); std::swap(ikey[slot].cap, k2.cap);
+    std::swap(its[slot].p, t2.p); std::swap(its[slot].cap, t2.cap);
+    std::swap(iargv[slot].p, v2.p); std::swap(iargv[slot].cap, v2.cap);
+    std::swap(iargn[slot].p, n2.p); std::swap(iargn[slot].cap, n2.cap);
+    icap[slot] = nc;
+    // (old contents are only needed for the carry slot, which is copied explicitly)
+  }
+
+  void ensure_groups(int64_t nkeys) {
+    if (nkeys <= g_nkeys) return;
+    int64_t nk = std::max<int64_t>(nkeys, g_nkeys * 2);
+    nk = std::max<int64_t>(nk, 1024);
+    DevBuf a, l, c;
+    int na = std::max(nagg, 1);
+    a.reserve(na * nk * 8);
+    l.reserve(na * nk * 8);
+    c.reserve(na * nk * 8);
+    SHD_HIP(hipMemsetAsync(a.p, 0, na * nk * 8, stream));
+    SHD_HIP(hipMemsetAsync(l.p, 0, na * nk * 8, stream));
+    SHD_HIP(hipMemsetAsync(c.p, 0, na * nk * 8, stream));
+    for (int g = 0; g < nagg && g_nkeys; g++) {
+      SHD_HIP(hipMemcpyAsync(a.as<double>() + g * nk, g_dsum.as<double>() + g * g_nkeys, g_nkeys * 8,
+                             hipMemcpyDeviceToDevice, stream));
+      SHD_HIP(hipMemcpyAsync(l.as<int64_t>() + g * nk, g_lsum.as<int64_t>() + g * g_nkeys, g_nkeys * 8,
+                             hipMemcpyDeviceToDevice, stream));
+      SHD_HIP(hipMemcpyAsync(c.as<int64_t>() + g * nk, g_cnt.as<int64_t>() + g * g_nkeys, g_nkeys * 8,
+                             hipMemcpyDeviceToDevice, stream));
+    }
+    SHD_HIP(hipStreamSynchronize(stream));
+    std::swap(g_dsum.p, a.p); std::swap(g_dsum.cap, a.cap);
+    std::swap(g_lsum.p, l.p); std::swap(g_lsum.cap, l.cap);
+    std::swap(g_cnt.p, c.p); std::swap(g_cnt.cap, c.cap);
+    g_nkeys = nk;
+  }
+
+  void push_agg(const Staged& b, int64_t ncalls, int64_t n) {
+    hipStream_t s = stream;
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t m = h_tot.as<uint32_t>()[0];
+    const int64_t total = C + m;
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 5, 0, 8, s));
+    if (total >= (int64_t)INT32_MAX) throw Error(SHD_E_CAPACITY, "window items exceed 2^31");
+    // items: carry slot `cur` already holds [0, C); build the new item set in slot `cur`
+    // (grow preserving the carry)
+    if (icap[cur] < total) {
+      int old = cur, nw = cur ^ 1;
+      ensure_items(nw, total);
+      if (C > 0) {
+        SHD_HIP(hipMemcpyAsync(ikey[nw].p, ikey[old].p, C * 8, hipMemcpyDeviceToDevice, s));
+        SHD_HIP(hipMemcpyAsync(its[nw].p, its[old].p, C * 8, hipMemcpyDeviceToDevice, s));
+        for (int g = 0; g < nagg; g++) {
+          SHD_HIP(hipMemcpyAsync(iargv[nw].as<uint64_t>() + g * icap[nw], iargv[old].as<uint64_t>() + g * icap[old],
+                                 C * 8, hipMemcpyDeviceToDevice, s));
+          SHD_HIP(hipMemcpyAsync(iargn[nw].as<uint8_t>() + g * icap[nw], iargn[old].as<uint8_t>() + g * icap[old], C,
+                                 hipMemcpyDeviceToDevice, s));
+        }
+      }
+      cur = nw;
+    }
+    const int64_t cap = icap[cur];
+    ievrow.reserve(cap * 4);
+    inow.reserve(cap * 8);
+    ItemArgs ia{};
+    ia.cs = b.cs;
+    ia.es = dset();
+    ia.nagg = nagg;
+    for (int g = 0; g < nagg; g++) {
+      ia.has_arg[g] = plan.aggs[g].expr >= 0;
+      if (ia.has_arg[g]) ia.agg_arg[g] = dexpr(plan.aggs[g].expr);
+    }
+    ia.ngroup = group_expr >= 0;
+    if (ia.ngroup) {
+      ia.group = dexpr(group_expr);
+      ia.group_col = group_col;
+      ia.group_type = group_type;
+    }
+    ia.C = C;
+    hipLaunchKernelGGL(k_make_items, dim3(grid_for(n)), dim3(kBlock), 0, s, ia, n,
+                       (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
+                       (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
+                       ikey[cur].as<uint64_t>(), its[cur].as<int64_t>(), iargv[cur].as<uint64_t>(),
+                       iargn[cur].as<uint8_t>(), ievrow.as<int32_t>(), inow.as<int64_t>(), cap,
+                       (uint32_t*)(d_tot.as<uint64_t>() + 5));
+    SHD_CHECK_LAUNCH();
+    mark("window_items");
+    // expiry positions
+    e_exp.reserve(std::max<int64_t>(total, 1) * 4);
+    hipLaunchKernelGGL(k_expiry, dim3(grid_for(total)), dim3(kBlock), 0, s, wkind, wparam, C, total,
+                       (const int64_t*)its[cur].as<int64_t>(), (const int64_t*)inow.as<int64_t>(), e_exp.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    if (wkind == SHD_W_TIME) {
+      hipLaunchKernelGGL(k_prefix_max_u32, dim3(1), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total);
+      SHD_CHECK_LAUNCH();
+    }
+    unsigned long long* d_x = (unsigned long long*)(d_tot.as<uint64_t>() + 1);
+    uint64_t* d_kmax = d_tot.as<uint64_t>() + 2;
+    SHD_HIP(hipMemsetAsync(d_x, 0, 8, s));
+    hipLaunchKernelGGL(k_count_expired, dim3(grid_for(total, 4, 2048)), dim3(kBlock), 0, s,
+                       (const uint32_t*)e_exp.as<uint32_t>(), total, d_x);
+    SHD_CHECK_LAUNCH();
+    reduce_max_u64(ikey[cur].as<uint64_t>(), total, d_kmax, s);
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 48, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    if (h_tot.as<uint32_t>()[10]) throw Error(SHD_E_UNSUPPORTED, "null group-by key on the device path");
+    const int64_t X = (int64_t)h_tot.as<uint64_t>()[1];
+    const uint64_t kmax = h_tot.as<uint64_t>()[2];
+    if ((int64_t)kmax >= kMaxDenseKey)
+      throw Error(SHD_E_UNSUPPORTED, "group-by key outside the dense device range");
+    ensure_groups((int64_t)kmax + 1);
+    const int64_t nops = m + X;
+    if (nops > 0) {
+      okey.reserve(nops * 8);
+      oref.reserve(nops * 4);
+      hipLaunchKernelGGL(k_make_ops, dim3(grid_for(total)), dim3(kBlock), 0, s, C, total,
+                         (const uint32_t*)e_exp.as<uint32_t>(), (const uint64_t*)ikey[cur].as<uint64_t>(),
+                         okey.as<uint64_t>(), oref.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      // stable key sort of the operation stream (op order kept inside a group)
+      okey32.reserve(nops * 4);
+      okey32_alt.reserve(nops * 4);
+      oref_alt.reserve(nops * 4);
+      hipLaunchKernelGGL(k_narrow, dim3(grid_for(nops)), dim3(kBlock), 0, s, (const uint64_t*)okey.as<uint64_t>(),
+                         okey32.as<uint32_t>(), nops);
+      SHD_CHECK_LAUNCH();
+      int bits = 0;
+      while (bits < 32 && (kmax >> bits)) bits++;
+      bool in_alt = false;
+      radix_sort_pairs_u32(okey32.as<uint32_t>(), oref.as<uint32_t>(), okey32_alt.as<uint32_t>(),
+                           oref_alt.as<uint32_t>(), nops, bits, d_sort, s, in_alt);
+      const uint32_t* sk = in_alt ? okey32_alt.as<uint32_t>() : okey32.as<uint32_t>();
+      const uint32_t* sr = in_alt ? oref_alt.as<uint32_t>() : oref.as<uint32_t>();
+      mark("group_sort");
+      heads.reserve(nops * 4);
+      hoff.reserve(nops * 4);
+      hipLaunchKernelGGL(k_seg_heads, dim3(grid_for(nops)), dim3(kBlock), 0, s, sk, nops, heads.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      uint32_t* d_h = (uint32_t*)(d_tot.as<uint64_t>() + 3);
+      scan_exclusive_u32(heads.as<uint32_t>(), hoff.as<uint32_t>(), nops, d_h, d_scan, s);
+      SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 3, d_h, 4, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipStreamSynchronize(s));
+      const int64_t nheads = h_tot.as<uint32_t>()[6];
+      hlist.reserve(std::max<int64_t>(nheads, 1) * 4);
+      hipLaunchKernelGGL(k_head_list, dim3(grid_for(nops)), dim3(kBlock), 0, s, (const uint32_t*)heads.as<uint32_t>(),
+                         (const uint32_t*)hoff.as<uint32_t>(), nops, hlist.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      resv.reserve(std::max(nagg, 1) * cap * 8);
+      resn.reserve(std::max(nagg, 1) * cap);
+      first.reserve(cap);
+      last_of.reserve(cap * 4);
+      SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
+      FoldArgs fo{};
+      fo.nagg = nagg;
+      for (int g = 0; g < nagg; g++) {
+        fo.kind[g] = plan.aggs[g].kind;
+        fo.type[g] = plan.aggs[g].type;
+      }
+      fo.cap = cap;
+      fo.dsum = g_dsum.as<double>();
+      fo.lsum = g_lsum.as<int64_t>();
+      fo.cnt = g_cnt.as<int64_t>();
+      fo.nkeys = g_nkeys;
+      hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, fo, (const uint32_t*)hlist.as<uint32_t>(),
+                         nheads, nops, sk, sr, (const uint64_t*)iargv[cur].as<uint64_t>(),
+                         (const uint8_t*)iargn[cur].as<uint8_t>(), (const int32_t*)ievrow.as<int32_t>(),
+                         (const int32_t*)d_call_of.as<int32_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(),
+                         first.as<uint8_t>(), last_of.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      mark("group_fold");
+      // emission: first-seen (call, group) rows in event order
+      if (m > 0) {
+        fcnt.reserve(m * 4);
+        foff.reserve(m * 4);
+        hipLaunchKernelGGL(k_first_counts, dim3(grid_for(m)), dim3(kBlock), 0, s, (const uint8_t*)first.as<uint8_t>(),
+                           C, total, fcnt.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+        uint32_t* d_f = (uint32_t*)(d_tot.as<uint64_t>() + 4);
+        scan_exclusive_u32(fcnt.as<uint32_t>(), foff.as<uint32_t>(), m, d_f, d_scan, s);
+        SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 4, d_f, 4, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        const int64_t nrows = h_tot.as<uint32_t>()[8];
+        if (nrows > 0) {
+          out.ensure(nrows, s);
+          EmitArgs ea{};
+          ea.cs = b.cs;
+          ea.es = dset();
+          ea.nout = (int)outs.size();
+          for (size_t c = 0; c < outs.size(); c++) ea.outs[c] = dexpr(outs[c]);
+          ea.nagg = nagg;
+          ea.cap = cap;
+          ea.C = C;
+          ea.row0 = out.count;
+          ea.chunk0 = chunk_seq;
+          hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, s, ea, m, (const uint32_t*)fcnt.as<uint32_t>(),
+                             (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
+                             (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
+                             (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(), out.d_chunk(),
+                             out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+          SHD_CHECK_LAUNCH();
+          out.count += nrows;
+          counters.matches += nrows;
+          mark("emit");
+        }
+      }
+    }
+    // carry: the unexpired suffix [X, total) becomes the new window contents
+    int64_t keep = wkind == 0 ? 0 : total - X;
+    if (keep > 0 && X > 0) {
+      int nw = cur ^ 1;
+      ensure_items(nw, keep);
+      SHD_HIP(hipMemcpyAsync(ikey[nw].p, ikey[cur].as<uint64_t>() + X, keep * 8, hipMemcpyDeviceToDevice, s));
+      SHD_HIP(hipMemcpyAsync(its[nw].p, its[cur].as<int64_t>() + X, keep * 8, hipMemcpyDeviceToDevice, s));
+      for (int g = 0; g < nagg; g++) {
+        SHD_HIP(hipMemcpyAsync(iargv[nw].as<uint64_t>() + g * icap[nw], iargv[cur].as<uint64_t>() + g * icap[cur] + X,
+                               keep * 8, hipMemcpyDeviceToDevice, s));
+        SHD_HIP(hipMemcpyAsync(iargn[nw].as<uint8_t>() + g * icap[nw], iargn[cur].as<uint8_t>() + g * icap[cur] + X,
+                               keep, hipMemcpyDeviceToDevice, s));
+      }
+      cur = nw;
+    }
+    C = keep;
+    counters.carry = C;
+    counters.partial_scans += nops;
+    chunk_seq += ncalls;
+  }
+};
+
+std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
+  if (p.kind != SHD_KIND_SINGLE) { why = "not a single-stream query"; return nullptr; }
+  auto e = std::make_unique<SingleEngine>();
+  e->types = p.stream_types[p.single_stream];
+  if (e->types.size() > (size_t)kMaxCols) { why = "too many attributes"; return nullptr; }
+  bool seen_window = false;
+  for (auto& h : p.handlers) {
+    if (h.kind == SHD_H_FILTER) {
+      if (seen_window) { why = "filter after window"; return nullptr; }
+      e->filters.push_back(h.expr);
+    } else {
+      seen_window = true;
+      e->wkind = h.wkind;
+      e->wparam = h.param;
+    }
+  }
+  if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
+  if (p.having >= 0) { why = "having"; return nullptr; }
+  for (auto& o : p.outputs) e->outs.push_back(o.second);
+  if (e->outs.size() > (size_t)kMaxCols) { why = "too many outputs"; return nullptr; }
+  e->nagg = (int)p.aggs.size();
+  if (e->nagg > kMaxAggs) { why = "too many aggregators"; return nullptr; }
+  e->partitioned = !p.part_keys.empty();
+  bool needs_agg = e->nagg > 0 || !p.group_by.empty();
+  if (p.expired_on && (needs_agg || e->wkind != 0)) { why = "expired-event output from a window"; return nullptr; }
+  if (e->wkind != 0 && e->wparam <= 0 && e->wkind == SHD_W_LENGTH) { why = "length(0) window"; return nullptr; }
+  e->agg_mode = needs_agg;
+  if (e->partitioned) {
+    if (e->agg_mode) { why = "partitioned window/aggregation"; return nullptr; }
+    e->key_expr = p.part_keys[0].second;
+    e->key_col = plain_load_attr(p, e->key_expr);
+    e->key_type = expr_result_type(p, e->key_expr, {});
+  }
+  if (p.group_by.size() > 1) { why = "multi-attribute group by"; return nullptr; }
+  if (!p.group_by.empty()) {
+    e->group_expr = p.group_by[0];
+    e->group_col = plain_load_attr(p, e->group_expr);
+    e->group_type = expr_result_type(p, e->group_expr, {});
+    if (e->group_type == SHD_T_FLOAT || e->group_type == SHD_T_DOUBLE) { why = "floating group key"; return nullptr; }
+  }
+  return e;
+}
+
+}  // namespace shd

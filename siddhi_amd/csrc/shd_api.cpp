@@ -1,0 +1,545 @@
+// shd_api.cpp -- the C-ABI of libsiddhi_hip (include/siddhi_hip.h): plan
+// decoding, engine selection, batch staging, output polling.
+#include <algorithm>
+#include <mutex>
+
+#include "engine.h"
+
+namespace shd {
+
+// ------------------------------------------------------------------ plan decode
+namespace {
+struct Reader {
+  const int32_t* w;
+  int64_t n, i = 0;
+  int32_t next() {
+    if (i >= n) throw Error(SHD_E_INVALID_PLAN, "plan IR truncated");
+    return w[i++];
+  }
+  int64_t next64() {
+    uint32_t lo = (uint32_t)next();
+    uint32_t hi = (uint32_t)next();
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }
+};
+
+PNode read_node(Reader& r, int depth) {
+  if (depth > 64) throw Error(SHD_E_INVALID_PLAN, "plan tree too deep");
+  PNode n;
+  n.kind = r.next();
+  switch (n.kind) {
+    case SHD_NODE_STREAM: {
+      n.state_id = r.next();
+      n.stream = r.next();
+      n.absent = r.next();
+      n.waiting = r.next64();
+      int nf = r.next();
+      if (nf < 0 || nf > 64) throw Error(SHD_E_INVALID_PLAN, "bad filter count");
+      for (int i = 0; i < nf; i++) n.filters.push_back(r.next());
+      break;
+    }
+    case SHD_NODE_NEXT:
+      n.kids.push_back(read_node(r, depth + 1));
+      n.kids.push_back(read_node(r, depth + 1));
+      break;
+    case SHD_NODE_EVERY:
+      n.kids.push_back(read_node(r, depth + 1));
+      break;
+    case SHD_NODE_LOGICAL:
+      n.ltype = r.next();
+      n.kids.push_back(read_node(r, depth + 1));
+      n.kids.push_back(read_node(r, depth + 1));
+      break;
+    case SHD_NODE_COUNT:
+      n.min = r.next();
+      n.max = r.next();
+      n.kids.push_back(read_node(r, depth + 1));
+      break;
+    default:
+      throw Error(SHD_E_INVALID_PLAN, "bad node kind");
+  }
+  return n;
+}
+}  // namespace
+
+Plan decode_plan(const int32_t* w, int64_t n) {
+  Reader r{w, n};
+  Plan p;
+  if (r.next() != (int32_t)SHD_IR_MAGIC) throw Error(SHD_E_INVALID_PLAN, "bad plan magic");
+  if (r.next() != SHD_IR_VERSION) throw Error(SHD_E_INVALID_PLAN, "unsupported plan version");
+  p.kind = r.next();
+  int ns = r.next();
+  if (ns < 0 || ns > 64) throw Error(SHD_E_INVALID_PLAN, "bad stream count");
+  for (int s = 0; s < ns; s++) {
+    int na = r.next();
+    if (na < 0 || na > 1024) throw Error(SHD_E_INVALID_PLAN, "bad attribute count");
+    std::vector<int> t;
+    for (int a = 0; a < na; a++) t.push_back(r.next());
+    p.stream_types.push_back(t);
+  }
+  int nc = r.next();
+  if (nc < 0) throw Error(SHD_E_INVALID_PLAN, "bad const count");
+  for (int i = 0; i < nc; i++) p.consts.push_back((uint64_t)r.next64());
+  int ne = r.next();
+  if (ne < 0) throw Error(SHD_E_INVALID_PLAN, "bad expression count");
+  for (int i = 0; i < ne; i++) {
+    int ni = r.next();
+    if (ni < 0 || ni > 4096) throw Error(SHD_E_INVALID_PLAN, "bad instruction count");
+    std::vector<Instr> code;
+    for (int k = 0; k < ni; k++) {
+      Instr in;
+      in.op = r.next();
+      in.a = r.next();
+      in.b = r.next();
+      in.c = r.next();
+      code.push_back(in);
+    }
+    p.exprs.push_back(code);
+  }
+  int nk = r.next();
+  for (int i = 0; i < nk; i++) {
+    int s = r.next();
+    int e = r.next();
+    p.part_keys.push_back({s, e});
+  }
+  if (p.kind == SHD_KIND_STATE) {
+    p.state_type = r.next();
+    p.within = r.next64();
+    p.n_states = r.next();
+    p.root = read_node(r, 0);
+  } else if (p.kind == SHD_KIND_SINGLE) {
+    p.single_stream = r.next();
+    int nh = r.next();
+    for (int i = 0; i < nh; i++) {
+      Plan::Handler h{};
+      h.kind = r.next();
+      if (h.kind == SHD_H_FILTER) h.expr = r.next();
+      else {
+        h.wkind = r.next();
+        h.param = r.next64();
+      }
+      p.handlers.push_back(h);
+    }
+  } else {
+    throw Error(SHD_E_INVALID_PLAN, "bad plan kind");
+  }
+  p.current_on = r.next();
+  p.expired_on = r.next();
+  int na = r.next();
+  for (int i = 0; i < na; i++) {
+    Plan::Agg a;
+    a.kind = r.next();
+    a.expr = r.next();
+    a.type = r.next();
+    p.aggs.push_back(a);
+  }
+  int ng = r.next();
+  for (int i = 0; i < ng; i++) p.group_by.push_back(r.next());
+  p.having = r.next();
+  int no = r.next();
+  for (int i = 0; i < no; i++) {
+    int t = r.next();
+    int e = r.next();
+    p.outputs.push_back({t, e});
+  }
+  // validation: expression ids, stack depth, constants
+  auto check_expr = [&](int e) {
+    if (e < 0 || e >= (int)p.exprs.size()) throw Error(SHD_E_INVALID_PLAN, "bad expression id");
+    if (expr_max_depth(p, e) > kMaxStack) throw Error(SHD_E_UNSUPPORTED, "expression stack too deep");
+    for (auto& in : p.exprs[e])
+      if (in.op == SHD_OP_CONST && (in.a < 0 || in.a >= (int)p.consts.size()))
+        throw Error(SHD_E_INVALID_PLAN, "bad constant index");
+  };
+  for (size_t e = 0; e < p.exprs.size(); e++) check_expr((int)e);
+  for (auto& o : p.outputs) check_expr(o.second);
+  return p;
+}
+
+int expr_max_depth(const Plan& p, int expr) {
+  int sp = 0, mx = 0;
+  for (auto& in : p.exprs[expr]) {
+    switch (in.op) {
+      case SHD_OP_CONST: case SHD_OP_NULL: case SHD_OP_LOAD: case SHD_OP_EVNULL: case SHD_OP_TS: case SHD_OP_AGG:
+        sp++;
+        break;
+      case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD: case SHD_OP_EQ:
+      case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE: case SHD_OP_AND:
+      case SHD_OP_OR:
+        sp--;
+        break;
+      default:
+        break;
+    }
+    if (sp < 0) throw Error(SHD_E_INVALID_PLAN, "expression stack underflow");
+    mx = std::max(mx, sp);
+  }
+  return mx;
+}
+
+int expr_result_type(const Plan& p, int expr, const std::vector<int>&) {
+  std::vector<int> st;
+  for (auto& in : p.exprs[expr]) {
+    switch (in.op) {
+      case SHD_OP_CONST: case SHD_OP_NULL: st.push_back(in.b); break;
+      case SHD_OP_LOAD: st.push_back(in.c >> 16); break;
+      case SHD_OP_EVNULL: st.push_back(SHD_T_BOOL); break;
+      case SHD_OP_TS: st.push_back(SHD_T_LONG); break;
+      case SHD_OP_CVT: if (!st.empty()) st.back() = in.b; break;
+      case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD:
+        if (st.size() >= 2) { st.pop_back(); st.back() = in.a; }
+        break;
+      case SHD_OP_EQ: case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE:
+      case SHD_OP_AND: case SHD_OP_OR:
+        if (st.size() >= 2) { st.pop_back(); st.back() = SHD_T_BOOL; }
+        break;
+      case SHD_OP_NOT: case SHD_OP_ISNULL: if (!st.empty()) st.back() = SHD_T_BOOL; break;
+      case SHD_OP_AGG: st.push_back(SHD_T_DOUBLE); break;
+    }
+  }
+  return st.empty() ? SHD_T_LONG : st.back();
+}
+
+void DevExprTable::upload(const Plan& p) {
+  std::vector<int4> all;
+  off.clear();
+  len.clear();
+  for (auto& code : p.exprs) {
+    off.push_back((int)all.size());
+    len.push_back((int)code.size());
+    for (auto& in : code) all.push_back(make_int4(in.op, in.a, in.b, in.c));
+  }
+  ins.reserve(std::max<size_t>(all.size(), 1) * sizeof(int4));
+  consts.reserve(std::max<size_t>(p.consts.size(), 1) * 8);
+  if (!all.empty()) SHD_HIP(hipMemcpy(ins.p, all.data(), all.size() * sizeof(int4), hipMemcpyHostToDevice));
+  if (!p.consts.empty()) SHD_HIP(hipMemcpy(consts.p, p.consts.data(), p.consts.size() * 8, hipMemcpyHostToDevice));
+}
+
+void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
+  int64_t need = count + extra;
+  if (need <= cap) return;
+  int64_t nc = std::max<int64_t>(need, std::max<int64_t>(cap * 2, 4096));
+  int w = std::max(ncols, 1);
+  DevBuf c2, t2, ts2, v2, n2;
+  c2.reserve(nc * 8);
+  t2.reserve(nc * 4);
+  ts2.reserve(nc * 8);
+  v2.reserve(nc * w * 8);
+  n2.reserve(nc * w);
+  if (count > 0) {
+    SHD_HIP(hipMemcpyAsync(c2.p, chunk.p, count * 8, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(t2.p, type.p, count * 4, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(ts2.p, ts.p, count * 8, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(v2.p, vals.p, count * w * 8, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(n2.p, nulls.p, count * w, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipStreamSynchronize(s));
+  }
+  std::swap(chunk.p, c2.p); std::swap(chunk.cap, c2.cap);
+  std::swap(type.p, t2.p); std::swap(type.cap, t2.cap);
+  std::swap(ts.p, ts2.p); std::swap(ts.cap, ts2.cap);
+  std::swap(vals.p, v2.p); std::swap(vals.cap, v2.cap);
+  std::swap(nulls.p, n2.p); std::swap(nulls.cap, n2.cap);
+  cap = nc;
+}
+
+void Engine::mark(const char* name) {
+  if (!sev[0]) {
+    for (int i = 0; i <= kMaxStages; i++) SHD_HIP(hipEventCreate(&sev[i]));
+  }
+  if (name == nullptr) {
+    SHD_HIP(hipEventRecord(sev[0], stream));
+    return;
+  }
+  if (n_stages >= kMaxStages) return;
+  stage_name[n_stages] = name;
+  SHD_HIP(hipEventRecord(sev[n_stages + 1], stream));
+  n_stages++;
+}
+
+void Engine::stage_end() {
+  if (n_stages == 0) return;
+  SHD_HIP(hipEventSynchronize(sev[n_stages]));
+  for (int i = 0; i < n_stages; i++) {
+    float ms = 0.f;
+    SHD_HIP(hipEventElapsedTime(&ms, sev[i], sev[i + 1]));
+    stage_ns[i] = (int64_t)((double)ms * 1e6);
+  }
+}
+
+Engine::~Engine() {
+  for (int i = 0; i <= kMaxStages; i++)
+    if (sev[i]) (void)hipEventDestroy(sev[i]);
+  if (ev0) (void)hipEventDestroy(ev0);
+  if (ev1) (void)hipEventDestroy(ev1);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+DFilters Engine::dfilters(const std::vector<int>& ids) const {
+  DFilters f{};
+  f.n = (int)ids.size();
+  if (f.n > 4) throw Error(SHD_E_UNSUPPORTED, "more than 4 filters on one state");
+  for (int i = 0; i < f.n; i++) f.f[i] = dexpr(ids[i]);
+  return f;
+}
+
+}  // namespace shd
+
+// ====================================================================== C-ABI
+using namespace shd;
+
+struct shd_ctx {
+  int device = 0;
+};
+
+struct shd_query {
+  shd_ctx* ctx = nullptr;
+  std::unique_ptr<Engine> eng;
+  // host staging for SHD_MEM_HOST batches
+  DevBuf stage_ts, stage_col[kMaxCols], stage_nul[kMaxCols];
+  // poll buffers (host)
+  std::vector<int64_t> h_chunk, h_ts;
+  std::vector<int32_t> h_type;
+  std::vector<uint64_t> h_vals;
+  std::vector<uint8_t> h_nulls;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (Error& e) {
+    return fail(e.code, e.what());
+  } catch (std::bad_alloc&) {
+    return fail(SHD_E_OOM, "host allocation failed");
+  } catch (std::exception& e) {
+    return fail(SHD_E_DEVICE, e.what());
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* shd_last_error(void) { return g_err.c_str(); }
+
+int shd_device_count(int* n) {
+  return guarded([&]() -> int {
+    if (!n) return fail(SHD_E_ARG, "null pointer");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+    return SHD_OK;
+  });
+}
+
+int shd_ctx_create(const int* device_ids, int n, shd_ctx** out) {
+  return guarded([&]() -> int {
+    if (!out) return fail(SHD_E_ARG, "null out");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(SHD_E_DEVICE, "no HIP device available");
+    auto* c = new shd_ctx();
+    c->device = (device_ids && n > 0) ? device_ids[0] : 0;
+    if (c->device < 0 || c->device >= count) {
+      delete c;
+      return fail(SHD_E_ARG, "bad device id");
+    }
+    SHD_HIP(hipSetDevice(c->device));
+    *out = c;
+    return SHD_OK;
+  });
+}
+
+int shd_ctx_destroy(shd_ctx* ctx) {
+  delete ctx;
+  return SHD_OK;
+}
+
+int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
+  return guarded([&]() -> int {
+    if (!ctx || !ir || !out || (len % 4) != 0) return fail(SHD_E_ARG, "bad arguments");
+    SHD_HIP(hipSetDevice(ctx->device));
+    Plan p = decode_plan((const int32_t*)ir, (int64_t)(len / 4));
+    std::string why1, why2;
+    std::unique_ptr<Engine> e;
+    if (p.kind == SHD_KIND_STATE) e = make_pattern_engine(p, why1);
+    else e = make_single_engine(p, why2);
+    if (!e) return fail(SHD_E_UNSUPPORTED, "plan outside the device path: " + why1 + why2);
+    e->plan = p;
+    e->ex.upload(p);
+    e->out.init((int)p.outputs.size());
+    SHD_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    SHD_HIP(hipEventCreate(&e->ev0));
+    SHD_HIP(hipEventCreate(&e->ev1));
+    e->reset();
+    auto* q = new shd_query();
+    q->ctx = ctx;
+    q->eng = std::move(e);
+    *out = q;
+    return SHD_OK;
+  });
+}
+
+int shd_plan_free(shd_query* q) {
+  if (q) {
+    if (q->eng && q->eng->stream) (void)hipStreamSynchronize(q->eng->stream);
+    delete q;
+  }
+  return SHD_OK;
+}
+
+int shd_plan_engine(shd_query* q, int* engine) {
+  if (!q || !engine) return fail(SHD_E_ARG, "null");
+  *engine = q->eng->kind();
+  return SHD_OK;
+}
+
+int shd_query_stream(shd_query* q, void** stream) {
+  if (!q || !stream) return fail(SHD_E_ARG, "null");
+  *stream = (void*)q->eng->stream;
+  return SHD_OK;
+}
+
+int shd_set_time(shd_query* q, int64_t ts) {
+  return guarded([&]() -> int {
+    if (!q) return fail(SHD_E_ARG, "null query");
+    q->eng->set_time(ts);
+    return SHD_OK;
+  });
+}
+
+int shd_push(shd_query* q, const shd_batch* b) {
+  return guarded([&]() -> int {
+    if (!q || !b) return fail(SHD_E_ARG, "null argument");
+    Engine& e = *q->eng;
+    if (b->stream < 0 || b->stream >= (int)e.plan.stream_types.size()) return fail(SHD_E_ARG, "bad stream index");
+    const auto& types = e.plan.stream_types[b->stream];
+    if (b->ncols != (int)types.size()) return fail(SHD_E_ARG, "column count does not match the stream schema");
+    if ((int)types.size() > kMaxCols) return fail(SHD_E_UNSUPPORTED, "too many attributes");
+    if (b->n < 0 || (b->n > 0 && (!b->ts || !b->cols))) return fail(SHD_E_ARG, "bad batch");
+    if (b->n == 0) return SHD_OK;
+    SHD_HIP(hipSetDevice(q->ctx->device));
+    Staged st;
+    st.stream = b->stream;
+    st.n = b->n;
+    st.advance_time = b->advance_time != 0;
+    if (b->ncalls > 0 && b->call_offsets) {
+      st.call_offsets.assign(b->call_offsets, b->call_offsets + b->ncalls + 1);
+      if (st.call_offsets.front() != 0 || st.call_offsets.back() != b->n) return fail(SHD_E_ARG, "bad call offsets");
+    } else {
+      st.call_offsets = {0, b->n};
+    }
+    st.cs.ncols = b->ncols;
+    if (b->mem == SHD_MEM_DEVICE) {
+      st.cs.ts = b->ts;
+      for (int c = 0; c < b->ncols; c++) {
+        st.cs.col[c] = b->cols[c];
+        st.cs.nul[c] = b->nulls ? b->nulls[c] : nullptr;
+        st.cs.type[c] = (int8_t)types[c];
+      }
+    } else {
+      hipStream_t s = e.stream;
+      q->stage_ts.reserve(b->n * 8);
+      SHD_HIP(hipMemcpyAsync(q->stage_ts.p, b->ts, b->n * 8, hipMemcpyHostToDevice, s));
+      st.cs.ts = q->stage_ts.as<int64_t>();
+      for (int c = 0; c < b->ncols; c++) {
+        size_t bytes = (size_t)b->n * type_size(types[c]);
+        q->stage_col[c].reserve(bytes);
+        SHD_HIP(hipMemcpyAsync(q->stage_col[c].p, b->cols[c], bytes, hipMemcpyHostToDevice, s));
+        st.cs.col[c] = q->stage_col[c].p;
+        st.cs.type[c] = (int8_t)types[c];
+        if (b->nulls && b->nulls[c]) {
+          q->stage_nul[c].reserve(b->n);
+          SHD_HIP(hipMemcpyAsync(q->stage_nul[c].p, b->nulls[c], b->n, hipMemcpyHostToDevice, s));
+          st.cs.nul[c] = q->stage_nul[c].as<uint8_t>();
+        } else {
+          st.cs.nul[c] = nullptr;
+        }
+      }
+    }
+    e.push(st);
+    return SHD_OK;
+  });
+}
+
+int shd_flush(shd_query* q) {
+  return guarded([&]() -> int {
+    if (!q) return fail(SHD_E_ARG, "null query");
+    SHD_HIP(hipStreamSynchronize(q->eng->stream));
+    return SHD_OK;
+  });
+}
+
+int shd_poll(shd_query* q, shd_out* out) {
+  return guarded([&]() -> int {
+    if (!q || !out) return fail(SHD_E_ARG, "null argument");
+    Engine& e = *q->eng;
+    hipStream_t s = e.stream;
+    int64_t n = e.out.count;
+    int nc = e.out.ncols;
+    q->h_chunk.resize(std::max<int64_t>(n, 1));
+    q->h_type.resize(std::max<int64_t>(n, 1));
+    q->h_ts.resize(std::max<int64_t>(n, 1));
+    q->h_vals.resize(std::max<int64_t>(n * nc, 1));
+    q->h_nulls.resize(std::max<int64_t>(n * nc, 1));
+    if (n > 0) {
+      SHD_HIP(hipMemcpyAsync(q->h_chunk.data(), e.out.chunk.p, n * 8, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(q->h_type.data(), e.out.type.p, n * 4, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(q->h_ts.data(), e.out.ts.p, n * 8, hipMemcpyDeviceToHost, s));
+      if (nc > 0) {
+        SHD_HIP(hipMemcpyAsync(q->h_vals.data(), e.out.vals.p, n * nc * 8, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipMemcpyAsync(q->h_nulls.data(), e.out.nulls.p, n * nc, hipMemcpyDeviceToHost, s));
+      }
+    }
+    SHD_HIP(hipStreamSynchronize(s));
+    e.out.count = 0;
+    out->n_rows = n;
+    out->n_cols = nc;
+    out->chunk = q->h_chunk.data();
+    out->type = q->h_type.data();
+    out->ts = q->h_ts.data();
+    out->values = q->h_vals.data();
+    out->nulls = q->h_nulls.data();
+    return SHD_OK;
+  });
+}
+
+int shd_discard_output(shd_query* q) {
+  if (!q) return fail(SHD_E_ARG, "null query");
+  q->eng->out.count = 0;
+  return SHD_OK;
+}
+
+int shd_reset(shd_query* q) {
+  return guarded([&]() -> int {
+    if (!q) return fail(SHD_E_ARG, "null query");
+    SHD_HIP(hipStreamSynchronize(q->eng->stream));
+    q->eng->reset();
+    return SHD_OK;
+  });
+}
+
+int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int* n) {
+  if (!q || !n) return fail(SHD_E_ARG, "null argument");
+  Engine& e = *q->eng;
+  int k = std::min(e.n_stages, max);
+  for (int i = 0; i < k; i++) {
+    if (ns) ns[i] = e.stage_ns[i];
+    if (names) names[i] = e.stage_name[i];
+  }
+  *n = k;
+  return SHD_OK;
+}
+
+int shd_get_counters(shd_query* q, shd_counters* c) {
+  if (!q || !c) return fail(SHD_E_ARG, "null argument");
+  *c = q->eng->counters;
+  return SHD_OK;
+}
+
+}  // extern "C"

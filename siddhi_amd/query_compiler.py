@@ -36,6 +36,10 @@ class SiddhiParserException(Exception):
     """Mirrors io.siddhi.query.compiler.exception.SiddhiParserException."""
 
 
+class OutOfScopeSyntax(SiddhiParserException):
+    """Valid SiddhiQL that the hot-path compiler does not cover."""
+
+
 # --------------------------------------------------------------------------- AST
 @dataclass
 class Const:
@@ -406,7 +410,7 @@ class Parser:
         while True:
             e = self.expression()
             if self.at_kw("as"):
-                raise SiddhiParserException("range partitions are out of scope")
+                raise OutOfScopeSyntax("range partitions are out of scope")
             self.expect("of")
             sid = self.name()
             withs.append((e, sid))
@@ -437,7 +441,7 @@ class Parser:
             sel = Selector(True, [])
         rate = None
         if self.at_kw("output"):
-            raise SiddhiParserException("output rate limiting is out of scope for the hot path")
+            raise OutOfScopeSyntax("output rate limiting is out of scope for the hot path")
         self.expect("insert")
         et = "current"
         if self.at_kw("all", "expired", "current", "events"):
@@ -532,7 +536,7 @@ class Parser:
             elif self.at("#") and self.peek(1).text == "[":
                 self.next()
             elif self.at("#"):
-                raise SiddhiParserException("stream functions are out of scope for the hot path")
+                raise OutOfScopeSyntax("stream functions are out of scope for the hot path")
             else:
                 break
         ref = None
@@ -616,7 +620,7 @@ class Parser:
 
     def basic_source(self):
         if self.accept("#"):
-            raise SiddhiParserException("partition-inner streams (#stream) are outside the hot path")
+            raise OutOfScopeSyntax("partition-inner streams (#stream) are outside the hot path")
         sid = self.name()
         filters = []
         while self.at("[") or (self.at("#") and self.peek(1).text == "["):
@@ -625,7 +629,7 @@ class Parser:
             filters.append(self.expression())
             self.expect("]")
         if self.at("#"):
-            raise SiddhiParserException("stream functions inside patterns are out of scope")
+            raise OutOfScopeSyntax("stream functions inside patterns are out of scope")
         return sid, filters
 
     # -- sequences (g4 every_sequence_source_chain)
@@ -677,7 +681,7 @@ class Parser:
         if self.accept("having"):
             sel.having = self.expression()
         if self.at_kw("order", "limit", "offset"):
-            raise SiddhiParserException("order by / limit / offset are out of scope for the hot path")
+            raise OutOfScopeSyntax("order by / limit / offset are out of scope for the hot path")
         return sel
 
     # -- expressions (g4 math_operation precedence)

@@ -1,0 +1,75 @@
+"""Seeded synthetic StockStream workloads of BASELINE.md / SURVEY.md §8d.
+
+    define stream StockStream (symbol string, price double, volume long);
+
+SplitMix64 (seed 20261015 + per-config offset); symbol uniform over K keys
+(dictionary ids 0..K-1, string "S%07d"); price = 50 + 50*U[0,1); volume
+uniform in [1, 1000]; ts = T0 + floor(i * delta) ms; InputHandler calls of
+1024 events.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 20261015
+T0 = 1_700_000_000_000
+STOCK_DEF = "define stream StockStream (symbol string, price double, volume long);"
+
+P1_QUERY = ("@info(name='q') from every e1=StockStream[price>70] -> "
+            "e2=StockStream[symbol==e1.symbol and price>e1.price*1.05] within 1 sec "
+            "select e1.symbol as symbol, e1.price as p1, e2.price as p2 insert into Alert;")
+
+P1_APP = "@app:playback " + STOCK_DEF + " " + P1_QUERY
+P3_APP = ("@app:playback " + STOCK_DEF + " partition with (symbol of StockStream) begin " + P1_QUERY + " end;")
+W2_LENGTH_APP = ("@app:playback " + STOCK_DEF + " @info(name='q') from StockStream[price>60]#window.length(1000) "
+                 "select symbol, avg(price) as a, sum(price) as s, count() as c group by symbol insert into O1;")
+W2_TIME_APP = ("@app:playback " + STOCK_DEF + " @info(name='q') from StockStream[price>60]#window.time(10 sec) "
+               "select symbol, avg(price) as a, sum(price) as s, count() as c group by symbol insert into O2;")
+
+CONFIGS = {
+    # name: (app, n_events, n_keys, delta_ms)
+    "P1": (P1_APP, 1_000_000, 1_000, 1.0),
+    "W2-length": (W2_LENGTH_APP, 100_000_000, 1_000, 0.1),
+    "W2-time": (W2_TIME_APP, 100_000_000, 1_000, 0.1),
+    "P3": (P3_APP, 100_000_000, 10_000_000, 0.01),
+    "P3-dense": (P3_APP, 100_000_000, 10_000_000, 1e-5),
+}
+
+
+def splitmix64(state: np.uint64, n: int) -> np.ndarray:
+    """n successive SplitMix64 outputs starting from `state` (vectorised)."""
+    with np.errstate(over="ignore"):
+        z = (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) + np.uint64(state)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def stock_stream(n: int, n_keys: int, delta_ms: float, seed_offset: int = 0, start: int = 0):
+    """Columns (symbol u32 ids, price f64, volume i64, ts i64) for events [start, start+n)."""
+    base = np.uint64(SEED + seed_offset)
+    with np.errstate(over="ignore"):
+        st = base + np.uint64(3 * start) * np.uint64(0x9E3779B97F4A7C15)
+    r = splitmix64(st, 3 * n).reshape(n, 3)
+    symbol = (r[:, 0] % np.uint64(n_keys)).astype(np.uint32)
+    price = 50.0 + 50.0 * ((r[:, 1] >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53)))
+    volume = (r[:, 2] % np.uint64(1000)).astype(np.int64) + 1
+    idx = np.arange(start, start + n, dtype=np.float64)
+    ts = (T0 + np.floor(idx * delta_ms)).astype(np.int64)
+    return symbol, price, volume, ts
+
+
+def call_offsets(n: int, call_size: int = 1024) -> np.ndarray:
+    offs = np.arange(0, n, call_size, dtype=np.int64)
+    return np.append(offs, np.int64(n))
+
+
+def symbol_name(i: int) -> str:
+    return "S%07d" % i
+
+
+def register_symbols(dictionary, n_keys: int):
+    """Make dictionary id i == symbol i (the generator's u32 ids)."""
+    for i in range(len(dictionary.strings), n_keys):
+        assert dictionary.id(symbol_name(i)) == i
