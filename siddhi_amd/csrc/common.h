@@ -31,7 +31,7 @@ struct Error : std::runtime_error {
 
 constexpr int kBlock = 256;
 constexpr int kMaxCols = 16;      // attributes per stream handled on device
-constexpr int kMaxStack = 16;     // expression stack depth
+constexpr int kMaxStack = 8;      // expression stack depth (validated at plan load)
 constexpr int kMaxAggs = 8;
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -30,6 +30,15 @@ __device__ __forceinline__ uint64_t p_f64(double d) { return (uint64_t)__double_
 // Typed column element -> 64-bit payload.
 __device__ __forceinline__ Val col_load(const ColSet& cs, int64_t row, int attr) {
   Val v;
+#ifdef SHD_DEBUG
+  if (attr < 0 || attr >= cs.ncols || row < 0 || cs.col[attr] == nullptr) {
+    printf("SHD_DEBUG col_load: attr %d ncols %d row %lld col %p\n", attr, cs.ncols, (long long)row,
+           attr >= 0 && attr < kMaxCols ? cs.col[attr] : nullptr);
+    v.b = 0;
+    v.null = 1;
+    return v;
+  }
+#endif
   const uint8_t* nm = cs.nul[attr];
   if (nm && nm[row]) {
     v.b = 0;
@@ -191,68 +200,101 @@ __device__ inline bool d_compare(int op, int t, uint64_t l, uint64_t r) {
 // Evaluate one expression. Ctx provides:
 //   Val load(int state, int idx, int attr) const;  bool evnull(int state, int idx) const;
 //   int64_t ts(int state, int idx) const;          Val agg(int i) const;
+// Value stack of the interpreter.  Slots live in named registers and are
+// addressed through unrolled selects (slot indices are wave-uniform), so the
+// evaluation never touches scratch memory: no dynamically indexed private
+// array exists for the compiler to spill or to speculate out of bounds.
+struct VStack {
+  uint64_t r[kMaxStack];
+  uint32_t nul;   // bit i = slot i is null
+  __device__ __forceinline__ uint64_t get(int i) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxStack; j++)
+      if (j == i) v = r[j];
+    return v;
+  }
+  __device__ __forceinline__ void set(int i, uint64_t v, int null) {
+#pragma unroll
+    for (int j = 0; j < kMaxStack; j++)
+      if (j == i) r[j] = v;
+    nul = null ? (nul | (1u << i)) : (nul & ~(1u << i));
+  }
+  __device__ __forceinline__ int isnull(int i) const { return (nul >> i) & 1u; }
+  __device__ __forceinline__ Val val(int i) const {
+    Val v;
+    v.b = get(i);
+    v.null = isnull(i);
+    return v;
+  }
+};
+
+// Evaluate one expression.  The host validated every expression of the plan
+// (stack depth <= kMaxStack, no underflow: shd_api.cpp decode_plan), so sp
+// stays inside [0, kMaxStack].
 template <class Ctx>
 __device__ inline Val eval_expr(const int4* code, int len, const uint64_t* consts, const Ctx& cx) {
-  Val st[kMaxStack];
+  VStack st;
+#pragma unroll
+  for (int j = 0; j < kMaxStack; j++) st.r[j] = 0;
+  st.nul = 0;
   int sp = 0;
   for (int k = 0; k < len; k++) {
-    int4 in = code[k];
+    const int4 in = code[k];
     switch (in.x) {
-      case SHD_OP_CONST: st[sp].b = consts[in.y]; st[sp].null = 0; sp++; break;
-      case SHD_OP_NULL: st[sp].b = 0; st[sp].null = 1; sp++; break;
-      case SHD_OP_LOAD: st[sp++] = cx.load(in.y, in.z, in.w & 0xFFFF); break;
-      case SHD_OP_EVNULL: st[sp].b = cx.evnull(in.y, in.z) ? 1 : 0; st[sp].null = 0; sp++; break;
-      case SHD_OP_TS: st[sp].b = (uint64_t)cx.ts(in.y, in.z); st[sp].null = 0; sp++; break;
+      case SHD_OP_CONST: st.set(sp++, consts[in.y], 0); break;
+      case SHD_OP_NULL: st.set(sp++, 0, 1); break;
+      case SHD_OP_LOAD: {
+        Val v = cx.load(in.y, in.z, in.w & 0xFFFF);
+        st.set(sp++, v.b, v.null);
+        break;
+      }
+      case SHD_OP_EVNULL: st.set(sp++, cx.evnull(in.y, in.z) ? 1 : 0, 0); break;
+      case SHD_OP_TS: st.set(sp++, (uint64_t)cx.ts(in.y, in.z), 0); break;
       case SHD_OP_CVT:
-        if (!st[sp - 1].null) st[sp - 1].b = d_cvt(st[sp - 1].b, in.y, in.z);
+        if (sp > 0 && !st.isnull(sp - 1)) st.set(sp - 1, d_cvt(st.get(sp - 1), in.y, in.z), 0);
         break;
       case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD: {
-        Val r = st[--sp];
-        Val l = st[--sp];
-        st[sp++] = d_arith(in.x, in.y, l, r);
+        if (sp < 2) break;
+        Val r = st.val(sp - 1);
+        Val l = st.val(sp - 2);
+        Val o = d_arith(in.x, in.y, l, r);
+        sp -= 2;
+        st.set(sp++, o.b, o.null);
         break;
       }
       case SHD_OP_EQ: case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE: {
-        Val r = st[--sp];
-        Val l = st[--sp];
-        st[sp].b = (!(l.null || r.null) && d_compare(in.x, in.y, l.b, r.b)) ? 1 : 0;
-        st[sp].null = 0;
-        sp++;
+        if (sp < 2) break;
+        Val r = st.val(sp - 1);
+        Val l = st.val(sp - 2);
+        sp -= 2;
+        st.set(sp++, (!(l.null || r.null) && d_compare(in.x, in.y, l.b, r.b)) ? 1 : 0, 0);
         break;
       }
-      case SHD_OP_AND: {
-        Val r = st[--sp];
-        Val l = st[--sp];
-        st[sp].b = ((!l.null && l.b) && (!r.null && r.b)) ? 1 : 0;
-        st[sp].null = 0;
-        sp++;
+      case SHD_OP_AND: case SHD_OP_OR: {
+        if (sp < 2) break;
+        Val r = st.val(sp - 1);
+        Val l = st.val(sp - 2);
+        bool lt = !l.null && l.b, rt = !r.null && r.b;
+        sp -= 2;
+        st.set(sp++, (in.x == SHD_OP_AND ? (lt && rt) : (lt || rt)) ? 1 : 0, 0);
         break;
       }
-      case SHD_OP_OR: {
-        Val r = st[--sp];
-        Val l = st[--sp];
-        st[sp].b = ((!l.null && l.b) || (!r.null && r.b)) ? 1 : 0;
-        st[sp].null = 0;
-        sp++;
+      case SHD_OP_NOT:
+        if (sp > 0) st.set(sp - 1, (!st.isnull(sp - 1) && st.get(sp - 1)) ? 0 : 1, 0);
+        break;
+      case SHD_OP_ISNULL:
+        if (sp > 0) st.set(sp - 1, st.isnull(sp - 1) ? 1 : 0, 0);
+        break;
+      case SHD_OP_AGG: {
+        Val v = cx.agg(in.y);
+        st.set(sp++, v.b, v.null);
         break;
       }
-      case SHD_OP_NOT: {
-        Val x = st[--sp];
-        st[sp].b = (!x.null && x.b) ? 0 : 1;
-        st[sp].null = 0;
-        sp++;
+      default:
         break;
-      }
-      case SHD_OP_ISNULL: {
-        Val x = st[--sp];
-        st[sp].b = x.null ? 1 : 0;
-        st[sp].null = 0;
-        sp++;
-        break;
-      }
-      case SHD_OP_AGG: st[sp++] = cx.agg(in.y); break;
-      default: break;
     }
+    if (sp > kMaxStack) sp = kMaxStack;
   }
   if (sp == 0) {
     Val z;
@@ -260,7 +302,7 @@ __device__ inline Val eval_expr(const int4* code, int len, const uint64_t* const
     z.null = 1;
     return z;
   }
-  return st[sp - 1];
+  return st.val(sp - 1);
 }
 
 template <class Ctx>

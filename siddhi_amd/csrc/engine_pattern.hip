@@ -103,18 +103,21 @@ struct PrepArgs {
 __global__ __launch_bounds__(kBlock) void k_prepare(PrepArgs a, int64_t n_ext, uint64_t* key, uint8_t* flags,
                                                     unsigned long long* n_new_cand) {
   uint64_t created = 0;
+  // kernel arguments live in the read-only kernarg segment: work on a private
+  // copy before taking addresses
+  const ExtRows x = a.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
-    if (r < a.x.C) {
+    if (r < x.C) {
       key[r] = a.partitioned ? a.carry_key[r] : 0;
       flags[r] = F_CAND;
       continue;
     }
-    PairCtx cx{&a.x, r, -1};
+    PairCtx cx{&x, r, -1};
     uint8_t f = F_NEW;
     uint64_t k = 0;
     if (a.partitioned) {
       Val kv;
-      if (a.key_col >= 0) kv = col_load(a.x.batch, r - a.x.C, a.key_col);
+      if (a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
       else kv = eval_expr(a.es.ins + a.key_expr.off, a.key_expr.len, a.es.consts, cx);
       if (kv.null) f |= F_SKIP;   // PartitionStreamReceiver drops null keys
       k = canon_key(kv, a.key_type);
@@ -152,13 +155,14 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(ScanArgs a, int64_t n_e
                                                          int32_t* match_j, uint8_t* status,
                                                          unsigned long long* steps_total, uint32_t* violation) {
   uint64_t steps = 0;
+  const ExtRows x = a.x;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_ext;
        p += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = perm ? (int64_t)perm[p] : p;
     uint8_t fr = flags[r];
     if (!(fr & F_CAND)) continue;
     uint64_t k = key[r];
-    int64_t tsi = a.x.ts(r);
+    int64_t tsi = x.ts(r);
     int64_t prev = tsi;
     uint8_t st = ST_OPEN;
     int32_t j = -1;
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(ScanArgs a, int64_t n_e
       if (a.partitioned && key[r2] != k) break;
       uint8_t f2 = flags[r2];
       if (!(f2 & F_NEW) || (f2 & F_SKIP)) continue;
-      int64_t t2 = a.x.ts(r2);
+      int64_t t2 = x.ts(r2);
       if (t2 < prev) {
         atomicOr(violation, 1u);
         break;
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(ScanArgs a, int64_t n_e
         break;
       }
       if (f2 & F_B) {
-        PairCtx cx{&a.x, r, r2};
+        PairCtx cx{&x, r, r2};
         if (eval_filters(a.es, a.f2, cx)) {
           st = ST_MATCH;
           j = (int32_t)r2;
@@ -230,18 +234,19 @@ struct ProjArgs {
 __global__ __launch_bounds__(kBlock) void k_project(ProjArgs a, const uint32_t* pj, const uint32_t* pi, int64_t m,
                                                     int64_t* o_chunk, int32_t* o_type, int64_t* o_ts,
                                                     uint64_t* o_vals, uint8_t* o_nul) {
+  const ExtRows x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t j = pj[k], i = pi[k];
-    PairCtx cx{&a.x, i, j};
+    PairCtx cx{&x, i, j};
     int64_t row = a.row0 + k;
     for (int c = 0; c < a.nout; c++) {
       Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
-    o_ts[row] = a.x.ts(j);
+    o_ts[row] = x.ts(j);
     o_type[row] = 0;
-    o_chunk[row] = a.multi ? a.x.seq(j) : a.chunk0 + k;
+    o_chunk[row] = a.multi ? x.seq(j) : a.chunk0 + k;
   }
 }
 
@@ -257,11 +262,12 @@ struct GatherArgs {
 };
 
 __global__ void k_gather_carry(GatherArgs a, const uint32_t* co, const uint32_t* oo, const uint64_t* key, int64_t n) {
+  const ExtRows x = a.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     if (!co[r]) continue;
     int64_t o = oo[r];
-    const ColSet& cs = a.x.cs(r);
-    int64_t row = a.x.row(r);
+    const ColSet& cs = x.cs(r);
+    int64_t row = x.row(r);
     for (int c = 0; c < a.ncols; c++) {
       Val v = col_load(cs, row, c);
       switch (a.types[c]) {
@@ -271,9 +277,9 @@ __global__ void k_gather_carry(GatherArgs a, const uint32_t* co, const uint32_t*
       }
       a.dnul[c][o] = (uint8_t)v.null;
     }
-    a.dts[o] = a.x.ts(r);
+    a.dts[o] = x.ts(r);
     a.dkey[o] = key[r];
-    a.dseq[o] = a.x.seq(r);
+    a.dseq[o] = x.seq(r);
   }
 }
 

@@ -107,12 +107,13 @@ struct FilterArgs {
 // flags: bit0 = passes filters, bit1 = has a (non-null) partition key
 __global__ __launch_bounds__(kBlock) void k_filter(FilterArgs a, int64_t n, uint8_t* flags, uint32_t* cnt,
                                                    uint64_t* pkey) {
+  const ColSet cs = a.cs;   // private copy (kernarg segment is read-only)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    RowCtx cx{&cs, i, nullptr, nullptr};
     uint8_t f = 0;
     bool keyed = true;
     if (a.partitioned) {
-      Val kv = a.key_col >= 0 ? col_load(a.cs, i, a.key_col)
+      Val kv = a.key_col >= 0 ? col_load(cs, i, a.key_col)
                               : eval_expr(a.es.ins + a.key.off, a.key.len, a.es.consts, cx);
       keyed = !kv.null;
       pkey[i] = canon_key(kv, a.key_type);
@@ -157,16 +158,17 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(ProjArgs a, int64_t n, 
                                                          const uint32_t* run_excl, const uint32_t* run_start,
                                                          int64_t* o_chunk, int32_t* o_type,
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+  const ColSet cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
     int64_t row = a.row0 + off[i];
-    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    RowCtx cx{&cs, i, nullptr, nullptr};
     for (int c = 0; c < a.nout; c++) {
       Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
-    o_ts[row] = a.cs.ts[i];
+    o_ts[row] = cs.ts[i];
     o_type[row] = 0;
     // run of event i = inclusive start count - 1
     o_chunk[row] = a.chunk0 + (a.partitioned ? (int64_t)run_excl[i] + run_start[i] - 1 : (int64_t)call_of[i]);
@@ -193,19 +195,20 @@ __global__ __launch_bounds__(kBlock) void k_make_items(ItemArgs a, int64_t n, co
                                                        uint64_t* ikey, int64_t* its, uint64_t* iargv, uint8_t* iargn,
                                                        int32_t* ievrow, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
+  const ColSet cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
     int64_t t = a.C + off[i];
-    RowCtx cx{&a.cs, i, nullptr, nullptr};
+    RowCtx cx{&cs, i, nullptr, nullptr};
     uint64_t k = 0;
     if (a.ngroup) {
-      Val kv = a.group_col >= 0 ? col_load(a.cs, i, a.group_col)
+      Val kv = a.group_col >= 0 ? col_load(cs, i, a.group_col)
                                 : eval_expr(a.es.ins + a.group.off, a.group.len, a.es.consts, cx);
       if (kv.null) atomicOr(null_key_flag, 1u);
       k = kv.null ? 0 : canon_key(kv, a.group_type);
     }
     ikey[t] = k;
-    its[t] = a.cs.ts[i];
+    its[t] = cs.ts[i];
     for (int g = 0; g < a.nagg; g++) {
       Val v;
       v.b = 0;
@@ -475,6 +478,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(EmitArgs a, int64_t nnew, const
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
                                                  const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
                                                  int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+  const ColSet cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
     if (!fcnt[t0]) continue;
     int64_t tf = a.C + t0;
@@ -486,14 +490,14 @@ __global__ __launch_bounds__(kBlock) void k_emit(EmitArgs a, int64_t nnew, const
       av[g] = resv[g * a.cap + tl];
       an[g] = resn[g * a.cap + tl];
     }
-    RowCtx cx{&a.cs, ev, av, an};
+    RowCtx cx{&cs, ev, av, an};
     int64_t row = a.row0 + foff[t0];
     for (int c = 0; c < a.nout; c++) {
       Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
-    o_ts[row] = a.cs.ts[ev];
+    o_ts[row] = cs.ts[ev];
     o_type[row] = 0;
     o_chunk[row] = a.chunk0 + call_of[ev];
   }
