@@ -10,6 +10,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 rc=$?
 echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if grep -qE "illegal memory access|APERTURE_VIOLATION|HSA_STATUS_ERROR" gpurun_out/pytest_gpu.log; then echo "GPU fault seen: stopping"; exit 3; fi
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 if [ $rc -ne 0 ]; then exit $rc; fi

@@ -53,7 +53,8 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    // a kernel still queued on a query stream may hold the old pointer
+    if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }
     p = nullptr;
     cap = 0;
   }
@@ -74,7 +75,7 @@ struct PinnedBuf {
   ~PinnedBuf() { if (p) (void)hipHostFree(p); }
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
-    if (p) (void)hipHostFree(p);
+    if (p) { (void)hipDeviceSynchronize(); (void)hipHostFree(p); }
     p = nullptr;
     size_t b = bytes < 256 ? 256 : bytes;
     SHD_HIP(hipHostMalloc(&p, b, hipHostMallocDefault));
@@ -137,6 +138,7 @@ struct ColSet {
   int8_t type[kMaxCols];
   int32_t ncols;
   const int64_t* ts;
+  int64_t n;        // rows (bounds checks in SHD_DEBUG builds)
 };
 
 inline int type_size(int t) {

@@ -31,14 +31,21 @@ __device__ __forceinline__ uint64_t p_f64(double d) { return (uint64_t)__double_
 __device__ __forceinline__ Val col_load(const ColSet& cs, int64_t row, int attr) {
   Val v;
 #ifdef SHD_DEBUG
-  if (attr < 0 || attr >= cs.ncols || row < 0 || cs.col[attr] == nullptr) {
-    printf("SHD_DEBUG col_load: attr %d ncols %d row %lld col %p\n", attr, cs.ncols, (long long)row,
+  if (attr < 0 || attr >= cs.ncols || row < 0 || row >= cs.n || cs.col[attr] == nullptr ||
+      ((uintptr_t)cs.col[attr] >> 47) != 0 || ((uintptr_t)cs.nul[attr] >> 47) != 0) {
+    printf("SHD_DEBUG col_load: attr %d ncols %d row %lld n %lld col %p\n", attr, cs.ncols, (long long)row,
+           (long long)cs.n,
            attr >= 0 && attr < kMaxCols ? cs.col[attr] : nullptr);
     v.b = 0;
     v.null = 1;
     return v;
   }
 #endif
+  if ((unsigned)attr >= (unsigned)cs.ncols) {   // plan validated at load; never index past the column table
+    v.b = 0;
+    v.null = 1;
+    return v;
+  }
   const uint8_t* nm = cs.nul[attr];
   if (nm && nm[row]) {
     v.b = 0;

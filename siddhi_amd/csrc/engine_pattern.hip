@@ -22,6 +22,8 @@
 // open partials carry to the next push.  A per-key timestamp decrease is
 // detected on device and rejected (SHD_E_UNSUPPORTED), never approximated.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "engine.h"
 
@@ -42,7 +44,15 @@ struct ExtRows {
   const int64_t* carry_seq;
   __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : batch; }
   __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : r - C; }
-  __device__ __forceinline__ int64_t ts(int64_t r) const { return r < C ? carry.ts[r] : batch.ts[r - C]; }
+  __device__ __forceinline__ int64_t ts(int64_t r) const {
+#ifdef SHD_DEBUG
+    if (r < 0 || r >= C + batch.n) {
+      printf("SHD_DEBUG ExtRows.ts: row %lld C %lld n %lld\n", (long long)r, (long long)C, (long long)batch.n);
+      return 0;
+    }
+#endif
+    return r < C ? carry.ts[r] : batch.ts[r - C];
+  }
   __device__ __forceinline__ int64_t seq(int64_t r) const { return r < C ? carry_seq[r] : seq0 + (r - C); }
 };
 
@@ -134,6 +144,31 @@ __global__ __launch_bounds__(kBlock) void k_prepare(PrepArgs a, int64_t n_ext, u
   }
   for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
   if ((threadIdx.x & 63) == 0 && created) atomicAdd(n_new_cand, (unsigned long long)created);
+}
+
+
+// Diagnostic (SHD_PROBE env): print the kernel's view of its arguments without
+// dereferencing any column pointer (stage 1), then the bytecode (stage 2).
+__global__ void k_probe(PrepArgs a, int64_t n_ext, int stage) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (stage == 1) {
+    printf("probe dev: n_ext %lld C %lld ncols %d ts %p is_a %d is_b %d part %d key_col %d f1.n %d ins %p consts %p\n",
+           (long long)n_ext, (long long)a.x.C, a.x.batch.ncols, (const void*)a.x.batch.ts, a.is_a, a.is_b,
+           a.partitioned, a.key_col, a.f1.n, (const void*)a.es.ins, (const void*)a.es.consts);
+    for (int c = 0; c < a.x.batch.ncols && c < kMaxCols; c++)
+      printf("probe dev: col %d %p nul %p type %d\n", c, a.x.batch.col[c], (const void*)a.x.batch.nul[c],
+             (int)a.x.batch.type[c]);
+    for (int i = 0; i < a.f1.n && i < 4; i++) printf("probe dev: f1[%d] off %d len %d\n", i, a.f1.f[i].off, a.f1.f[i].len);
+  } else {
+    auto sane = [](const void* q) { return q != nullptr && ((uintptr_t)q >> 47) == 0; };
+    if (!sane(a.es.ins) || !sane(a.x.batch.ts)) { printf("probe dev: insane pointer, skipping loads\n"); return; }
+    for (int i = 0; i < a.f1.n && i < 4; i++)
+      for (int k = 0; k < a.f1.f[i].len && k < 16; k++) {
+        int4 in = a.es.ins[a.f1.f[i].off + k];
+        printf("probe dev: f1[%d][%d] op %d a %d b %d c %d\n", i, k, in.x, in.y, in.z, in.w);
+      }
+    if (n_ext > a.x.C) printf("probe dev: ts[0] %lld\n", (long long)a.x.batch.ts[0]);
+  }
 }
 
 __global__ void k_narrow_keys(const uint64_t* in, uint32_t* out, int64_t n) {
@@ -358,7 +393,11 @@ struct PatternEngine : Engine {
     counters = shd_counters{};
   }
 
-  ColSet carry_cs() const { return carry[cur].colset(typesA); }
+  ColSet carry_cs() const {
+    ColSet cs = carry[cur].colset(typesA);
+    cs.n = C;
+    return cs;
+  }
 
   void push(const Staged& b) override {
     if (b.advance_time) {
@@ -409,6 +448,21 @@ struct PatternEngine : Engine {
     }
     pa.carry_key = carry[cur].key.as<uint64_t>();
     SHD_HIP(hipMemsetAsync(d_tot.p, 0, 64, s));
+    if (const char* pr = std::getenv("SHD_PROBE")) {
+      fprintf(stderr, "probe host: n_ext %lld C %lld ncols %d ts %p is_a %d f1.n %d ins %p consts %p sizeof(PrepArgs) %zu\n",
+              (long long)n_ext, (long long)pa.x.C, pa.x.batch.ncols, (const void*)pa.x.batch.ts, pa.is_a, pa.f1.n,
+              (const void*)pa.es.ins, (const void*)pa.es.consts, sizeof(PrepArgs));
+      for (int c = 0; c < pa.x.batch.ncols; c++)
+        fprintf(stderr, "probe host: col %d %p nul %p type %d\n", c, pa.x.batch.col[c], (const void*)pa.x.batch.nul[c],
+                (int)pa.x.batch.type[c]);
+      SHD_HIP(hipStreamSynchronize(s));
+      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, pa, n_ext, 1);
+      SHD_HIP(hipStreamSynchronize(s));
+      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, pa, n_ext, 2);
+      SHD_HIP(hipStreamSynchronize(s));
+      fflush(stdout);
+      if (pr[0] != 'r') throw Error(SHD_E_UNSUPPORTED, "SHD_PROBE: stopped before k_prepare");
+    }
     hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, pa, n_ext, d_key.as<uint64_t>(),
                        d_flags.as<uint8_t>(), (unsigned long long*)(d_tot.as<uint64_t>() + 6));
     SHD_CHECK_LAUNCH();

@@ -546,13 +546,14 @@ struct SingleEngine : Engine {
     out.count = 0;
     counters = shd_counters{};
     if (g_nkeys) {
-      SHD_HIP(hipMemset(g_dsum.p, 0, g_dsum.cap));
-      SHD_HIP(hipMemset(g_lsum.p, 0, g_lsum.cap));
-      SHD_HIP(hipMemset(g_cnt.p, 0, g_cnt.cap));
+      SHD_HIP(hipMemsetAsync(g_dsum.p, 0, g_dsum.cap, stream));
+      SHD_HIP(hipMemsetAsync(g_lsum.p, 0, g_lsum.cap, stream));
+      SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
   }
 
   std::vector<int64_t> h_offs;   // lives until the next push (async H2D source)
+  PinnedBuf h_last, h_offs_pin;
 
   void stage_calls(const Staged& b, int64_t& ncalls) {
     h_offs = b.call_offsets;
@@ -560,7 +561,10 @@ struct SingleEngine : Engine {
     std::vector<int64_t>& offs = h_offs;
     ncalls = (int64_t)offs.size() - 1;
     d_offs.reserve(offs.size() * 8);
-    SHD_HIP(hipMemcpyAsync(d_offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, stream));
+    // pinned source: the previous push ended with a stream sync, so the area is free
+    h_offs_pin.reserve(offs.size() * 8);
+    std::memcpy(h_offs_pin.p, offs.data(), offs.size() * 8);
+    SHD_HIP(hipMemcpyAsync(d_offs.p, h_offs_pin.p, offs.size() * 8, hipMemcpyHostToDevice, stream));
     d_call_of.reserve(b.n * 4);
     d_last_ts.reserve(ncalls * 8);
     d_now.reserve(ncalls * 8);
@@ -615,7 +619,10 @@ struct SingleEngine : Engine {
     // TimestampGeneratorImpl: time moves to the last call's ts if later
     if (b.advance_time || true) {
       int64_t last = 0;
-      SHD_HIP(hipMemcpy(&last, d_now.as<int64_t>() + (ncalls - 1), 8, hipMemcpyDeviceToHost));
+      h_last.reserve(8);
+      SHD_HIP(hipMemcpyAsync(h_last.p, d_now.as<int64_t>() + (ncalls - 1), 8, hipMemcpyDeviceToHost, stream));
+      SHD_HIP(hipStreamSynchronize(stream));
+      last = *h_last.as<int64_t>();
       if (last > now) now = last;
     }
     seq += n;

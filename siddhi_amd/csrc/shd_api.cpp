@@ -212,6 +212,10 @@ void DevExprTable::upload(const Plan& p) {
   consts.reserve(std::max<size_t>(p.consts.size(), 1) * 8);
   if (!all.empty()) SHD_HIP(hipMemcpy(ins.p, all.data(), all.size() * sizeof(int4), hipMemcpyHostToDevice));
   if (!p.consts.empty()) SHD_HIP(hipMemcpy(consts.p, p.consts.data(), p.consts.size() * 8, hipMemcpyHostToDevice));
+  // hipMemcpy from pageable memory may return before the DMA lands, and the
+  // engines run on non-blocking streams that do not order after the null
+  // stream: wait here so no kernel can read a half-written program.
+  SHD_HIP(hipDeviceSynchronize());
 }
 
 void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
@@ -295,6 +299,7 @@ struct shd_query {
   std::unique_ptr<Engine> eng;
   // host staging for SHD_MEM_HOST batches
   DevBuf stage_ts, stage_col[kMaxCols], stage_nul[kMaxCols];
+  PinnedBuf pin;   // host staging for SHD_MEM_HOST batches
   // poll buffers (host)
   std::vector<int64_t> h_chunk, h_ts;
   std::vector<int32_t> h_type;
@@ -435,6 +440,7 @@ int shd_push(shd_query* q, const shd_batch* b) {
       st.call_offsets = {0, b->n};
     }
     st.cs.ncols = b->ncols;
+    st.cs.n = b->n;
     if (b->mem == SHD_MEM_DEVICE) {
       st.cs.ts = b->ts;
       for (int c = 0; c < b->ncols; c++) {
@@ -443,20 +449,34 @@ int shd_push(shd_query* q, const shd_batch* b) {
         st.cs.type[c] = (int8_t)types[c];
       }
     } else {
+      // Host batches: copy into library-owned pinned memory (the caller's
+      // buffers may be pageable and are only valid until we return), then
+      // H2D on the query's stream.  The previous push's copies must have
+      // drained before the pinned area is reused.
       hipStream_t s = e.stream;
-      q->stage_ts.reserve(b->n * 8);
-      SHD_HIP(hipMemcpyAsync(q->stage_ts.p, b->ts, b->n * 8, hipMemcpyHostToDevice, s));
-      st.cs.ts = q->stage_ts.as<int64_t>();
+      SHD_HIP(hipStreamSynchronize(s));
+      size_t total = (size_t)b->n * 8;
+      for (int c = 0; c < b->ncols; c++) {
+        total += (size_t)b->n * type_size(types[c]) + 64;
+        if (b->nulls && b->nulls[c]) total += (size_t)b->n + 64;
+      }
+      q->pin.reserve(total + 64);
+      char* hp = q->pin.as<char>();
+      size_t used = 0;
+      auto stage = [&](DevBuf& dst, const void* src, size_t bytes) -> void* {
+        dst.reserve(bytes);
+        std::memcpy(hp + used, src, bytes);
+        SHD_HIP(hipMemcpyAsync(dst.p, hp + used, bytes, hipMemcpyHostToDevice, s));
+        used += (bytes + 63) & ~size_t(63);
+        return dst.p;
+      };
+      st.cs.ts = (const int64_t*)stage(q->stage_ts, b->ts, (size_t)b->n * 8);
       for (int c = 0; c < b->ncols; c++) {
         size_t bytes = (size_t)b->n * type_size(types[c]);
-        q->stage_col[c].reserve(bytes);
-        SHD_HIP(hipMemcpyAsync(q->stage_col[c].p, b->cols[c], bytes, hipMemcpyHostToDevice, s));
-        st.cs.col[c] = q->stage_col[c].p;
+        st.cs.col[c] = stage(q->stage_col[c], b->cols[c], bytes);
         st.cs.type[c] = (int8_t)types[c];
         if (b->nulls && b->nulls[c]) {
-          q->stage_nul[c].reserve(b->n);
-          SHD_HIP(hipMemcpyAsync(q->stage_nul[c].p, b->nulls[c], b->n, hipMemcpyHostToDevice, s));
-          st.cs.nul[c] = q->stage_nul[c].as<uint8_t>();
+          st.cs.nul[c] = (const uint8_t*)stage(q->stage_nul[c], b->nulls[c], (size_t)b->n);
         } else {
           st.cs.nul[c] = nullptr;
         }
