@@ -62,6 +62,33 @@ struct Engine {
   }
   virtual void reset() = 0;
 
+  // Kernel argument blocks (column tables, expression handles) are placed in
+  // device memory and kernels receive a pointer: the kernels index column
+  // tables with lane-dependent values, and vector loads from the kernarg
+  // segment fault on the MI355X boxes (HSA aperture violation, see DESIGN.md
+  // "kernel arguments").  Bump arena, reset at the start of each push.
+  static constexpr size_t kArgArena = size_t(1) << 20;
+  DevBuf arg_dev;
+  PinnedBuf arg_host;
+  size_t arg_used = 0;
+  void args_begin() {
+    if (!arg_dev.p) {
+      arg_dev.reserve(kArgArena);
+      arg_host.reserve(kArgArena);
+    }
+    SHD_HIP(hipStreamSynchronize(stream));   // previous push's argument copies have landed
+    arg_used = 0;
+  }
+  template <class T> const T* dev_args(const T& a) {
+    size_t off = (arg_used + 255) & ~size_t(255);
+    if (!arg_dev.p || off + sizeof(T) > kArgArena) throw Error(SHD_E_CAPACITY, "kernel argument arena exhausted");
+    std::memcpy(arg_host.as<char>() + off, &a, sizeof(T));
+    SHD_HIP(hipMemcpyAsync(arg_dev.as<char>() + off, arg_host.as<char>() + off, sizeof(T), hipMemcpyHostToDevice,
+                           stream));
+    arg_used = off + sizeof(T);
+    return reinterpret_cast<const T*>(arg_dev.as<char>() + off);
+  }
+
   DExpr dexpr(int e) const { return DExpr{ex.off[e], ex.len[e]}; }
   DExprSet dset() const { return DExprSet{ex.ins.as<int4>(), ex.consts.as<uint64_t>()}; }
   DFilters dfilters(const std::vector<int>& ids) const;

@@ -110,12 +110,13 @@ struct PrepArgs {
 };
 
 // Per extended row: key, flags (candidate / new / B / skip).
-__global__ __launch_bounds__(kBlock) void k_prepare(PrepArgs a, int64_t n_ext, uint64_t* key, uint8_t* flags,
+__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, uint64_t* key, uint8_t* flags,
                                                     unsigned long long* n_new_cand) {
+  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   uint64_t created = 0;
   // kernel arguments live in the read-only kernarg segment: work on a private
   // copy before taking addresses
-  const ExtRows x = a.x;
+  const ExtRows& x = a.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
     if (r < x.C) {
       key[r] = a.partitioned ? a.carry_key[r] : 0;
@@ -147,9 +148,55 @@ __global__ __launch_bounds__(kBlock) void k_prepare(PrepArgs a, int64_t n_ext, u
 }
 
 
+// ---- fault bisection variants (SHD_PROBE=variants): same loop as k_prepare
+// with progressively more of the expression machinery switched on.
+struct ConstCtx {
+  __device__ __forceinline__ Val load(int, int, int) const { Val v; v.b = 0x42c80000u; v.null = 0; return v; }
+  __device__ __forceinline__ bool evnull(int, int) const { return false; }
+  __device__ __forceinline__ int64_t ts(int, int) const { return 0; }
+  __device__ __forceinline__ Val agg(int) const { Val v; v.b = 0; v.null = 1; return v; }
+};
+struct RawCtx {
+  const ExtRows* x;
+  int64_t r1;
+  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
+    Val v; v.b = 0; v.null = 1;
+    if (st != 0 || (unsigned)attr >= (unsigned)x->batch.ncols) return v;
+    v.null = 0;
+    v.b = ((const uint32_t*)x->batch.col[attr])[r1 - x->C];
+    return v;
+  }
+  __device__ __forceinline__ bool evnull(int, int) const { return false; }
+  __device__ __forceinline__ int64_t ts(int, int) const { return 0; }
+  __device__ __forceinline__ Val agg(int) const { Val v; v.b = 0; v.null = 1; return v; }
+};
+template <int V>
+__global__ __launch_bounds__(kBlock) void k_prepare_v(const PrepArgs* __restrict__ ap, int64_t n_ext, uint64_t* key, uint8_t* flags,
+                                                      unsigned long long* n_new_cand) {
+  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  uint64_t created = 0;
+  const ExtRows& x = a.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
+    if (r < x.C) { key[r] = 0; flags[r] = F_CAND; continue; }
+    uint8_t f = F_NEW;
+    bool pass = false;
+    if (V == 0) pass = a.is_a;
+    if (V == 1) { ConstCtx c; pass = a.is_a && eval_filters(a.es, a.f1, c); }
+    if (V == 2) { RawCtx c{&x, r}; pass = a.is_a && eval_filters(a.es, a.f1, c); }
+    if (V == 3) { PairCtx c{&x, r, -1}; pass = a.is_a && eval_filters(a.es, a.f1, c); }
+    if (V == 4) { PairCtx c{&x, r, -1}; Val v = c.load(0, -1, 1); pass = a.is_a && !v.null && v.b != 0; }
+    if (pass) { f |= F_CAND; created++; }
+    key[r] = 0;
+    flags[r] = f;
+  }
+  for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
+  if ((threadIdx.x & 63) == 0 && created) atomicAdd(n_new_cand, (unsigned long long)created);
+}
+
 // Diagnostic (SHD_PROBE env): print the kernel's view of its arguments without
 // dereferencing any column pointer (stage 1), then the bytecode (stage 2).
-__global__ void k_probe(PrepArgs a, int64_t n_ext, int stage) {
+__global__ void k_probe(const PrepArgs* __restrict__ ap, int64_t n_ext, int stage) {
+  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (stage == 1) {
     printf("probe dev: n_ext %lld C %lld ncols %d ts %p is_a %d is_b %d part %d key_col %d f1.n %d ins %p consts %p\n",
@@ -185,12 +232,13 @@ struct ScanArgs {
 };
 
 // One lane per candidate partial: forward walk over the later events of its key.
-__global__ __launch_bounds__(kBlock) void k_forward_scan(ScanArgs a, int64_t n_ext, const uint32_t* perm,
+__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext, const uint32_t* perm,
                                                          const uint64_t* key, const uint8_t* flags,
                                                          int32_t* match_j, uint8_t* status,
                                                          unsigned long long* steps_total, uint32_t* violation) {
+  const ScanArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   uint64_t steps = 0;
-  const ExtRows x = a.x;
+  const ExtRows& x = a.x;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_ext;
        p += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = perm ? (int64_t)perm[p] : p;
@@ -266,10 +314,11 @@ struct ProjArgs {
   int64_t row0;         // output buffer offset
 };
 
-__global__ __launch_bounds__(kBlock) void k_project(ProjArgs a, const uint32_t* pj, const uint32_t* pi, int64_t m,
+__global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj, const uint32_t* pi, int64_t m,
                                                     int64_t* o_chunk, int32_t* o_type, int64_t* o_ts,
                                                     uint64_t* o_vals, uint8_t* o_nul) {
-  const ExtRows x = a.x;
+  const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ExtRows& x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t j = pj[k], i = pi[k];
     PairCtx cx{&x, i, j};
@@ -296,8 +345,9 @@ struct GatherArgs {
   int64_t* dseq;
 };
 
-__global__ void k_gather_carry(GatherArgs a, const uint32_t* co, const uint32_t* oo, const uint64_t* key, int64_t n) {
-  const ExtRows x = a.x;
+__global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t* co, const uint32_t* oo, const uint64_t* key, int64_t n) {
+  const GatherArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ExtRows& x = a.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     if (!co[r]) continue;
     int64_t o = oo[r];
@@ -456,14 +506,33 @@ struct PatternEngine : Engine {
         fprintf(stderr, "probe host: col %d %p nul %p type %d\n", c, pa.x.batch.col[c], (const void*)pa.x.batch.nul[c],
                 (int)pa.x.batch.type[c]);
       SHD_HIP(hipStreamSynchronize(s));
-      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, pa, n_ext, 1);
+      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, dev_args(pa), n_ext, 1);
       SHD_HIP(hipStreamSynchronize(s));
-      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, pa, n_ext, 2);
+      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, dev_args(pa), n_ext, 2);
       SHD_HIP(hipStreamSynchronize(s));
       fflush(stdout);
+      if (pr[0] == 'v') {
+        auto chk = [&](int v) {
+          SHD_HIP(hipStreamSynchronize(s));
+          fprintf(stderr, "probe: variant %d ok\n", v);
+          fflush(stderr);
+        };
+        unsigned long long* nc = (unsigned long long*)(d_tot.as<uint64_t>() + 6);
+        hipLaunchKernelGGL(k_prepare_v<0>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
+        chk(0);
+        hipLaunchKernelGGL(k_prepare_v<1>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
+        chk(1);
+        hipLaunchKernelGGL(k_prepare_v<2>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
+        chk(2);
+        hipLaunchKernelGGL(k_prepare_v<4>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
+        chk(4);
+        hipLaunchKernelGGL(k_prepare_v<3>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
+        chk(3);
+        throw Error(SHD_E_UNSUPPORTED, "SHD_PROBE: variants done");
+      }
       if (pr[0] != 'r') throw Error(SHD_E_UNSUPPORTED, "SHD_PROBE: stopped before k_prepare");
     }
-    hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, pa, n_ext, d_key.as<uint64_t>(),
+    hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(),
                        d_flags.as<uint8_t>(), (unsigned long long*)(d_tot.as<uint64_t>() + 6));
     SHD_CHECK_LAUNCH();
     mark("prepare");
@@ -513,7 +582,7 @@ struct PatternEngine : Engine {
     sa.partitioned = partitioned;
     unsigned long long* d_steps = (unsigned long long*)d_tot.as<uint64_t>();
     uint32_t* d_viol = (uint32_t*)(d_tot.as<uint64_t>() + 1);
-    hipLaunchKernelGGL(k_forward_scan, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, sa, n_ext, perm,
+    hipLaunchKernelGGL(k_forward_scan, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, perm,
                        (const uint64_t*)d_key.as<uint64_t>(), (const uint8_t*)d_flags.as<uint8_t>(),
                        d_match.as<int32_t>(), d_status.as<uint8_t>(), d_steps, d_viol);
     SHD_CHECK_LAUNCH();
@@ -567,7 +636,7 @@ struct PatternEngine : Engine {
       pr.multi = (sA == sB);
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
-      hipLaunchKernelGGL(k_project, dim3(grid_for(m)), dim3(kBlock), 0, s, pr, pj, pi, (int64_t)m, out.d_chunk(),
+      hipLaunchKernelGGL(k_project, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m, out.d_chunk(),
                          out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
       SHD_CHECK_LAUNCH();
       out.count += m;
@@ -590,7 +659,7 @@ struct PatternEngine : Engine {
       ga.dts = carry[nxt].ts.as<int64_t>();
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
-      hipLaunchKernelGGL(k_gather_carry, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, ga,
+      hipLaunchKernelGGL(k_gather_carry, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(ga),
                          (const uint32_t*)d_co.as<uint32_t>(), (const uint32_t*)d_oo.as<uint32_t>(),
                          (const uint64_t*)d_key.as<uint64_t>(), n_ext);
       SHD_CHECK_LAUNCH();

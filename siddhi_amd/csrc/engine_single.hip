@@ -105,9 +105,10 @@ struct FilterArgs {
 };
 
 // flags: bit0 = passes filters, bit1 = has a (non-null) partition key
-__global__ __launch_bounds__(kBlock) void k_filter(FilterArgs a, int64_t n, uint8_t* flags, uint32_t* cnt,
+__global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict__ ap, int64_t n, uint8_t* flags, uint32_t* cnt,
                                                    uint64_t* pkey) {
-  const ColSet cs = a.cs;   // private copy (kernarg segment is read-only)
+  const FilterArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     RowCtx cx{&cs, i, nullptr, nullptr};
     uint8_t f = 0;
@@ -153,12 +154,13 @@ struct ProjArgs {
   int partitioned;
 };
 
-__global__ __launch_bounds__(kBlock) void k_project_rows(ProjArgs a, int64_t n, const uint32_t* cnt,
+__global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restrict__ ap, int64_t n, const uint32_t* cnt,
                                                          const uint32_t* off, const int32_t* call_of,
                                                          const uint32_t* run_excl, const uint32_t* run_start,
                                                          int64_t* o_chunk, int32_t* o_type,
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
-  const ColSet cs = a.cs;
+  const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
     int64_t row = a.row0 + off[i];
@@ -190,12 +192,13 @@ struct ItemArgs {
 };
 
 // New window items (one per filtered event), appended after the carried ones.
-__global__ __launch_bounds__(kBlock) void k_make_items(ItemArgs a, int64_t n, const uint32_t* cnt, const uint32_t* off,
+__global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restrict__ ap, int64_t n, const uint32_t* cnt, const uint32_t* off,
                                                        const int32_t* call_of, const int64_t* call_now,
                                                        uint64_t* ikey, int64_t* its, uint64_t* iargv, uint8_t* iargn,
                                                        int32_t* ievrow, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
-  const ColSet cs = a.cs;
+  const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
     int64_t t = a.C + off[i];
@@ -346,11 +349,12 @@ struct FoldArgs {
 };
 
 // One lane per group segment: the reference's sequential add/remove order.
-__global__ __launch_bounds__(kBlock) void k_fold(FoldArgs a, const uint32_t* heads, int64_t nheads, int64_t nops,
+__global__ __launch_bounds__(kBlock) void k_fold(const FoldArgs* __restrict__ ap, const uint32_t* heads, int64_t nheads, int64_t nops,
                                                  const uint32_t* okey_sorted, const uint32_t* oref_sorted,
                                                  const uint64_t* iargv, const uint8_t* iargn, const int32_t* ievrow,
                                                  const int32_t* call_of, uint64_t* resv, uint8_t* resn,
                                                  uint8_t* first, uint32_t* last_of) {
+  const FoldArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nheads; h += (int64_t)gridDim.x * blockDim.x) {
     int64_t q0 = heads[h];
     int64_t q1 = h + 1 < nheads ? (int64_t)heads[h + 1] : nops;
@@ -474,11 +478,12 @@ struct EmitArgs {
   int64_t chunk0;
 };
 
-__global__ __launch_bounds__(kBlock) void k_emit(EmitArgs a, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
+__global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
                                                  const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
                                                  int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
-  const ColSet cs = a.cs;
+  const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  const ColSet& cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
     if (!fcnt[t0]) continue;
     int64_t tf = a.C + t0;
@@ -601,7 +606,7 @@ struct SingleEngine : Engine {
       fa.key_col = key_col;
       fa.key_type = key_type;
     }
-    hipLaunchKernelGGL(k_filter, dim3(grid_for(n)), dim3(kBlock), 0, s, fa, n, d_flags.as<uint8_t>(),
+    hipLaunchKernelGGL(k_filter, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(fa), n, d_flags.as<uint8_t>(),
                        d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
     SHD_CHECK_LAUNCH();
     uint32_t* d_m = (uint32_t*)d_tot.p;
@@ -657,7 +662,7 @@ struct SingleEngine : Engine {
       // exclusive run ids: the run of event i is start-scan[i] (+0 if i is a start it is its own index)
       pa.chunk0 = chunk_seq;
       pa.partitioned = partitioned;
-      hipLaunchKernelGGL(k_project_rows, dim3(grid_for(n)), dim3(kBlock), 0, s, pa, n,
+      hipLaunchKernelGGL(k_project_rows, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(pa), n,
                          (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                          (const int32_t*)d_call_of.as<int32_t>(), (const uint32_t*)d_run.as<uint32_t>(),
                          (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
@@ -754,7 +759,7 @@ struct SingleEngine : Engine {
       ia.group_type = group_type;
     }
     ia.C = C;
-    hipLaunchKernelGGL(k_make_items, dim3(grid_for(n)), dim3(kBlock), 0, s, ia, n,
+    hipLaunchKernelGGL(k_make_items, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(ia), n,
                        (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
                        ikey[cur].as<uint64_t>(), its[cur].as<int64_t>(), iargv[cur].as<uint64_t>(),
@@ -838,7 +843,7 @@ struct SingleEngine : Engine {
       fo.lsum = g_lsum.as<int64_t>();
       fo.cnt = g_cnt.as<int64_t>();
       fo.nkeys = g_nkeys;
-      hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, fo, (const uint32_t*)hlist.as<uint32_t>(),
+      hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, dev_args(fo), (const uint32_t*)hlist.as<uint32_t>(),
                          nheads, nops, sk, sr, (const uint64_t*)iargv[cur].as<uint64_t>(),
                          (const uint8_t*)iargn[cur].as<uint8_t>(), (const int32_t*)ievrow.as<int32_t>(),
                          (const int32_t*)d_call_of.as<int32_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(),
@@ -869,7 +874,7 @@ struct SingleEngine : Engine {
           ea.C = C;
           ea.row0 = out.count;
           ea.chunk0 = chunk_seq;
-          hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, s, ea, m, (const uint32_t*)fcnt.as<uint32_t>(),
+          hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
                              (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
                              (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
                              (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(), out.d_chunk(),

@@ -413,6 +413,7 @@ int shd_query_stream(shd_query* q, void** stream) {
 int shd_set_time(shd_query* q, int64_t ts) {
   return guarded([&]() -> int {
     if (!q) return fail(SHD_E_ARG, "null query");
+    q->eng->args_begin();
     q->eng->set_time(ts);
     return SHD_OK;
   });
@@ -482,6 +483,7 @@ int shd_push(shd_query* q, const shd_batch* b) {
         }
       }
     }
+    e.args_begin();
     e.push(st);
     return SHD_OK;
   });
