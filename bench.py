@@ -212,7 +212,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "events/sec ingested (partitioned pattern P3, %s)" % args.config,
+            "metric": "events/sec ingested + matches/sec (partitioned pattern, 1\u20138 GPU); % HBM peak",
             "value": round(value, 1),
             "unit": "events/s",
             "n_gpus": world,

@@ -60,7 +60,7 @@ def run_device(qp, batches):
     for si, b in batches:
         cols = [np.ascontiguousarray(c) for c in b.cols]
         ts = np.ascontiguousarray(b.ts, np.int64)
-        dq.set_time(int(ts[-1]))
+        # playback time advances per InputHandler call inside the batch (advance_time)
         dq.push_raw(si, b.n, ts.ctypes.data, [c.ctypes.data for c in cols], [0] * len(cols), SHD_MEM_HOST,
                     b.call_offsets if len(b.call_offsets) > 2 else None, True)
         r = dq.poll()

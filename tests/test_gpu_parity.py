@@ -51,7 +51,7 @@ def test_single_event_calls_match_oracle(hip_available):
     # B = 1 variant: every InputHandler call carries one event
     qp, _ = compile_single_query(wl.W2_LENGTH_APP.replace("length(1000)", "length(7)"))
     sym, price, vol, ts = wl.stock_stream(3000, 13, 1.0, seed_offset=3)
-    batches = [(0, stock_batch(sym, price, vol, ts, call=1))]
+    batches = [(0, stock_batch(sym, price, vol, ts, call_size=1))]
     assert_same_rows(run_device(qp, batches)[0], run_oracle(qp, batches))
 
 
