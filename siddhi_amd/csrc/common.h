@@ -127,6 +127,7 @@ struct DevExprTable {
   DevBuf ins;      // int4 per instruction
   DevBuf consts;   // u64
   std::vector<int> off, len;
+  int nins = 0, nconsts = 0;
   void upload(const Plan& p);
 };
 

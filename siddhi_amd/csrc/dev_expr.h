@@ -327,7 +327,32 @@ struct DExpr {
 struct DExprSet {
   const int4* ins;
   const uint64_t* consts;
+  int nins, nconsts;
 };
+
+// The whole expression program of a plan is staged into LDS at kernel start:
+// every lane of a wave decodes the same (uniform) instruction stream, so LDS
+// broadcast reads replace dependent global loads in the interpreter loop.
+// Plans that do not fit are rejected at load (DevExprTable::upload).
+constexpr int kLdsIns = 256;
+constexpr int kLdsConsts = 64;
+struct LdsProg {
+  int4 ins[kLdsIns];
+  uint64_t consts[kLdsConsts];
+};
+
+// Cooperative copy; every thread of the block must call it (contains a barrier).
+__device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
+  for (int i = threadIdx.x; i < g.nins; i += blockDim.x) s.ins[i] = g.ins[i];
+  for (int i = threadIdx.x; i < g.nconsts; i += blockDim.x) s.consts[i] = g.consts[i];
+  __syncthreads();
+  DExprSet l;
+  l.ins = s.ins;
+  l.consts = s.consts;
+  l.nins = g.nins;
+  l.nconsts = g.nconsts;
+  return l;
+}
 
 // Conjunction of up to 4 filter expressions (FilterProcessor chain).
 struct DFilters {

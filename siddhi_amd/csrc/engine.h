@@ -90,7 +90,7 @@ struct Engine {
   }
 
   DExpr dexpr(int e) const { return DExpr{ex.off[e], ex.len[e]}; }
-  DExprSet dset() const { return DExprSet{ex.ins.as<int4>(), ex.consts.as<uint64_t>()}; }
+  DExprSet dset() const { return DExprSet{ex.ins.as<int4>(), ex.consts.as<uint64_t>(), ex.nins, ex.nconsts}; }
   DFilters dfilters(const std::vector<int>& ids) const;
 };
 

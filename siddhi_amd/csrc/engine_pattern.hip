@@ -31,8 +31,15 @@ namespace shd {
 
 namespace {
 
-enum : uint8_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
-enum : uint8_t { ST_OPEN = 0, ST_DEAD = 1, ST_MATCH = 2 };
+enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
+// Per-position scan result (positions = key-sorted order when partitioned).
+enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3 };
+
+// Sort payload: row index of the extended batch (28 bits) | flags (4 bits).
+constexpr int kRowBits = 28;
+constexpr uint32_t kRowMask = (1u << kRowBits) - 1;
+__device__ __forceinline__ uint32_t pv_row(uint32_t pv) { return pv & kRowMask; }
+__device__ __forceinline__ uint32_t pv_flags(uint32_t pv) { return pv >> kRowBits; }
 
 // Row addressing over the extended batch: rows [0, C) are carried partials
 // (stream A columns), rows [C, C+n) are the pushed batch.
@@ -96,125 +103,99 @@ __device__ __forceinline__ uint64_t canon_key(Val v, int type) {
   }
 }
 
+// Batch-wide aggregates written by k_prepare (one 64-byte block):
+//   [0] candidates created  [1] max key  [2] min batch ts  [3] max batch ts
+struct PrepAgg {
+  unsigned long long n_cand;
+  unsigned long long kmax;
+  long long ts_min;
+  long long ts_max;
+};
+
 struct PrepArgs {
   ExtRows x;
   DExprSet es;
   DFilters f1;
   int is_a, is_b;           // pushed stream plays A and/or B
   int partitioned;
-  DExpr key_carry_unused;
+  int key64;                // key written as u64 (long / double / float keys)
   DExpr key_expr;           // key expression of the pushed stream
   int key_type;
   int key_col;              // >= 0: plain attribute key of the pushed stream
   const uint64_t* carry_key;
 };
 
-// Per extended row: key, flags (candidate / new / B / skip).
-__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, uint64_t* key, uint8_t* flags,
-                                                    unsigned long long* n_new_cand) {
-  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  uint64_t created = 0;
-  // kernel arguments live in the read-only kernarg segment: work on a private
-  // copy before taking addresses
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_min(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+
+// Per extended row: key and packed (flags, row) sort payload.  One pass over
+// the pushed columns (key, f1 inputs, ts); the f1 bytecode is read from LDS.
+__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, uint32_t* k32,
+                                                    uint64_t* k64, uint32_t* pv, PrepAgg* agg) {
+  const PrepArgs& a = *ap;
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
+  unsigned long long created = 0, kmax = 0;
+  long long tmin = LLONG_MAX, tmax = LLONG_MIN;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
-    if (r < x.C) {
-      key[r] = a.partitioned ? a.carry_key[r] : 0;
-      flags[r] = F_CAND;
-      continue;
-    }
-    PairCtx cx{&x, r, -1};
-    uint8_t f = F_NEW;
+    uint32_t f;
     uint64_t k = 0;
+    if (r < x.C) {
+      k = a.partitioned ? a.carry_key[r] : 0;
+      f = F_CAND;
+    } else {
+      PairCtx cx{&x, r, -1};
+      f = F_NEW;
+      if (a.partitioned) {
+        Val kv;
+        if (a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
+        else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
+        if (kv.null) f |= F_SKIP;   // PartitionStreamReceiver drops null keys
+        k = kv.null ? 0 : canon_key(kv, a.key_type);
+      }
+      if (!(f & F_SKIP)) {
+        if (a.is_b) f |= F_B;
+        if (a.is_a && eval_filters(es, a.f1, cx)) {
+          f |= F_CAND;
+          created++;
+        }
+      }
+      long long t = (long long)x.batch.ts[r - x.C];
+      tmin = t < tmin ? t : tmin;
+      tmax = t > tmax ? t : tmax;
+    }
     if (a.partitioned) {
-      Val kv;
-      if (a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
-      else kv = eval_expr(a.es.ins + a.key_expr.off, a.key_expr.len, a.es.consts, cx);
-      if (kv.null) f |= F_SKIP;   // PartitionStreamReceiver drops null keys
-      k = canon_key(kv, a.key_type);
+      if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
+      if (a.key64) k64[r] = k;
+      else k32[r] = (uint32_t)k;
+      kmax = k > kmax ? k : kmax;
     }
-    if (!(f & F_SKIP)) {
-      if (a.is_b) f |= F_B;
-      if (a.is_a && eval_filters(a.es, a.f1, cx)) {
-        f |= F_CAND;
-        created++;
-      }
-    }
-    key[r] = k;
-    flags[r] = f;
+    pv[r] = (f << kRowBits) | (uint32_t)r;
   }
   for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
-  if ((threadIdx.x & 63) == 0 && created) atomicAdd(n_new_cand, (unsigned long long)created);
-}
-
-
-// ---- fault bisection variants (SHD_PROBE=variants): same loop as k_prepare
-// with progressively more of the expression machinery switched on.
-struct ConstCtx {
-  __device__ __forceinline__ Val load(int, int, int) const { Val v; v.b = 0x42c80000u; v.null = 0; return v; }
-  __device__ __forceinline__ bool evnull(int, int) const { return false; }
-  __device__ __forceinline__ int64_t ts(int, int) const { return 0; }
-  __device__ __forceinline__ Val agg(int) const { Val v; v.b = 0; v.null = 1; return v; }
-};
-struct RawCtx {
-  const ExtRows* x;
-  int64_t r1;
-  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
-    Val v; v.b = 0; v.null = 1;
-    if (st != 0 || (unsigned)attr >= (unsigned)x->batch.ncols) return v;
-    v.null = 0;
-    v.b = ((const uint32_t*)x->batch.col[attr])[r1 - x->C];
-    return v;
-  }
-  __device__ __forceinline__ bool evnull(int, int) const { return false; }
-  __device__ __forceinline__ int64_t ts(int, int) const { return 0; }
-  __device__ __forceinline__ Val agg(int) const { Val v; v.b = 0; v.null = 1; return v; }
-};
-template <int V>
-__global__ __launch_bounds__(kBlock) void k_prepare_v(const PrepArgs* __restrict__ ap, int64_t n_ext, uint64_t* key, uint8_t* flags,
-                                                      unsigned long long* n_new_cand) {
-  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  uint64_t created = 0;
-  const ExtRows& x = a.x;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
-    if (r < x.C) { key[r] = 0; flags[r] = F_CAND; continue; }
-    uint8_t f = F_NEW;
-    bool pass = false;
-    if (V == 0) pass = a.is_a;
-    if (V == 1) { ConstCtx c; pass = a.is_a && eval_filters(a.es, a.f1, c); }
-    if (V == 2) { RawCtx c{&x, r}; pass = a.is_a && eval_filters(a.es, a.f1, c); }
-    if (V == 3) { PairCtx c{&x, r, -1}; pass = a.is_a && eval_filters(a.es, a.f1, c); }
-    if (V == 4) { PairCtx c{&x, r, -1}; Val v = c.load(0, -1, 1); pass = a.is_a && !v.null && v.b != 0; }
-    if (pass) { f |= F_CAND; created++; }
-    key[r] = 0;
-    flags[r] = f;
-  }
-  for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
-  if ((threadIdx.x & 63) == 0 && created) atomicAdd(n_new_cand, (unsigned long long)created);
-}
-
-// Diagnostic (SHD_PROBE env): print the kernel's view of its arguments without
-// dereferencing any column pointer (stage 1), then the bytecode (stage 2).
-__global__ void k_probe(const PrepArgs* __restrict__ ap, int64_t n_ext, int stage) {
-  const PrepArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (stage == 1) {
-    printf("probe dev: n_ext %lld C %lld ncols %d ts %p is_a %d is_b %d part %d key_col %d f1.n %d ins %p consts %p\n",
-           (long long)n_ext, (long long)a.x.C, a.x.batch.ncols, (const void*)a.x.batch.ts, a.is_a, a.is_b,
-           a.partitioned, a.key_col, a.f1.n, (const void*)a.es.ins, (const void*)a.es.consts);
-    for (int c = 0; c < a.x.batch.ncols && c < kMaxCols; c++)
-      printf("probe dev: col %d %p nul %p type %d\n", c, a.x.batch.col[c], (const void*)a.x.batch.nul[c],
-             (int)a.x.batch.type[c]);
-    for (int i = 0; i < a.f1.n && i < 4; i++) printf("probe dev: f1[%d] off %d len %d\n", i, a.f1.f[i].off, a.f1.f[i].len);
-  } else {
-    auto sane = [](const void* q) { return q != nullptr && ((uintptr_t)q >> 47) == 0; };
-    if (!sane(a.es.ins) || !sane(a.x.batch.ts)) { printf("probe dev: insane pointer, skipping loads\n"); return; }
-    for (int i = 0; i < a.f1.n && i < 4; i++)
-      for (int k = 0; k < a.f1.f[i].len && k < 16; k++) {
-        int4 in = a.es.ins[a.f1.f[i].off + k];
-        printf("probe dev: f1[%d][%d] op %d a %d b %d c %d\n", i, k, in.x, in.y, in.z, in.w);
-      }
-    if (n_ext > a.x.C) printf("probe dev: ts[0] %lld\n", (long long)a.x.batch.ts[0]);
+  kmax = wave_max(kmax);
+  tmin = wave_min(tmin);
+  tmax = wave_max(tmax);
+  if ((threadIdx.x & 63) == 0) {
+    if (created) atomicAdd(&agg->n_cand, created);
+    if (kmax) atomicMax(&agg->kmax, kmax);
+    if (tmin != LLONG_MAX) atomicMin(&agg->ts_min, tmin);
+    if (tmax != LLONG_MIN) atomicMax(&agg->ts_max, tmax);
   }
 }
 
@@ -229,77 +210,97 @@ struct ScanArgs {
   DFilters f2;
   int64_t within;
   int partitioned;
+  int prune;            // drop partials that can no longer match (horizon guard on later pushes)
+  int64_t t_end;        // latest event time of this push
 };
 
-// One lane per candidate partial: forward walk over the later events of its key.
-__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext, const uint32_t* perm,
-                                                         const uint64_t* key, const uint8_t* flags,
-                                                         int32_t* match_j, uint8_t* status,
-                                                         unsigned long long* steps_total, uint32_t* violation) {
-  const ScanArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  uint64_t steps = 0;
+struct ScanOut {
+  unsigned long long steps;   // (partial, event) pairs examined
+  unsigned long long pruned;  // open partials dropped by the horizon rule
+  uint32_t violation;         // per-key timestamp decrease seen
+  uint32_t pad;
+};
+
+// One lane per position; candidates walk forward over the later events of
+// their key (sorted positions when partitioned, ext rows otherwise).  Reads of
+// flags / keys are sequential; only event timestamps (and f2 operands when an
+// event falls inside `within`) are gathered by row.  Writes the compaction
+// counts for matches (cm) and still-open partials (co) per position.
+template <bool K64>
+__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
+                                                         const uint32_t* skey32, const uint64_t* skey64,
+                                                         const uint32_t* spv, int32_t* match_row, uint32_t* cm,
+                                                         uint32_t* co, ScanOut* so) {
+  const ScanArgs& a = *ap;
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_ext;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = perm ? (int64_t)perm[p] : p;
-    uint8_t fr = flags[r];
-    if (!(fr & F_CAND)) continue;
-    uint64_t k = key[r];
-    int64_t tsi = x.ts(r);
-    int64_t prev = tsi;
-    uint8_t st = ST_OPEN;
-    int32_t j = -1;
-    for (int64_t q = p + 1; q < n_ext; q++) {
-      int64_t r2 = perm ? (int64_t)perm[q] : q;
-      if (a.partitioned && key[r2] != k) break;
-      uint8_t f2 = flags[r2];
-      if (!(f2 & F_NEW) || (f2 & F_SKIP)) continue;
-      int64_t t2 = x.ts(r2);
-      if (t2 < prev) {
-        atomicOr(violation, 1u);
-        break;
-      }
-      prev = t2;
-      steps++;
-      // stabilizeStates -> expireEvents: |ts_i - t| > within
-      if (t2 - tsi > a.within) {
-        st = ST_DEAD;
-        break;
-      }
-      if (f2 & F_B) {
-        PairCtx cx{&x, r, r2};
-        if (eval_filters(a.es, a.f2, cx)) {
-          st = ST_MATCH;
-          j = (int32_t)r2;
+  uint64_t steps = 0, pruned = 0;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_ext; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t pvp = spv[p];
+    uint32_t m = 0, o = 0;
+    if (pv_flags(pvp) & F_CAND) {
+      const int64_t r = pv_row(pvp);
+      const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
+      const int64_t tsi = x.ts(r);
+      int64_t prev = tsi;
+      uint8_t st = ST_OPEN;
+      int32_t j = -1;
+      for (int64_t q = p + 1; q < n_ext; q++) {
+        if (a.partitioned && (K64 ? skey64[q] : skey32[q]) != k) break;
+        const uint32_t pq = spv[q];
+        const uint32_t fq = pv_flags(pq);
+        if (!(fq & F_NEW) || (fq & F_SKIP)) continue;
+        const int64_t r2 = pv_row(pq);
+        const int64_t t2 = x.ts(r2);
+        if (t2 < prev) {
+          atomicOr(&so->violation, 1u);
           break;
         }
+        prev = t2;
+        steps++;
+        // stabilizeStates -> expireEvents: |ts_i - t| > within
+        if (t2 - tsi > a.within) {
+          st = ST_DEAD;
+          break;
+        }
+        if (fq & F_B) {
+          PairCtx cx{&x, r, r2};
+          if (eval_filters(es, a.f2, cx)) {
+            st = ST_MATCH;
+            j = (int32_t)r2;
+            break;
+          }
+        }
       }
+      if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) {
+        st = ST_DEAD;   // every later event is at or after t_end: it would expire this partial
+        pruned++;
+      }
+      match_row[p] = j;
+      m = st == ST_MATCH;
+      o = st == ST_OPEN;
     }
-    match_j[r] = j;
-    status[r] = st;
+    cm[p] = m;
+    co[p] = o;
   }
-  // one atomic per wave
-  for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o, 64);
-  if ((threadIdx.x & 63) == 0 && steps) atomicAdd(steps_total, (unsigned long long)steps);
-}
-
-// counts for compaction: matches and still-open partials, in ext (= creation) order
-__global__ void k_flags_to_counts(const uint8_t* flags, const uint8_t* status, int64_t n, uint32_t* cm,
-                                  uint32_t* co) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    bool c = flags[r] & F_CAND;
-    cm[r] = (c && status[r] == ST_MATCH) ? 1u : 0u;
-    co[r] = (c && status[r] == ST_OPEN) ? 1u : 0u;
+  for (int o2 = 32; o2 > 0; o2 >>= 1) {
+    steps += __shfl_xor(steps, o2, 64);
+    pruned += __shfl_xor(pruned, o2, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (steps) atomicAdd(&so->steps, (unsigned long long)steps);
+    if (pruned) atomicAdd(&so->pruned, (unsigned long long)pruned);
   }
 }
 
-__global__ void k_emit_pairs(const uint32_t* cm, const uint32_t* om, const int32_t* match_j, int64_t n,
-                             uint32_t* pj, uint32_t* pi) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    if (cm[r]) {
-      uint32_t o = om[r];
-      pj[o] = (uint32_t)match_j[r];
-      pi[o] = (uint32_t)r;
+__global__ void k_emit_pairs(const uint32_t* cm, const uint32_t* om, const int32_t* match_row, const uint32_t* spv,
+                             int64_t n, uint32_t* pj, uint32_t* pi) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    if (cm[p]) {
+      uint32_t o = om[p];
+      pj[o] = (uint32_t)match_row[p];
+      pi[o] = pv_row(spv[p]);
     }
   }
 }
@@ -314,17 +315,19 @@ struct ProjArgs {
   int64_t row0;         // output buffer offset
 };
 
-__global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj, const uint32_t* pi, int64_t m,
-                                                    int64_t* o_chunk, int32_t* o_type, int64_t* o_ts,
-                                                    uint64_t* o_vals, uint8_t* o_nul) {
-  const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+__global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj,
+                                                    const uint32_t* pi, int64_t m, int64_t* o_chunk, int32_t* o_type,
+                                                    int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+  const ProjArgs& a = *ap;
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t j = pj[k], i = pi[k];
     PairCtx cx{&x, i, j};
     int64_t row = a.row0 + k;
     for (int c = 0; c < a.nout; c++) {
-      Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
+      Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
@@ -337,6 +340,8 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
 struct GatherArgs {
   ExtRows x;
   int ncols;
+  int partitioned;
+  int key64;
   int8_t types[kMaxCols];
   void* dcol[kMaxCols];
   uint8_t* dnul[kMaxCols];
@@ -345,12 +350,16 @@ struct GatherArgs {
   int64_t* dseq;
 };
 
-__global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t* co, const uint32_t* oo, const uint64_t* key, int64_t n) {
-  const GatherArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+// Still-open partials -> next push's carry rows (position order: per key in
+// creation order, which is all the stable key sort of the next push needs).
+__global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t* co, const uint32_t* oo,
+                               const uint32_t* spv, const uint32_t* skey32, const uint64_t* skey64, int64_t n) {
+  const GatherArgs& a = *ap;
   const ExtRows& x = a.x;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    if (!co[r]) continue;
-    int64_t o = oo[r];
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    if (!co[p]) continue;
+    int64_t o = oo[p];
+    int64_t r = pv_row(spv[p]);
     const ColSet& cs = x.cs(r);
     int64_t row = x.row(r);
     for (int c = 0; c < a.ncols; c++) {
@@ -363,7 +372,7 @@ __global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t
       a.dnul[c][o] = (uint8_t)v.null;
     }
     a.dts[o] = x.ts(r);
-    a.dkey[o] = key[r];
+    a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
     a.dseq[o] = x.seq(r);
   }
 }
@@ -405,14 +414,6 @@ int plain_load_attr(const Plan& p, int e) {
   return -1;
 }
 
-int key_class(int t) {
-  switch (t) {
-    case SHD_T_INT: case SHD_T_LONG: return 1;
-    case SHD_T_FLOAT: case SHD_T_DOUBLE: return 2;
-    case SHD_T_BOOL: return 3;
-  }
-  return 4;
-}
 
 }  // namespace
 
@@ -427,10 +428,15 @@ struct PatternEngine : Engine {
   CarryTable carry[2];
   int cur = 0;
   int64_t C = 0;
+  // horizon rule: once open partials were dropped because every later event
+  // (time >= horizon) would expire them, later pushes must not go back before it
+  bool have_horizon = false;
+  int64_t horizon = INT64_MIN;
+  static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
-  DevBuf d_key, d_flags, d_perm, d_perm_alt, d_k32, d_k32_alt, d_k64_alt, d_match, d_status, d_cm, d_co, d_om,
-      d_oo, d_pj, d_pi, d_pj_alt, d_pi_alt, d_tot, d_sort, d_scan;
-  PinnedBuf h_tot;
+  DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_match, d_cm, d_co, d_om, d_oo, d_pj, d_pi, d_pj_alt,
+      d_pi_alt, d_agg, d_sort, d_scan;
+  PinnedBuf h_agg;
 
   int kind() const override { return ENG_PATTERN; }
 
@@ -441,6 +447,8 @@ struct PatternEngine : Engine {
     chunk_seq = 0;
     out.count = 0;
     counters = shd_counters{};
+    have_horizon = false;
+    horizon = INT64_MIN;
   }
 
   ColSet carry_cs() const {
@@ -449,30 +457,31 @@ struct PatternEngine : Engine {
     return cs;
   }
 
+  static bool type_key64(int t) { return t == SHD_T_LONG || t == SHD_T_DOUBLE || t == SHD_T_FLOAT; }
+
   void push(const Staged& b) override {
-    if (b.advance_time) {
-      for (size_t c = 0; c + 1 < b.call_offsets.size(); c++) {
-        // last ts of each call: time only matters for expiry (event ts), kept for set_time parity
-      }
-    }
     const int64_t n = b.n;
     if (n <= 0) return;
     const bool isA = b.stream == sA, isB = b.stream == sB;
     const int64_t n_ext = C + n;
-    if (n_ext >= (int64_t)INT32_MAX) throw Error(SHD_E_CAPACITY, "pattern batch + carry exceeds 2^31 rows");
+    if (n_ext > (int64_t)kRowMask) throw Error(SHD_E_CAPACITY, "pattern batch + carried partials exceed 2^28 rows");
     hipStream_t s = stream;
     SHD_HIP(hipEventRecord(ev0, s));
     stage_begin();
-    d_key.reserve(n_ext * 8);
-    d_flags.reserve(n_ext);
+    const int slot = isA ? 0 : 1;
+    const bool key64 = partitioned && type_key64(key_type[slot]);
+    d_pv.reserve(n_ext * 4);
+    if (partitioned) {
+      if (key64) d_k64.reserve(n_ext * 8);
+      d_k32.reserve(n_ext * 4);
+    }
     d_match.reserve(n_ext * 4);
-    d_status.reserve(n_ext);
     d_cm.reserve(n_ext * 4);
     d_co.reserve(n_ext * 4);
     d_om.reserve(n_ext * 4);
     d_oo.reserve(n_ext * 4);
-    d_tot.reserve(64);
-    h_tot.reserve(64);
+    d_agg.reserve(256);
+    h_agg.reserve(256);
 
     ExtRows x{};
     x.carry = carry_cs();
@@ -488,7 +497,7 @@ struct PatternEngine : Engine {
     pa.is_a = isA;
     pa.is_b = isB;
     pa.partitioned = partitioned;
-    int slot = isA ? 0 : 1;
+    pa.key64 = key64;
     if (partitioned) {
       pa.key_expr = dexpr(key_expr[slot]);
       pa.key_col = key_col[slot];
@@ -497,118 +506,97 @@ struct PatternEngine : Engine {
       pa.key_col = -1;
     }
     pa.carry_key = carry[cur].key.as<uint64_t>();
-    SHD_HIP(hipMemsetAsync(d_tot.p, 0, 64, s));
-    if (const char* pr = std::getenv("SHD_PROBE")) {
-      fprintf(stderr, "probe host: n_ext %lld C %lld ncols %d ts %p is_a %d f1.n %d ins %p consts %p sizeof(PrepArgs) %zu\n",
-              (long long)n_ext, (long long)pa.x.C, pa.x.batch.ncols, (const void*)pa.x.batch.ts, pa.is_a, pa.f1.n,
-              (const void*)pa.es.ins, (const void*)pa.es.consts, sizeof(PrepArgs));
-      for (int c = 0; c < pa.x.batch.ncols; c++)
-        fprintf(stderr, "probe host: col %d %p nul %p type %d\n", c, pa.x.batch.col[c], (const void*)pa.x.batch.nul[c],
-                (int)pa.x.batch.type[c]);
-      SHD_HIP(hipStreamSynchronize(s));
-      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, dev_args(pa), n_ext, 1);
-      SHD_HIP(hipStreamSynchronize(s));
-      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, s, dev_args(pa), n_ext, 2);
-      SHD_HIP(hipStreamSynchronize(s));
-      fflush(stdout);
-      if (pr[0] == 'v') {
-        auto chk = [&](int v) {
-          SHD_HIP(hipStreamSynchronize(s));
-          fprintf(stderr, "probe: variant %d ok\n", v);
-          fflush(stderr);
-        };
-        unsigned long long* nc = (unsigned long long*)(d_tot.as<uint64_t>() + 6);
-        hipLaunchKernelGGL(k_prepare_v<0>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
-        chk(0);
-        hipLaunchKernelGGL(k_prepare_v<1>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
-        chk(1);
-        hipLaunchKernelGGL(k_prepare_v<2>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
-        chk(2);
-        hipLaunchKernelGGL(k_prepare_v<4>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
-        chk(4);
-        hipLaunchKernelGGL(k_prepare_v<3>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(), d_flags.as<uint8_t>(), nc);
-        chk(3);
-        throw Error(SHD_E_UNSUPPORTED, "SHD_PROBE: variants done");
-      }
-      if (pr[0] != 'r') throw Error(SHD_E_UNSUPPORTED, "SHD_PROBE: stopped before k_prepare");
-    }
-    hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_key.as<uint64_t>(),
-                       d_flags.as<uint8_t>(), (unsigned long long*)(d_tot.as<uint64_t>() + 6));
+    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN};
+    PrepAgg* d_pa = d_agg.as<PrepAgg>();
+    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
+    std::memcpy(h_agg.p, &init, sizeof(init));
+    std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
+    SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_k32.as<uint32_t>(),
+                       d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_pa);
     SHD_CHECK_LAUNCH();
+    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    PrepAgg pg;
+    std::memcpy(&pg, h_agg.p, sizeof(pg));
     mark("prepare");
+    if (have_horizon && (int64_t)pg.ts_min < horizon)
+      throw Error(SHD_E_UNSUPPORTED,
+                  "pattern engine: an event precedes the pruning horizon of an earlier push (timestamps must not "
+                  "go back across pushes once partials were retired)");
+    counters.partials += (int64_t)pg.n_cand;
 
-    // ---- key-sort the extended batch (stable: creation order within a key)
-    const uint32_t* perm = nullptr;
+    // ---- key-sort the extended batch (stable: creation order within a key),
+    //      carrying the packed (flags, row) payload
+    const uint32_t* skey32 = nullptr;
+    const uint64_t* skey64 = nullptr;
+    const uint32_t* spv = d_pv.as<uint32_t>();
+    bool sorted64 = false;
     if (partitioned) {
-      uint64_t* dmax = d_tot.as<uint64_t>() + 4;
-      reduce_max_u64(d_key.as<uint64_t>(), n_ext, dmax, s);
-      SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 4, dmax, 8, hipMemcpyDeviceToHost, s));
-      SHD_HIP(hipStreamSynchronize(s));
-      uint64_t kmax = h_tot.as<uint64_t>()[4];
+      uint64_t kmax = pg.kmax;
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
-      d_perm.reserve(n_ext * 4);
-      d_perm_alt.reserve(n_ext * 4);
-      fill_iota_u32(d_perm.as<uint32_t>(), n_ext, 0, s);
+      d_pv_alt.reserve(n_ext * 4);
       bool in_alt = false;
-      if (bits <= 32) {
-        d_k32.reserve(n_ext * 4);
-        d_k32_alt.reserve(n_ext * 4);
-        hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_key.as<uint64_t>(),
+      if (key64 && bits <= 32) {
+        hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
                            d_k32.as<uint32_t>(), n_ext);
         SHD_CHECK_LAUNCH();
-        radix_sort_pairs_u32(d_k32.as<uint32_t>(), d_perm.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
-                             d_perm_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
+      }
+      if (bits <= 32) {
+        d_k32_alt.reserve(n_ext * 4);
+        radix_sort_pairs_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
+                             d_pv_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
+        skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);
-        DevBuf k64;
-        k64.reserve(n_ext * 8);
-        SHD_HIP(hipMemcpyAsync(k64.p, d_key.p, n_ext * 8, hipMemcpyDeviceToDevice, s));
-        radix_sort_pairs_u64(k64.as<uint64_t>(), d_perm.as<uint32_t>(), d_k64_alt.as<uint64_t>(),
-                             d_perm_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
-        SHD_HIP(hipStreamSynchronize(s));
+        radix_sort_pairs_u64(d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_k64_alt.as<uint64_t>(),
+                             d_pv_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
+        skey64 = in_alt ? d_k64_alt.as<uint64_t>() : d_k64.as<uint64_t>();
+        sorted64 = true;
       }
-      perm = in_alt ? d_perm_alt.as<uint32_t>() : d_perm.as<uint32_t>();
+      spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
       mark("key_sort");
     }
 
-    // ---- forward scan, one lane per candidate partial
-    SHD_HIP(hipMemsetAsync(d_tot.p, 0, 32, s));   // keeps the candidate count at word 6
+    // ---- forward scan, one lane per position
     ScanArgs sa{};
     sa.x = x;
     sa.es = dset();
     sa.f2 = dfilters(f2);
     sa.within = W;
     sa.partitioned = partitioned;
-    unsigned long long* d_steps = (unsigned long long*)d_tot.as<uint64_t>();
-    uint32_t* d_viol = (uint32_t*)(d_tot.as<uint64_t>() + 1);
-    hipLaunchKernelGGL(k_forward_scan, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, perm,
-                       (const uint64_t*)d_key.as<uint64_t>(), (const uint8_t*)d_flags.as<uint8_t>(),
-                       d_match.as<int32_t>(), d_status.as<uint8_t>(), d_steps, d_viol);
+    sa.prune = n_ext >= kPruneMinRows && W != INT64_MAX;
+    const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
+    sa.t_end = t_end;
+    if (sorted64)
+      hipLaunchKernelGGL(k_forward_scan<true>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
+                         skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
+    else
+      hipLaunchKernelGGL(k_forward_scan<false>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
+                         skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
 
-    // ---- compaction offsets for matches (ordered by creation) and open partials
-    hipLaunchKernelGGL(k_flags_to_counts, dim3(grid_for(n_ext)), dim3(kBlock), 0, s,
-                       (const uint8_t*)d_flags.as<uint8_t>(), (const uint8_t*)d_status.as<uint8_t>(), n_ext,
-                       d_cm.as<uint32_t>(), d_co.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    uint32_t* d_m = (uint32_t*)(d_tot.as<uint64_t>() + 2);
-    uint32_t* d_o = d_m + 1;
-    scan_exclusive_u32(d_cm.as<uint32_t>(), d_om.as<uint32_t>(), n_ext, d_m, d_scan, s);
-    scan_exclusive_u32(d_co.as<uint32_t>(), d_oo.as<uint32_t>(), n_ext, d_o, d_scan, s);
+    // ---- compaction offsets for matches and open partials (position order)
+    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
+    scan_exclusive_u32(d_cm.as<uint32_t>(), d_om.as<uint32_t>(), n_ext, d_mo, d_scan, s);
+    scan_exclusive_u32(d_co.as<uint32_t>(), d_oo.as<uint32_t>(), n_ext, d_mo + 1, d_scan, s);
     mark("compact");
-    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 56, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    uint64_t steps = h_tot.as<uint64_t>()[0];
-    counters.partials += (int64_t)h_tot.as<uint64_t>()[6];
-    uint32_t viol = (uint32_t)h_tot.as<uint64_t>()[1];
-    uint32_t m = h_tot.as<uint32_t>()[4];
-    uint32_t n_open = h_tot.as<uint32_t>()[5];
-    if (viol)
+    ScanOut so;
+    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
+    const uint32_t m = h_agg.as<uint32_t>()[32];
+    const uint32_t n_open = h_agg.as<uint32_t>()[33];
+    if (so.violation)
       throw Error(SHD_E_UNSUPPORTED,
                   "pattern engine: event timestamps decrease within a key; the forward-scan formulation "
                   "requires per-key non-decreasing timestamps");
+    if (so.pruned) {
+      have_horizon = true;
+      horizon = std::max(horizon, t_end);
+    }
 
     // ---- matches ordered by (e2 event, creation) -> projected output rows
     if (m > 0) {
@@ -616,13 +604,15 @@ struct PatternEngine : Engine {
       d_pi.reserve((int64_t)m * 4);
       d_pj_alt.reserve((int64_t)m * 4);
       d_pi_alt.reserve((int64_t)m * 4);
-      hipLaunchKernelGGL(k_emit_pairs, dim3(grid_for(n_ext)), dim3(kBlock), 0, s,
-                         (const uint32_t*)d_cm.as<uint32_t>(), (const uint32_t*)d_om.as<uint32_t>(),
-                         (const int32_t*)d_match.as<int32_t>(), n_ext, d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
+      hipLaunchKernelGGL(k_emit_pairs, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, (const uint32_t*)d_cm.as<uint32_t>(),
+                         (const uint32_t*)d_om.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
+                         d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
       SHD_CHECK_LAUNCH();
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
       bool in_alt = false;
+      // pairs come out in (key, creation) order; the stable sort by j leaves the
+      // partials of one e2 event in creation order (pending-list order)
       radix_sort_pairs_u32(d_pj.as<uint32_t>(), d_pi.as<uint32_t>(), d_pj_alt.as<uint32_t>(),
                            d_pi_alt.as<uint32_t>(), m, bits, d_sort, s, in_alt);
       const uint32_t* pj = in_alt ? d_pj_alt.as<uint32_t>() : d_pj.as<uint32_t>();
@@ -636,21 +626,23 @@ struct PatternEngine : Engine {
       pr.multi = (sA == sB);
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
-      hipLaunchKernelGGL(k_project, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m, out.d_chunk(),
-                         out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+      hipLaunchKernelGGL(k_project, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
+                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
       SHD_CHECK_LAUNCH();
       out.count += m;
       if (sA != sB) chunk_seq += m;
       mark("order_project");
     }
 
-    // ---- carry the still-open partials (in creation order)
+    // ---- carry the still-open partials
     int nxt = cur ^ 1;
     carry[nxt].reserve(n_open, typesA);
     if (n_open > 0) {
       GatherArgs ga{};
       ga.x = x;
       ga.ncols = (int)typesA.size();
+      ga.partitioned = partitioned;
+      ga.key64 = sorted64;
       for (size_t c = 0; c < typesA.size(); c++) {
         ga.types[c] = (int8_t)typesA[c];
         ga.dcol[c] = carry[nxt].col[c].p;
@@ -660,8 +652,8 @@ struct PatternEngine : Engine {
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
       hipLaunchKernelGGL(k_gather_carry, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(ga),
-                         (const uint32_t*)d_co.as<uint32_t>(), (const uint32_t*)d_oo.as<uint32_t>(),
-                         (const uint64_t*)d_key.as<uint64_t>(), n_ext);
+                         (const uint32_t*)d_co.as<uint32_t>(), (const uint32_t*)d_oo.as<uint32_t>(), spv, skey32,
+                         skey64, n_ext);
       SHD_CHECK_LAUNCH();
       mark("carry");
     }
@@ -671,13 +663,12 @@ struct PatternEngine : Engine {
     float ms = 0.f;
     SHD_HIP(hipEventElapsedTime(&ms, ev0, ev1));
     cur = nxt;
-    int64_t created = 0;
-    (void)created;
     C = n_open;
     seq += n;
+    if (b.advance_time && t_end > now) now = t_end;
     counters.events += n;
     counters.matches += m;
-    counters.partial_scans += (int64_t)steps;
+    counters.partial_scans += (int64_t)so.steps;
     counters.carry = C;
     counters.kernel_ns = (int64_t)(ms * 1e6);
   }
@@ -724,8 +715,8 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
       int slot = pk.first == a.stream ? 0 : (pk.first == b.stream ? 1 : -1);
       if (slot < 0) continue;
       int t = expr_result_type(p, pk.second, {});
-      if (cls >= 0 && key_class(t) != cls) { why = "partition keys of different types"; return nullptr; }
-      cls = key_class(t);
+      if (cls >= 0 && t != cls) { why = "partition keys of different types"; return nullptr; }
+      cls = t;
       e->key_expr[slot] = pk.second;
       e->key_col[slot] = plain_load_attr(p, pk.second);
       e->key_type[slot] = t;

@@ -108,6 +108,8 @@ struct FilterArgs {
 __global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict__ ap, int64_t n, uint8_t* flags, uint32_t* cnt,
                                                    uint64_t* pkey) {
   const FilterArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -115,13 +117,13 @@ __global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict_
     bool keyed = true;
     if (a.partitioned) {
       Val kv = a.key_col >= 0 ? col_load(cs, i, a.key_col)
-                              : eval_expr(a.es.ins + a.key.off, a.key.len, a.es.consts, cx);
+                              : eval_expr(es.ins + a.key.off, a.key.len, es.consts, cx);
       keyed = !kv.null;
       pkey[i] = canon_key(kv, a.key_type);
     }
     if (keyed) {
       f |= 2;
-      if (eval_filters(a.es, a.filters, cx)) f |= 1;
+      if (eval_filters(es, a.filters, cx)) f |= 1;
     }
     flags[i] = f;
     cnt[i] = (f & 3) == 3 ? 1u : 0u;
@@ -160,13 +162,15 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
                                                          int64_t* o_chunk, int32_t* o_type,
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
     int64_t row = a.row0 + off[i];
     RowCtx cx{&cs, i, nullptr, nullptr};
     for (int c = 0; c < a.nout; c++) {
-      Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
+      Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
@@ -198,6 +202,8 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
                                                        int32_t* ievrow, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
     uint64_t k = 0;
     if (a.ngroup) {
       Val kv = a.group_col >= 0 ? col_load(cs, i, a.group_col)
-                                : eval_expr(a.es.ins + a.group.off, a.group.len, a.es.consts, cx);
+                                : eval_expr(es.ins + a.group.off, a.group.len, es.consts, cx);
       if (kv.null) atomicOr(null_key_flag, 1u);
       k = kv.null ? 0 : canon_key(kv, a.group_type);
     }
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
       Val v;
       v.b = 0;
       v.null = 1;
-      if (a.has_arg[g]) v = eval_expr(a.es.ins + a.agg_arg[g].off, a.agg_arg[g].len, a.es.consts, cx);
+      if (a.has_arg[g]) v = eval_expr(es.ins + a.agg_arg[g].off, a.agg_arg[g].len, es.consts, cx);
       iargv[g * cap + t] = v.b;
       iargn[g * cap + t] = (uint8_t)v.null;
     }
@@ -483,6 +489,8 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
                                                  const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
                                                  int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(es, prog);
   const ColSet& cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
     if (!fcnt[t0]) continue;
@@ -498,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
     RowCtx cx{&cs, ev, av, an};
     int64_t row = a.row0 + foff[t0];
     for (int c = 0; c < a.nout; c++) {
-      Val v = eval_expr(a.es.ins + a.outs[c].off, a.outs[c].len, a.es.consts, cx);
+      Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }

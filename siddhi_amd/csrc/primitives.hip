@@ -140,14 +140,39 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const K* keys, int64_t n, in
   hist[(int64_t)tid * nb + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
+// Scatter one 4096-key tile: stable in-tile ranking (ballots), the tile is
+// first reordered by digit in LDS, then written out so that consecutive lanes
+// store consecutive addresses of one digit bucket (coalesced runs instead of
+// one scattered dword per key).
 template <class K>
 __global__ __launch_bounds__(kBlock) void k_rs_scatter(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout,
-                                                       int64_t n, int shift, const uint32_t* offs, int nb) {
-  __shared__ uint32_t base[256];
+                                                       int64_t n, int shift, const uint32_t* hist,
+                                                       const uint32_t* offs, int nb) {
+  __shared__ K sk[kRsTile];
+  __shared__ uint32_t sv[kRsTile];
+  __shared__ uint32_t lpre[256];    // tile-local first position of each digit
+  __shared__ uint32_t lbase[256];   // running tile-local position per digit
+  __shared__ uint32_t gbase[256];   // global first position of this tile's digit run
   __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t wsum[4];
   int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int64_t t0 = (int64_t)blockIdx.x * kRsTile;
-  base[tid] = offs[(int64_t)tid * nb + blockIdx.x];
+  // tile-local exclusive prefix over digits from this tile's histogram column
+  {
+    uint32_t c = hist[(int64_t)tid * nb + blockIdx.x];
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int i = 0; i < w; i++) pre += wsum[i];
+    lpre[tid] = pre + inc - c;
+    lbase[tid] = pre + inc - c;
+    gbase[tid] = offs[(int64_t)tid * nb + blockIdx.x];
+  }
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int r = 0; r < kRsRounds; r++) {
     int64_t idx = t0 + r * kBlock + tid;
@@ -169,14 +194,22 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const K* kin, const uint3
     if (valid && (peers & lt) == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
     __syncthreads();
     if (valid) {
-      uint32_t pos = base[d] + rank;
+      uint32_t pos = lbase[d] + rank;
       for (int ww = 0; ww < w; ww++) pos += wcnt[ww][d];
-      kout[pos] = k;
-      vout[pos] = v;
+      sk[pos] = k;
+      sv[pos] = v;
     }
     __syncthreads();
-    base[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-    __syncthreads();
+    lbase[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+  }
+  __syncthreads();
+  int64_t tile_n = n - t0 < kRsTile ? n - t0 : kRsTile;
+  for (int i = tid; i < tile_n; i += kBlock) {
+    K k = sk[i];
+    uint32_t d = (uint32_t)((k >> shift) & 255u);
+    uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
+    kout[o] = k;
+    vout[o] = sv[i];
   }
 }
 
@@ -199,7 +232,7 @@ static void radix_sort_impl(K* keys, uint32_t* vals, K* keys_alt, uint32_t* vals
     SHD_CHECK_LAUNCH();
     scan_raw(hist, offs, nh, nullptr, sscr, s);
     hipLaunchKernelGGL(k_rs_scatter<K>, dim3(nb), dim3(kBlock), 0, s, (const K*)ki, (const uint32_t*)vi, ko, vo, n,
-                       shift, (const uint32_t*)offs, nb);
+                       shift, (const uint32_t*)hist, (const uint32_t*)offs, nb);
     SHD_CHECK_LAUNCH();
     std::swap(ki, ko);
     std::swap(vi, vo);

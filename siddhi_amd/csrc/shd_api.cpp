@@ -208,6 +208,10 @@ void DevExprTable::upload(const Plan& p) {
     len.push_back((int)code.size());
     for (auto& in : code) all.push_back(make_int4(in.op, in.a, in.b, in.c));
   }
+  if (all.size() > (size_t)kLdsIns || p.consts.size() > (size_t)kLdsConsts)
+    throw Error(SHD_E_UNSUPPORTED, "expression program larger than the device LDS program store");
+  nins = (int)all.size();
+  nconsts = (int)p.consts.size();
   ins.reserve(std::max<size_t>(all.size(), 1) * sizeof(int4));
   consts.reserve(std::max<size_t>(p.consts.size(), 1) * 8);
   if (!all.empty()) SHD_HIP(hipMemcpy(ins.p, all.data(), all.size() * sizeof(int4), hipMemcpyHostToDevice));

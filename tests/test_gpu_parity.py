@@ -76,3 +76,33 @@ def test_two_stream_pattern_matches_oracle(hip_available):
     dev, _, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
+
+
+def test_pruned_partials_and_horizon_guard(hip_available):
+    """Large pushes retire open partials that every later event would expire
+    (StreamPreStateProcessor.isExpired, `within`); results stay identical to the
+    oracle, and a later push that goes back before the retirement horizon is
+    refused (SHD_E_UNSUPPORTED) instead of silently diverging."""
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST, SiddhiHipError, SHD_E_UNSUPPORTED
+    qp, _ = compile_single_query(wl.P3_APP)
+    sym, price, vol, ts = wl.stock_stream(300_000, 100_000, 0.05, seed_offset=41)
+    batches = split(sym, price, vol, ts, 3)
+    ora = run_oracle(qp, batches)
+    dev, counters, _ = run_device(qp, batches)
+    assert_same_rows(dev, ora)
+    assert counters["carry"] < 20_000   # partials older than `within` were retired
+    dq = DeviceQuery(qp.ir)
+    try:
+        for si, b in batches:
+            cols = [np.ascontiguousarray(c) for c in b.cols]
+            t = np.ascontiguousarray(b.ts, np.int64)
+            dq.push_raw(si, b.n, t.ctypes.data, [c.ctypes.data for c in cols], [0] * 3, SHD_MEM_HOST, None, True)
+            dq.discard()
+        si, b = batches[0]
+        cols = [np.ascontiguousarray(c) for c in b.cols]
+        t = np.ascontiguousarray(b.ts, np.int64)
+        with pytest.raises(SiddhiHipError) as ei:
+            dq.push_raw(si, b.n, t.ctypes.data, [c.ctypes.data for c in cols], [0] * 3, SHD_MEM_HOST, None, True)
+        assert ei.value.code == SHD_E_UNSUPPORTED
+    finally:
+        dq.close()
