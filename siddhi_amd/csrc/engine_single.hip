@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict_
                                                    uint64_t* pkey) {
   const FilterArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(es, prog);
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(es, prog);
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(es, prog);
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!cnt[i]) continue;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
                                                  int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(es, prog);
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
     if (!fcnt[t0]) continue;
