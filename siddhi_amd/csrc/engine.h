@@ -61,6 +61,8 @@ struct Engine {
     if (t >= now) now = t;
   }
   virtual void reset() = 0;
+  // called once the plan's expression table is on the device
+  virtual void on_loaded() {}
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column
@@ -96,5 +98,6 @@ struct Engine {
 
 std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
+std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why);
 
 }  // namespace shd

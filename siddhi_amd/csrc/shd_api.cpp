@@ -376,12 +376,20 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
     Plan p = decode_plan((const int32_t*)ir, (int64_t)(len / 4));
     std::string why1, why2;
     std::unique_ptr<Engine> e;
-    if (p.kind == SHD_KIND_STATE) e = make_pattern_engine(p, why1);
-    else e = make_single_engine(p, why2);
+    if (p.kind == SHD_KIND_STATE) {
+      // the 2-state every-pattern shape (P1/P3) has a dedicated forward-scan
+      // engine; every other state plan runs on the generic per-key NFA
+      e = make_pattern_engine(p, why1);
+      if (!e) e = make_nfa_engine(p, why2);
+      if (!e) why1 += "; ";
+    } else {
+      e = make_single_engine(p, why2);
+    }
     if (!e) return fail(SHD_E_UNSUPPORTED, "plan outside the device path: " + why1 + why2);
     e->plan = p;
     e->ex.upload(p);
     e->out.init((int)p.outputs.size());
+    e->on_loaded();
     SHD_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     SHD_HIP(hipEventCreate(&e->ev0));
     SHD_HIP(hipEventCreate(&e->ev1));

@@ -26,6 +26,33 @@ W2_LENGTH_APP = ("@app:playback " + STOCK_DEF + " @info(name='q') from StockStre
 W2_TIME_APP = ("@app:playback " + STOCK_DEF + " @info(name='q') from StockStream[price>60]#window.time(10 sec) "
                "select symbol, avg(price) as a, sum(price) as s, count() as c group by symbol insert into O2;")
 
+# config S4: counting sequence with e2[last], logical and/or,
+# absent `not ... for`
+S4_SEQ_QUERY = ("@info(name='q') from every e1=StockStream, e2=StockStream[price>e1.price]<2:5>, "
+                "e3=StockStream[price<e2[last].price] "
+                "select e1.price as p1, e2[0].price as p2a, e2[last].price as p2z, e3.price as p3 insert into O;")
+S4_SEQPLUS_QUERY = ("@info(name='q') from every e1=StockStream, e2=StockStream[price>e1.price]+, "
+                    "e3=StockStream[price<e2[last].price] "
+                    "select e1.price as p1, e2[0].price as p2a, e2[last].price as p2z, e3.price as p3 insert into O;")
+S4_OR_QUERY = ("@info(name='q') from every e1=StockStream[price>70] -> "
+               "(e2=StockStream[price>e1.price] or e3=StockStream[price<e1.price*0.9]) "
+               "select e1.price as p1, e2.price as p2, e3.price as p3 insert into O;")
+S4_AND_QUERY = ("@info(name='q') from every e1=StockStream[price>70] -> "
+                "e2=StockStream[price>e1.price*1.2] and e3=StockStream[price<e1.price*0.8] within 1 sec "
+                "select e1.price as p1, e2.price as p2, e3.price as p3 insert into O;")
+S4_NOT_QUERY = ("@info(name='q') from every e1=StockStream[price>98] -> "
+                "not StockStream[price>e1.price] for 1 sec "
+                "select e1.symbol as symbol, e1.price as p1 insert into O;")
+S4_BARE_QUERY = ("@info(name='q') from e1=StockStream, e2=StockStream[price>e1.price]<2:5>, "
+                 "e3=StockStream[price<e2[last].price] "
+                 "select e1.price as p1, e2[last].price as p2z, e3.price as p3 insert into O;")
+S4_APPS = {k: "@app:playback " + STOCK_DEF + " " + q for k, q in
+           (("seq", S4_SEQ_QUERY), ("seqplus", S4_SEQPLUS_QUERY), ("or", S4_OR_QUERY), ("and", S4_AND_QUERY), ("not", S4_NOT_QUERY),
+            ("bare", S4_BARE_QUERY))}
+S4_PART_APPS = {k: "@app:playback " + STOCK_DEF + " partition with (symbol of StockStream) begin " + q + " end;"
+                for k, q in (("seq", S4_SEQ_QUERY), ("seqplus", S4_SEQPLUS_QUERY), ("or", S4_OR_QUERY), ("and", S4_AND_QUERY),
+                             ("not", S4_NOT_QUERY))}
+
 CONFIGS = {
     # name: (app, n_events, n_keys, delta_ms)
     "P1": (P1_APP, 1_000_000, 1_000, 1.0),
@@ -33,6 +60,12 @@ CONFIGS = {
     "W2-time": (W2_TIME_APP, 100_000_000, 1_000, 0.1),
     "P3": (P3_APP, 100_000_000, 10_000_000, 0.01),
     "P3-dense": (P3_APP, 100_000_000, 10_000_000, 1e-5),
+    "S4-seq": (S4_APPS["seq"], 1_000_000, 1_000, 1.0),
+    "S4-or": (S4_APPS["or"], 1_000_000, 1_000, 1.0),
+    "S4-and": (S4_APPS["and"], 1_000_000, 1_000, 1.0),
+    "S4-not": (S4_APPS["not"], 1_000_000, 1_000, 1.0),
+    "S4-seqplus": (S4_APPS["seqplus"], 1_000_000, 1_000, 1.0),
+    "S4P-seqplus": (S4_PART_APPS["seqplus"], 10_000_000, 100_000, 0.01),
 }
 
 

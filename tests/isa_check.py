@@ -43,6 +43,9 @@ def scan(path):
             continue
         if op.startswith("v_") and set(srcs) & tainted and "lshl_add_u64" in op:
             bad.append((kern, ln, line.strip()))
+        # VOP3b forms (v_mad_u64_u32, v_*_co_*) also write an SGPR carry-out as operand 1
+        if len(args) > 1 and (op.startswith(("v_mad_u64_u32", "v_mad_i64_i32")) or "_co_" in op or op.endswith("_co")):
+            tainted.difference_update(regs(args[1].split()[0]))
         if args:
             dst = regs(args[0])
             if dst:

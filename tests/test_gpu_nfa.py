@@ -1,0 +1,131 @@
+"""Generic per-key NFA engine (libsiddhi_hip engine 4) vs the CPU oracle:
+config S4 shapes (counting sequences with e2[last], logical and/or, absent
+`not ... for` with playback timers), unpartitioned and inside
+`partition with`, across micro-batch splits and per-event calls.  Every
+output row (values, nulls, timestamps, event types, callback chunking) must
+be identical."""
+import os
+
+import numpy as np
+import pytest
+
+from parity import assert_same_rows, compile_single_query, run_device, run_oracle, stock_batch
+from siddhi_amd import workloads as wl
+
+pytestmark = pytest.mark.gpu
+
+ENGINE_NFA = 4
+
+
+def split(sym, price, vol, ts, parts, call=1024):
+    n = len(ts)
+    cuts = sorted(set([0, n] + [int(n * k / parts) // call * call for k in range(1, parts)]))
+    return [(0, stock_batch(sym[a:b], price[a:b], vol[a:b], ts[a:b], call)) for a, b in zip(cuts[:-1], cuts[1:])
+            if b > a]
+
+
+UNPART = [(k, wl.S4_APPS[k]) for k in ("seq", "seqplus", "or", "and", "not", "bare")]
+PART = [("P" + k, wl.S4_PART_APPS[k]) for k in ("seq", "seqplus", "or", "and", "not")]
+
+
+@pytest.mark.parametrize("name,app", UNPART, ids=[c[0] for c in UNPART])
+@pytest.mark.parametrize("parts", [1, 3])
+def test_s4_unpartitioned_equals_oracle(hip_available, name, app, parts):
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(12000, 1000, 1.0, seed_offset=hash(name) % 1000)
+    batches = split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == ENGINE_NFA
+    assert_same_rows(dev, ora)
+    assert counters["events"] == len(ts)
+
+
+@pytest.mark.parametrize("name,app", PART, ids=[c[0] for c in PART])
+@pytest.mark.parametrize("parts", [1, 4])
+def test_s4_partitioned_equals_oracle(hip_available, name, app, parts):
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(60000, 300, 1.0, seed_offset=hash(name) % 1000)
+    batches = split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == ENGINE_NFA
+    if name != "Pseq":
+        assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+
+
+@pytest.mark.parametrize("name", ["seqplus", "or", "not"])
+def test_s4_single_event_calls(hip_available, name):
+    # B = 1: every InputHandler call carries one event (per-call time advance and timers)
+    qp, _ = compile_single_query(wl.S4_APPS[name])
+    sym, price, vol, ts = wl.stock_stream(3000, 20, 3.0, seed_offset=5)
+    batches = [(0, stock_batch(sym, price, vol, ts, call_size=1))]
+    assert_same_rows(run_device(qp, batches)[0], run_oracle(qp, batches))
+
+
+def test_absent_timer_fires_on_set_time(hip_available):
+    """`not ... for` partials complete on a playback time change alone
+    (Scheduler.onTimeChange from InputHandler-less setCurrentTimestamp)."""
+    from oracle_engine import OracleQueryEngine
+    from parity import concat_rows
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
+    app = wl.S4_PART_APPS["not"]
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(4000, 40, 1.0, seed_offset=9)
+    b = stock_batch(sym, price, vol, ts)
+    t_end = int(ts[-1]) + 5000
+    # oracle
+    eng = OracleQueryEngine(qp, None)
+    parts = []
+    cid = 0
+    offs = b.call_offsets
+    from siddhi_amd.runtime import ColumnBatch
+    for c in range(len(offs) - 1):
+        s, e = int(offs[c]), int(offs[c + 1])
+        sub = ColumnBatch(b.ts[s:e], [x[s:e] for x in b.cols], [None] * 3)
+        for ch in eng.set_time(int(b.ts[e - 1])) + eng.push(0, sub):
+            parts.append((np.full(len(ch.ts), cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+            cid += 1
+    for ch in eng.set_time(t_end):
+        parts.append((np.full(len(ch.ts), cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+        cid += 1
+    eng.close()
+    ora = concat_rows(parts)
+    # device
+    dq = DeviceQuery(qp.ir)
+    dev_parts = []
+    cols = [np.ascontiguousarray(x) for x in b.cols]
+    tts = np.ascontiguousarray(b.ts, np.int64)
+    dq.push_raw(0, b.n, tts.ctypes.data, [x.ctypes.data for x in cols], [0] * 3, SHD_MEM_HOST, b.call_offsets, True)
+    r = dq.poll()
+    if r is not None:
+        dev_parts.append(r)
+    n_before = sum(len(p[2]) for p in dev_parts)
+    dq.set_time(t_end)
+    r = dq.poll()
+    if r is not None:
+        dev_parts.append(r)
+    dq.close()
+    dev = concat_rows(dev_parts)
+    assert len(dev[2]) > n_before   # the time change alone completed partials
+    assert_same_rows(dev, ora)
+
+
+def test_capacity_overflow_is_reported(hip_available, monkeypatch):
+    """A per-key pending list that overflows raises SHD_E_CAPACITY (never drops)."""
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST, SiddhiHipError, SHD_E_CAPACITY
+    monkeypatch.setenv("SHD_NFA_LIST", "4")
+    qp, _ = compile_single_query(wl.S4_APPS["and"])
+    sym, price, vol, ts = wl.stock_stream(5000, 1000, 1.0, seed_offset=2)
+    b = stock_batch(sym, price, vol, ts)
+    dq = DeviceQuery(qp.ir)
+    try:
+        cols = [np.ascontiguousarray(x) for x in b.cols]
+        tts = np.ascontiguousarray(b.ts, np.int64)
+        with pytest.raises(SiddhiHipError) as ei:
+            dq.push_raw(0, b.n, tts.ctypes.data, [x.ctypes.data for x in cols], [0] * 3, SHD_MEM_HOST,
+                        b.call_offsets, True)
+        assert ei.value.code == SHD_E_CAPACITY
+    finally:
+        dq.close()
