@@ -27,7 +27,10 @@ struct Error : std::runtime_error {
                          std::string(#call) + ": " + hipGetErrorString(e_));           \
   } while (0)
 
-#define SHD_CHECK_LAUNCH() SHD_HIP(hipGetLastError())
+// Launch check.  With SHD_SYNC_CHECK=1 in the environment every launch is
+// also synchronised, so a faulting kernel is reported at its own launch site.
+void check_launch(const char* file, int line);
+#define SHD_CHECK_LAUNCH() ::shd::check_launch(__FILE__, __LINE__)
 
 constexpr int kBlock = 256;
 constexpr int kMaxCols = 16;      // attributes per stream handled on device

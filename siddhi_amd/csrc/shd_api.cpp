@@ -1,11 +1,24 @@
 // shd_api.cpp -- the C-ABI of libsiddhi_hip (include/siddhi_hip.h): plan
 // decoding, engine selection, batch staging, output polling.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "engine.h"
 
 namespace shd {
+
+void check_launch(const char* file, int line) {
+  static const bool sync = [] {
+    const char* v = std::getenv("SHD_SYNC_CHECK");
+    return v && *v && *v != '0';
+  }();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && sync) e = hipDeviceSynchronize();
+  if (e != hipSuccess)
+    throw Error(e == hipErrorOutOfMemory ? SHD_E_OOM : SHD_E_DEVICE,
+                std::string("kernel launched at ") + file + ":" + std::to_string(line) + ": " + hipGetErrorString(e));
+}
 
 // ------------------------------------------------------------------ plan decode
 namespace {
