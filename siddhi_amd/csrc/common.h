@@ -45,6 +45,19 @@ inline int grid_for(int64_t n, int per_thread = 1, int cap = 256 * 64) {
   return (int)g;
 }
 
+// One thread per element, no grid-stride loop.  Kernels that stage their
+// expression program in LDS use this form: their loops then never read the
+// hidden launch-geometry kernel arguments (hipcc reads gridDim.x with a vector
+// load from the kernarg segment when it is used below divergent staging loops,
+// and vector loads from the kernarg segment fault on the MI355X pool; the ISA
+// test tests/test_kernel_isa.py enforces this).  Body: `for (i = blockIdx.x *
+// kBlock + threadIdx.x; i < n; i = n)` -- a loop that runs at most once, so
+// `continue` keeps working.
+inline unsigned grid_cover(int64_t n) {
+  int64_t g = ceil_div(n, kBlock);
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
 // ------------------------------------------------------------------ device buffers
 // Grow-only device allocation owned by an engine (allocated outside launch
 // sequences so push() can be captured into a hipGraph later).

@@ -341,10 +341,13 @@ struct LdsProg {
   uint64_t consts[kLdsConsts];
 };
 
-// Cooperative copy; every thread of the block must call it (contains a barrier).
+// Cooperative copy; every thread of the block must call it (contains a
+// barrier).  NT = the kernel's block size (a constant: no launch-geometry
+// kernel argument is read, see grid_cover in common.h).
+template <int NT = kBlock>
 __device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
-  for (int i = threadIdx.x; i < g.nins; i += blockDim.x) s.ins[i] = g.ins[i];
-  for (int i = threadIdx.x; i < g.nconsts; i += blockDim.x) s.consts[i] = g.consts[i];
+  for (int i = threadIdx.x; i < g.nins; i += NT) s.ins[i] = g.ins[i];
+  for (int i = threadIdx.x; i < g.nconsts; i += NT) s.consts[i] = g.consts[i];
   __syncthreads();
   DExprSet l;
   l.ins = s.ins;

@@ -1102,14 +1102,14 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   {
     const int* src = reinterpret_cast<const int*>(gprog);
     int* dst = reinterpret_cast<int*>(&sprog);
-    for (int i = threadIdx.x; i < (int)(sizeof(NfaProg) / 4); i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(NfaProg) / 4); i += kLaneBlock) dst[i] = src[i];
     const int* s2 = reinterpret_cast<const int*>(glay);
     int* d2 = reinterpret_cast<int*>(&slay);
-    for (int i = threadIdx.x; i < (int)(sizeof(NfaLayout) / 4); i += blockDim.x) d2[i] = s2[i];
+    for (int i = threadIdx.x; i < (int)(sizeof(NfaLayout) / 4); i += kLaneBlock) d2[i] = s2[i];
   }
   const NfaRunArgs& a = *ap;
-  const DExprSet es = stage_prog(a.es, prog);   // contains the barrier
-  const int64_t lane_id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const DExprSet es = stage_prog<kLaneBlock>(a.es, prog);   // contains the barrier
+  const int64_t lane_id = (int64_t)blockIdx.x * kLaneBlock + threadIdx.x;
   if (lane_id >= a.nlanes) return;
   int64_t seg, slot;
   if (a.lanes_over_slots) {
@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   unsigned long long m = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     BatchCtx cx{&a.batch, i};
     Val kv = a.key_col >= 0 ? col_load(a.batch, i, a.key_col)
                             : eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
@@ -1776,7 +1776,7 @@ struct NfaEngine : Engine {
     ka.key_col = key_col[si];
     ka.key_type = key_type[si];
     SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
-    hipLaunchKernelGGL(k_nfa_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(ka), n, d_key.as<uint64_t>(),
+    hipLaunchKernelGGL(k_nfa_keys, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ka), n, d_key.as<uint64_t>(),
                        d_keyed.as<uint32_t>(), &d_ctl.as<NfaCtl>()->kmax);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_nfa_run_starts, dim3(grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)d_keyed.as<uint32_t>(),

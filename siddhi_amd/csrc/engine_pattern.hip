@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   const ExtRows& x = a.x;
   unsigned long long created = 0, kmax = 0;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_ext; r += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r = n_ext) {
     uint32_t f;
     uint64_t k = 0;
     if (r < x.C) {
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   uint64_t steps = 0, pruned = 0;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_ext; p += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p = n_ext) {
     const uint32_t pvp = spv[p];
     uint32_t m = 0, o = 0;
     if (pv_flags(pvp) & F_CAND) {
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < m; k = m) {
     int64_t j = pj[k], i = pi[k];
     PairCtx cx{&x, i, j};
     int64_t row = a.row0 + k;
@@ -512,7 +512,7 @@ struct PatternEngine : Engine {
     std::memcpy(h_agg.p, &init, sizeof(init));
     std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_prepare, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_k32.as<uint32_t>(),
+    hipLaunchKernelGGL(k_prepare, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_k32.as<uint32_t>(),
                        d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_pa);
     SHD_CHECK_LAUNCH();
     SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
@@ -570,10 +570,10 @@ struct PatternEngine : Engine {
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     if (sorted64)
-      hipLaunchKernelGGL(k_forward_scan<true>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
+      hipLaunchKernelGGL(k_forward_scan<true>, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
                          skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
     else
-      hipLaunchKernelGGL(k_forward_scan<false>, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
+      hipLaunchKernelGGL(k_forward_scan<false>, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
                          skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
@@ -626,7 +626,7 @@ struct PatternEngine : Engine {
       pr.multi = (sA == sB);
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
-      hipLaunchKernelGGL(k_project, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
+      hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
                          out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
       SHD_CHECK_LAUNCH();
       out.count += m;

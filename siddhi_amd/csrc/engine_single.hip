@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict_
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     RowCtx cx{&cs, i, nullptr, nullptr};
     uint8_t f = 0;
     bool keyed = true;
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
     int64_t row = a.row0 + off[i];
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
     int64_t t = a.C + off[i];
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
-  for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nnew; t0 += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < nnew; t0 = nnew) {
     if (!fcnt[t0]) continue;
     int64_t tf = a.C + t0;
     int64_t tl = last_of[tf];
@@ -614,7 +614,7 @@ struct SingleEngine : Engine {
       fa.key_col = key_col;
       fa.key_type = key_type;
     }
-    hipLaunchKernelGGL(k_filter, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(fa), n, d_flags.as<uint8_t>(),
+    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(fa), n, d_flags.as<uint8_t>(),
                        d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
     SHD_CHECK_LAUNCH();
     uint32_t* d_m = (uint32_t*)d_tot.p;
@@ -670,7 +670,7 @@ struct SingleEngine : Engine {
       // exclusive run ids: the run of event i is start-scan[i] (+0 if i is a start it is its own index)
       pa.chunk0 = chunk_seq;
       pa.partitioned = partitioned;
-      hipLaunchKernelGGL(k_project_rows, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(pa), n,
+      hipLaunchKernelGGL(k_project_rows, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(pa), n,
                          (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                          (const int32_t*)d_call_of.as<int32_t>(), (const uint32_t*)d_run.as<uint32_t>(),
                          (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
@@ -767,7 +767,7 @@ struct SingleEngine : Engine {
       ia.group_type = group_type;
     }
     ia.C = C;
-    hipLaunchKernelGGL(k_make_items, dim3(grid_for(n)), dim3(kBlock), 0, s, dev_args(ia), n,
+    hipLaunchKernelGGL(k_make_items, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ia), n,
                        (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
                        ikey[cur].as<uint64_t>(), its[cur].as<int64_t>(), iargv[cur].as<uint64_t>(),
@@ -882,7 +882,7 @@ struct SingleEngine : Engine {
           ea.C = C;
           ea.row0 = out.count;
           ea.chunk0 = chunk_seq;
-          hipLaunchKernelGGL(k_emit, dim3(grid_for(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
+          hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
                              (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
                              (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
                              (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(), out.d_chunk(),
