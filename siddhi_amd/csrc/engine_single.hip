@@ -21,6 +21,8 @@
 // Emission: one row per (call, group) with a CURRENT event, in first-seen
 // order, carrying the values after the group's last event of the call.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "engine.h"
 
@@ -614,7 +616,9 @@ struct SingleEngine : Engine {
       fa.key_col = key_col;
       fa.key_type = key_type;
     }
-    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(fa), n, d_flags.as<uint8_t>(),
+    const FilterArgs* d_fa = dev_args(fa);
+    if (std::getenv("SHD_DEBUG_ARGS")) debug_filter_args(d_fa, fa, n);
+    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, d_fa, n, d_flags.as<uint8_t>(),
                        d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
     SHD_CHECK_LAUNCH();
     uint32_t* d_m = (uint32_t*)d_tot.p;
@@ -639,6 +643,40 @@ struct SingleEngine : Engine {
       if (last > now) now = last;
     }
     seq += n;
+  }
+
+  // Debug hook (SHD_DEBUG_ARGS=1): read the argument block back from the
+  // device, print it with the allocation each pointer belongs to, and stop
+  // before the launch.
+  void debug_filter_args(const FilterArgs* d_fa, const FilterArgs& fa, int64_t n) {
+    SHD_HIP(hipStreamSynchronize(stream));
+    FilterArgs h{};
+    SHD_HIP(hipMemcpy(&h, d_fa, sizeof(h), hipMemcpyDeviceToHost));
+    auto where = [](const void* p) {
+      if (!p) return std::string("null");
+      hipPointerAttribute_t at{};
+      hipError_t e = hipPointerGetAttributes(&at, p);
+      char buf[160];
+      std::snprintf(buf, sizeof buf, "%p type=%d dev=%d err=%d", p, e == hipSuccess ? (int)at.type : -1,
+                    e == hipSuccess ? at.device : -1, (int)e);
+      (void)hipGetLastError();
+      return std::string(buf);
+    };
+    std::fprintf(stderr, "SHD_DEBUG_ARGS k_filter n=%lld same=%d sizeof=%zu\n", (long long)n,
+                 (int)(std::memcmp(&h, &fa, sizeof(h)) == 0), sizeof(h));
+    std::fprintf(stderr, "  es.ins %s nins=%d consts %s nconsts=%d\n", where(h.es.ins).c_str(), h.es.nins,
+                 where(h.es.consts).c_str(), h.es.nconsts);
+    for (int c = 0; c < h.cs.ncols; c++)
+      std::fprintf(stderr, "  col[%d] %s nul %s type=%d\n", c, where(h.cs.col[c]).c_str(), where(h.cs.nul[c]).c_str(),
+                   (int)h.cs.type[c]);
+    std::fprintf(stderr, "  ts %s n=%lld ncols=%d filters.n=%d f0=(%d,%d) part=%d\n", where(h.cs.ts).c_str(),
+                 (long long)h.cs.n, h.cs.ncols, h.filters.n, h.filters.f[0].off, h.filters.f[0].len, h.partitioned);
+    std::fprintf(stderr, "  flags %s cnt %s pkey %s argdev %s\n", where(d_flags.p).c_str(), where(d_cnt.p).c_str(),
+                 where(d_pkey.p).c_str(), where(d_fa).c_str());
+    std::vector<int4> ins(std::max(h.es.nins, 1));
+    SHD_HIP(hipMemcpy(ins.data(), h.es.ins, h.es.nins * sizeof(int4), hipMemcpyDeviceToHost));
+    for (int i = 0; i < h.es.nins; i++) std::fprintf(stderr, "  ins[%d] = %d %d %d %d\n", i, ins[i].x, ins[i].y, ins[i].z, ins[i].w);
+    throw Error(SHD_E_DEVICE, "SHD_DEBUG_ARGS: stopped before k_filter");
   }
 
   void push_filter(const Staged& b, int64_t ncalls, int64_t n) {

@@ -1,0 +1,115 @@
+"""Key-hash routing of micro-batches across GPUs.
+
+A partitioned query keeps all of its state per partition key
+(PartitionStateHolder.getState, modules/siddhi-core/src/main/java/io/siddhi/
+core/util/snapshot/state/PartitionStateHolder.java:43-48; per-key seeding in
+PartitionStreamReceiver.send, .../partition/PartitionStreamReceiver.java:262-283),
+so keys are sharded over ranks: owner(key) = hash32(key) % world.  Input that
+arrives pre-partitioned is pushed by its owner directly.  Input that does not
+is re-routed with ONE all-to-all per micro-batch (torch.distributed: backend
+"nccl" is RCCL over xGMI on MI355X, "gloo" in the CPU tests): every rank
+buckets its events by owner, exchanges bucket sizes, then the packed event
+rows; the receiver restores global arrival order with a stable sort on the
+event sequence number.  Per key this reproduces exactly the event order and
+InputHandler-call membership the reference sees, which is all a partitioned
+query's output depends on.
+
+Columns travel as one packed int64 matrix (one collective for all columns):
+int32 / uint32 ids widen to int64, float64 travels as its bit pattern.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+_M32 = 0xFFFFFFFF
+
+
+def hash32(keys: torch.Tensor) -> torch.Tensor:
+    """Murmur3 fmix32 of the low 32 bits of integer keys (dictionary ids)."""
+    x = keys.to(torch.int64) & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & _M32
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & _M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def owner_of(keys: torch.Tensor, world: int) -> torch.Tensor:
+    return hash32(keys) % world
+
+
+def pack(cols: List[torch.Tensor]) -> torch.Tensor:
+    """[n, k] int64 matrix; float64 columns by bit pattern, int columns widened."""
+    out = []
+    for c in cols:
+        if c.dtype == torch.float64:
+            out.append(c.view(torch.int64))
+        elif c.dtype == torch.float32:
+            out.append(c.view(torch.int32).to(torch.int64))
+        else:
+            out.append(c.to(torch.int64))
+    return torch.stack(out, dim=1).contiguous()
+
+
+def unpack(m: torch.Tensor, dtypes: List[torch.dtype]) -> List[torch.Tensor]:
+    cols = []
+    for j, dt in enumerate(dtypes):
+        c = m[:, j].contiguous()
+        if dt == torch.float64:
+            cols.append(c.view(torch.float64))
+        elif dt == torch.float32:
+            cols.append(c.to(torch.int32).view(torch.float32))
+        else:
+            cols.append(c.to(dt))
+    return cols
+
+
+def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int,
+          group: Optional[dist.ProcessGroup] = None) -> Tuple[List[torch.Tensor], torch.Tensor, Dict[str, int]]:
+    """All-to-all re-route of one micro-batch by key owner.
+
+    cols: the event columns (1-D, equal length, any of int32/int64/float64);
+    key:  the partition key of every event (integer ids);
+    seq:  global arrival sequence numbers (int64).
+    Returns (received columns, received seq, stats), in increasing seq order.
+    """
+    dtypes = [c.dtype for c in cols]
+    if world == 1:
+        order = torch.argsort(seq, stable=True)
+        return [c[order] for c in cols], seq[order], {"sent": 0, "received": 0}
+    owner = owner_of(key, world)
+    order = torch.argsort(owner, stable=True)
+    send = pack(list(cols) + [seq])[order]
+    counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    k = send.shape[1]
+    in_splits = (counts * k).tolist()
+    out_splits = (recv_counts * k).tolist()
+    recv = torch.empty(int(sum(out_splits)), dtype=torch.int64, device=send.device)
+    dist.all_to_all_single(recv, send.reshape(-1), out_splits, in_splits, group=group)
+    recv = recv.view(-1, k)
+    rseq = recv[:, k - 1].contiguous()
+    o = torch.argsort(rseq, stable=True)
+    recv = recv[o]
+    out = unpack(recv[:, :k - 1], dtypes)
+    rank = dist.get_rank(group)
+    stats = {"sent": int(counts.sum().item() - counts[rank].item()),
+             "received": int(recv_counts.sum().item() - recv_counts[rank].item())}
+    return out, recv[:, k - 1].contiguous(), stats
+
+
+def call_offsets_from_seq(seq: torch.Tensor, call_size: int) -> torch.Tensor:
+    """InputHandler-call boundaries of a seq-sorted event slice: calls of the
+    global stream are consecutive runs of `call_size` sequence numbers."""
+    n = seq.numel()
+    if n == 0:
+        return torch.zeros(1, dtype=torch.int64)
+    call = seq // call_size
+    starts = torch.nonzero(torch.cat([torch.ones(1, dtype=torch.bool, device=seq.device),
+                                      call[1:] != call[:-1]])).flatten()
+    return torch.cat([starts.to(torch.int64).cpu(), torch.tensor([n], dtype=torch.int64)])

@@ -93,6 +93,27 @@ def stock_stream(n: int, n_keys: int, delta_ms: float, seed_offset: int = 0, sta
     return symbol, price, volume, ts
 
 
+def stock_stream_at(idx: np.ndarray, n_keys: int, delta_ms: float, seed_offset: int = 0):
+    """The same columns as stock_stream for an arbitrary set of global event
+    indices (the generator is counter based: event g, column j draws output
+    3*g + j + 1 of the SplitMix64 sequence)."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    base = np.uint64(SEED + seed_offset)
+    g = np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        cols = []
+        for j in range(3):
+            z = (np.uint64(3) * idx + np.uint64(j + 1)) * g + base
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            cols.append(z ^ (z >> np.uint64(31)))
+    symbol = (cols[0] % np.uint64(n_keys)).astype(np.uint32)
+    price = 50.0 + 50.0 * ((cols[1] >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53)))
+    volume = (cols[2] % np.uint64(1000)).astype(np.int64) + 1
+    ts = (T0 + np.floor(idx.astype(np.float64) * delta_ms)).astype(np.int64)
+    return symbol, price, volume, ts
+
+
 def call_offsets(n: int, call_size: int = 1024) -> np.ndarray:
     offs = np.arange(0, n, call_size, dtype=np.int64)
     return np.append(offs, np.int64(n))
