@@ -330,31 +330,25 @@ struct DExprSet {
   int nins, nconsts;
 };
 
-// The whole expression program of a plan is staged into LDS at kernel start:
-// every lane of a wave decodes the same (uniform) instruction stream, so LDS
-// broadcast reads replace dependent global loads in the interpreter loop.
-// Plans that do not fit are rejected at load (DevExprTable::upload).
+// Expression program placement.  Staging the program into LDS at kernel start
+// (every lane decodes the same uniform instruction stream) was measured to
+// fault on the MI355X pool in the single-stream kernels (k_filter: memory
+// aperture violation for any batch size, while the identical kernels reading
+// the program from global memory pass: scripts/probe_filter.py, DESIGN.md
+// "LDS program staging").  The program therefore stays in global memory,
+// where the uniform instruction reads are served by the scalar/L1 caches;
+// stage_prog keeps the call sites and reserves no LDS.  Plans larger than
+// the former LDS store are still rejected at load (DevExprTable::upload).
 constexpr int kLdsIns = 256;
 constexpr int kLdsConsts = 64;
 struct LdsProg {
-  int4 ins[kLdsIns];
-  uint64_t consts[kLdsConsts];
+  int4 ins[1];
 };
 
-// Cooperative copy; every thread of the block must call it (contains a
-// barrier).  NT = the kernel's block size (a constant: no launch-geometry
-// kernel argument is read, see grid_cover in common.h).
 template <int NT = kBlock>
 __device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
-  for (int i = threadIdx.x; i < g.nins; i += NT) s.ins[i] = g.ins[i];
-  for (int i = threadIdx.x; i < g.nconsts; i += NT) s.consts[i] = g.consts[i];
-  __syncthreads();
-  DExprSet l;
-  l.ins = s.ins;
-  l.consts = s.consts;
-  l.nins = g.nins;
-  l.nconsts = g.nconsts;
-  return l;
+  (void)s;
+  return g;
 }
 
 // Conjunction of up to 4 filter expressions (FilterProcessor chain).

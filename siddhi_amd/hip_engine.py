@@ -17,7 +17,7 @@ from . import planner as pl
 from .runtime import OutputChunk, split_chunks
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsiddhi_hip.so")
+LIB_PATH = os.environ.get("SHD_LIB") or os.path.join(_HERE, "libsiddhi_hip.so")
 
 SHD_OK, SHD_E_INVALID_PLAN, SHD_E_UNSUPPORTED, SHD_E_OOM, SHD_E_DEVICE, SHD_E_CAPACITY, SHD_E_ARG = \
     0, -1, -2, -3, -4, -5, -6
