@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=25_000_000, help="micro-batch size (events)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
+    ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
+                    help="roundrobin: every rank holds a round-robin share of the global stream and events are "
+                         "re-routed to their key's owner with one RCCL all-to-all per micro-batch (default for N>1)")
     return ap.parse_args()
 
 
@@ -57,6 +60,28 @@ def gen_device_columns(torch, n, keys, delta, seed_offset, key_base, dev):
         vol[a:b] = torch.from_numpy(v)
         ts[a:b] = torch.from_numpy(t)
     return sym, price, vol, ts
+
+
+def gen_roundrobin_columns(torch, n, keys_total, delta, rank, world, dev):
+    """Rank `rank`'s round-robin share (global events rank, rank+world, ...) of one
+    global StockStream over keys_total keys, resident in HBM, with global seq."""
+    from siddhi_amd import workloads as wl
+    sym = torch.empty(n, dtype=torch.int32, device=dev)
+    price = torch.empty(n, dtype=torch.float64, device=dev)
+    vol = torch.empty(n, dtype=torch.int64, device=dev)
+    ts = torch.empty(n, dtype=torch.int64, device=dev)
+    seq = torch.empty(n, dtype=torch.int64, device=dev)
+    chunk = 5_000_000
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        idx = np.arange(a, b, dtype=np.int64) * world + rank
+        s_, p_, v_, t_ = wl.stock_stream_at(idx, keys_total, delta, seed_offset=0)
+        sym[a:b] = torch.from_numpy(s_.astype(np.int32))
+        price[a:b] = torch.from_numpy(p_)
+        vol[a:b] = torch.from_numpy(v_)
+        ts[a:b] = torch.from_numpy(t_)
+        seq[a:b] = torch.from_numpy(idx)
+    return sym, price, vol, ts, seq
 
 
 def alg_bytes_pattern(c, n):
@@ -131,26 +156,51 @@ def main():
     else:
         qp = plan_query(qa, item, StringDictionary())
 
-    # inputs resident in HBM before the timed region; rank r owns key slice r (pre-partitioned)
-    sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=rank * keys, dev=dev)
+    mode = args.input if args.input != "auto" else ("prepartitioned" if world == 1 else "roundrobin")
+    if mode == "roundrobin" and not pattern:
+        mode = "prepartitioned"   # window configs are unpartitioned: replicas
+    # inputs resident in HBM before the timed region
+    if mode == "prepartitioned":
+        # rank r owns key slice r and its own events (no data-path collective)
+        sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=rank * keys, dev=dev)
+        seqs = None
+    else:
+        # one global stream over world*keys keys, held round-robin; re-routed per micro-batch
+        sym, price, vol, ts, seqs = gen_roundrobin_columns(torch, n, keys * world, delta, rank, world, dev)
     torch.cuda.synchronize()
+    from siddhi_amd import exchange as ex
     he.context(local)
     dq = he.DeviceQuery(qp.ir, device=local)
     batch = min(args.batch, n)
     cuts = list(range(0, n, batch)) + [n]
     offs_all = wl.call_offsets(n)
 
+    routed_total = [0]
+
     def run_step(collect=None):
         dq.reset()
         tot = {}
         for a, b in zip(cuts[:-1], cuts[1:]):
-            # InputHandler calls of 1024 events inside the micro-batch
-            lo = np.searchsorted(offs_all, a)
-            hi = np.searchsorted(offs_all, b)
-            co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
-            cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
-            dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE,
-                        co.astype(np.int64), True)
+            if seqs is None:
+                # InputHandler calls of 1024 events inside the micro-batch
+                lo = np.searchsorted(offs_all, a)
+                hi = np.searchsorted(offs_all, b)
+                co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
+                cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
+                dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE,
+                            co.astype(np.int64), True)
+            else:
+                # RCCL all-to-all: every event to its key's owner, arrival order restored by seq
+                (rs, rp, rv, rt), rseq, _ = ex.route([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b],
+                                                     seqs[a:b], world)
+                m = rs.numel()
+                routed_total[0] += m
+                if m == 0:
+                    continue
+                co = ex.call_offsets_from_seq(rseq, 1024).numpy()   # (host copy: orders torch's stream)
+                torch.cuda.current_stream().synchronize()   # routed columns complete before the engine's stream reads them
+                dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
+                            he.SHD_MEM_DEVICE, co.astype(np.int64), True)
             dq.discard()
             if collect is not None:
                 for k, v in dq.stage_times().items():
@@ -189,9 +239,9 @@ def main():
     dominant = max(stages, key=stages.get) if stages else None
     step_dev_ns = sum(stages.values())
     if pattern:
-        bytes_step, derived = alg_bytes_pattern(counters, n)
+        bytes_step, derived = alg_bytes_pattern(counters, counters["events"])
     else:
-        bytes_step, derived = alg_bytes_window(counters, n, len(qp.output_names))
+        bytes_step, derived = alg_bytes_window(counters, counters["events"], len(qp.output_names))
     launches = len(cuts) - 1
     roof = None
     if dominant:
@@ -225,7 +275,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
             "config": {"workload": args.config, "events_per_gpu": n, "keys_per_gpu": keys, "delta_ms": delta,
-                       "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world},
+                       "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world,
+                       "input": mode + (" (RCCL all-to-all re-route)" if mode == "roundrobin" else "")},
             "matches_per_s": round(matches_per_s, 1),
             "counters": {k: counters[k] for k in ("events", "matches", "partials", "partial_scans", "carry")},
             "derived": {k: round(v, 4) for k, v in derived.items()},
