@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=25_000_000, help="micro-batch size (events)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
+    ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
     ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
                     help="roundrobin: every rank holds a round-robin share of the global stream and events are "
                          "re-routed to their key's owner with one RCCL all-to-all per micro-batch (default for N>1)")
@@ -177,7 +178,7 @@ def main():
 
     routed_total = [0]
 
-    def run_step(collect=None):
+    def run_step(collect=None, cuts=cuts):
         dq.reset()
         tot = {}
         for a, b in zip(cuts[:-1], cuts[1:]):
@@ -208,6 +209,23 @@ def main():
         if collect is not None:
             collect.append(tot)
         return dq.counters()
+
+    for sb in [int(x) for x in args.sweep_batches.split(",") if x]:
+        # micro-batch size sweep (diagnostic): same data, same query
+        sc = list(range(0, n, sb)) + [n]
+        run_step(cuts=sc)
+        torch.cuda.synchronize()
+        sr = []
+        t0 = time.perf_counter()
+        for _ in range(max(args.steps, 1)):
+            run_step(sr, cuts=sc)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / max(args.steps, 1)
+        st = {k: round(sum(r.get(k, 0) for r in sr) / len(sr) / 1e6, 3) for k in sr[0]} if sr else {}
+        if rank == 0:
+            print(json.dumps({"sweep_batch": sb, "ms_per_step": round(dt * 1e3, 3),
+                              "events_per_s": round(n * world / dt, 1), "stage_ms_per_step": st}),
+                  file=sys.stderr, flush=True)
 
     for _ in range(args.warmup):
         run_step()

@@ -1202,13 +1202,13 @@ __device__ __forceinline__ uint64_t canon_key(Val v, int type) {
 }
 
 // partition key per event (ValuePartitionExecutor; null key -> event dropped)
-__global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__ ap, int64_t n, uint64_t* key,
-                                                     uint32_t* keyed, unsigned long long* kmax) {
+__global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__ ap, int64_t n, int64_t stride,
+                                                     uint64_t* key, uint32_t* keyed, unsigned long long* kmax) {
   const KeyArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   unsigned long long m = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     BatchCtx cx{&a.batch, i};
     Val kv = a.key_col >= 0 ? col_load(a.batch, i, a.key_col)
                             : eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
@@ -1221,7 +1221,13 @@ __global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__
     unsigned long long t = __shfl_xor(m, o, 64);
     m = t > m ? t : m;
   }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(kmax, m);
+  __shared__ unsigned long long wm[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {   // one atomic per block (the grid is capped by grid_for)
+    for (int w = 1; w < kBlock / 64; w++) m = wm[w] > m ? wm[w] : m;
+    if (m) atomicMax(kmax, m);
+  }
 }
 
 // Same-key runs of one call (PartitionStreamReceiver.receive(Event[]) :189-214)
@@ -1776,8 +1782,9 @@ struct NfaEngine : Engine {
     ka.key_col = key_col[si];
     ka.key_type = key_type[si];
     SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
-    hipLaunchKernelGGL(k_nfa_keys, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ka), n, d_key.as<uint64_t>(),
-                       d_keyed.as<uint32_t>(), &d_ctl.as<NfaCtl>()->kmax);
+    const int nblk = grid_for(n);
+    hipLaunchKernelGGL(k_nfa_keys, dim3(nblk), dim3(kBlock), 0, s, dev_args(ka), n, (int64_t)nblk * kBlock,
+                       d_key.as<uint64_t>(), d_keyed.as<uint32_t>(), &d_ctl.as<NfaCtl>()->kmax);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_nfa_run_starts, dim3(grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)d_keyed.as<uint32_t>(),
                        (const uint64_t*)d_key.as<uint64_t>(), (const int32_t*)d_call_of.as<int32_t>(), n,

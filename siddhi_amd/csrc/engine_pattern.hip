@@ -144,15 +144,15 @@ __device__ __forceinline__ T wave_min(T v) {
 
 // Per extended row: key and packed (flags, row) sort payload.  One pass over
 // the pushed columns (key, f1 inputs, ts); the f1 bytecode is read from LDS.
-__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, uint32_t* k32,
-                                                    uint64_t* k64, uint32_t* pv, PrepAgg* agg) {
+__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
+                                                    uint32_t* k32, uint64_t* k64, uint32_t* pv, PrepAgg* blk) {
   const PrepArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   unsigned long long created = 0, kmax = 0;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN;
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r = n_ext) {
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r += stride) {
     uint32_t f;
     uint64_t k = 0;
     if (r < x.C) {
@@ -187,15 +187,52 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
     }
     pv[r] = (f << kRowBits) | (uint32_t)r;
   }
+  // one partial per block (plain store; k_finish_prep folds them): no
+  // same-address atomics from every wave of a large grid
   for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
   kmax = wave_max(kmax);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
-  if ((threadIdx.x & 63) == 0) {
-    if (created) atomicAdd(&agg->n_cand, created);
-    if (kmax) atomicMax(&agg->kmax, kmax);
-    if (tmin != LLONG_MAX) atomicMin(&agg->ts_min, tmin);
-    if (tmax != LLONG_MIN) atomicMax(&agg->ts_max, tmax);
+  __shared__ PrepAgg wpart[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    PrepAgg r = wpart[0];
+    for (int w = 1; w < kBlock / 64; w++) {
+      r.n_cand += wpart[w].n_cand;
+      r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
+      r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
+      r.ts_max = wpart[w].ts_max > r.ts_max ? wpart[w].ts_max : r.ts_max;
+    }
+    blk[blockIdx.x] = r;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
+  unsigned long long c = 0, km = 0;
+  long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+  for (int b = threadIdx.x; b < nblk; b += kBlock) {
+    c += blk[b].n_cand;
+    km = blk[b].kmax > km ? blk[b].kmax : km;
+    tmin = blk[b].ts_min < tmin ? blk[b].ts_min : tmin;
+    tmax = blk[b].ts_max > tmax ? blk[b].ts_max : tmax;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  km = wave_max(km);
+  tmin = wave_min(tmin);
+  tmax = wave_max(tmax);
+  __shared__ PrepAgg wpart[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    PrepAgg r = wpart[0];
+    for (int w = 1; w < kBlock / 64; w++) {
+      r.n_cand += wpart[w].n_cand;
+      r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
+      r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
+      r.ts_max = wpart[w].ts_max > r.ts_max ? wpart[w].ts_max : r.ts_max;
+    }
+    *out = r;
   }
 }
 
@@ -228,15 +265,17 @@ struct ScanOut {
 // counts for matches (cm) and still-open partials (co) per position.
 template <bool K64>
 __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
-                                                         const uint32_t* skey32, const uint64_t* skey64,
-                                                         const uint32_t* spv, int32_t* match_row, uint32_t* cm,
-                                                         uint32_t* co, ScanOut* so) {
+                                                         int64_t stride, const uint32_t* skey32,
+                                                         const uint64_t* skey64, const uint32_t* spv,
+                                                         int32_t* match_row, uint32_t* cm, uint32_t* co,
+                                                         ScanOut* blk) {
   const ScanArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   uint64_t steps = 0, pruned = 0;
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p = n_ext) {
+  uint32_t viol = 0;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p += stride) {
     const uint32_t pvp = spv[p];
     uint32_t m = 0, o = 0;
     if (pv_flags(pvp) & F_CAND) {
@@ -254,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
         const int64_t r2 = pv_row(pq);
         const int64_t t2 = x.ts(r2);
         if (t2 < prev) {
-          atomicOr(&so->violation, 1u);
+          viol = 1;
           break;
         }
         prev = t2;
@@ -287,10 +326,46 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   for (int o2 = 32; o2 > 0; o2 >>= 1) {
     steps += __shfl_xor(steps, o2, 64);
     pruned += __shfl_xor(pruned, o2, 64);
+    viol |= __shfl_xor(viol, o2, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (steps) atomicAdd(&so->steps, (unsigned long long)steps);
-    if (pruned) atomicAdd(&so->pruned, (unsigned long long)pruned);
+  __shared__ ScanOut wpart[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ScanOut r = wpart[0];
+    for (int w = 1; w < kBlock / 64; w++) {
+      r.steps += wpart[w].steps;
+      r.pruned += wpart[w].pruned;
+      r.violation |= wpart[w].violation;
+    }
+    blk[blockIdx.x] = r;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int nblk, ScanOut* out) {
+  unsigned long long st = 0, pr = 0;
+  uint32_t v = 0;
+  for (int b = threadIdx.x; b < nblk; b += kBlock) {
+    st += blk[b].steps;
+    pr += blk[b].pruned;
+    v |= blk[b].violation;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    st += __shfl_xor(st, o, 64);
+    pr += __shfl_xor(pr, o, 64);
+    v |= __shfl_xor(v, o, 64);
+  }
+  __shared__ ScanOut wpart[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{st, pr, v, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ScanOut r = wpart[0];
+    for (int w = 1; w < kBlock / 64; w++) {
+      r.steps += wpart[w].steps;
+      r.pruned += wpart[w].pruned;
+      r.violation |= wpart[w].violation;
+    }
+    *out = r;
   }
 }
 
@@ -435,7 +510,7 @@ struct PatternEngine : Engine {
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_match, d_cm, d_co, d_om, d_oo, d_pj, d_pi, d_pj_alt,
-      d_pi_alt, d_agg, d_sort, d_scan;
+      d_pi_alt, d_agg, d_sort, d_scan, d_blk;
   PinnedBuf h_agg;
 
   int kind() const override { return ENG_PATTERN; }
@@ -512,8 +587,12 @@ struct PatternEngine : Engine {
     std::memcpy(h_agg.p, &init, sizeof(init));
     std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_prepare, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(pa), n_ext, d_k32.as<uint32_t>(),
-                       d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_pa);
+    const int nblk = grid_for(n_ext);
+    d_blk.reserve((size_t)nblk * 32);
+    hipLaunchKernelGGL(k_prepare, dim3(nblk), dim3(kBlock), 0, s, dev_args(pa), n_ext, (int64_t)nblk * kBlock,
+                       d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
     SHD_CHECK_LAUNCH();
     SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
@@ -569,12 +648,17 @@ struct PatternEngine : Engine {
     sa.prune = n_ext >= kPruneMinRows && W != INT64_MAX;
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
+    const ScanArgs* d_sa = dev_args(sa);
     if (sorted64)
-      hipLaunchKernelGGL(k_forward_scan<true>, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
-                         skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
+      hipLaunchKernelGGL(k_forward_scan<true>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
+                         skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
+                         d_blk.as<ScanOut>());
     else
-      hipLaunchKernelGGL(k_forward_scan<false>, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(sa), n_ext, skey32,
-                         skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(), d_so);
+      hipLaunchKernelGGL(k_forward_scan<false>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
+                         skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
+                         d_blk.as<ScanOut>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nblk, d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
 
