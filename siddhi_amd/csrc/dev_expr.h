@@ -330,23 +330,25 @@ struct DExprSet {
   int nins, nconsts;
 };
 
-// Expression program placement.  The bytecode and constants of a plan live
-// in global memory (DevExprTable) and are handed to every evaluating kernel
-// as `const __restrict__` kernel parameters as well: the backend then knows
-// the program is read-only and fetches each (wave-uniform) instruction with
-// a scalar load (s_load_dwordx4) instead of 64 identical per-lane loads.
-// (An earlier LDS-staged copy of the program faulted in the single-stream
-// kernels on the MI355X pool; DESIGN.md "Expression programs".)  Plans are
-// bounded by kLdsIns / kLdsConsts at load (DevExprTable::upload).
+// Expression program placement.  Staging the program into LDS at kernel start
+// (every lane decodes the same uniform instruction stream) was measured to
+// fault on the MI355X pool in the single-stream kernels (k_filter: memory
+// aperture violation for any batch size, while the identical kernels reading
+// the program from global memory pass: scripts/probe_filter.py, DESIGN.md
+// "LDS program staging").  The program therefore stays in global memory,
+// where the uniform instruction reads are served by the scalar/L1 caches;
+// stage_prog keeps the call sites and reserves no LDS.  Plans larger than
+// the former LDS store are still rejected at load (DevExprTable::upload).
 constexpr int kLdsIns = 256;
 constexpr int kLdsConsts = 64;
+struct LdsProg {
+  int4 ins[1];
+};
 
-__device__ __forceinline__ DExprSet bind_prog(const DExprSet& g, const int4* __restrict__ ins,
-                                              const uint64_t* __restrict__ consts) {
-  DExprSet l = g;
-  l.ins = ins;
-  l.consts = consts;
-  return l;
+template <int NT = kBlock>
+__device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
+  (void)s;
+  return g;
 }
 
 // Conjunction of up to 4 filter expressions (FilterProcessor chain).

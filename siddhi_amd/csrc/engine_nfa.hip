@@ -1095,11 +1095,10 @@ __device__ int64_t SECtx::ts(int, int) const { return L->sts(se); }
 // One lane = one partition key (or the single unpartitioned key).
 __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restrict__ gprog,
                                                         const NfaLayout* __restrict__ glay,
-                                                        const NfaRunArgs* __restrict__ ap,
-                                                        const int4* __restrict__ pins,
-                                                        const uint64_t* __restrict__ pconsts) {
+                                                        const NfaRunArgs* __restrict__ ap) {
   __shared__ NfaProg sprog;
   __shared__ NfaLayout slay;
+  __shared__ LdsProg prog;
   {
     const int* src = reinterpret_cast<const int*>(gprog);
     int* dst = reinterpret_cast<int*>(&sprog);
@@ -1109,8 +1108,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     for (int i = threadIdx.x; i < (int)(sizeof(NfaLayout) / 4); i += kLaneBlock) d2[i] = s2[i];
   }
   const NfaRunArgs& a = *ap;
-  __syncthreads();
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  const DExprSet es = stage_prog<kLaneBlock>(a.es, prog);   // contains the barrier
   const int64_t lane_id = (int64_t)blockIdx.x * kLaneBlock + threadIdx.x;
   if (lane_id >= a.nlanes) return;
   int64_t seg, slot;
@@ -1204,11 +1202,11 @@ __device__ __forceinline__ uint64_t canon_key(Val v, int type) {
 }
 
 // partition key per event (ValuePartitionExecutor; null key -> event dropped)
-__global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n, int64_t stride,
+__global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__ ap, int64_t n, int64_t stride,
                                                      uint64_t* key, uint32_t* keyed, unsigned long long* kmax) {
   const KeyArgs& a = *ap;
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   unsigned long long m = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     BatchCtx cx{&a.batch, i};
@@ -1785,7 +1783,7 @@ struct NfaEngine : Engine {
     ka.key_type = key_type[si];
     SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
     const int nblk = grid_for(n);
-    hipLaunchKernelGGL(k_nfa_keys, dim3(nblk), dim3(kBlock), 0, s, dev_args(ka), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n, (int64_t)nblk * kBlock,
+    hipLaunchKernelGGL(k_nfa_keys, dim3(nblk), dim3(kBlock), 0, s, dev_args(ka), n, (int64_t)nblk * kBlock,
                        d_key.as<uint64_t>(), d_keyed.as<uint32_t>(), &d_ctl.as<NfaCtl>()->kmax);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_nfa_run_starts, dim3(grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)d_keyed.as<uint32_t>(),
@@ -1978,7 +1976,7 @@ struct NfaEngine : Engine {
       const NfaProg* dp = dev_args(prog);
       const NfaLayout* dl = dev_args(lay);
       hipLaunchKernelGGL(k_nfa_run, dim3((unsigned)ceil_div(ra.nlanes, kLaneBlock)), dim3(kLaneBlock), 0, s, dp, dl,
-                         dev_args(ra), ex.ins.as<int4>(), ex.consts.as<uint64_t>());
+                         dev_args(ra));
       SHD_CHECK_LAUNCH();
       hc = read_ctl();
     }

@@ -81,40 +81,13 @@ struct PairCtx {
       v.null = 1;
       return v;
     }
-    // branch on the row's table instead of selecting a per-lane ColSet
-    // pointer: each branch reads a wave-uniform column table (scalar loads)
-    if (r < x->C) return col_load(x->carry, r, attr);
-    return col_load(x->batch, r - x->C, attr);
+    return col_load(x->cs(r), x->row(r), attr);
   }
   __device__ __forceinline__ bool evnull(int st, int idx) const { return slot(st, idx) < 0; }
   __device__ __forceinline__ int64_t ts(int st, int idx) const {
     int64_t r = slot(st, idx);
     return r < 0 ? 0 : x->ts(r);
   }
-  __device__ __forceinline__ Val agg(int) const {
-    Val v;
-    v.b = 0;
-    v.null = 1;
-    return v;
-  }
-};
-
-// Expression context of k_prepare: the pushed event as state 0 (stream-state
-// chain of one event), read from the uniform batch column table.
-struct BatchRowCtx {
-  const ColSet* cs;
-  int64_t row;
-  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
-    if (st != 0 || !(idx == 0 || idx == SHD_IDX_CURRENT)) {
-      Val v;
-      v.b = 0;
-      v.null = 1;
-      return v;
-    }
-    return col_load(*cs, row, attr);
-  }
-  __device__ __forceinline__ bool evnull(int st, int idx) const { return !(st == 0 && (idx == 0 || idx == SHD_IDX_CURRENT)); }
-  __device__ __forceinline__ int64_t ts(int st, int idx) const { return evnull(st, idx) ? 0 : cs->ts[row]; }
   __device__ __forceinline__ Val agg(int) const {
     Val v;
     v.b = 0;
@@ -171,11 +144,11 @@ __device__ __forceinline__ T wave_min(T v) {
 
 // Per extended row: key and packed (flags, row) sort payload.  One pass over
 // the pushed columns (key, f1 inputs, ts); the f1 bytecode is read from LDS.
-__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n_ext, int64_t stride,
+__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
                                                     uint32_t* k32, uint64_t* k64, uint32_t* pv, PrepAgg* blk) {
   const PrepArgs& a = *ap;
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   unsigned long long created = 0, kmax = 0;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN;
@@ -186,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       k = a.partitioned ? a.carry_key[r] : 0;
       f = F_CAND;
     } else {
-      BatchRowCtx cx{&x.batch, r - x.C};
+      PairCtx cx{&x, r, -1};
       f = F_NEW;
       if (a.partitioned) {
         Val kv;
@@ -291,14 +264,14 @@ struct ScanOut {
 // event falls inside `within`) are gathered by row.  Writes the compaction
 // counts for matches (cm) and still-open partials (co) per position.
 template <bool K64>
-__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n_ext,
+__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                          int64_t stride, const uint32_t* skey32,
                                                          const uint64_t* skey64, const uint32_t* spv,
                                                          int32_t* match_row, uint32_t* cm, uint32_t* co,
                                                          ScanOut* blk) {
   const ScanArgs& a = *ap;
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   uint64_t steps = 0, pruned = 0;
   uint32_t viol = 0;
@@ -417,12 +390,12 @@ struct ProjArgs {
   int64_t row0;         // output buffer offset
 };
 
-__global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, const uint32_t* pj,
+__global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj,
                                                     const uint32_t* pi, int64_t m, int64_t* o_chunk, int32_t* o_type,
                                                     int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const ProjArgs& a = *ap;
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < m; k = m) {
     int64_t j = pj[k], i = pi[k];
@@ -616,7 +589,7 @@ struct PatternEngine : Engine {
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
     const int nblk = grid_for(n_ext);
     d_blk.reserve((size_t)nblk * 32);
-    hipLaunchKernelGGL(k_prepare, dim3(nblk), dim3(kBlock), 0, s, dev_args(pa), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n_ext, (int64_t)nblk * kBlock,
+    hipLaunchKernelGGL(k_prepare, dim3(nblk), dim3(kBlock), 0, s, dev_args(pa), n_ext, (int64_t)nblk * kBlock,
                        d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
@@ -677,11 +650,11 @@ struct PatternEngine : Engine {
     sa.t_end = t_end;
     const ScanArgs* d_sa = dev_args(sa);
     if (sorted64)
-      hipLaunchKernelGGL(k_forward_scan<true>, dim3(nblk), dim3(kBlock), 0, s, d_sa, ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n_ext, (int64_t)nblk * kBlock,
+      hipLaunchKernelGGL(k_forward_scan<true>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
                          skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
                          d_blk.as<ScanOut>());
     else
-      hipLaunchKernelGGL(k_forward_scan<false>, dim3(nblk), dim3(kBlock), 0, s, d_sa, ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n_ext, (int64_t)nblk * kBlock,
+      hipLaunchKernelGGL(k_forward_scan<false>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
                          skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
                          d_blk.as<ScanOut>());
     SHD_CHECK_LAUNCH();
@@ -737,7 +710,7 @@ struct PatternEngine : Engine {
       pr.multi = (sA == sB);
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
-      hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), pj, pi, (int64_t)m,
+      hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
                          out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
       SHD_CHECK_LAUNCH();
       out.count += m;

@@ -107,11 +107,11 @@ struct FilterArgs {
 };
 
 // flags: bit0 = passes filters, bit1 = has a (non-null) partition key
-__global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n, uint8_t* flags, uint32_t* cnt,
+__global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict__ ap, int64_t n, uint8_t* flags, uint32_t* cnt,
                                                    uint64_t* pkey) {
   const FilterArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -158,14 +158,14 @@ struct ProjArgs {
   int partitioned;
 };
 
-__global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n, const uint32_t* cnt,
+__global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restrict__ ap, int64_t n, const uint32_t* cnt,
                                                          const uint32_t* off, const int32_t* call_of,
                                                          const uint32_t* run_excl, const uint32_t* run_start,
                                                          int64_t* o_chunk, int32_t* o_type,
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
@@ -198,14 +198,14 @@ struct ItemArgs {
 };
 
 // New window items (one per filtered event), appended after the carried ones.
-__global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t n, const uint32_t* cnt, const uint32_t* off,
+__global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restrict__ ap, int64_t n, const uint32_t* cnt, const uint32_t* off,
                                                        const int32_t* call_of, const int64_t* call_now,
                                                        uint64_t* ikey, int64_t* its, uint64_t* iargv, uint8_t* iargn,
                                                        int32_t* ievrow, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
@@ -486,13 +486,13 @@ struct EmitArgs {
   int64_t chunk0;
 };
 
-__global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, const int4* __restrict__ pins,
-    const uint64_t* __restrict__ pconsts, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
+__global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
                                                  const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
                                                  int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  const DExprSet es = bind_prog(a.es, pins, pconsts);
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
   const ColSet& cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < nnew; t0 = nnew) {
     if (!fcnt[t0]) continue;
@@ -618,7 +618,7 @@ struct SingleEngine : Engine {
     }
     const FilterArgs* d_fa = dev_args(fa);
     if (std::getenv("SHD_DEBUG_ARGS")) debug_filter_args(d_fa, fa, n);
-    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, d_fa, ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n, d_flags.as<uint8_t>(),
+    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, d_fa, n, d_flags.as<uint8_t>(),
                        d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
     SHD_CHECK_LAUNCH();
     uint32_t* d_m = (uint32_t*)d_tot.p;
@@ -708,7 +708,7 @@ struct SingleEngine : Engine {
       // exclusive run ids: the run of event i is start-scan[i] (+0 if i is a start it is its own index)
       pa.chunk0 = chunk_seq;
       pa.partitioned = partitioned;
-      hipLaunchKernelGGL(k_project_rows, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(pa), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n,
+      hipLaunchKernelGGL(k_project_rows, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(pa), n,
                          (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                          (const int32_t*)d_call_of.as<int32_t>(), (const uint32_t*)d_run.as<uint32_t>(),
                          (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
@@ -805,7 +805,7 @@ struct SingleEngine : Engine {
       ia.group_type = group_type;
     }
     ia.C = C;
-    hipLaunchKernelGGL(k_make_items, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ia), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), n,
+    hipLaunchKernelGGL(k_make_items, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ia), n,
                        (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
                        ikey[cur].as<uint64_t>(), its[cur].as<int64_t>(), iargv[cur].as<uint64_t>(),
@@ -920,7 +920,7 @@ struct SingleEngine : Engine {
           ea.C = C;
           ea.row0 = out.count;
           ea.chunk0 = chunk_seq;
-          hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), ex.ins.as<int4>(), ex.consts.as<uint64_t>(), m, (const uint32_t*)fcnt.as<uint32_t>(),
+          hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
                              (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
                              (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
                              (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(), out.d_chunk(),
