@@ -81,13 +81,40 @@ struct PairCtx {
       v.null = 1;
       return v;
     }
-    return col_load(x->cs(r), x->row(r), attr);
+    // branch on the row's table instead of selecting a per-lane ColSet
+    // pointer: each branch reads a wave-uniform column table (scalar loads)
+    if (r < x->C) return col_load(x->carry, r, attr);
+    return col_load(x->batch, r - x->C, attr);
   }
   __device__ __forceinline__ bool evnull(int st, int idx) const { return slot(st, idx) < 0; }
   __device__ __forceinline__ int64_t ts(int st, int idx) const {
     int64_t r = slot(st, idx);
     return r < 0 ? 0 : x->ts(r);
   }
+  __device__ __forceinline__ Val agg(int) const {
+    Val v;
+    v.b = 0;
+    v.null = 1;
+    return v;
+  }
+};
+
+// Expression context of k_prepare: the pushed event as state 0 (stream-state
+// chain of one event), read from the uniform batch column table.
+struct BatchRowCtx {
+  const ColSet* cs;
+  int64_t row;
+  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
+    if (st != 0 || !(idx == 0 || idx == SHD_IDX_CURRENT)) {
+      Val v;
+      v.b = 0;
+      v.null = 1;
+      return v;
+    }
+    return col_load(*cs, row, attr);
+  }
+  __device__ __forceinline__ bool evnull(int st, int idx) const { return !(st == 0 && (idx == 0 || idx == SHD_IDX_CURRENT)); }
+  __device__ __forceinline__ int64_t ts(int st, int idx) const { return evnull(st, idx) ? 0 : cs->ts[row]; }
   __device__ __forceinline__ Val agg(int) const {
     Val v;
     v.b = 0;
@@ -159,7 +186,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       k = a.partitioned ? a.carry_key[r] : 0;
       f = F_CAND;
     } else {
-      PairCtx cx{&x, r, -1};
+      BatchRowCtx cx{&x.batch, r - x.C};
       f = F_NEW;
       if (a.partitioned) {
         Val kv;
