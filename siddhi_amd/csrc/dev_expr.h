@@ -351,14 +351,81 @@ __device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
   return g;
 }
 
+// ---------------------------------------------------------------- fast predicates
+// Filter chains whose bytecode is a conjunction of comparisons between simple
+// terms are pre-decoded on the host (compile_fast_pred, shd_api.cpp) into a
+// fixed-shape descriptor evaluated as straight-line code: no instruction
+// fetch per event.  The descriptor is wave-uniform (it sits in the kernel's
+// argument block), so every branch below is a scalar branch.  It applies the
+// same operations as the interpreter in the same order (d_cvt / d_arith /
+// d_compare, null propagation), so results are identical; any other bytecode
+// shape falls back to eval_expr.
+//   atom := LOAD | CONST | NULL, optionally followed by one CVT
+//   term := atom | atom atom ARITH
+//   cmp  := term term COMPARE          pred := cmp (AND cmp)*   (<= 4 cmps)
+enum : int8_t { FA_NONE = 0, FA_LOAD = 1, FA_CONST = 2, FA_NULL = 3 };
+struct FAtom {
+  int8_t kind, st, idx, cvt_from, cvt_to, pad0;
+  int16_t attr;
+  uint64_t cval;
+};
+struct FTerm {
+  FAtom a, b;
+  int8_t aop, atype, pad[6];
+};
+struct FCmp {
+  FTerm l, r;
+  int8_t op, type, pad[6];
+};
+struct FPred {
+  int32_t ok;     // 1: the filter chain is this conjunction
+  int32_t n;      // comparisons
+  FCmp c[4];
+};
+
+template <class Ctx>
+__device__ __forceinline__ Val fp_atom(const FAtom& a, const Ctx& cx) {
+  Val v;
+  v.b = 0;
+  v.null = 1;
+  if (a.kind == FA_LOAD) v = cx.load(a.st, a.idx, a.attr);
+  else if (a.kind == FA_CONST) {
+    v.b = a.cval;
+    v.null = 0;
+  }
+  if (a.cvt_to >= 0 && !v.null) v.b = d_cvt(v.b, a.cvt_from, a.cvt_to);
+  return v;
+}
+
+template <class Ctx>
+__device__ __forceinline__ Val fp_term(const FTerm& t, const Ctx& cx) {
+  Val l = fp_atom(t.a, cx);
+  if (t.aop == 0) return l;
+  Val r = fp_atom(t.b, cx);
+  return d_arith(t.aop, t.atype, l, r);
+}
+
+template <class Ctx>
+__device__ __forceinline__ bool eval_fpred(const FPred& p, const Ctx& cx) {
+  for (int i = 0; i < p.n; i++) {
+    const FCmp& c = p.c[i];
+    Val l = fp_term(c.l, cx);
+    Val r = fp_term(c.r, cx);
+    if (l.null || r.null || !d_compare(c.op, c.type, l.b, r.b)) return false;
+  }
+  return true;
+}
+
 // Conjunction of up to 4 filter expressions (FilterProcessor chain).
 struct DFilters {
   DExpr f[4];
   int n;
+  FPred fp;
 };
 
 template <class Ctx>
 __device__ __forceinline__ bool eval_filters(const DExprSet& es, const DFilters& fs, const Ctx& cx) {
+  if (fs.fp.ok) return eval_fpred(fs.fp, cx);
   for (int i = 0; i < fs.n; i++)
     if (!eval_bool(es.ins + fs.f[i].off, fs.f[i].len, es.consts, cx)) return false;
   return true;

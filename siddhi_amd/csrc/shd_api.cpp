@@ -294,11 +294,134 @@ Engine::~Engine() {
   if (stream) (void)hipStreamDestroy(stream);
 }
 
+// Pre-decode a filter chain into a fixed-shape conjunction (dev_expr.h,
+// "fast predicates"); returns false when any expression has another shape.
+bool compile_fast_pred(const Plan& p, const std::vector<int>& ids, FPred& out) {
+  out = FPred{};
+  enum { N_ATOM, N_TERM, N_CMP, N_AND };
+  struct Node {
+    int kind;
+    FAtom atom;
+    FTerm term;
+    std::vector<FCmp> cmps;
+  };
+  auto no_atom = [] {
+    FAtom a{};
+    a.kind = FA_NONE;
+    a.cvt_from = a.cvt_to = -1;
+    return a;
+  };
+  auto as_term = [&](const Node& n, FTerm& t) {
+    t = FTerm{};
+    if (n.kind == N_ATOM) {
+      t.a = n.atom;
+      t.b = no_atom();
+      t.aop = 0;
+      return true;
+    }
+    if (n.kind == N_TERM) {
+      t = n.term;
+      return true;
+    }
+    return false;
+  };
+  std::vector<FCmp> all;
+  for (int e : ids) {
+    std::vector<Node> st;
+    for (const Instr& in : p.exprs[e]) {
+      switch (in.op) {
+        case SHD_OP_LOAD: case SHD_OP_CONST: case SHD_OP_NULL: {
+          Node n{};
+          n.kind = N_ATOM;
+          n.atom = no_atom();
+          if (in.op == SHD_OP_LOAD) {
+            if (in.b < -2 || in.b > 127 || in.a < 0 || in.a > 127) return false;
+            n.atom.kind = FA_LOAD;
+            n.atom.st = (int8_t)in.a;
+            n.atom.idx = (int8_t)in.b;
+            n.atom.attr = (int16_t)(in.c & 0xFFFF);
+          } else if (in.op == SHD_OP_CONST) {
+            n.atom.kind = FA_CONST;
+            n.atom.cval = p.consts[in.a];
+          } else {
+            n.atom.kind = FA_NULL;
+          }
+          st.push_back(n);
+          break;
+        }
+        case SHD_OP_CVT:
+          if (st.empty() || st.back().kind != N_ATOM || st.back().atom.cvt_to >= 0) return false;
+          st.back().atom.cvt_from = (int8_t)in.a;
+          st.back().atom.cvt_to = (int8_t)in.b;
+          break;
+        case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD: {
+          if (st.size() < 2) return false;
+          Node r = st.back();
+          st.pop_back();
+          Node l = st.back();
+          st.pop_back();
+          if (l.kind != N_ATOM || r.kind != N_ATOM) return false;
+          Node n{};
+          n.kind = N_TERM;
+          n.term.a = l.atom;
+          n.term.b = r.atom;
+          n.term.aop = (int8_t)in.op;
+          n.term.atype = (int8_t)in.a;
+          st.push_back(n);
+          break;
+        }
+        case SHD_OP_EQ: case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE: {
+          if (st.size() < 2) return false;
+          Node r = st.back();
+          st.pop_back();
+          Node l = st.back();
+          st.pop_back();
+          FCmp c{};
+          if (!as_term(l, c.l) || !as_term(r, c.r)) return false;
+          c.op = (int8_t)in.op;
+          c.type = (int8_t)in.a;
+          Node n{};
+          n.kind = N_CMP;
+          n.cmps.push_back(c);
+          st.push_back(n);
+          break;
+        }
+        case SHD_OP_AND: {
+          if (st.size() < 2) return false;
+          Node r = st.back();
+          st.pop_back();
+          Node l = st.back();
+          st.pop_back();
+          if ((l.kind != N_CMP && l.kind != N_AND) || (r.kind != N_CMP && r.kind != N_AND)) return false;
+          Node n{};
+          n.kind = N_AND;
+          n.cmps = l.cmps;
+          n.cmps.insert(n.cmps.end(), r.cmps.begin(), r.cmps.end());
+          st.push_back(n);
+          break;
+        }
+        default:
+          return false;
+      }
+    }
+    if (st.size() != 1 || (st[0].kind != N_CMP && st[0].kind != N_AND)) return false;
+    all.insert(all.end(), st[0].cmps.begin(), st[0].cmps.end());
+  }
+  if (all.size() > 4) return false;
+  out.ok = 1;
+  out.n = (int)all.size();
+  for (size_t i = 0; i < all.size(); i++) out.c[i] = all[i];
+  return true;
+}
+
 DFilters Engine::dfilters(const std::vector<int>& ids) const {
   DFilters f{};
   f.n = (int)ids.size();
   if (f.n > 4) throw Error(SHD_E_UNSUPPORTED, "more than 4 filters on one state");
   for (int i = 0; i < f.n; i++) f.f[i] = dexpr(ids[i]);
+  const char* nf = std::getenv("SHD_NO_FAST_PRED");   // interpreter only (cross-check in tests)
+  const bool no_fast = nf && *nf && *nf != '0';
+  if (no_fast || !compile_fast_pred(plan, ids, f.fp)) f.fp.ok = 0;
   return f;
 }
 

@@ -59,9 +59,11 @@ def run_device(qp, batches):
     parts = []
     for si, b in batches:
         cols = [np.ascontiguousarray(c) for c in b.cols]
+        nuls = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in b.nulls]
         ts = np.ascontiguousarray(b.ts, np.int64)
         # playback time advances per InputHandler call inside the batch (advance_time)
-        dq.push_raw(si, b.n, ts.ctypes.data, [c.ctypes.data for c in cols], [0] * len(cols), SHD_MEM_HOST,
+        dq.push_raw(si, b.n, ts.ctypes.data, [c.ctypes.data for c in cols],
+                    [0 if x is None else x.ctypes.data for x in nuls], SHD_MEM_HOST,
                     b.call_offsets if len(b.call_offsets) > 2 else None, True)
         r = dq.poll()
         if r is not None:
