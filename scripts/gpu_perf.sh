@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-perf}
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_nfa.py -m gpu -q --timeout 180 \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_nfa.py tests/test_gpu_fastpred.py -m gpu -q --timeout 180 \
     --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
