@@ -171,6 +171,9 @@ __device__ __forceinline__ T wave_min(T v) {
 
 // Per extended row: key and packed (flags, row) sort payload.  One pass over
 // the pushed columns (key, f1 inputs, ts); the f1 bytecode is read from LDS.
+// FAST: the f1 chain is a pre-decoded conjunction and the key a plain column,
+// so this variant carries no interpreter (far fewer registers, more waves).
+template <bool FAST>
 __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
                                                     uint32_t* k32, uint64_t* k64, uint32_t* pv, PrepAgg* blk) {
   const PrepArgs& a = *ap;
@@ -190,14 +193,14 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       f = F_NEW;
       if (a.partitioned) {
         Val kv;
-        if (a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
+        if (FAST || a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
         else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
         if (kv.null) f |= F_SKIP;   // PartitionStreamReceiver drops null keys
         k = kv.null ? 0 : canon_key(kv, a.key_type);
       }
       if (!(f & F_SKIP)) {
         if (a.is_b) f |= F_B;
-        if (a.is_a && eval_filters(es, a.f1, cx)) {
+        if (a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx))) {
           f |= F_CAND;
           created++;
         }
@@ -290,7 +293,7 @@ struct ScanOut {
 // flags / keys are sequential; only event timestamps (and f2 operands when an
 // event falls inside `within`) are gathered by row.  Writes the compaction
 // counts for matches (cm) and still-open partials (co) per position.
-template <bool K64>
+template <bool K64, bool FAST>
 __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                          int64_t stride, const uint32_t* skey32,
                                                          const uint64_t* skey64, const uint32_t* spv,
@@ -332,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
         }
         if (fq & F_B) {
           PairCtx cx{&x, r, r2};
-          if (eval_filters(es, a.f2, cx)) {
+          if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
             st = ST_MATCH;
             j = (int32_t)r2;
             break;
@@ -616,8 +619,14 @@ struct PatternEngine : Engine {
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
     const int nblk = grid_for(n_ext);
     d_blk.reserve((size_t)nblk * 32);
-    hipLaunchKernelGGL(k_prepare, dim3(nblk), dim3(kBlock), 0, s, dev_args(pa), n_ext, (int64_t)nblk * kBlock,
-                       d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
+    const PrepArgs* d_pa_args = dev_args(pa);
+    const bool fast1 = (!isA || pa.f1.fp.ok) && (!partitioned || pa.key_col >= 0);
+    if (fast1)
+      hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
+    else
+      hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
     SHD_CHECK_LAUNCH();
@@ -676,14 +685,19 @@ struct PatternEngine : Engine {
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     const ScanArgs* d_sa = dev_args(sa);
-    if (sorted64)
-      hipLaunchKernelGGL(k_forward_scan<true>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
-                         skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
-                         d_blk.as<ScanOut>());
-    else
-      hipLaunchKernelGGL(k_forward_scan<false>, dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext, (int64_t)nblk * kBlock,
-                         skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(), d_co.as<uint32_t>(),
-                         d_blk.as<ScanOut>());
+    const bool fast2 = sa.f2.fp.ok != 0;
+#define SHD_LAUNCH_SCAN(K64, FAST)                                                                              \
+  hipLaunchKernelGGL((k_forward_scan<K64, FAST>), dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext,                  \
+                     (int64_t)nblk * kBlock, skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(),   \
+                     d_co.as<uint32_t>(), d_blk.as<ScanOut>())
+    if (sorted64) {
+      if (fast2) SHD_LAUNCH_SCAN(true, true);
+      else SHD_LAUNCH_SCAN(true, false);
+    } else {
+      if (fast2) SHD_LAUNCH_SCAN(false, true);
+      else SHD_LAUNCH_SCAN(false, false);
+    }
+#undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nblk, d_so);
     SHD_CHECK_LAUNCH();
