@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--config", default="P3")
     ap.add_argument("--events", type=int, default=0, help="override events per GPU")
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
-    ap.add_argument("--batch", type=int, default=25_000_000, help="micro-batch size (events)")
+    ap.add_argument("--batch", type=int, default=50_000_000, help="micro-batch size (events)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
     ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
