@@ -34,6 +34,8 @@ namespace {
 enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
 // Per-position scan result (positions = key-sorted order when partitioned).
 enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3 };
+// per-position outcome stored by k_forward_scan for the compaction kernels
+enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2 };
 
 // Sort payload: row index of the extended batch (28 bits) | flags (4 bits).
 constexpr int kRowBits = 28;
@@ -295,17 +297,20 @@ struct ScanOut {
 // counts for matches (cm) and still-open partials (co) per position.
 template <bool K64, bool FAST>
 __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
-                                                         int64_t stride, const uint32_t* skey32,
+                                                         int64_t tile, const uint32_t* skey32,
                                                          const uint64_t* skey64, const uint32_t* spv,
-                                                         int32_t* match_row, uint32_t* cm, uint32_t* co,
+                                                         int32_t* match_row, uint8_t* pst, uint32_t* bcnt,
                                                          ScanOut* blk) {
   const ScanArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
   uint64_t steps = 0, pruned = 0;
-  uint32_t viol = 0;
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p += stride) {
+  uint32_t viol = 0, nm = 0, no = 0;
+  // this block's contiguous tile of positions (compaction offsets are per block)
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
+  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
     const uint32_t pvp = spv[p];
     uint32_t m = 0, o = 0;
     if (pv_flags(pvp) & F_CAND) {
@@ -350,25 +355,64 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
       m = st == ST_MATCH;
       o = st == ST_OPEN;
     }
-    cm[p] = m;
-    co[p] = o;
+    pst[p] = (uint8_t)(m ? PS_MATCH : (o ? PS_OPEN : PS_NONE));
+    nm += m;
+    no += o;
   }
   for (int o2 = 32; o2 > 0; o2 >>= 1) {
     steps += __shfl_xor(steps, o2, 64);
     pruned += __shfl_xor(pruned, o2, 64);
     viol |= __shfl_xor(viol, o2, 64);
+    nm += __shfl_xor(nm, o2, 64);
+    no += __shfl_xor(no, o2, 64);
   }
   __shared__ ScanOut wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol, 0};
+  __shared__ uint32_t wcnt[2][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol, 0};
+    wcnt[0][threadIdx.x >> 6] = nm;
+    wcnt[1][threadIdx.x >> 6] = no;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     ScanOut r = wpart[0];
+    uint32_t tm = wcnt[0][0], to = wcnt[1][0];
     for (int w = 1; w < kBlock / 64; w++) {
       r.steps += wpart[w].steps;
       r.pruned += wpart[w].pruned;
       r.violation |= wpart[w].violation;
+      tm += wcnt[0][w];
+      to += wcnt[1][w];
     }
     blk[blockIdx.x] = r;
+    bcnt[blockIdx.x] = tm;               // matches of this tile
+    bcnt[gridDim.x + blockIdx.x] = to;   // still-open partials of this tile
+  }
+}
+
+// Stable compaction of one block's tile: position p with pst[p] == want gets
+// output index base + (# such positions before p in the tile).  Chunks of
+// kBlock positions; wave ballots + per-wave totals in LDS.
+template <class F>
+__device__ __forceinline__ void tile_compact(const uint8_t* pst, int64_t t0, int64_t t1, uint8_t want, uint32_t base,
+                                             F&& emit) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
+    const int64_t p = c0 + threadIdx.x;
+    const bool f = p < t1 && pst[p] == want;
+    const uint64_t bal = __ballot(f);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = base + (uint32_t)__popcll(bal & lt), tot = 0;
+    for (int k = 0; k < kBlock / 64; k++) {
+      if (k < w) pre += wsum[k];
+      tot += wsum[k];
+    }
+    if (f) emit(p, pre);
+    base += tot;
+    __syncthreads();
   }
 }
 
@@ -399,15 +443,15 @@ __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int 
   }
 }
 
-__global__ void k_emit_pairs(const uint32_t* cm, const uint32_t* om, const int32_t* match_row, const uint32_t* spv,
-                             int64_t n, uint32_t* pj, uint32_t* pi) {
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-    if (cm[p]) {
-      uint32_t o = om[p];
-      pj[o] = (uint32_t)match_row[p];
-      pi[o] = pv_row(spv[p]);
-    }
-  }
+__global__ __launch_bounds__(kBlock) void k_emit_pairs(const uint8_t* pst, const uint32_t* boff,
+                                                       const int32_t* match_row, const uint32_t* spv, int64_t n,
+                                                       int64_t tile, uint32_t* pj, uint32_t* pi) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  tile_compact(pst, t0, t1, PS_MATCH, boff[blockIdx.x], [&](int64_t p, uint32_t o) {
+    pj[o] = (uint32_t)match_row[p];
+    pi[o] = pv_row(spv[p]);
+  });
 }
 
 struct ProjArgs {
@@ -457,13 +501,16 @@ struct GatherArgs {
 
 // Still-open partials -> next push's carry rows (position order: per key in
 // creation order, which is all the stable key sort of the next push needs).
-__global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t* co, const uint32_t* oo,
-                               const uint32_t* spv, const uint32_t* skey32, const uint64_t* skey64, int64_t n) {
+__global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __restrict__ ap, const uint8_t* pst,
+                                                         const uint32_t* boff, const uint32_t* spv,
+                                                         const uint32_t* skey32, const uint64_t* skey64, int64_t n,
+                                                         int64_t tile) {
   const GatherArgs& a = *ap;
   const ExtRows& x = a.x;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-    if (!co[p]) continue;
-    int64_t o = oo[p];
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  tile_compact(pst, t0, t1, PS_OPEN, boff[gridDim.x + blockIdx.x], [&](int64_t p, uint32_t o32) {
+    const int64_t o = o32;
     int64_t r = pv_row(spv[p]);
     const ColSet& cs = x.cs(r);
     int64_t row = x.row(r);
@@ -479,7 +526,7 @@ __global__ void k_gather_carry(const GatherArgs* __restrict__ ap, const uint32_t
     a.dts[o] = x.ts(r);
     a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
     a.dseq[o] = x.seq(r);
-  }
+  });
 }
 
 struct CarryTable {
@@ -539,7 +586,7 @@ struct PatternEngine : Engine {
   int64_t horizon = INT64_MIN;
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
-  DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_match, d_cm, d_co, d_om, d_oo, d_pj, d_pi, d_pj_alt,
+  DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_match, d_pst, d_bcnt, d_boff, d_pj, d_pi, d_pj_alt,
       d_pi_alt, d_agg, d_sort, d_scan, d_blk;
   PinnedBuf h_agg;
 
@@ -581,10 +628,7 @@ struct PatternEngine : Engine {
       d_k32.reserve(n_ext * 4);
     }
     d_match.reserve(n_ext * 4);
-    d_cm.reserve(n_ext * 4);
-    d_co.reserve(n_ext * 4);
-    d_om.reserve(n_ext * 4);
-    d_oo.reserve(n_ext * 4);
+    d_pst.reserve(n_ext);
     d_agg.reserve(256);
     h_agg.reserve(256);
 
@@ -686,10 +730,15 @@ struct PatternEngine : Engine {
     sa.t_end = t_end;
     const ScanArgs* d_sa = dev_args(sa);
     const bool fast2 = sa.f2.fp.ok != 0;
+    // contiguous tiles of positions per block (compaction offsets per block)
+    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
+    const int ntile = (int)ceil_div(n_ext, tile);
+    d_bcnt.reserve((size_t)2 * ntile * 4);
+    d_boff.reserve((size_t)2 * ntile * 4);
 #define SHD_LAUNCH_SCAN(K64, FAST)                                                                              \
-  hipLaunchKernelGGL((k_forward_scan<K64, FAST>), dim3(nblk), dim3(kBlock), 0, s, d_sa, n_ext,                  \
-                     (int64_t)nblk * kBlock, skey32, skey64, spv, d_match.as<int32_t>(), d_cm.as<uint32_t>(),   \
-                     d_co.as<uint32_t>(), d_blk.as<ScanOut>())
+  hipLaunchKernelGGL((k_forward_scan<K64, FAST>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,   \
+                     skey64, spv, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(),             \
+                     d_blk.as<ScanOut>())
     if (sorted64) {
       if (fast2) SHD_LAUNCH_SCAN(true, true);
       else SHD_LAUNCH_SCAN(true, false);
@@ -699,14 +748,14 @@ struct PatternEngine : Engine {
     }
 #undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nblk, d_so);
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), ntile, d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
 
-    // ---- compaction offsets for matches and open partials (position order)
+    // ---- per-tile compaction offsets for matches and open partials (position order)
     uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
-    scan_exclusive_u32(d_cm.as<uint32_t>(), d_om.as<uint32_t>(), n_ext, d_mo, d_scan, s);
-    scan_exclusive_u32(d_co.as<uint32_t>(), d_oo.as<uint32_t>(), n_ext, d_mo + 1, d_scan, s);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
     mark("compact");
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
@@ -729,9 +778,9 @@ struct PatternEngine : Engine {
       d_pi.reserve((int64_t)m * 4);
       d_pj_alt.reserve((int64_t)m * 4);
       d_pi_alt.reserve((int64_t)m * 4);
-      hipLaunchKernelGGL(k_emit_pairs, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, (const uint32_t*)d_cm.as<uint32_t>(),
-                         (const uint32_t*)d_om.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
-                         d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
+      hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                         (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
+                         tile, d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
       SHD_CHECK_LAUNCH();
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
@@ -776,9 +825,9 @@ struct PatternEngine : Engine {
       ga.dts = carry[nxt].ts.as<int64_t>();
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
-      hipLaunchKernelGGL(k_gather_carry, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, dev_args(ga),
-                         (const uint32_t*)d_co.as<uint32_t>(), (const uint32_t*)d_oo.as<uint32_t>(), spv, skey32,
-                         skey64, n_ext);
+      hipLaunchKernelGGL(k_gather_carry, dim3(ntile), dim3(kBlock), 0, s, dev_args(ga),
+                         (const uint8_t*)d_pst.as<uint8_t>(), (const uint32_t*)d_boff.as<uint32_t>(), spv, skey32,
+                         skey64, n_ext, tile);
       SHD_CHECK_LAUNCH();
       mark("carry");
     }
