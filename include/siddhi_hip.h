@@ -62,7 +62,8 @@ typedef struct shd_batch {
   const int64_t* ts;            /* [n] event timestamps (ms)                     */
   int32_t ncols;                /* == number of attributes of the stream        */
   const void* const* cols;      /* [ncols] typed columns: string=u32 dictionary id,
-                                   int=i32, long=i64, float=f32, double=f64, bool=u8 */
+                                   int=i32, long=i64, float=f32, double=f64, bool=u8;
+                                   never NULL: null rows keep a (any) value slot */
   const uint8_t* const* nulls;  /* [ncols] NULL or [n] bytes, 1 = null; may be NULL */
   int32_t ncalls;               /* InputHandler.send calls in this batch (>= 1)  */
   const int64_t* call_offsets;  /* host array [ncalls+1]; NULL = one call        */

@@ -149,10 +149,20 @@ struct DevExprTable {
 
 // ------------------------------------------------------------------ columns
 // A set of typed device columns (one stream's batch, or a carry table).
+// Load element i of a device array through a global-address-space pointer.
+// Column pointers read from argument structs are generic to the compiler and
+// would become flat loads, which also count against lgkmcnt: every scalar
+// load of the next column pointer then waits for all vector loads in flight.
+template <class T>
+__device__ __forceinline__ T gld(const T* p, int64_t i) {
+  typedef __attribute__((address_space(1))) const T* GP;
+  return ((GP)p)[i];
+}
+
 struct ColSet {
   const void* col[kMaxCols];
   const uint8_t* nul[kMaxCols];
-  int8_t type[kMaxCols];
+  int32_t type[kMaxCols];   // 32-bit: uniform fields load through the scalar cache (gfx9 has no s_load_byte)
   int32_t ncols;
   const int64_t* ts;
   int64_t n;        // rows (bounds checks in SHD_DEBUG builds)
@@ -177,6 +187,11 @@ void radix_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, ui
 void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, uint32_t* vals_alt,
                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& result_in_alt);
 // Device-wide max of u64 keys (result to dev ptr).
+// Same, carrying a second 32-bit payload word per key.
+void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
+void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
 void reduce_max_u64(const uint64_t* in, int64_t n, uint64_t* out_dev, hipStream_t s);
 void fill_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s);
 

@@ -46,21 +46,22 @@ __device__ __forceinline__ Val col_load(const ColSet& cs, int64_t row, int attr)
     v.null = 1;
     return v;
   }
+  // value and null byte are loaded together (a null row still has a value
+  // slot), so the two loads overlap instead of costing two round trips
   const uint8_t* nm = cs.nul[attr];
-  if (nm && nm[row]) {
-    v.b = 0;
-    v.null = 1;
-    return v;
-  }
   v.null = 0;
   switch (cs.type[attr]) {
-    case SHD_T_STRING: v.b = ((const uint32_t*)cs.col[attr])[row]; break;
-    case SHD_T_INT: v.b = p_i32(((const int32_t*)cs.col[attr])[row]); break;
-    case SHD_T_LONG: v.b = (uint64_t)((const int64_t*)cs.col[attr])[row]; break;
-    case SHD_T_FLOAT: v.b = (uint64_t)((const uint32_t*)cs.col[attr])[row]; break;
-    case SHD_T_DOUBLE: v.b = ((const uint64_t*)cs.col[attr])[row]; break;
-    case SHD_T_BOOL: v.b = ((const uint8_t*)cs.col[attr])[row] ? 1 : 0; break;
+    case SHD_T_STRING: v.b = gld((const uint32_t*)cs.col[attr], row); break;
+    case SHD_T_INT: v.b = p_i32(gld((const int32_t*)cs.col[attr], row)); break;
+    case SHD_T_LONG: v.b = (uint64_t)gld((const int64_t*)cs.col[attr], row); break;
+    case SHD_T_FLOAT: v.b = (uint64_t)gld((const uint32_t*)cs.col[attr], row); break;
+    case SHD_T_DOUBLE: v.b = gld((const uint64_t*)cs.col[attr], row); break;
+    case SHD_T_BOOL: v.b = gld((const uint8_t*)cs.col[attr], row) ? 1 : 0; break;
     default: v.b = 0; v.null = 1;
+  }
+  if (nm && gld(nm, row)) {
+    v.b = 0;
+    v.null = 1;
   }
   return v;
 }
@@ -363,19 +364,20 @@ __device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
 //   atom := LOAD | CONST | NULL, optionally followed by one CVT
 //   term := atom | atom atom ARITH
 //   cmp  := term term COMPARE          pred := cmp (AND cmp)*   (<= 4 cmps)
-enum : int8_t { FA_NONE = 0, FA_LOAD = 1, FA_CONST = 2, FA_NULL = 3 };
+enum : int32_t { FA_NONE = 0, FA_LOAD = 1, FA_CONST = 2, FA_NULL = 3 };
+// All fields are 32/64-bit: the descriptor is wave-uniform and must load with
+// s_load_dword (sub-dword fields would become vector loads + vmcnt waits).
 struct FAtom {
-  int8_t kind, st, idx, cvt_from, cvt_to, pad0;
-  int16_t attr;
+  int32_t kind, st, idx, cvt_from, cvt_to, attr;
   uint64_t cval;
 };
 struct FTerm {
   FAtom a, b;
-  int8_t aop, atype, pad[6];
+  int32_t aop, atype;
 };
 struct FCmp {
   FTerm l, r;
-  int8_t op, type, pad[6];
+  int32_t op, type;
 };
 struct FPred {
   int32_t ok;     // 1: the filter chain is this conjunction

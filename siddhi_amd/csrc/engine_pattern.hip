@@ -60,7 +60,7 @@ struct ExtRows {
       return 0;
     }
 #endif
-    return r < C ? carry.ts[r] : batch.ts[r - C];
+    return r < C ? gld(carry.ts, r) : gld(batch.ts, r - C);
   }
   __device__ __forceinline__ int64_t seq(int64_t r) const { return r < C ? carry_seq[r] : seq0 + (r - C); }
 };
@@ -139,6 +139,7 @@ struct PrepAgg {
   unsigned long long kmax;
   long long ts_min;
   long long ts_max;
+  unsigned long long ovf;   // some row's ts - batch.ts[0] does not fit in int32
 };
 
 struct PrepArgs {
@@ -177,37 +178,51 @@ __device__ __forceinline__ T wave_min(T v) {
 // so this variant carries no interpreter (far fewer registers, more waves).
 template <bool FAST>
 __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
-                                                    uint32_t* k32, uint64_t* k64, uint32_t* pv, PrepAgg* blk) {
+                                                    uint32_t* __restrict__ k32, uint64_t* __restrict__ k64,
+                                                    uint32_t* __restrict__ pv, int32_t* __restrict__ tso,
+                                                    PrepAgg* __restrict__ blk) {
   const PrepArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
-  unsigned long long created = 0, kmax = 0;
+  unsigned long long created = 0, kmax = 0, ovf = 0;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+  // timestamps travel with the key sort as 32-bit offsets from the batch's
+  // first event (ovf: the push falls back to a 64-bit gather after the sort)
+  const int64_t tbase = x.batch.ts[0];
   for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r += stride) {
     uint32_t f;
     uint64_t k = 0;
+    long long t;
     if (r < x.C) {
-      k = a.partitioned ? a.carry_key[r] : 0;
+      k = a.partitioned ? gld(a.carry_key, r) : 0;
       f = F_CAND;
+      t = (long long)gld(x.carry.ts, r);
     } else {
-      BatchRowCtx cx{&x.batch, r - x.C};
-      f = F_NEW;
+      // every load of the row is issued before the first use (no serial
+      // round trips): ts, key, f1 operands; the null-key test comes last
+      const int64_t br = r - x.C;
+      BatchRowCtx cx{&x.batch, br};
+      t = (long long)gld(x.batch.ts, br);
+      Val kv;
+      kv.b = 0;
+      kv.null = 0;
       if (a.partitioned) {
-        Val kv;
-        if (FAST || a.key_col >= 0) kv = col_load(x.batch, r - x.C, a.key_col);
+        if (FAST || a.key_col >= 0) kv = col_load(x.batch, br, a.key_col);
         else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
-        if (kv.null) f |= F_SKIP;   // PartitionStreamReceiver drops null keys
-        k = kv.null ? 0 : canon_key(kv, a.key_type);
       }
-      if (!(f & F_SKIP)) {
+      const bool p1 = a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx));
+      f = F_NEW;
+      if (kv.null) {
+        f |= F_SKIP;   // PartitionStreamReceiver drops null keys
+      } else {
         if (a.is_b) f |= F_B;
-        if (a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx))) {
+        if (p1) {
           f |= F_CAND;
           created++;
         }
+        k = canon_key(kv, a.key_type);
       }
-      long long t = (long long)x.batch.ts[r - x.C];
       tmin = t < tmin ? t : tmin;
       tmax = t > tmax ? t : tmax;
     }
@@ -218,19 +233,26 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       kmax = k > kmax ? k : kmax;
     }
     pv[r] = (f << kRowBits) | (uint32_t)r;
+    const int64_t dt = (int64_t)t - tbase;
+    ovf |= dt != (int64_t)(int32_t)dt;
+    tso[r] = (int32_t)dt;
   }
   // one partial per block (plain store; k_finish_prep folds them): no
   // same-address atomics from every wave of a large grid
-  for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    created += __shfl_xor(created, o, 64);
+    ovf |= __shfl_xor(ovf, o, 64);
+  }
   kmax = wave_max(kmax);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
     for (int w = 1; w < kBlock / 64; w++) {
+      r.ovf |= wpart[w].ovf;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -241,24 +263,30 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
 }
 
 __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
-  unsigned long long c = 0, km = 0;
+  unsigned long long c = 0, km = 0, ov = 0;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+#pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
+    ov |= blk[b].ovf;
     c += blk[b].n_cand;
     km = blk[b].kmax > km ? blk[b].kmax : km;
     tmin = blk[b].ts_min < tmin ? blk[b].ts_min : tmin;
     tmax = blk[b].ts_max > tmax ? blk[b].ts_max : tmax;
   }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o, 64);
+    ov |= __shfl_xor(ov, o, 64);
+  }
   km = wave_max(km);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax, ov};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
     for (int w = 1; w < kBlock / 64; w++) {
+      r.ovf |= wpart[w].ovf;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -271,6 +299,15 @@ __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int 
 __global__ void k_narrow_keys(const uint64_t* in, uint32_t* out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (uint32_t)in[i];
+}
+
+// Overflow path (a timestamp offset does not fit in 32 bits): full event
+// timestamps at sorted positions, gathered by row after the key sort.
+__global__ __launch_bounds__(kBlock) void k_sorted_ts64(const ExtRows* __restrict__ xp,
+                                                        const uint32_t* __restrict__ spv, int64_t n,
+                                                        int64_t* __restrict__ sts64) {
+  const ExtRows& x = *xp;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p = n) sts64[p] = x.ts(pv_row(spv[p]));
 }
 
 struct ScanArgs {
@@ -289,18 +326,24 @@ struct ScanOut {
   uint32_t violation;         // per-key timestamp decrease seen
   uint32_t pad;
 };
+// d_agg layout: PrepAgg at 0, ScanOut at 64, match / open totals at 128
+static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
 
 // One lane per position; candidates walk forward over the later events of
-// their key (sorted positions when partitioned, ext rows otherwise).  Reads of
-// flags / keys are sequential; only event timestamps (and f2 operands when an
-// event falls inside `within`) are gathered by row.  Writes the compaction
-// counts for matches (cm) and still-open partials (co) per position.
-template <bool K64, bool FAST>
+// their key (sorted positions when partitioned, ext rows otherwise).  Keys,
+// flags and timestamps are read at sorted positions (timestamps travel with
+// the key sort), so the walk is sequential; only f2 operands of events inside
+// `within` are gathered by row.  Writes a 1-byte outcome per position and the
+// per-tile match / open counts.
+template <bool K64, bool FAST, bool TS64>
 __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
-                                                         int64_t tile, const uint32_t* skey32,
-                                                         const uint64_t* skey64, const uint32_t* spv,
-                                                         int32_t* match_row, uint8_t* pst, uint32_t* bcnt,
-                                                         ScanOut* blk) {
+                                                         int64_t tile, const uint32_t* __restrict__ skey32,
+                                                         const uint64_t* __restrict__ skey64,
+                                                         const uint32_t* __restrict__ spv,
+                                                         const int32_t* __restrict__ sts32,
+                                                         const int64_t* __restrict__ sts64,
+                                                         int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                         uint32_t* __restrict__ bcnt, ScanOut* __restrict__ blk) {
   const ScanArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -310,41 +353,58 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   // this block's contiguous tile of positions (compaction offsets are per block)
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
+  // sorted timestamps: 32-bit offsets from the batch's first event, or full
+  // 64-bit values when some offset overflowed (separate instantiation: a
+  // run-time choice merges the two loads and serialises every load after it)
+  const int64_t tbase = TS64 ? 0 : x.batch.ts[0];
+  auto ts_at = [&](int64_t i) -> int64_t { return TS64 ? sts64[i] : tbase + (int64_t)sts32[i]; };
   for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
+    // the position and its first successor are loaded together (sequential,
+    // shared cache lines) before any of them is used
     const uint32_t pvp = spv[p];
+    const int64_t tsi = ts_at(p);
+    const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
+    int64_t q = p + 1;
+    const int64_t q0 = q < n_ext ? q : n_ext - 1;
+    uint32_t pq = spv[q0];
+    int64_t tq = ts_at(q0);
+    uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q0] : skey32[q0]);
     uint32_t m = 0, o = 0;
     if (pv_flags(pvp) & F_CAND) {
       const int64_t r = pv_row(pvp);
-      const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
-      const int64_t tsi = x.ts(r);
       int64_t prev = tsi;
       uint8_t st = ST_OPEN;
       int32_t j = -1;
-      for (int64_t q = p + 1; q < n_ext; q++) {
-        if (a.partitioned && (K64 ? skey64[q] : skey32[q]) != k) break;
-        const uint32_t pq = spv[q];
+      while (q < n_ext) {
+        if (a.partitioned && kq != k) break;
         const uint32_t fq = pv_flags(pq);
-        if (!(fq & F_NEW) || (fq & F_SKIP)) continue;
-        const int64_t r2 = pv_row(pq);
-        const int64_t t2 = x.ts(r2);
-        if (t2 < prev) {
-          viol = 1;
-          break;
-        }
-        prev = t2;
-        steps++;
-        // stabilizeStates -> expireEvents: |ts_i - t| > within
-        if (t2 - tsi > a.within) {
-          st = ST_DEAD;
-          break;
-        }
-        if (fq & F_B) {
-          PairCtx cx{&x, r, r2};
-          if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
-            st = ST_MATCH;
-            j = (int32_t)r2;
+        if ((fq & F_NEW) && !(fq & F_SKIP)) {
+          if (tq < prev) {
+            viol = 1;
             break;
           }
+          prev = tq;
+          steps++;
+          // stabilizeStates -> expireEvents: |ts_i - t| > within
+          if (tq - tsi > a.within) {
+            st = ST_DEAD;
+            break;
+          }
+          if (fq & F_B) {
+            const int64_t r2 = pv_row(pq);
+            PairCtx cx{&x, r, r2};
+            if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+              st = ST_MATCH;
+              j = (int32_t)r2;
+              break;
+            }
+          }
+        }
+        q++;
+        if (q < n_ext) {
+          pq = spv[q];
+          tq = ts_at(q);
+          if (a.partitioned) kq = K64 ? skey64[q] : skey32[q];
         }
       }
       if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) {
@@ -391,26 +451,50 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
 }
 
 // Stable compaction of one block's tile: position p with pst[p] == want gets
-// output index base + (# such positions before p in the tile).  Chunks of
-// kBlock positions; wave ballots + per-wave totals in LDS.
+// output index base + (# such positions before p in the tile).  Each thread
+// takes 16 consecutive outcome bytes per round (one 16-byte load; tiles start
+// on 256-byte boundaries and pst is padded by kCompactPad bytes), block-wide
+// exclusive scan of the per-thread counts, then emits its positions in order.
+constexpr int kCompactPad = kBlock * 16;
 template <class F>
-__device__ __forceinline__ void tile_compact(const uint8_t* pst, int64_t t0, int64_t t1, uint8_t want, uint32_t base,
-                                             F&& emit) {
+__device__ __forceinline__ void tile_compact(const uint8_t* __restrict__ pst, int64_t t0, int64_t t1, uint8_t want,
+                                             uint32_t base, F&& emit) {
   __shared__ uint32_t wsum[kBlock / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
-    const int64_t p = c0 + threadIdx.x;
-    const bool f = p < t1 && pst[p] == want;
-    const uint64_t bal = __ballot(f);
-    if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+  for (int64_t c0 = t0; c0 < t1; c0 += kBlock * 16) {
+    const int64_t pb = c0 + (int64_t)threadIdx.x * 16;
+    uint32_t wv[4] = {0u, 0u, 0u, 0u};
+    if (pb < t1) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
+      wv[0] = raw.x;
+      wv[1] = raw.y;
+      wv[2] = raw.z;
+      wv[3] = raw.w;
+    }
+    uint32_t hit = 0;   // bit i: position pb + i is wanted
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+      if (((wv[i >> 2] >> ((i & 3) * 8)) & 255u) == want && pb + i < t1) hit |= 1u << i;
+    const uint32_t cnt = (uint32_t)__popc(hit);
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
     __syncthreads();
-    uint32_t pre = base + (uint32_t)__popcll(bal & lt), tot = 0;
+    uint32_t pre = base + inc - cnt, tot = 0;
+#pragma unroll
     for (int k = 0; k < kBlock / 64; k++) {
       if (k < w) pre += wsum[k];
       tot += wsum[k];
     }
-    if (f) emit(p, pre);
+    while (hit) {
+      const int i = __ffs(hit) - 1;
+      hit &= hit - 1;
+      emit(pb + i, pre++);
+    }
     base += tot;
     __syncthreads();
   }
@@ -419,6 +503,7 @@ __device__ __forceinline__ void tile_compact(const uint8_t* pst, int64_t t0, int
 __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int nblk, ScanOut* out) {
   unsigned long long st = 0, pr = 0;
   uint32_t v = 0;
+#pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
     st += blk[b].steps;
     pr += blk[b].pruned;
@@ -491,7 +576,7 @@ struct GatherArgs {
   int ncols;
   int partitioned;
   int key64;
-  int8_t types[kMaxCols];
+  int32_t types[kMaxCols];
   void* dcol[kMaxCols];
   uint8_t* dnul[kMaxCols];
   int64_t* dts;
@@ -546,7 +631,7 @@ struct CarryTable {
     for (size_t c = 0; c < types.size(); c++) {
       cs.col[c] = col[c].p;
       cs.nul[c] = nul[c].as<uint8_t>();
-      cs.type[c] = (int8_t)types[c];
+      cs.type[c] = (int32_t)types[c];
     }
     cs.ts = ts.as<int64_t>();
     return cs;
@@ -586,8 +671,8 @@ struct PatternEngine : Engine {
   int64_t horizon = INT64_MIN;
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
-  DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_match, d_pst, d_bcnt, d_boff, d_pj, d_pi, d_pj_alt,
-      d_pi_alt, d_agg, d_sort, d_scan, d_blk;
+  DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
+      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk;
   PinnedBuf h_agg;
 
   int kind() const override { return ENG_PATTERN; }
@@ -623,12 +708,13 @@ struct PatternEngine : Engine {
     const int slot = isA ? 0 : 1;
     const bool key64 = partitioned && type_key64(key_type[slot]);
     d_pv.reserve(n_ext * 4);
+    d_ts.reserve(n_ext * 4);
     if (partitioned) {
       if (key64) d_k64.reserve(n_ext * 8);
       d_k32.reserve(n_ext * 4);
     }
     d_match.reserve(n_ext * 4);
-    d_pst.reserve(n_ext);
+    d_pst.reserve(n_ext + kCompactPad);
     d_agg.reserve(256);
     h_agg.reserve(256);
 
@@ -655,22 +741,24 @@ struct PatternEngine : Engine {
       pa.key_col = -1;
     }
     pa.carry_key = carry[cur].key.as<uint64_t>();
-    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN};
+    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0};
     PrepAgg* d_pa = d_agg.as<PrepAgg>();
     ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
     std::memcpy(h_agg.p, &init, sizeof(init));
     std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
     const int nblk = grid_for(n_ext);
-    d_blk.reserve((size_t)nblk * 32);
+    d_blk.reserve((size_t)nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!partitioned || pa.key_col >= 0);
     if (fast1)
       hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
     else
       hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_blk.as<PrepAgg>());
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
     SHD_CHECK_LAUNCH();
@@ -686,16 +774,19 @@ struct PatternEngine : Engine {
     counters.partials += (int64_t)pg.n_cand;
 
     // ---- key-sort the extended batch (stable: creation order within a key),
-    //      carrying the packed (flags, row) payload
+    //      carrying the packed (flags, row) payload and the event timestamp
     const uint32_t* skey32 = nullptr;
     const uint64_t* skey64 = nullptr;
     const uint32_t* spv = d_pv.as<uint32_t>();
+    const int32_t* sts32 = d_ts.as<int32_t>();
+    const int64_t* sts64 = nullptr;
     bool sorted64 = false;
     if (partitioned) {
       uint64_t kmax = pg.kmax;
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
       d_pv_alt.reserve(n_ext * 4);
+      d_ts_alt.reserve(n_ext * 4);
       bool in_alt = false;
       if (key64 && bits <= 32) {
         hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
@@ -704,18 +795,29 @@ struct PatternEngine : Engine {
       }
       if (bits <= 32) {
         d_k32_alt.reserve(n_ext * 4);
-        radix_sort_pairs_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
-                             d_pv_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
+        radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
+                               d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
+                               bits, d_sort, s, in_alt);
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);
-        radix_sort_pairs_u64(d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_k64_alt.as<uint64_t>(),
-                             d_pv_alt.as<uint32_t>(), n_ext, bits, d_sort, s, in_alt);
+        radix_sort_triples_u64(d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
+                               d_k64_alt.as<uint64_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
+                               bits, d_sort, s, in_alt);
         skey64 = in_alt ? d_k64_alt.as<uint64_t>() : d_k64.as<uint64_t>();
         sorted64 = true;
       }
       spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
+      sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
       mark("key_sort");
+    }
+    if (pg.ovf || getenv("SHD_TS64")) {   // SHD_TS64: force the 64-bit path (tests)
+      // some timestamp is more than 2^31 ms away from the batch's first event
+      d_ts64.reserve(n_ext * 8);
+      hipLaunchKernelGGL(k_sorted_ts64, dim3(grid_cover(n_ext)), dim3(kBlock), 0, s, dev_args(x), spv, n_ext,
+                         d_ts64.as<int64_t>());
+      SHD_CHECK_LAUNCH();
+      sts64 = d_ts64.as<int64_t>();
     }
 
     // ---- forward scan, one lane per position
@@ -735,17 +837,21 @@ struct PatternEngine : Engine {
     const int ntile = (int)ceil_div(n_ext, tile);
     d_bcnt.reserve((size_t)2 * ntile * 4);
     d_boff.reserve((size_t)2 * ntile * 4);
-#define SHD_LAUNCH_SCAN(K64, FAST)                                                                              \
-  hipLaunchKernelGGL((k_forward_scan<K64, FAST>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,   \
-                     skey64, spv, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(),             \
-                     d_blk.as<ScanOut>())
+#define SHD_LAUNCH_SCAN(K64, FAST, TS64)                                                                        \
+  hipLaunchKernelGGL((k_forward_scan<K64, FAST, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile,      \
+                     skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(),              \
+                     d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>())
+    const bool ts64 = sts64 != nullptr;
+#define SHD_LAUNCH_SCAN2(K64, FAST) \
+  if (ts64) SHD_LAUNCH_SCAN(K64, FAST, true); else SHD_LAUNCH_SCAN(K64, FAST, false)
     if (sorted64) {
-      if (fast2) SHD_LAUNCH_SCAN(true, true);
-      else SHD_LAUNCH_SCAN(true, false);
+      if (fast2) { SHD_LAUNCH_SCAN2(true, true); }
+      else { SHD_LAUNCH_SCAN2(true, false); }
     } else {
-      if (fast2) SHD_LAUNCH_SCAN(false, true);
-      else SHD_LAUNCH_SCAN(false, false);
+      if (fast2) { SHD_LAUNCH_SCAN2(false, true); }
+      else { SHD_LAUNCH_SCAN2(false, false); }
     }
+#undef SHD_LAUNCH_SCAN2
 #undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), ntile, d_so);
@@ -818,7 +924,7 @@ struct PatternEngine : Engine {
       ga.partitioned = partitioned;
       ga.key64 = sorted64;
       for (size_t c = 0; c < typesA.size(); c++) {
-        ga.types[c] = (int8_t)typesA[c];
+        ga.types[c] = (int32_t)typesA[c];
         ga.dcol[c] = carry[nxt].col[c].p;
         ga.dnul[c] = carry[nxt].nul[c].as<uint8_t>();
       }

@@ -1,9 +1,11 @@
 // primitives.hip -- device-wide building blocks on gfx950 (wave64):
 //   * exclusive scan of u32 counts (reduce -> scan block sums -> downsweep),
-//   * stable LSD radix sort of (key, u32 value) pairs, 8-bit digits, tiles of
-//     4096 keys per 256-thread workgroup, per-wave LDS histograms, stable
-//     in-tile ranking from eight 64-bit ballots per round,
+//   * stable LSD radix sort of (key, u32 value[, u32 value]) tuples, 8-bit
+//     digits, register-resident tiles of 4096 keys per 256-thread workgroup,
+//     XCD-aware tile order, stable in-wave ranking from ballots,
 //   * small helpers (iota, u64 max).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace shd {
@@ -118,136 +120,220 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* 
 }
 
 // ============================================================ radix sort
-constexpr int kRsRounds = 16;
-constexpr int kRsTile = kBlock * kRsRounds;   // 4096 keys per workgroup
+// One workgroup (kRsBlock threads, kRsWaves waves) sorts a tile of
+// R*kRsBlock keys per pass.  Wave w owns the contiguous slice
+// [t0 + w*64R, t0 + (w+1)*64R) and holds its R keys per lane in registers
+// (all loads issued up front).  Stable in-wave ranking from eight 64-bit
+// ballots per round and a per-wave running count per digit in LDS (the wave
+// executes in order, so no barrier between rounds); a tile needs four
+// workgroup barriers.  The tile is reordered by digit in LDS and written out
+// in per-digit runs, so consecutive lanes store consecutive addresses.
+// Optional second payload: a 32-bit word per key.
+#ifndef SHD_RS_ROUNDS
+#define SHD_RS_ROUNDS 24
+#endif
+#ifndef SHD_RS_BLOCK
+#define SHD_RS_BLOCK 256
+#endif
+constexpr int kRsRounds = SHD_RS_ROUNDS;
+constexpr int kRsBlock = SHD_RS_BLOCK;
+constexpr int kRsWaves = kRsBlock / 64;
+static_assert(kRsBlock >= 256 && kRsBlock % 64 == 0, "one thread per digit in the digit phases");
 
-template <class K>
-__global__ __launch_bounds__(kBlock) void k_rs_hist(const K* keys, int64_t n, int shift, uint32_t* hist, int nb) {
-  __shared__ uint32_t h[4][256];
-  int tid = threadIdx.x, w = tid >> 6;
-#pragma unroll
-  for (int i = 0; i < 4; i++) h[i][tid] = 0;
-  __syncthreads();
-  int64_t t0 = (int64_t)blockIdx.x * kRsTile;
-  for (int r = 0; r < kRsRounds; r++) {
-    int64_t idx = t0 + r * kBlock + tid;
-    if (idx < n) {
-      uint32_t d = (uint32_t)((keys[idx] >> shift) & 255u);
-      atomicAdd(&h[w][d], 1u);
-    }
-  }
-  __syncthreads();
-  hist[(int64_t)tid * nb + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+__host__ __device__ constexpr int rs_tile(int rounds) { return kRsBlock * rounds; }
+
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+// (blocks b and b+8 share one), so block b takes tile (b%8)*per + b/8: the
+// tiles of one XCD are consecutive, and the per-digit runs that neighbouring
+// tiles write next to each other meet in the same L2 (fewer partial-line
+// write-backs).  Any bijection is correct; this one is for speed only.
+__device__ __forceinline__ int rs_tile_of(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7, x = b & 7, i = b >> 3;
+  return x * per + (x < rem ? x : rem) + i;
 }
 
-// Scatter one 4096-key tile: stable in-tile ranking (ballots), the tile is
-// first reordered by digit in LDS, then written out so that consecutive lanes
-// store consecutive addresses of one digit bucket (coalesced runs instead of
-// one scattered dword per key).
 template <class K>
-__global__ __launch_bounds__(kBlock) void k_rs_scatter(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout,
-                                                       int64_t n, int shift, const uint32_t* hist,
-                                                       const uint32_t* offs, int nb) {
-  __shared__ K sk[kRsTile];
-  __shared__ uint32_t sv[kRsTile];
-  __shared__ uint32_t lpre[256];    // tile-local first position of each digit
-  __shared__ uint32_t lbase[256];   // running tile-local position per digit
-  __shared__ uint32_t gbase[256];   // global first position of this tile's digit run
-  __shared__ uint32_t wcnt[4][256];
+__device__ __forceinline__ uint32_t rs_digit(K k, int shift) { return (uint32_t)((k >> shift) & 255u); }
+
+template <class K, int R>
+__global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys, int64_t n, int shift,
+                                                      uint32_t* __restrict__ hist, int nb, int xcd) {
+  __shared__ uint32_t h[kRsWaves][256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
+  const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
+  const int64_t wb = (int64_t)tile * rs_tile(R) + (int64_t)w * 64 * R;
+  K k[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    k[r] = keys[idx < n ? idx : n - 1];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_digit(k[r], shift)], 1u);
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < kRsWaves; i++) c += h[i][tid];
+    hist[(int64_t)tid * nb + tile] = c;
+  }
+}
+
+template <class K, int R, bool P2>
+__global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                         const uint32_t* __restrict__ win, K* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout, uint32_t* __restrict__ wout,
+                                                         int64_t n, int shift, const uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ offs, int nb, int xcd) {
+  constexpr int T = rs_tile(R);
+  __shared__ K sk[T];
+  __shared__ uint32_t sv[T];
+  __shared__ uint32_t sw[P2 ? T : 1];
+  __shared__ uint32_t lpre[256];             // tile-local first position of each digit
+  __shared__ uint32_t gbase[256];            // global first position of this tile's digit run
+  __shared__ uint32_t wcnt[kRsWaves][256];   // per-wave running digit counts, then per-wave digit bases
   __shared__ uint32_t wsum[4];
-  int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int64_t t0 = (int64_t)blockIdx.x * kRsTile;
-  // tile-local exclusive prefix over digits from this tile's histogram column
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
+  const int64_t t0 = (int64_t)tile * T;
+  const int64_t wb = t0 + (int64_t)w * 64 * R;
+  K k[R];
+  uint32_t v[R];
+  uint32_t x[P2 ? R : 1];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    const int64_t li = idx < n ? idx : n - 1;
+    k[r] = kin[li];
+    v[r] = vin[li];
+    if (P2) x[r] = win[li];
+  }
+  for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&wcnt[0][0])[i] = 0;
   {
-    uint32_t c = hist[(int64_t)tid * nb + blockIdx.x];
+    // tile-local exclusive prefix over digits from this tile's histogram
+    // column (threads 0..255, one digit each)
+    const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
     uint32_t inc = c;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      uint32_t t = __shfl_up(inc, o, 64);
+      const uint32_t t = __shfl_up(inc, o, 64);
       if (lane >= o) inc += t;
     }
-    if (lane == 63) wsum[w] = inc;
+    if (lane == 63 && w < 4) wsum[w] = inc;
+    if (tid < 256) gbase[tid] = offs[(int64_t)tid * nb + tile];
     __syncthreads();
-    uint32_t pre = 0;
-    for (int i = 0; i < w; i++) pre += wsum[i];
-    lpre[tid] = pre + inc - c;
-    lbase[tid] = pre + inc - c;
-    gbase[tid] = offs[(int64_t)tid * nb + blockIdx.x];
+    if (tid < 256) {
+      uint32_t pre = 0;
+      for (int i = 0; i < w; i++) pre += wsum[i];
+      lpre[tid] = pre + inc - c;
+    }
   }
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int r = 0; r < kRsRounds; r++) {
-    int64_t idx = t0 + r * kBlock + tid;
-    bool valid = idx < n;
-    K k = valid ? kin[idx] : (K)0;
-    uint32_t v = valid ? vin[idx] : 0u;
-    uint32_t d = (uint32_t)((k >> shift) & 255u);
+  uint32_t lr[R];
 #pragma unroll
-    for (int i = 0; i < 4; i++) wcnt[i][tid] = 0;
-    __syncthreads();
-    uint64_t peers = __ballot(valid);
+  for (int r = 0; r < R; r++) {
+    const bool ok = wb + r * 64 + lane < n;
+    const uint32_t d = rs_digit(k[r], shift);
+    uint64_t peers = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      bool bit = (d >> b) & 1u;
-      uint64_t m = __ballot(bit);
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
       peers &= bit ? m : ~m;
     }
-    int rank = __popcll(peers & lt);
-    if (valid && (peers & lt) == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = lbase[d] + rank;
-      for (int ww = 0; ww < w; ww++) pos += wcnt[ww][d];
-      sk[pos] = k;
-      sv[pos] = v;
-    }
-    __syncthreads();
-    lbase[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+    const uint64_t below = peers & lt;
+    const uint32_t c = wcnt[w][d];
+    lr[r] = c + (uint32_t)__popcll(below);
+    __builtin_amdgcn_wave_barrier();
+    if (ok && below == 0) wcnt[w][d] = c + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  int64_t tile_n = n - t0 < kRsTile ? n - t0 : kRsTile;
-  for (int i = tid; i < tile_n; i += kBlock) {
-    K k = sk[i];
-    uint32_t d = (uint32_t)((k >> shift) & 255u);
-    uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
-    kout[o] = k;
+  if (tid < 256) {
+    uint32_t acc = lpre[tid];
+#pragma unroll
+    for (int i = 0; i < kRsWaves; i++) {
+      const uint32_t c = wcnt[i][tid];
+      wcnt[i][tid] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (wb + r * 64 + lane < n) {
+      const uint32_t pos = wcnt[w][rs_digit(k[r], shift)] + lr[r];
+      sk[pos] = k[r];
+      sv[pos] = v[r];
+      if (P2) sw[pos] = x[r];
+    }
+  }
+  __syncthreads();
+  const int tile_n = n - t0 < T ? (int)(n - t0) : T;
+#pragma unroll 4
+  for (int i = tid; i < tile_n; i += kRsBlock) {
+    const K kk = sk[i];
+    const uint32_t d = rs_digit(kk, shift);
+    const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
+    kout[o] = kk;
     vout[o] = sv[i];
+    if (P2) wout[o] = sw[i];
   }
 }
 
-template <class K>
-static void radix_sort_impl(K* keys, uint32_t* vals, K* keys_alt, uint32_t* vals_alt, int64_t n, int bits,
-                            DevBuf& scratch, hipStream_t s, bool& in_alt) {
+template <class K, int R, bool P2>
+static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, uint32_t* vals_alt, uint32_t* w_alt,
+                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
   in_alt = false;
   if (n <= 1 || bits <= 0) return;
-  int nb = (int)ceil_div(n, kRsTile);
-  int64_t nh = (int64_t)nb * 256;
+  const int nb = (int)ceil_div(n, rs_tile(R));
+  const int64_t nh = (int64_t)nb * 256;
   // scratch layout: hist[nh] | offs[nh] | scan scratch
-  size_t need = (size_t)(2 * nh + scan_need(nh)) * sizeof(uint32_t);
+  const size_t need = (size_t)(2 * nh + scan_need(nh)) * sizeof(uint32_t);
   scratch.reserve(need);
   uint32_t* hist = scratch.as<uint32_t>();
   uint32_t* offs = hist + nh;
   uint32_t* sscr = offs + nh;
-  K* ki = keys; uint32_t* vi = vals; K* ko = keys_alt; uint32_t* vo = vals_alt;
+  const int xcd = getenv("SHD_RS_NOXCD") ? 0 : 1;   // A/B switch for the tile order
+  K* ki = keys; uint32_t* vi = vals; uint32_t* wi = w;
+  K* ko = keys_alt; uint32_t* vo = vals_alt; uint32_t* wo = w_alt;
   for (int shift = 0; shift < bits; shift += 8) {
-    hipLaunchKernelGGL(k_rs_hist<K>, dim3(nb), dim3(kBlock), 0, s, (const K*)ki, n, shift, hist, nb);
+    hipLaunchKernelGGL((k_rs_hist<K, R>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd);
     SHD_CHECK_LAUNCH();
     scan_raw(hist, offs, nh, nullptr, sscr, s);
-    hipLaunchKernelGGL(k_rs_scatter<K>, dim3(nb), dim3(kBlock), 0, s, (const K*)ki, (const uint32_t*)vi, ko, vo, n,
-                       shift, (const uint32_t*)hist, (const uint32_t*)offs, nb);
+    hipLaunchKernelGGL((k_rs_scatter<K, R, P2>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, (const uint32_t*)vi,
+                       (const uint32_t*)wi, ko, vo, wo, n, shift, (const uint32_t*)hist, (const uint32_t*)offs, nb, xcd);
     SHD_CHECK_LAUNCH();
     std::swap(ki, ko);
     std::swap(vi, vo);
+    std::swap(wi, wo);
     in_alt = !in_alt;
   }
 }
 
 void radix_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int64_t n,
                           int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
-  radix_sort_impl<uint32_t>(keys, vals, keys_alt, vals_alt, n, bits, scratch, s, in_alt);
+  radix_sort_run<uint32_t, kRsRounds, false>(keys, vals, nullptr, keys_alt, vals_alt, nullptr, n, bits, scratch, s,
+                                             in_alt);
 }
 
 void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, uint32_t* vals_alt, int64_t n,
                           int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
-  radix_sort_impl<uint64_t>(keys, vals, keys_alt, vals_alt, n, bits, scratch, s, in_alt);
+  radix_sort_run<uint64_t, kRsRounds, false>(keys, vals, nullptr, keys_alt, vals_alt, nullptr, n, bits, scratch, s,
+                                             in_alt);
+}
+
+void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
+  radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt);
+}
+
+void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
+  radix_sort_run<uint64_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt);
 }
 
 // ============================================================ helpers

@@ -577,6 +577,10 @@ int shd_push(shd_query* q, const shd_batch* b) {
     if ((int)types.size() > kMaxCols) return fail(SHD_E_UNSUPPORTED, "too many attributes");
     if (b->n < 0 || (b->n > 0 && (!b->ts || !b->cols))) return fail(SHD_E_ARG, "bad batch");
     if (b->n == 0) return SHD_OK;
+    // every column carries n value slots, null rows included (device kernels
+    // load the value and the null byte together)
+    for (int c = 0; c < b->ncols; c++)
+      if (!b->cols[c]) return fail(SHD_E_ARG, "null column pointer (null rows still need a value slot)");
     SHD_HIP(hipSetDevice(q->ctx->device));
     Staged st;
     st.stream = b->stream;

@@ -106,3 +106,26 @@ def test_pruned_partials_and_horizon_guard(hip_available):
         assert ei.value.code == SHD_E_UNSUPPORTED
     finally:
         dq.close()
+
+
+@pytest.mark.parametrize("within", ["within 40 days", ""])
+def test_timestamps_beyond_32bit_offsets(hip_available, within):
+    """Timestamps travel with the key sort as 32-bit offsets from the batch's
+    first event; a batch spanning more than 2^31 ms (with or without `within`)
+    takes the 64-bit path and must give the same matches."""
+    app = ("define stream S (k int, p double); partition with (k of S) begin "
+           "@info(name='q') from every e1=S[p>50] -> e2=S[p>e1.p] " + within +
+           " select e1.k as k, e1.p as p1, e2.p as p2, e2.p - e1.p as d insert into O; end;")
+    qp, _ = compile_single_query(app)
+    rng = np.random.default_rng(17)
+    n = 20000
+    k = rng.integers(0, 500, n).astype(np.int32)
+    p = rng.uniform(0, 100, n)
+    ts = 1_600_000_000_000 + np.cumsum(rng.integers(0, 400_000, n)).astype(np.int64)   # ~46 days
+    assert ts[-1] - ts[0] > 2 ** 31
+    batches = [(0, ColumnBatch(ts[a:b], [k[a:b], p[a:b]], [None, None], np.arange(a, b + 1, 1000) - a))
+               for a, b in ((0, 7000), (7000, n))]
+    ora = run_oracle(qp, batches)
+    dev, _, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
