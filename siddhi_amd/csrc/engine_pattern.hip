@@ -33,9 +33,9 @@ namespace {
 
 enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
 // Per-position scan result (positions = key-sorted order when partitioned).
-enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3 };
+enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5 };
 // per-position outcome stored by k_forward_scan for the compaction kernels
-enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2 };
+enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3 };
 
 // Sort payload: row index of the extended batch (28 bits) | flags (4 bits).
 constexpr int kRowBits = 28;
@@ -329,96 +329,79 @@ struct ScanOut {
 // d_agg layout: PrepAgg at 0, ScanOut at 64, match / open totals at 128
 static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
 
-// One lane per position; candidates walk forward over the later events of
-// their key (sorted positions when partitioned, ext rows otherwise).  Keys,
-// flags and timestamps are read at sorted positions (timestamps travel with
-// the key sort), so the walk is sequential; only f2 operands of events inside
-// `within` are gathered by row.  Writes a 1-byte outcome per position and the
-// per-tile match / open counts.
-template <bool K64, bool FAST, bool TS64>
-__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
-                                                         int64_t tile, const uint32_t* __restrict__ skey32,
-                                                         const uint64_t* __restrict__ skey64,
-                                                         const uint32_t* __restrict__ spv,
-                                                         const int32_t* __restrict__ sts32,
-                                                         const int64_t* __restrict__ sts64,
-                                                         int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
-                                                         uint32_t* __restrict__ bcnt, ScanOut* __restrict__ blk) {
-  const ScanArgs& a = *ap;
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
-  const ExtRows& x = a.x;
-  uint64_t steps = 0, pruned = 0;
-  uint32_t viol = 0, nm = 0, no = 0;
-  // this block's contiguous tile of positions (compaction offsets are per block)
-  const int64_t t0 = (int64_t)blockIdx.x * tile;
-  const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
-  // sorted timestamps: 32-bit offsets from the batch's first event, or full
-  // 64-bit values when some offset overflowed (separate instantiation: a
-  // run-time choice merges the two loads and serialises every load after it)
-  const int64_t tbase = TS64 ? 0 : x.batch.ts[0];
-  auto ts_at = [&](int64_t i) -> int64_t { return TS64 ? sts64[i] : tbase + (int64_t)sts32[i]; };
-  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
-    // the position and its first successor are loaded together (sequential,
-    // shared cache lines) before any of them is used
-    const uint32_t pvp = spv[p];
-    const int64_t tsi = ts_at(p);
-    const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
-    int64_t q = p + 1;
-    const int64_t q0 = q < n_ext ? q : n_ext - 1;
-    uint32_t pq = spv[q0];
-    int64_t tq = ts_at(q0);
-    uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q0] : skey32[q0]);
-    uint32_t m = 0, o = 0;
-    if (pv_flags(pvp) & F_CAND) {
-      const int64_t r = pv_row(pvp);
-      int64_t prev = tsi;
-      uint8_t st = ST_OPEN;
-      int32_t j = -1;
-      while (q < n_ext) {
-        if (a.partitioned && kq != k) break;
-        const uint32_t fq = pv_flags(pq);
-        if ((fq & F_NEW) && !(fq & F_SKIP)) {
-          if (tq < prev) {
-            viol = 1;
+// Walk of one candidate partial P (row r, key k, timestamp tsi) over the
+// later events of its key, starting at position q whose pv / ts / key are
+// already loaded (pq, tq, kq).  StreamPreStateProcessor.processAndReturn for
+// this plan shape: expire when ts - tsi > within, complete at the first
+// B event with f2(P, event).
+//   DEFER: f2 is not evaluated here; the walk stops at the first B event
+//          inside `within` and returns ST_DEFER with q at that event (the
+//          step is already counted).  Keeps the hot kernel free of the f2
+//          code (its registers and instruction footprint).
+//   f2_first: resume at a deferred event: evaluate f2 at q first.
+template <bool K64, bool TS64, bool DEFER, bool FAST>
+__device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext,
+                                                const uint32_t* __restrict__ skey32,
+                                                const uint64_t* __restrict__ skey64,
+                                                const uint32_t* __restrict__ spv, const int32_t* __restrict__ sts32,
+                                                const int64_t* __restrict__ sts64, int64_t tbase, int64_t r,
+                                                uint64_t k, int64_t tsi, int64_t& q, uint32_t pq, int64_t tq,
+                                                uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
+                                                uint64_t& steps, uint32_t& viol) {
+  uint8_t st = ST_OPEN;
+  while (q < n_ext) {
+    if (!f2_now) {
+      if (a.partitioned && kq != k) break;
+      const uint32_t fq = pv_flags(pq);
+      if ((fq & F_NEW) && !(fq & F_SKIP)) {
+        if (tq < prev) {
+          viol = 1;
+          break;
+        }
+        prev = tq;
+        steps++;
+        // stabilizeStates -> expireEvents: |ts_i - t| > within
+        if (tq - tsi > a.within) {
+          st = ST_DEAD;
+          break;
+        }
+        if (fq & F_B) {
+          if (DEFER) {
+            st = ST_DEFER;
             break;
           }
-          prev = tq;
-          steps++;
-          // stabilizeStates -> expireEvents: |ts_i - t| > within
-          if (tq - tsi > a.within) {
-            st = ST_DEAD;
-            break;
-          }
-          if (fq & F_B) {
-            const int64_t r2 = pv_row(pq);
-            PairCtx cx{&x, r, r2};
-            if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
-              st = ST_MATCH;
-              j = (int32_t)r2;
-              break;
-            }
-          }
-        }
-        q++;
-        if (q < n_ext) {
-          pq = spv[q];
-          tq = ts_at(q);
-          if (a.partitioned) kq = K64 ? skey64[q] : skey32[q];
+          f2_now = true;
         }
       }
-      if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) {
-        st = ST_DEAD;   // every later event is at or after t_end: it would expire this partial
-        pruned++;
-      }
-      match_row[p] = j;
-      m = st == ST_MATCH;
-      o = st == ST_OPEN;
     }
-    pst[p] = (uint8_t)(m ? PS_MATCH : (o ? PS_OPEN : PS_NONE));
-    nm += m;
-    no += o;
+    if constexpr (!DEFER) {
+      if (f2_now) {
+        f2_now = false;
+        const int64_t r2 = pv_row(pq);
+        PairCtx cx{&a.x, r, r2};
+        if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+          st = ST_MATCH;
+          j = (int32_t)r2;
+          break;
+        }
+      }
+    }
+    q++;
+    if (q < n_ext) {
+      pq = spv[q];
+      tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
+      if (a.partitioned) kq = K64 ? skey64[q] : skey32[q];
+    }
   }
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+  return st;
+}
+
+// Per-block reduction of the scan counters: ScanOut partial at blk[slot] and
+// the tile's match / open counts (plain store, or added for the resume pass).
+__device__ __forceinline__ void scan_block_reduce(uint64_t steps, uint64_t pruned, uint32_t viol, uint32_t nm,
+                                                  uint32_t no, ScanOut* blk, int slot, uint32_t* bcnt, int tile,
+                                                  int ntile, bool add) {
   for (int o2 = 32; o2 > 0; o2 >>= 1) {
     steps += __shfl_xor(steps, o2, 64);
     pruned += __shfl_xor(pruned, o2, 64);
@@ -444,10 +427,135 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
       tm += wcnt[0][w];
       to += wcnt[1][w];
     }
-    blk[blockIdx.x] = r;
-    bcnt[blockIdx.x] = tm;               // matches of this tile
-    bcnt[gridDim.x + blockIdx.x] = to;   // still-open partials of this tile
+    blk[slot] = r;
+    if (add) {
+      if (tm) atomicAdd(&bcnt[tile], tm);
+      if (to) atomicAdd(&bcnt[ntile + tile], to);
+    } else {
+      bcnt[tile] = tm;           // matches of this tile
+      bcnt[ntile + tile] = to;   // still-open partials of this tile
+    }
   }
+}
+
+// One lane per position; candidates walk forward over the later events of
+// their key (sorted positions when partitioned, ext rows otherwise).  Keys,
+// flags and timestamps are read at sorted positions (timestamps travel with
+// the key sort), so the walk is sequential.  A walk that reaches a B event
+// inside `within` is deferred to k_forward_resume (pst = PS_DEFER, resume
+// position in match_row).  Writes a 1-byte outcome per position and the
+// per-tile match / open counts.
+template <bool K64, bool TS64>
+__global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
+                                                         int64_t tile, const uint32_t* __restrict__ skey32,
+                                                         const uint64_t* __restrict__ skey64,
+                                                         const uint32_t* __restrict__ spv,
+                                                         const int32_t* __restrict__ sts32,
+                                                         const int64_t* __restrict__ sts64,
+                                                         int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                         uint32_t* __restrict__ bcnt, ScanOut* __restrict__ blk) {
+  const ScanArgs& a = *ap;
+  const DExprSet es{};
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0, nm = 0, no = 0;
+  // this block's contiguous tile of positions (compaction offsets are per block)
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
+  // sorted timestamps: 32-bit offsets from the batch's first event, or full
+  // 64-bit values when some offset overflowed (separate instantiation: a
+  // run-time choice merges the two loads and serialises every load after it)
+  const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
+  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
+    // the position and its first successor are loaded together (sequential,
+    // shared cache lines) before any of them is used
+    const int64_t q0 = p + 1 < n_ext ? p + 1 : n_ext - 1;
+    const uint32_t pvp = spv[p];
+    const int64_t tsi = TS64 ? sts64[p] : tbase + (int64_t)sts32[p];
+    const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
+    const uint32_t pq = spv[q0];
+    const int64_t tq = TS64 ? sts64[q0] : tbase + (int64_t)sts32[q0];
+    const uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q0] : skey32[q0]);
+    uint8_t out = PS_NONE;
+    if (pv_flags(pvp) & F_CAND) {
+      int64_t q = p + 1;
+      int32_t j = -1;
+      const uint8_t st = walk_partial<K64, TS64, true, false>(a, es, n_ext, skey32, skey64, spv, sts32, sts64, tbase,
+                                                              pv_row(pvp), k, tsi, q, pq, tq, kq, tsi, false, j,
+                                                              steps, viol);
+      if (st == ST_DEFER) {
+        out = PS_DEFER;
+        match_row[p] = (int32_t)q;   // resume position (< 2^28)
+      } else if (st == ST_OPEN) {
+        out = PS_OPEN;
+        no++;
+      } else if (st == ST_PRUNED) {
+        pruned++;   // every later event is at or after t_end: it would expire this partial
+      }
+    }
+    pst[p] = out;
+  }
+  scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
+}
+
+// Deferred walks: positions whose walk reached a B event inside `within`
+// evaluate f2 there (FAST: pre-decoded predicate, else the interpreter) and
+// continue.  Same tiles as k_forward_scan; 16 outcome bytes per thread.
+template <bool K64, bool FAST, bool TS64>
+__global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __restrict__ ap, int64_t n_ext,
+                                                           int64_t tile, const uint32_t* __restrict__ skey32,
+                                                           const uint64_t* __restrict__ skey64,
+                                                           const uint32_t* __restrict__ spv,
+                                                           const int32_t* __restrict__ sts32,
+                                                           const int64_t* __restrict__ sts64,
+                                                           int32_t* __restrict__ match_row,
+                                                           uint8_t* __restrict__ pst, uint32_t* __restrict__ bcnt,
+                                                           ScanOut* __restrict__ blk) {
+  const ScanArgs& a = *ap;
+  __shared__ LdsProg prog;
+  const DExprSet es = stage_prog(a.es, prog);
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0, nm = 0, no = 0;
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
+  const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
+  for (int64_t c0 = t0; c0 < t1; c0 += kBlock * 16) {
+    const int64_t pb = c0 + (int64_t)threadIdx.x * 16;
+    if (pb >= t1) continue;
+    const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
+    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+    uint32_t hit = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+      if (((wv[i >> 2] >> ((i & 3) * 8)) & 255u) == PS_DEFER && pb + i < t1) hit |= 1u << i;
+    while (hit) {
+      const int64_t p = pb + __ffs(hit) - 1;
+      hit &= hit - 1;
+      int64_t q = match_row[p];
+      const uint32_t pvp = spv[p];
+      const int64_t tsi = TS64 ? sts64[p] : tbase + (int64_t)sts32[p];
+      const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
+      const uint32_t pq = spv[q];
+      const int64_t tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
+      const uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q] : skey32[q]);
+      int32_t j = -1;
+      const uint8_t st = walk_partial<K64, TS64, false, FAST>(a, es, n_ext, skey32, skey64, spv, sts32, sts64, tbase,
+                                                              pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j,
+                                                              steps, viol);
+      uint8_t out = PS_NONE;
+      if (st == ST_MATCH) {
+        out = PS_MATCH;
+        match_row[p] = j;
+        nm++;
+      } else if (st == ST_OPEN) {
+        out = PS_OPEN;
+        no++;
+      } else if (st == ST_PRUNED) {
+        pruned++;
+      }
+      pst[p] = out;
+    }
+  }
+  scan_block_reduce(steps, pruned, viol, nm, no, blk, gridDim.x + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
 }
 
 // Stable compaction of one block's tile: position p with pst[p] == want gets
@@ -748,7 +856,7 @@ struct PatternEngine : Engine {
     std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
     const int nblk = grid_for(n_ext);
-    d_blk.reserve((size_t)nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
+    d_blk.reserve((size_t)2 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!partitioned || pa.key_col >= 0);
     if (fast1)
@@ -837,24 +945,36 @@ struct PatternEngine : Engine {
     const int ntile = (int)ceil_div(n_ext, tile);
     d_bcnt.reserve((size_t)2 * ntile * 4);
     d_boff.reserve((size_t)2 * ntile * 4);
-#define SHD_LAUNCH_SCAN(K64, FAST, TS64)                                                                        \
-  hipLaunchKernelGGL((k_forward_scan<K64, FAST, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile,      \
+    const bool ts64 = sts64 != nullptr;
+    // hot walk without f2 (deferrals), then the deferred walks with f2
+#define SHD_LAUNCH_SCAN(K64, TS64)                                                                              \
+  hipLaunchKernelGGL((k_forward_scan<K64, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
+                     skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), \
+                     d_blk.as<ScanOut>())
+#define SHD_LAUNCH_RESUME(K64, FAST, TS64)                                                                      \
+  hipLaunchKernelGGL((k_forward_resume<K64, FAST, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile,    \
                      skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(),              \
                      d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>())
-    const bool ts64 = sts64 != nullptr;
-#define SHD_LAUNCH_SCAN2(K64, FAST) \
-  if (ts64) SHD_LAUNCH_SCAN(K64, FAST, true); else SHD_LAUNCH_SCAN(K64, FAST, false)
+#define SHD_LAUNCH_RESUME2(K64, FAST) \
+  if (ts64) SHD_LAUNCH_RESUME(K64, FAST, true); else SHD_LAUNCH_RESUME(K64, FAST, false)
     if (sorted64) {
-      if (fast2) { SHD_LAUNCH_SCAN2(true, true); }
-      else { SHD_LAUNCH_SCAN2(true, false); }
+      if (ts64) SHD_LAUNCH_SCAN(true, true); else SHD_LAUNCH_SCAN(true, false);
+      SHD_CHECK_LAUNCH();
+      if (fast2) { SHD_LAUNCH_RESUME2(true, true); }
+      else { SHD_LAUNCH_RESUME2(true, false); }
     } else {
-      if (fast2) { SHD_LAUNCH_SCAN2(false, true); }
-      else { SHD_LAUNCH_SCAN2(false, false); }
+      if (ts64) SHD_LAUNCH_SCAN(false, true); else SHD_LAUNCH_SCAN(false, false);
+      SHD_CHECK_LAUNCH();
+      if (fast2) { SHD_LAUNCH_RESUME2(false, true); }
+      else { SHD_LAUNCH_RESUME2(false, false); }
     }
-#undef SHD_LAUNCH_SCAN2
+#undef SHD_LAUNCH_RESUME2
+#undef SHD_LAUNCH_RESUME
 #undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), ntile, d_so);
+    // partials: [0, ntile) hot walk, [ntile, 2 ntile) deferred walks
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), 2 * ntile,
+                       d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
 

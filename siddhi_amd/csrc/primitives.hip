@@ -163,16 +163,37 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
   for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
   const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
   const int64_t wb = (int64_t)tile * rs_tile(R) + (int64_t)w * 64 * R;
-  K k[R];
+  bool done = false;
+  if constexpr (sizeof(K) == 4 && R % 4 == 0) {
+    if ((int64_t)(tile + 1) * rs_tile(R) <= n) {
+      // full tile of 32-bit keys: 16-byte loads (counting needs no order)
+      const uint4* kv = reinterpret_cast<const uint4*>(keys + wb);
+      uint4 q[R / 4];
 #pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int64_t idx = wb + r * 64 + lane;
-    k[r] = keys[idx < n ? idx : n - 1];
+      for (int i = 0; i < R / 4; i++) q[i] = kv[i * 64 + lane];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < R / 4; i++) {
+        atomicAdd(&h[w][(q[i].x >> shift) & 255u], 1u);
+        atomicAdd(&h[w][(q[i].y >> shift) & 255u], 1u);
+        atomicAdd(&h[w][(q[i].z >> shift) & 255u], 1u);
+        atomicAdd(&h[w][(q[i].w >> shift) & 255u], 1u);
+      }
+      done = true;
+    }
   }
-  __syncthreads();
+  if (!done) {
+    K k[R];
 #pragma unroll
-  for (int r = 0; r < R; r++)
-    if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_digit(k[r], shift)], 1u);
+    for (int r = 0; r < R; r++) {
+      const int64_t idx = wb + r * 64 + lane;
+      k[r] = keys[idx < n ? idx : n - 1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r++)
+      if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_digit(k[r], shift)], 1u);
+  }
   __syncthreads();
   if (tid < 256) {
     uint32_t c = 0;
@@ -200,6 +221,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
   const int64_t t0 = (int64_t)tile * T;
   const int64_t wb = t0 + (int64_t)w * 64 * R;
+  // this tile's histogram column and global digit offsets are loaded first:
+  // the digit prefix below then waits only for them, while the key loads
+  // issued after them are still in flight (in-order vmcnt)
+  const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t gb = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
   K k[R];
   uint32_t v[R];
   uint32_t x[P2 ? R : 1];
@@ -213,9 +239,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   }
   for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&wcnt[0][0])[i] = 0;
   {
-    // tile-local exclusive prefix over digits from this tile's histogram
-    // column (threads 0..255, one digit each)
-    const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
+    // tile-local exclusive prefix over digits (threads 0..255, one digit each)
     uint32_t inc = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -223,7 +247,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
       if (lane >= o) inc += t;
     }
     if (lane == 63 && w < 4) wsum[w] = inc;
-    if (tid < 256) gbase[tid] = offs[(int64_t)tid * nb + tile];
+    if (tid < 256) gbase[tid] = gb;
     __syncthreads();
     if (tid < 256) {
       uint32_t pre = 0;
@@ -277,7 +301,14 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   for (int i = tid; i < tile_n; i += kRsBlock) {
     const K kk = sk[i];
     const uint32_t d = rs_digit(kk, shift);
+#if defined(SHD_RS_EXP) && SHD_RS_EXP == 1   // timing experiment: coalesced identity write-out
+    const uint32_t o = (uint32_t)(t0 + i) + 0 * (gbase[d] - lpre[d]);
+#elif defined(SHD_RS_EXP) && SHD_RS_EXP == 2   // timing experiment: no write-out
     const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
+    if (i != 0) continue;
+#else
+    const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
+#endif
     kout[o] = kk;
     vout[o] = sv[i];
     if (P2) wout[o] = sw[i];
@@ -289,6 +320,9 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
                            int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
   in_alt = false;
   if (n <= 1 || bits <= 0) return;
+  // k_rs_hist reads full tiles of 32-bit keys with 16-byte loads
+  if ((reinterpret_cast<uintptr_t>(keys) | reinterpret_cast<uintptr_t>(keys_alt)) & 15)
+    throw Error(SHD_E_ARG, "radix sort: key arrays must be 16-byte aligned");
   const int nb = (int)ceil_div(n, rs_tile(R));
   const int64_t nh = (int64_t)nb * 256;
   // scratch layout: hist[nh] | offs[nh] | scan scratch
