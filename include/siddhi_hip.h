@@ -90,7 +90,9 @@ typedef struct shd_counters {
   int64_t bytes_touched;        /* algorithmic bytes             */
   int64_t kernel_ns;            /* device time of the last push                  */
   int64_t carry;                /* open partials / window items carried          */
-  int64_t reserved;
+  int64_t group_bits;           /* pattern engine: sort bits of the last push's key
+                                   grouping (hashed buckets when below the key
+                                   width), 0 when not partitioned              */
 } shd_counters;
 
 int shd_device_count(int* n);

@@ -177,6 +177,14 @@ inline int type_size(int t) {
   return 8;
 }
 
+// Bijective 32-bit mix (odd multiply, then xor-shift by half the width):
+// equal keys map to equal values, and the low bits depend on every key bit,
+// so its low bits make well-spread buckets for any key distribution.
+__host__ __device__ __forceinline__ uint32_t key_bucket_mix(uint32_t k) {
+  const uint32_t h = k * 0x9E3779B1u;
+  return h ^ (h >> 16);
+}
+
 // ------------------------------------------------------------------ primitives (primitives.hip)
 // Exclusive scan of u32 counts -> u32 offsets; returns nothing (total read from out[n-1]+in[n-1]).
 void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev,
@@ -188,8 +196,12 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& result_in_alt);
 // Device-wide max of u64 keys (result to dev ptr).
 // Same, carrying a second 32-bit payload word per key.
+// hashed: digits are taken from key_bucket_mix(key) instead of the key, so
+// bits < 32 groups equal keys into 2^bits buckets (stable: input order inside
+// a bucket) while the array still carries the raw keys.
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
-                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
+                            bool hashed = false);
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
 void reduce_max_u64(const uint64_t* in, int64_t n, uint64_t* out_dev, hipStream_t s);

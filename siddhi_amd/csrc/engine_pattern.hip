@@ -22,6 +22,7 @@
 // open partials carry to the next push.  A per-key timestamp decrease is
 // detected on device and rejected (SHD_E_UNSUPPORTED), never approximated.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -140,6 +141,8 @@ struct PrepAgg {
   long long ts_min;
   long long ts_max;
   unsigned long long ovf;   // some row's ts - batch.ts[0] does not fit in int32
+  unsigned long long unmono;   // some batch row's ts is below its predecessor's
+  long long carry_tmax;        // latest carried partial (LLONG_MIN: none)
 };
 
 struct PrepArgs {
@@ -185,8 +188,8 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
-  unsigned long long created = 0, kmax = 0, ovf = 0;
-  long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+  unsigned long long created = 0, kmax = 0, ovf = 0, unmono = 0;
+  long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctmax = LLONG_MIN;
   // timestamps travel with the key sort as 32-bit offsets from the batch's
   // first event (ovf: the push falls back to a 64-bit gather after the sort)
   const int64_t tbase = x.batch.ts[0];
@@ -198,12 +201,14 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       k = a.partitioned ? gld(a.carry_key, r) : 0;
       f = F_CAND;
       t = (long long)gld(x.carry.ts, r);
+      ctmax = t > ctmax ? t : ctmax;
     } else {
       // every load of the row is issued before the first use (no serial
       // round trips): ts, key, f1 operands; the null-key test comes last
       const int64_t br = r - x.C;
       BatchRowCtx cx{&x.batch, br};
       t = (long long)gld(x.batch.ts, br);
+      const long long tprev = br > 0 ? (long long)gld(x.batch.ts, br - 1) : t;
       Val kv;
       kv.b = 0;
       kv.null = 0;
@@ -225,6 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       }
       tmin = t < tmin ? t : tmin;
       tmax = t > tmax ? t : tmax;
+      unmono |= tprev > t;
     }
     if (a.partitioned) {
       if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
@@ -242,17 +248,21 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   for (int o = 32; o > 0; o >>= 1) {
     created += __shfl_xor(created, o, 64);
     ovf |= __shfl_xor(ovf, o, 64);
+    unmono |= __shfl_xor(unmono, o, 64);
   }
   kmax = wave_max(kmax);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
+  ctmax = wave_max(ctmax);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf, unmono, ctmax};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
     for (int w = 1; w < kBlock / 64; w++) {
       r.ovf |= wpart[w].ovf;
+      r.unmono |= wpart[w].unmono;
+      r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -263,11 +273,13 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
 }
 
 __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
-  unsigned long long c = 0, km = 0, ov = 0;
-  long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+  unsigned long long c = 0, km = 0, ov = 0, um = 0;
+  long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctm = LLONG_MIN;
 #pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
     ov |= blk[b].ovf;
+    um |= blk[b].unmono;
+    ctm = blk[b].carry_tmax > ctm ? blk[b].carry_tmax : ctm;
     c += blk[b].n_cand;
     km = blk[b].kmax > km ? blk[b].kmax : km;
     tmin = blk[b].ts_min < tmin ? blk[b].ts_min : tmin;
@@ -276,17 +288,21 @@ __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int 
   for (int o = 32; o > 0; o >>= 1) {
     c += __shfl_xor(c, o, 64);
     ov |= __shfl_xor(ov, o, 64);
+    um |= __shfl_xor(um, o, 64);
   }
   km = wave_max(km);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
+  ctm = wave_max(ctm);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax, ov};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax, ov, um, ctm};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
     for (int w = 1; w < kBlock / 64; w++) {
       r.ovf |= wpart[w].ovf;
+      r.unmono |= wpart[w].unmono;
+      r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -318,6 +334,11 @@ struct ScanArgs {
   int partitioned;
   int prune;            // drop partials that can no longer match (horizon guard on later pushes)
   int64_t t_end;        // latest event time of this push
+  // hashed buckets (0: positions are sorted by the full key): positions are
+  // grouped by the low bits of key_bucket_mix(key), keys of one bucket
+  // interleaved in input order.  Only set when the batch rows are globally
+  // time-ordered, carried partials precede them in time, and prune is on.
+  uint32_t hash_mask;
 };
 
 struct ScanOut {
@@ -339,58 +360,109 @@ static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
 //          step is already counted).  Keeps the hot kernel free of the f2
 //          code (its registers and instruction footprint).
 //   f2_first: resume at a deferred event: evaluate f2 at q first.
-template <bool K64, bool TS64, bool DEFER, bool FAST>
-__device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext,
-                                                const uint32_t* __restrict__ skey32,
-                                                const uint64_t* __restrict__ skey64,
-                                                const uint32_t* __restrict__ spv, const int32_t* __restrict__ sts32,
-                                                const int64_t* __restrict__ sts64, int64_t tbase, int64_t r,
-                                                uint64_t k, int64_t tsi, int64_t& q, uint32_t pq, int64_t tq,
-                                                uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
+// Position loads (flags/row, timestamp, key at sorted position q) from global memory.
+template <bool K64, bool TS64>
+struct GlobalPos {
+  const uint32_t* __restrict__ skey32;
+  const uint64_t* __restrict__ skey64;
+  const uint32_t* __restrict__ spv;
+  const int32_t* __restrict__ sts32;
+  const int64_t* __restrict__ sts64;
+  int64_t tbase;
+  int partitioned;
+  __device__ __forceinline__ void operator()(int64_t q, uint32_t& pq, int64_t& tq, uint64_t& kq) const {
+    pq = spv[q];
+    tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
+    if (partitioned) kq = K64 ? skey64[q] : skey32[q];
+  }
+};
+
+// WIN: positions are loaded WIN at a time (one round trip for WIN steps);
+// walks over hashed buckets step over a few other keys, and a wave waits for
+// its longest walk, so they fetch ahead.
+template <bool DEFER, bool FAST, int WIN, class Ld>
+__device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
+                                                int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
+                                                int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
                                                 uint64_t& steps, uint32_t& viol) {
   uint8_t st = ST_OPEN;
-  while (q < n_ext) {
-    if (!f2_now) {
-      if (a.partitioned && kq != k) break;
-      const uint32_t fq = pv_flags(pq);
-      if ((fq & F_NEW) && !(fq & F_SKIP)) {
-        if (tq < prev) {
-          viol = 1;
-          break;
-        }
-        prev = tq;
-        steps++;
-        // stabilizeStates -> expireEvents: |ts_i - t| > within
-        if (tq - tsi > a.within) {
-          st = ST_DEAD;
-          break;
-        }
-        if (fq & F_B) {
-          if (DEFER) {
-            st = ST_DEFER;
+  bool stop = false, first = true;
+  while (!stop && q < n_ext) {
+    uint32_t wp[WIN];
+    int64_t wt[WIN];
+    uint64_t wk[WIN];
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+      wk[i] = 0;
+      if (i == 0 && first) {
+        wp[0] = pq;
+        wt[0] = tq;
+        wk[0] = kq;
+      } else {
+        const int64_t qi = q + i < n_ext ? q + i : n_ext - 1;
+        ld(qi, wp[i], wt[i], wk[i]);
+      }
+    }
+    first = false;
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+      if (q >= n_ext) {
+        stop = true;
+        break;
+      }
+      pq = wp[i];
+      tq = wt[i];
+      kq = wk[i];
+      if (!f2_now && a.partitioned && kq != k) {
+        stop = true;
+        if (!a.hash_mask) break;   // end of the key's run
+        if ((key_bucket_mix((uint32_t)kq) ^ key_bucket_mix((uint32_t)k)) & a.hash_mask) break;   // end of the bucket
+        // another key of the bucket: pushed rows are time-ordered, so once one is
+        // beyond `within` every later event of this key is too -- the partial
+        // can no longer match (OPEN here; the horizon rule below retires it,
+        // t_end >= tq > tsi + within)
+        if (pv_row(pq) >= (uint32_t)a.x.C && tq - tsi > a.within) break;
+        stop = false;
+      } else if (!f2_now) {
+        const uint32_t fq = pv_flags(pq);
+        if ((fq & F_NEW) && !(fq & F_SKIP)) {
+          if (tq < prev) {
+            viol = 1;
+            stop = true;
             break;
           }
-          f2_now = true;
+          prev = tq;
+          steps++;
+          // stabilizeStates -> expireEvents: |ts_i - t| > within
+          if (tq - tsi > a.within) {
+            st = ST_DEAD;
+            stop = true;
+            break;
+          }
+          if (fq & F_B) {
+            if (DEFER) {
+              st = ST_DEFER;
+              stop = true;
+              break;
+            }
+            f2_now = true;
+          }
         }
       }
-    }
-    if constexpr (!DEFER) {
-      if (f2_now) {
-        f2_now = false;
-        const int64_t r2 = pv_row(pq);
-        PairCtx cx{&a.x, r, r2};
-        if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
-          st = ST_MATCH;
-          j = (int32_t)r2;
-          break;
+      if constexpr (!DEFER) {
+        if (f2_now) {
+          f2_now = false;
+          const int64_t r2 = pv_row(pq);
+          PairCtx cx{&a.x, r, r2};
+          if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+            st = ST_MATCH;
+            j = (int32_t)r2;
+            stop = true;
+            break;
+          }
         }
       }
-    }
-    q++;
-    if (q < n_ext) {
-      pq = spv[q];
-      tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
-      if (a.partitioned) kq = K64 ? skey64[q] : skey32[q];
+      q++;
     }
   }
   if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
@@ -445,7 +517,8 @@ __device__ __forceinline__ void scan_block_reduce(uint64_t steps, uint64_t prune
 // inside `within` is deferred to k_forward_resume (pst = PS_DEFER, resume
 // position in match_row).  Writes a 1-byte outcome per position and the
 // per-tile match / open counts.
-template <bool K64, bool TS64>
+// HASH: hashed-bucket positions (walks fetch 4 positions per round trip).
+template <bool K64, bool TS64, bool HASH>
 __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                          int64_t tile, const uint32_t* __restrict__ skey32,
                                                          const uint64_t* __restrict__ skey64,
@@ -465,23 +538,20 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   // 64-bit values when some offset overflowed (separate instantiation: a
   // run-time choice merges the two loads and serialises every load after it)
   const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
-  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
-    // the position and its first successor are loaded together (sequential,
-    // shared cache lines) before any of them is used
+  auto visit = [&](int64_t p, const auto& ld) {
+    uint32_t pvp, pq;
+    int64_t tsi, tq;
+    uint64_t k = 0, kq = 0;
+    // the position and its first successor are loaded together before use
     const int64_t q0 = p + 1 < n_ext ? p + 1 : n_ext - 1;
-    const uint32_t pvp = spv[p];
-    const int64_t tsi = TS64 ? sts64[p] : tbase + (int64_t)sts32[p];
-    const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
-    const uint32_t pq = spv[q0];
-    const int64_t tq = TS64 ? sts64[q0] : tbase + (int64_t)sts32[q0];
-    const uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q0] : skey32[q0]);
+    ld(p, pvp, tsi, k);
+    ld(q0, pq, tq, kq);
     uint8_t out = PS_NONE;
     if (pv_flags(pvp) & F_CAND) {
       int64_t q = p + 1;
       int32_t j = -1;
-      const uint8_t st = walk_partial<K64, TS64, true, false>(a, es, n_ext, skey32, skey64, spv, sts32, sts64, tbase,
-                                                              pv_row(pvp), k, tsi, q, pq, tq, kq, tsi, false, j,
-                                                              steps, viol);
+      const uint8_t st = walk_partial<true, false, HASH ? 4 : 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq,
+                                                                 kq, tsi, false, j, steps, viol);
       if (st == ST_DEFER) {
         out = PS_DEFER;
         match_row[p] = (int32_t)q;   // resume position (< 2^28)
@@ -493,7 +563,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
       }
     }
     pst[p] = out;
-  }
+  };
+  const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
+  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) visit(p, ld);
   scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
 }
 
@@ -518,6 +590,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
   const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
+  const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
   for (int64_t c0 = t0; c0 < t1; c0 += kBlock * 16) {
     const int64_t pb = c0 + (int64_t)threadIdx.x * 16;
     if (pb >= t1) continue;
@@ -531,16 +604,14 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       const int64_t p = pb + __ffs(hit) - 1;
       hit &= hit - 1;
       int64_t q = match_row[p];
-      const uint32_t pvp = spv[p];
-      const int64_t tsi = TS64 ? sts64[p] : tbase + (int64_t)sts32[p];
-      const uint64_t k = !a.partitioned ? 0 : (K64 ? skey64[p] : skey32[p]);
-      const uint32_t pq = spv[q];
-      const int64_t tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
-      const uint64_t kq = !a.partitioned ? 0 : (K64 ? skey64[q] : skey32[q]);
+      uint32_t pvp, pq;
+      int64_t tsi, tq;
+      uint64_t k = 0, kq = 0;
+      ld(p, pvp, tsi, k);
+      ld(q, pq, tq, kq);
       int32_t j = -1;
-      const uint8_t st = walk_partial<K64, TS64, false, FAST>(a, es, n_ext, skey32, skey64, spv, sts32, sts64, tbase,
-                                                              pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j,
-                                                              steps, viol);
+      const uint8_t st = walk_partial<false, FAST, 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true,
+                                                      j, steps, viol);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
         out = PS_MATCH;
@@ -804,6 +875,40 @@ struct PatternEngine : Engine {
 
   static bool type_key64(int t) { return t == SHD_T_LONG || t == SHD_T_DOUBLE || t == SHD_T_FLOAT; }
 
+  // Key grouping by hashed buckets instead of the full key: the sort then
+  // needs ceil(b/8) passes instead of ceil(key_bits/8), and a walk steps over
+  // the other keys of its bucket until one is beyond `within` (valid only
+  // when the pushed rows are time-ordered, every carried partial precedes
+  // them, and the horizon rule is on -- see walk_partial).  b is chosen from
+  // the expected number of other-key events of a bucket inside one `within`
+  // span, E = n * (W+1) / (T+1) / 2^b, against the passes saved.
+  // SHD_HASH_BITS=b forces b (tests), SHD_NO_HASH disables.
+  int hashed_bucket_bits(const PrepAgg& pg, int64_t n_ext, int key_bits, bool prune) const {
+    if (getenv("SHD_NO_HASH")) return 0;
+    if (!prune || pg.unmono || (C > 0 && pg.carry_tmax > pg.ts_min) || pg.ts_max < pg.ts_min) return 0;
+    if (const char* f = getenv("SHD_HASH_BITS")) {
+      const int b = atoi(f);
+      return b > 0 && b <= 32 ? b : 0;
+    }
+    const int exact_passes = (key_bits + 7) / 8;
+    const double span = (double)(pg.ts_max - pg.ts_min) + 1.0;
+    const double per_w = std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span);
+    double best = exact_passes;
+    int best_b = 0;
+    for (int p = 1; p < exact_passes; p++) {
+      const double e = per_w / std::ldexp(1.0, 8 * p);
+      // calibrated on MI355X (P3, 50M-event pushes): a sort pass ~0.29 ms, the
+      // walks over E = 1.5 other keys per bucket ~ +0.32 ms of scan time, i.e.
+      // one other-key step per walk ~ 0.7 of a pass
+      const double cost = p + 0.7 * e;
+      if (cost < best) {
+        best = cost;
+        best_b = 8 * p;
+      }
+    }
+    return best_b;
+  }
+
   void push(const Staged& b) override {
     const int64_t n = b.n;
     if (n <= 0) return;
@@ -849,13 +954,16 @@ struct PatternEngine : Engine {
       pa.key_col = -1;
     }
     pa.carry_key = carry[cur].key.as<uint64_t>();
-    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0};
+    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN};
     PrepAgg* d_pa = d_agg.as<PrepAgg>();
     ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
     std::memcpy(h_agg.p, &init, sizeof(init));
     std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
     SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
-    const int nblk = grid_for(n_ext);
+    // 4096 workgroups (16 waves per SIMD at full occupancy): enough to stream
+    // at full bandwidth, and the one-block folds of the per-block partials
+    // (k_finish_prep / k_finish_scan) stay short
+    const int nblk = grid_for(n_ext, 1, 4096);
     d_blk.reserve((size_t)2 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!partitioned || pa.key_col >= 0);
@@ -889,10 +997,19 @@ struct PatternEngine : Engine {
     const int32_t* sts32 = d_ts.as<int32_t>();
     const int64_t* sts64 = nullptr;
     bool sorted64 = false;
+    const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX;
+    uint32_t hash_mask = 0;
     if (partitioned) {
       uint64_t kmax = pg.kmax;
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
+      if (bits <= 32) {
+        const int hb = hashed_bucket_bits(pg, n_ext, bits, prune);
+        if (hb > 0) {
+          bits = hb;
+          hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
+        }
+      }
       d_pv_alt.reserve(n_ext * 4);
       d_ts_alt.reserve(n_ext * 4);
       bool in_alt = false;
@@ -905,7 +1022,7 @@ struct PatternEngine : Engine {
         d_k32_alt.reserve(n_ext * 4);
         radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
                                d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
-                               bits, d_sort, s, in_alt);
+                               bits, d_sort, s, in_alt, hash_mask != 0);
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);
@@ -918,6 +1035,7 @@ struct PatternEngine : Engine {
       spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
       sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
       mark("key_sort");
+      counters.group_bits = bits;
     }
     if (pg.ovf || getenv("SHD_TS64")) {   // SHD_TS64: force the 64-bit path (tests)
       // some timestamp is more than 2^31 ms away from the batch's first event
@@ -935,7 +1053,8 @@ struct PatternEngine : Engine {
     sa.f2 = dfilters(f2);
     sa.within = W;
     sa.partitioned = partitioned;
-    sa.prune = n_ext >= kPruneMinRows && W != INT64_MAX;
+    sa.prune = prune;
+    sa.hash_mask = hash_mask;
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     const ScanArgs* d_sa = dev_args(sa);
@@ -947,8 +1066,8 @@ struct PatternEngine : Engine {
     d_boff.reserve((size_t)2 * ntile * 4);
     const bool ts64 = sts64 != nullptr;
     // hot walk without f2 (deferrals), then the deferred walks with f2
-#define SHD_LAUNCH_SCAN(K64, TS64)                                                                              \
-  hipLaunchKernelGGL((k_forward_scan<K64, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
+#define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
+  hipLaunchKernelGGL((k_forward_scan<K64, TS64, H>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
                      skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), \
                      d_blk.as<ScanOut>())
 #define SHD_LAUNCH_RESUME(K64, FAST, TS64)                                                                      \
@@ -958,12 +1077,16 @@ struct PatternEngine : Engine {
 #define SHD_LAUNCH_RESUME2(K64, FAST) \
   if (ts64) SHD_LAUNCH_RESUME(K64, FAST, true); else SHD_LAUNCH_RESUME(K64, FAST, false)
     if (sorted64) {
-      if (ts64) SHD_LAUNCH_SCAN(true, true); else SHD_LAUNCH_SCAN(true, false);
+      if (ts64) SHD_LAUNCH_SCAN(true, true, false); else SHD_LAUNCH_SCAN(true, false, false);
       SHD_CHECK_LAUNCH();
       if (fast2) { SHD_LAUNCH_RESUME2(true, true); }
       else { SHD_LAUNCH_RESUME2(true, false); }
     } else {
-      if (ts64) SHD_LAUNCH_SCAN(false, true); else SHD_LAUNCH_SCAN(false, false);
+      if (hash_mask) {
+        if (ts64) SHD_LAUNCH_SCAN(false, true, true); else SHD_LAUNCH_SCAN(false, false, true);
+      } else {
+        if (ts64) SHD_LAUNCH_SCAN(false, true, false); else SHD_LAUNCH_SCAN(false, false, false);
+      }
       SHD_CHECK_LAUNCH();
       if (fast2) { SHD_LAUNCH_RESUME2(false, true); }
       else { SHD_LAUNCH_RESUME2(false, false); }

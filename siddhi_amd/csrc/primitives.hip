@@ -154,8 +154,14 @@ __device__ __forceinline__ int rs_tile_of(int b, int nb) {
 
 template <class K>
 __device__ __forceinline__ uint32_t rs_digit(K k, int shift) { return (uint32_t)((k >> shift) & 255u); }
+// H: digits of key_bucket_mix(key) (hashed bucket sort; 32-bit keys only)
+template <bool H, class K>
+__device__ __forceinline__ uint32_t rs_hdigit(K k, int shift) {
+  if constexpr (H) return (key_bucket_mix((uint32_t)k) >> shift) & 255u;
+  else return rs_digit(k, shift);
+}
 
-template <class K, int R>
+template <class K, int R, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys, int64_t n, int shift,
                                                       uint32_t* __restrict__ hist, int nb, int xcd) {
   __shared__ uint32_t h[kRsWaves][256];
@@ -174,10 +180,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < R / 4; i++) {
-        atomicAdd(&h[w][(q[i].x >> shift) & 255u], 1u);
-        atomicAdd(&h[w][(q[i].y >> shift) & 255u], 1u);
-        atomicAdd(&h[w][(q[i].z >> shift) & 255u], 1u);
-        atomicAdd(&h[w][(q[i].w >> shift) & 255u], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>(q[i].x, shift)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>(q[i].y, shift)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>(q[i].z, shift)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>(q[i].w, shift)], 1u);
       }
       done = true;
     }
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r++)
-      if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_digit(k[r], shift)], 1u);
+      if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_hdigit<H>(k[r], shift)], 1u);
   }
   __syncthreads();
   if (tid < 256) {
@@ -203,7 +209,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
   }
 }
 
-template <class K, int R, bool P2>
+template <class K, int R, bool P2, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                          const uint32_t* __restrict__ win, K* __restrict__ kout,
                                                          uint32_t* __restrict__ vout, uint32_t* __restrict__ wout,
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool ok = wb + r * 64 + lane < n;
-    const uint32_t d = rs_digit(k[r], shift);
+    const uint32_t d = rs_hdigit<H>(k[r], shift);
     uint64_t peers = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (wb + r * 64 + lane < n) {
-      const uint32_t pos = wcnt[w][rs_digit(k[r], shift)] + lr[r];
+      const uint32_t pos = wcnt[w][rs_hdigit<H>(k[r], shift)] + lr[r];
       sk[pos] = k[r];
       sv[pos] = v[r];
       if (P2) sw[pos] = x[r];
@@ -300,7 +306,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll 4
   for (int i = tid; i < tile_n; i += kRsBlock) {
     const K kk = sk[i];
-    const uint32_t d = rs_digit(kk, shift);
+    const uint32_t d = rs_hdigit<H>(kk, shift);
 #if defined(SHD_RS_EXP) && SHD_RS_EXP == 1   // timing experiment: coalesced identity write-out
     const uint32_t o = (uint32_t)(t0 + i) + 0 * (gbase[d] - lpre[d]);
 #elif defined(SHD_RS_EXP) && SHD_RS_EXP == 2   // timing experiment: no write-out
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   }
 }
 
-template <class K, int R, bool P2>
+template <class K, int R, bool P2, bool H = false>
 static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, uint32_t* vals_alt, uint32_t* w_alt,
                            int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
   in_alt = false;
@@ -335,10 +341,10 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
   K* ki = keys; uint32_t* vi = vals; uint32_t* wi = w;
   K* ko = keys_alt; uint32_t* vo = vals_alt; uint32_t* wo = w_alt;
   for (int shift = 0; shift < bits; shift += 8) {
-    hipLaunchKernelGGL((k_rs_hist<K, R>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd);
+    hipLaunchKernelGGL((k_rs_hist<K, R, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd);
     SHD_CHECK_LAUNCH();
     scan_raw(hist, offs, nh, nullptr, sscr, s);
-    hipLaunchKernelGGL((k_rs_scatter<K, R, P2>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, (const uint32_t*)vi,
+    hipLaunchKernelGGL((k_rs_scatter<K, R, P2, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, (const uint32_t*)vi,
                        (const uint32_t*)wi, ko, vo, wo, n, shift, (const uint32_t*)hist, (const uint32_t*)offs, nb, xcd);
     SHD_CHECK_LAUNCH();
     std::swap(ki, ko);
@@ -361,8 +367,13 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
 }
 
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
-                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
-  radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt);
+                            uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
+                            bool hashed) {
+  if (hashed)
+    radix_sort_run<uint32_t, kRsRounds, true, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s,
+                                                    in_alt);
+  else
+    radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt);
 }
 
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,

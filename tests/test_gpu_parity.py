@@ -129,3 +129,46 @@ def test_timestamps_beyond_32bit_offsets(hip_available, within):
     dev, _, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
+
+
+@pytest.mark.parametrize("bits", ["auto", "2", "8", "12"])
+@pytest.mark.parametrize("parts", [1, 3])
+def test_hashed_bucket_grouping(hip_available, monkeypatch, bits, parts):
+    """Partitioned pattern with the key sort replaced by a sort on the low bits
+    of a key hash (several keys per bucket, walks step over the other keys of
+    their bucket).  bits=2 puts ~1/4 of all keys in one bucket: results must
+    still equal the oracle's row for row.  'auto' on 2^20 keys must choose it."""
+    if bits != "auto":
+        monkeypatch.setenv("SHD_HASH_BITS", bits)
+    qp, _ = compile_single_query(wl.P3_APP)
+    n, keys = 300_000, (1 << 20) if bits == "auto" else 20_000
+    # auto: 2^20 keys (3 exact passes), ~10k events per `within` span -> 16-bit buckets
+    sym, price, vol, ts = wl.stock_stream(n, keys, 0.1 if bits == "auto" else 0.01, seed_offset=77)
+    batches = split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    dev, counters, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+    assert counters["group_bits"] == (16 if bits == "auto" else int(bits))
+
+
+def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
+    """Pushed rows that are not globally time-ordered (per-key order intact)
+    keep the exact key sort even when hashed buckets are requested."""
+    monkeypatch.setenv("SHD_HASH_BITS", "8")
+    app = ("define stream S (k int, p double); partition with (k of S) begin "
+           "@info(name='q') from every e1=S[p>50] -> e2=S[p>e1.p] within 30 milliseconds "
+           "select e1.k as k, e1.p as p1, e2.p as p2 insert into O; end;")
+    qp, _ = compile_single_query(app)
+    rng = np.random.default_rng(23)
+    n = 100_000
+    k = rng.integers(0, 3000, n).astype(np.int32)
+    p = rng.uniform(0, 100, n)
+    # per key non-decreasing, globally not: key-dependent clock offsets
+    ts = 1_000_000 + np.arange(n, dtype=np.int64) // 4 + (k.astype(np.int64) % 7) * 50
+    batches = [(0, ColumnBatch(ts, [k, p], [None, None], np.arange(0, n + 1, 1000)))]
+    ora = run_oracle(qp, batches)
+    dev, counters, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+    assert counters["group_bits"] == 12   # exact: bit length of the largest key
