@@ -99,6 +99,22 @@ def alg_bytes_window(c, n, n_out):
     return (20 + 12 + 36 * o) * n, dict(o=o)
 
 
+def pmc_traffic(cfg_name, stage, events_per_launch):
+    """HBM bytes per launch of `stage` from the newest committed rocprofv3 PMC
+    summary (profiles/rNN_pmc_<config>.json, written by scripts/pmc_summary.py
+    from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections),
+    scaled from its bytes per event to this run's events per launch."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % cfg_name)))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    st = d.get("stages", {}).get(stage)
+    if not st:
+        return None, None
+    return round(st["hbm_bytes_per_event"] * events_per_launch), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg_name, app, keys, delta, sample):
     """CPU oracle (C++ restatement, 1 core) on the first `sample` events of the same stream."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -267,8 +283,10 @@ def main():
         per_launch_bytes = bytes_step / launches
         per_launch_s = stages[dominant] / launches * 1e-9
         ach = per_launch_bytes / per_launch_s / 1e9
+        traffic, tsrc = pmc_traffic(args.config, dominant, counters["events"] / launches)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_stage": dominant,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "kernel_stage": dominant,
                 "path_achieved": round(bytes_step / (step_dev_ns * 1e-9) / 1e9, 1),
                 "path_frac": round(bytes_step / (step_dev_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
     matches_per_s = counters["matches"] * world * args.steps / elapsed

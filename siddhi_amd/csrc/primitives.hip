@@ -209,12 +209,56 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
   }
 }
 
+// Exclusive scan of one digit's row of per-tile counts (one workgroup per
+// digit): offs[d*nb + t] = digit d's count in tiles before t, total[d] = its
+// count in the whole array.  The scatter adds the exclusive prefix of the 256
+// digit totals itself, so a pass is three launches (hist, row scan, scatter).
+__global__ __launch_bounds__(kRsBlock) void k_rs_digit_scan(const uint32_t* __restrict__ hist, int nb,
+                                                            uint32_t* __restrict__ offs, uint32_t* __restrict__ total) {
+  constexpr int kRowLds = 16384;   // rows up to 16k tiles (~100M keys) are staged in LDS
+  __shared__ uint32_t wsum[kRsWaves];
+  __shared__ uint32_t lrow[kRowLds];
+  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t* grow = hist + (int64_t)d * nb;
+  uint32_t* orow = offs + (int64_t)d * nb;
+  // coalesced copy of the row into LDS; each thread then walks a contiguous run
+  const bool staged = nb <= kRowLds;
+  if (staged)
+    for (int t = tid; t < nb; t += kRsBlock) lrow[t] = grow[t];
+  __syncthreads();
+  const uint32_t* row = staged ? lrow : grow;
+  const int per = (nb + kRsBlock - 1) / kRsBlock;   // contiguous run of tiles per thread
+  const int a = tid * per, b = a + per < nb ? a + per : nb;
+  uint32_t s = 0;
+  for (int t = a; t < b; t++) s += row[t];
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = inc - s, tot = 0;
+  for (int i = 0; i < kRsWaves; i++) {
+    if (i < w) pre += wsum[i];
+    tot += wsum[i];
+  }
+  for (int t = a; t < b; t++) {
+    const uint32_t c = row[t];
+    orow[t] = pre;
+    pre += c;
+  }
+  if (tid == 0) total[d] = tot;
+}
+
 template <class K, int R, bool P2, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                          const uint32_t* __restrict__ win, K* __restrict__ kout,
                                                          uint32_t* __restrict__ vout, uint32_t* __restrict__ wout,
                                                          int64_t n, int shift, const uint32_t* __restrict__ hist,
-                                                         const uint32_t* __restrict__ offs, int nb, int xcd) {
+                                                         const uint32_t* __restrict__ offs,
+                                                         const uint32_t* __restrict__ dtotal, int nb, int xcd) {
   constexpr int T = rs_tile(R);
   __shared__ K sk[T];
   __shared__ uint32_t sv[T];
@@ -222,7 +266,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   __shared__ uint32_t lpre[256];             // tile-local first position of each digit
   __shared__ uint32_t gbase[256];            // global first position of this tile's digit run
   __shared__ uint32_t wcnt[kRsWaves][256];   // per-wave running digit counts, then per-wave digit bases
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wsum[4], dsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
   const int64_t t0 = (int64_t)tile * T;
@@ -231,7 +275,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   // the digit prefix below then waits only for them, while the key loads
   // issued after them are still in flight (in-order vmcnt)
   const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
-  const uint32_t gb = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
   K k[R];
   uint32_t v[R];
   uint32_t x[P2 ? R : 1];
@@ -245,20 +290,31 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
   }
   for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&wcnt[0][0])[i] = 0;
   {
-    // tile-local exclusive prefix over digits (threads 0..255, one digit each)
-    uint32_t inc = c;
+    // tile-local exclusive prefix over digits (threads 0..255, one digit
+    // each), and the global base of each digit (prefix of the digit totals)
+    uint32_t inc = c, dinc = dt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
+      const uint32_t u = __shfl_up(dinc, o, 64);
+      if (lane >= o) {
+        inc += t;
+        dinc += u;
+      }
     }
-    if (lane == 63 && w < 4) wsum[w] = inc;
-    if (tid < 256) gbase[tid] = gb;
+    if (lane == 63 && w < 4) {
+      wsum[w] = inc;
+      dsum[w] = dinc;
+    }
     __syncthreads();
     if (tid < 256) {
-      uint32_t pre = 0;
-      for (int i = 0; i < w; i++) pre += wsum[i];
+      uint32_t pre = 0, dpre = 0;
+      for (int i = 0; i < w; i++) {
+        pre += wsum[i];
+        dpre += dsum[i];
+      }
       lpre[tid] = pre + inc - c;
+      gbase[tid] = dpre + dinc - dt + gr;
     }
   }
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -331,21 +387,23 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
     throw Error(SHD_E_ARG, "radix sort: key arrays must be 16-byte aligned");
   const int nb = (int)ceil_div(n, rs_tile(R));
   const int64_t nh = (int64_t)nb * 256;
-  // scratch layout: hist[nh] | offs[nh] | scan scratch
-  const size_t need = (size_t)(2 * nh + scan_need(nh)) * sizeof(uint32_t);
+  // scratch layout: hist[nh] | offs[nh] | digit totals[256]
+  const size_t need = (size_t)(2 * nh + 256) * sizeof(uint32_t);
   scratch.reserve(need);
   uint32_t* hist = scratch.as<uint32_t>();
   uint32_t* offs = hist + nh;
-  uint32_t* sscr = offs + nh;
+  uint32_t* dtot = offs + nh;
   const int xcd = getenv("SHD_RS_NOXCD") ? 0 : 1;   // A/B switch for the tile order
   K* ki = keys; uint32_t* vi = vals; uint32_t* wi = w;
   K* ko = keys_alt; uint32_t* vo = vals_alt; uint32_t* wo = w_alt;
   for (int shift = 0; shift < bits; shift += 8) {
     hipLaunchKernelGGL((k_rs_hist<K, R, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd);
     SHD_CHECK_LAUNCH();
-    scan_raw(hist, offs, nh, nullptr, sscr, s);
+    hipLaunchKernelGGL(k_rs_digit_scan, dim3(256), dim3(kRsBlock), 0, s, (const uint32_t*)hist, nb, offs, dtot);
+    SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_rs_scatter<K, R, P2, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, (const uint32_t*)vi,
-                       (const uint32_t*)wi, ko, vo, wo, n, shift, (const uint32_t*)hist, (const uint32_t*)offs, nb, xcd);
+                       (const uint32_t*)wi, ko, vo, wo, n, shift, (const uint32_t*)hist, (const uint32_t*)offs,
+                       (const uint32_t*)dtot, nb, xcd);
     SHD_CHECK_LAUNCH();
     std::swap(ki, ko);
     std::swap(vi, vo);
