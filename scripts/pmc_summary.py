@@ -68,7 +68,7 @@ def main():
     t_stage, t_push = per_stage(tnames, tdur, 1.0)
     kern = defaultdict(lambda: [0, 0.0])
     for nm, d in zip(tnames, tdur):
-        short = nm.split("(")[0].replace("void ", "").replace("shd::(anonymous namespace)::", "").replace("shd::", "")
+        short = nm.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("shd::", "")
         kern[short][0] += 1
         kern[short][1] += d
 
