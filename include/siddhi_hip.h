@@ -22,6 +22,10 @@
  *                      InsertIntoStreamCallback.send
  *                      (C/query/output/ratelimit/OutputRateLimiter.java:64-107).
  *   shd_plan_free   <- QueryRuntime stop / SiddhiAppRuntime.shutdown.
+ *   shd_snapshot /  <- SiddhiAppRuntime.snapshot()/restore(byte[]) -> SnapshotService.fullSnapshot/restore
+ *   shd_restore        (C/SiddhiAppRuntimeImpl.java:695-717, C/util/snapshot/SnapshotService.java:90,333)
+ *                      for this query's element states (State.snapshot/restore, e.g.
+ *                       ST/StreamPreStateProcessor.java:450-469, LengthWindowProcessor.java:171-196).
  *
  * Conventions: every function returns an int status (0 = OK, < 0 = shd_status);
  * no exception crosses the ABI; shd_last_error() returns a thread-local message.
@@ -112,6 +116,14 @@ int shd_poll(shd_query* q, shd_out* out);      /* buffers valid until next call 
 int shd_discard_output(shd_query* q);          /* drop pending rows (benchmarks)   */
 int shd_reset(shd_query* q);                   /* back to freshly-started state   */
 int shd_get_counters(shd_query* q, shd_counters* c);
+/* Opaque image of the query's device state (open partial matches, NFA key
+ * blocks, window contents, aggregates) plus its arrival / time / chunk
+ * counters.  The image is library-owned and valid until the next
+ * shd_snapshot on q; pending output must have been polled.  shd_restore
+ * replaces the query's state with an image taken from a query loaded with
+ * the same plan IR (SHD_E_ARG otherwise). */
+int shd_snapshot(shd_query* q, const void** data, size_t* len);
+int shd_restore(shd_query* q, const void* data, size_t len);
 /* Optional: the HIP stream (hipStream_t) a query launches on, for event timing. */
 int shd_query_stream(shd_query* q, void** stream);
 /* Profiling hook: per-stage device time of the last push, measured with HIP

@@ -1,6 +1,9 @@
 // engine.h -- query engines behind the C-ABI (one per loaded plan).
 #pragma once
+#include <algorithm>
+#include <cstring>
 #include <memory>
+#include <vector>
 
 #include "common.h"
 #include "dev_expr.h"
@@ -34,6 +37,73 @@ struct Staged {
   bool advance_time = false;
 };
 
+// Snapshot streams (shd_snapshot / shd_restore): a flat little-endian byte
+// image of an engine's cross-push state.  Device buffers are copied with
+// synchronous hipMemcpy on the query's stream after it drained.
+struct SnapW {
+  std::vector<uint8_t> b;
+  hipStream_t s = nullptr;
+  template <class T> void put(const T& v) {
+    const size_t o = b.size();
+    b.resize(o + sizeof(T));
+    std::memcpy(b.data() + o, &v, sizeof(T));
+  }
+  void bytes(const void* src, size_t n) {
+    const size_t o = b.size();
+    b.resize(o + n);
+    if (n) std::memcpy(b.data() + o, src, n);
+  }
+  // n bytes of device memory at p
+  void dev(const void* p, size_t n) {
+    put<uint64_t>(n);
+    const size_t o = b.size();
+    b.resize(o + n);
+    if (n) {
+      SHD_HIP(hipMemcpyAsync(b.data() + o, p, n, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipStreamSynchronize(s));
+    }
+  }
+};
+
+struct SnapR {
+  const uint8_t* p = nullptr;
+  size_t n = 0, at = 0;
+  hipStream_t s = nullptr;
+  void need(size_t k) const {
+    if (at + k > n) throw Error(SHD_E_ARG, "snapshot truncated or from a different plan");
+  }
+  template <class T> T get() {
+    need(sizeof(T));
+    T v;
+    std::memcpy(&v, p + at, sizeof(T));
+    at += sizeof(T);
+    return v;
+  }
+  // device section into buf (reserved to at least its size); returns its size
+  size_t dev(DevBuf& buf, size_t extra_cap = 0) {
+    const size_t k = (size_t)get<uint64_t>();
+    need(k);
+    buf.reserve(std::max<size_t>(k, extra_cap));
+    if (k) {
+      SHD_HIP(hipMemcpyAsync(buf.p, p + at, k, hipMemcpyHostToDevice, s));
+      SHD_HIP(hipStreamSynchronize(s));
+    }
+    at += k;
+    return k;
+  }
+  // device section into p (exactly `expect` bytes)
+  void dev_into(void* dst, size_t expect) {
+    const size_t k = (size_t)get<uint64_t>();
+    if (k != expect) throw Error(SHD_E_ARG, "snapshot section size mismatch");
+    need(k);
+    if (k) {
+      SHD_HIP(hipMemcpyAsync(dst, p + at, k, hipMemcpyHostToDevice, s));
+      SHD_HIP(hipStreamSynchronize(s));
+    }
+    at += k;
+  }
+};
+
 struct Engine {
   Plan plan;
   DevExprTable ex;
@@ -63,6 +133,14 @@ struct Engine {
   virtual void reset() = 0;
   // called once the plan's expression table is on the device
   virtual void on_loaded() {}
+  // Cross-push state (partial-match tables, window contents, aggregates) for
+  // SiddhiAppRuntime.snapshot()/restore() (C/SiddhiAppRuntimeImpl.java:695-717,
+  // SnapshotService.fullSnapshot/restore C/util/snapshot/SnapshotService.java:90,333,
+  // the per-processor State.snapshot/restore maps, e.g.
+  // ST/StreamPreStateProcessor.java:450-469).  The common fields (seq, time,
+  // chunk ids, counters) are written by shd_snapshot itself.
+  virtual void save_state(SnapW&) { throw Error(SHD_E_UNSUPPORTED, "engine has no snapshot support"); }
+  virtual void load_state(SnapR&) { throw Error(SHD_E_UNSUPPORTED, "engine has no snapshot support"); }
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column

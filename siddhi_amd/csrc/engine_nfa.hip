@@ -1685,6 +1685,38 @@ struct NfaEngine : Engine {
     SHD_HIP(hipDeviceSynchronize());
   }
 
+  // key blocks (all per-key NFA state) + key directory, byte for byte
+  void save_state(SnapW& w) override {
+    w.put<int64_t>(slot_cap);
+    w.put<int64_t>(nslots);
+    w.put<int64_t>(ht_cap);
+    w.put<uint32_t>(epoch);
+    w.put<int64_t>((int64_t)lay.blk);
+    w.dev(state.p, (size_t)(slot_cap / kLaneBlock) * lay.blk);
+    w.dev(ht_state.p, (size_t)ht_cap * 4);
+    w.dev(ht_key.p, (size_t)ht_cap * 8);
+    w.dev(ht_slot.p, (size_t)ht_cap * 4);
+  }
+  void load_state(SnapR& r) override {
+    const int64_t sc = r.get<int64_t>(), ns = r.get<int64_t>(), hc = r.get<int64_t>();
+    const uint32_t ep = r.get<uint32_t>();
+    if (r.get<int64_t>() != (int64_t)lay.blk || sc < 0 || ns < 0 || ns > sc || hc < 0 || sc % kLaneBlock)
+      throw Error(SHD_E_ARG, "snapshot of a different plan");
+    const size_t sb = (size_t)(sc / kLaneBlock) * lay.blk;
+    state.reserve(std::max<size_t>(sb, 1));
+    r.dev_into(state.p, sb);
+    ht_state.reserve(std::max<int64_t>(hc, 1) * 4);
+    ht_key.reserve(std::max<int64_t>(hc, 1) * 8);
+    ht_slot.reserve(std::max<int64_t>(hc, 1) * 4);
+    r.dev_into(ht_state.p, (size_t)hc * 4);
+    r.dev_into(ht_key.p, (size_t)hc * 8);
+    r.dev_into(ht_slot.p, (size_t)hc * 4);
+    slot_cap = sc;
+    nslots = ns;
+    ht_cap = hc;
+    epoch = ep;
+  }
+
   void set_time(int64_t t) override {
     // shd_set_time: a time change without events (Scheduler TIMERs still fire)
     if (t < now) return;

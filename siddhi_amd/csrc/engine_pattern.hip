@@ -867,6 +867,40 @@ struct PatternEngine : Engine {
     horizon = INT64_MIN;
   }
 
+  // open partials (carry table) + horizon guard
+  void save_state(SnapW& w) override {
+    w.put<int64_t>(C);
+    w.put<int32_t>(have_horizon ? 1 : 0);
+    w.put<int64_t>(horizon);
+    w.put<int32_t>((int32_t)typesA.size());
+    const CarryTable& t = carry[cur];
+    for (size_t c = 0; c < typesA.size(); c++) {
+      w.dev(t.col[c].p, (size_t)C * type_size(typesA[c]));
+      w.dev(t.nul[c].p, (size_t)C);
+    }
+    w.dev(t.ts.p, (size_t)C * 8);
+    w.dev(t.key.p, (size_t)C * 8);
+    w.dev(t.seq.p, (size_t)C * 8);
+  }
+  void load_state(SnapR& r) override {
+    const int64_t c0 = r.get<int64_t>();
+    have_horizon = r.get<int32_t>() != 0;
+    horizon = r.get<int64_t>();
+    if (r.get<int32_t>() != (int32_t)typesA.size() || c0 < 0) throw Error(SHD_E_ARG, "snapshot of a different plan");
+    cur = 0;
+    CarryTable& t = carry[0];
+    t.reserve(c0, typesA);
+    for (size_t c = 0; c < typesA.size(); c++) {
+      r.dev_into(t.col[c].p, (size_t)c0 * type_size(typesA[c]));
+      r.dev_into(t.nul[c].p, (size_t)c0);
+    }
+    r.dev_into(t.ts.p, (size_t)c0 * 8);
+    r.dev_into(t.key.p, (size_t)c0 * 8);
+    r.dev_into(t.seq.p, (size_t)c0 * 8);
+    C = c0;
+    counters.carry = C;
+  }
+
   ColSet carry_cs() const {
     ColSet cs = carry[cur].colset(typesA);
     cs.n = C;

@@ -567,6 +567,58 @@ struct SingleEngine : Engine {
     }
   }
 
+  // window contents (items [0, C) of slot `cur`) + dense per-group aggregates
+  void save_state(SnapW& w) override {
+    w.put<int64_t>(C);
+    w.put<int32_t>(nagg);
+    w.put<int64_t>(g_nkeys);
+    if (C > 0) {
+      w.dev(ikey[cur].p, (size_t)C * 8);
+      w.dev(its[cur].p, (size_t)C * 8);
+      for (int g = 0; g < nagg; g++) {
+        w.dev(iargv[cur].as<uint64_t>() + g * icap[cur], (size_t)C * 8);
+        w.dev(iargn[cur].as<uint8_t>() + g * icap[cur], (size_t)C);
+      }
+    }
+    if (g_nkeys > 0) {
+      const size_t gb = (size_t)std::max(nagg, 1) * g_nkeys * 8;
+      w.dev(g_dsum.p, gb);
+      w.dev(g_lsum.p, gb);
+      w.dev(g_cnt.p, gb);
+    }
+  }
+  void load_state(SnapR& r) override {
+    const int64_t c0 = r.get<int64_t>();
+    if (r.get<int32_t>() != nagg || c0 < 0) throw Error(SHD_E_ARG, "snapshot of a different plan");
+    const int64_t nk = r.get<int64_t>();
+    cur = 0;
+    if (c0 > 0) {
+      ensure_items(0, c0);
+      r.dev_into(ikey[0].p, (size_t)c0 * 8);
+      r.dev_into(its[0].p, (size_t)c0 * 8);
+      for (int g = 0; g < nagg; g++) {
+        r.dev_into(iargv[0].as<uint64_t>() + g * icap[0], (size_t)c0 * 8);
+        r.dev_into(iargn[0].as<uint8_t>() + g * icap[0], (size_t)c0);
+      }
+    }
+    C = c0;
+    if (nk > 0) {
+      const size_t gb = (size_t)std::max(nagg, 1) * nk * 8;
+      g_dsum.reserve(gb);
+      g_lsum.reserve(gb);
+      g_cnt.reserve(gb);
+      r.dev_into(g_dsum.p, gb);
+      r.dev_into(g_lsum.p, gb);
+      r.dev_into(g_cnt.p, gb);
+    } else if (g_nkeys) {
+      SHD_HIP(hipMemsetAsync(g_dsum.p, 0, g_dsum.cap, stream));
+      SHD_HIP(hipMemsetAsync(g_lsum.p, 0, g_lsum.cap, stream));
+      SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
+    }
+    if (nk > 0 || !g_nkeys) g_nkeys = nk;
+    counters.carry = C;
+  }
+
   std::vector<int64_t> h_offs;   // lives until the next push (async H2D source)
   PinnedBuf h_last, h_offs_pin;
 

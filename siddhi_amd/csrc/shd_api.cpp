@@ -445,6 +445,8 @@ struct shd_query {
   std::vector<int32_t> h_type;
   std::vector<uint64_t> h_vals;
   std::vector<uint8_t> h_nulls;
+  uint64_t plan_hash = 0;         // FNV-1a of the plan IR (snapshot compatibility)
+  std::vector<uint8_t> snap;      // last shd_snapshot image (library-owned)
 };
 
 namespace {
@@ -533,6 +535,9 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
     auto* q = new shd_query();
     q->ctx = ctx;
     q->eng = std::move(e);
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < len; i++) h = (h ^ ((const uint8_t*)ir)[i]) * 1099511628211ull;
+    q->plan_hash = h;
     *out = q;
     return SHD_OK;
   });
@@ -708,6 +713,64 @@ int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int*
   }
   *n = k;
   return SHD_OK;
+}
+
+// Snapshot image: magic, version, engine kind, plan hash, the Engine's common
+// fields (arrival seq, playback time, next chunk id, counters), then the
+// engine's own section (Engine::save_state).  Pending output rows must have
+// been polled (the runtime drains after every push).
+static constexpr uint32_t kSnapMagic = 0x53444853u;   // "SHDS"
+static constexpr uint32_t kSnapVersion = 1;
+
+int shd_snapshot(shd_query* q, const void** data, size_t* len) {
+  return guarded([&]() -> int {
+    if (!q || !data || !len) return fail(SHD_E_ARG, "null argument");
+    Engine& e = *q->eng;
+    SHD_HIP(hipStreamSynchronize(e.stream));
+    if (e.out.count > 0) return fail(SHD_E_ARG, "snapshot with unpolled output rows");
+    SnapW w;
+    w.s = e.stream;
+    w.put<uint32_t>(kSnapMagic);
+    w.put<uint32_t>(kSnapVersion);
+    w.put<int32_t>(e.kind());
+    w.put<uint64_t>(q->plan_hash);
+    w.put<int64_t>(e.seq);
+    w.put<int64_t>(e.now);
+    w.put<int64_t>(e.chunk_seq);
+    w.put<shd_counters>(e.counters);
+    e.save_state(w);
+    q->snap.swap(w.b);
+    *data = q->snap.data();
+    *len = q->snap.size();
+    return SHD_OK;
+  });
+}
+
+int shd_restore(shd_query* q, const void* data, size_t len) {
+  return guarded([&]() -> int {
+    if (!q || (!data && len)) return fail(SHD_E_ARG, "null argument");
+    Engine& e = *q->eng;
+    SHD_HIP(hipStreamSynchronize(e.stream));
+    SnapR r;
+    r.p = (const uint8_t*)data;
+    r.n = len;
+    r.s = e.stream;
+    if (r.get<uint32_t>() != kSnapMagic || r.get<uint32_t>() != kSnapVersion)
+      return fail(SHD_E_ARG, "not a libsiddhi_hip snapshot (or another version)");
+    if (r.get<int32_t>() != e.kind() || r.get<uint64_t>() != q->plan_hash)
+      return fail(SHD_E_ARG, "snapshot was taken from a different plan");
+    e.reset();
+    const int64_t seq = r.get<int64_t>(), now = r.get<int64_t>(), chunk = r.get<int64_t>();
+    const shd_counters c = r.get<shd_counters>();
+    e.load_state(r);
+    if (r.at != r.n) return fail(SHD_E_ARG, "trailing bytes in snapshot");
+    e.seq = seq;
+    e.now = now;
+    e.chunk_seq = chunk;
+    e.counters = c;
+    e.out.count = 0;
+    return SHD_OK;
+  });
 }
 
 int shd_get_counters(shd_query* q, shd_counters* c) {

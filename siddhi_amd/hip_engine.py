@@ -26,7 +26,8 @@ ENGINE_NAMES = {1: "pattern-forward-scan", 2: "window-aggregate", 3: "filter-pro
 
 EXPORTED = ["shd_device_count", "shd_ctx_create", "shd_ctx_destroy", "shd_plan_load", "shd_plan_free",
             "shd_plan_engine", "shd_set_time", "shd_push", "shd_flush", "shd_poll", "shd_discard_output",
-            "shd_reset", "shd_get_counters", "shd_query_stream", "shd_stage_times", "shd_last_error"]
+            "shd_reset", "shd_get_counters", "shd_query_stream", "shd_stage_times", "shd_snapshot", "shd_restore",
+            "shd_last_error"]
 
 
 class SiddhiHipError(RuntimeError):
@@ -84,6 +85,8 @@ def load_library(path: str = LIB_PATH):
         lib.shd_query_stream.argtypes = [P, ctypes.POINTER(P)]
         lib.shd_stage_times.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_char_p), I,
                                         ctypes.POINTER(I)]
+        lib.shd_snapshot.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+        lib.shd_restore.argtypes = [P, P, ctypes.c_size_t]
         lib.shd_last_error.restype = ctypes.c_char_p
         for f in EXPORTED:
             if f != "shd_last_error":
@@ -200,6 +203,16 @@ class DeviceQuery:
         _check(self.lib.shd_stage_times(self.q, ns, names, 16, ctypes.byref(n)))
         return {names[i].decode(): ns[i] for i in range(n.value)}
 
+    def snapshot(self) -> bytes:
+        """Device state image (shd_snapshot); pending output must have been polled."""
+        data, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.shd_snapshot(self.q, ctypes.byref(data), ctypes.byref(n)))
+        return ctypes.string_at(data, n.value)
+
+    def restore(self, image: bytes):
+        buf = ctypes.create_string_buffer(image, len(image))
+        _check(self.lib.shd_restore(self.q, buf, len(image)))
+
     def stream_handle(self):
         s = ctypes.c_void_p()
         _check(self.lib.shd_query_stream(self.q, ctypes.byref(s)))
@@ -247,3 +260,9 @@ class HipQueryEngine:
 
     def counters(self):
         return self.dq.counters()
+
+    def snapshot(self) -> bytes:
+        return self.dq.snapshot()
+
+    def restore(self, image: bytes):
+        self.dq.restore(image)

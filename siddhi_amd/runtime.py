@@ -20,6 +20,9 @@ due timers before the events are routed.
 """
 from __future__ import annotations
 
+import hashlib
+import json
+import struct
 import time
 from typing import Callable, Dict, List, Optional
 
@@ -231,6 +234,7 @@ class SiddhiAppRuntime:
         self.stream_callbacks: Dict[str, List[StreamCallback]] = {}
         self.subscribers: Dict[str, List[tuple]] = {}
         self.started = False
+        self.persistence_store = None
         self._last_wall = 0
         extra = {}
         anon = 0
@@ -279,6 +283,71 @@ class SiddhiAppRuntime:
 
     def start(self):
         self.started = True
+
+    # -- state persistence (C/SiddhiAppRuntimeImpl.java:677-745)
+    _SNAP_MAGIC = b"SIDDHI-AMD-SNAPSHOT-1\n"
+
+    def snapshot(self) -> bytes:
+        """SiddhiAppRuntime.snapshot(): the full state of every query (device
+        partial-match tables, window contents, aggregates, arrival/time
+        counters) plus the host string dictionary the device ids refer to."""
+        blobs = [q.engine.snapshot() for q in self.queries]
+        head = {"app": hashlib.sha256(self.app_text.encode()).hexdigest(),
+                "dictionary": self.dictionary.strings, "last_wall": self._last_wall,
+                "queries": [q.name for q in self.queries], "sizes": [len(b) for b in blobs]}
+        hb = json.dumps(head).encode()
+        return self._SNAP_MAGIC + struct.pack("<Q", len(hb)) + hb + b"".join(blobs)
+
+    def restore(self, snapshot: bytes):
+        """SiddhiAppRuntime.restore(byte[]) (SnapshotService.restore, C/util/snapshot/SnapshotService.java:333)."""
+        m = self._SNAP_MAGIC
+        if not snapshot.startswith(m):
+            raise CannotRestoreSiddhiAppStateException("not a siddhi_amd snapshot")
+        (hl,) = struct.unpack_from("<Q", snapshot, len(m))
+        at = len(m) + 8
+        head = json.loads(snapshot[at:at + hl].decode())
+        at += hl
+        if head["app"] != hashlib.sha256(self.app_text.encode()).hexdigest() or \
+                head["queries"] != [q.name for q in self.queries]:
+            raise CannotRestoreSiddhiAppStateException("snapshot was taken from a different Siddhi app")
+        strings = head["dictionary"]
+        cur = self.dictionary.strings
+        if strings[:len(cur)] != cur:
+            raise CannotRestoreSiddhiAppStateException("string dictionary of the snapshot does not extend this app's")
+        for x in strings[len(cur):]:
+            self.dictionary.id(x)
+        self._last_wall = max(self._last_wall, int(head["last_wall"]))
+        for q, n in zip(self.queries, head["sizes"]):
+            q.engine.restore(snapshot[at:at + n])
+            at += n
+
+    def persist(self) -> "PersistenceReference":
+        """SiddhiAppRuntime.persist(): snapshot saved to the manager's persistence store."""
+        store = self._store()
+        rev = "%d_%s" % (int(time.time() * 1000), self.name)
+        store.save(self.name, rev, self.snapshot())
+        return PersistenceReference(rev)
+
+    def restoreRevision(self, revision: str):  # noqa: N802
+        data = self._store().load(self.name, revision)
+        if data is None:
+            raise CannotRestoreSiddhiAppStateException("no revision '%s' for app '%s'" % (revision, self.name))
+        self.restore(data)
+
+    def restoreLastRevision(self):  # noqa: N802
+        store = self._store()
+        rev = store.getLastRevision(self.name)
+        if rev is not None:
+            self.restore(store.load(self.name, rev))
+        return rev
+
+    def clearAllRevisions(self):  # noqa: N802
+        self._store().clearAllRevisions(self.name)
+
+    def _store(self):
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException("No persistence store assigned for siddhi app " + str(self.name))
+        return self.persistence_store
 
     def shutdown(self):
         for q in self.queries:
@@ -386,12 +455,57 @@ def _bits_to_col(bits: np.ndarray, t: int) -> np.ndarray:
     return bits.astype(np.uint32)
 
 
+class CannotRestoreSiddhiAppStateException(Exception):
+    pass
+
+
+class NoPersistenceStoreException(Exception):
+    pass
+
+
+class PersistenceReference:
+    """io.siddhi.core.util.snapshot.PersistenceReference"""
+
+    def __init__(self, revision):
+        self.revision = revision
+
+    def getRevision(self):  # noqa: N802
+        return self.revision
+
+
+class InMemoryPersistenceStore:
+    """io.siddhi.core.util.persistence.InMemoryPersistenceStore: revisions per app, in order."""
+
+    def __init__(self):
+        self._revs: Dict[str, Dict[str, bytes]] = {}
+
+    def save(self, app_name, revision, snapshot: bytes):
+        self._revs.setdefault(app_name, {})[revision] = bytes(snapshot)
+
+    def load(self, app_name, revision):
+        return self._revs.get(app_name, {}).get(revision)
+
+    def getLastRevision(self, app_name):  # noqa: N802
+        revs = self._revs.get(app_name)
+        return next(reversed(revs)) if revs else None
+
+    def clearAllRevisions(self, app_name):  # noqa: N802
+        self._revs.pop(app_name, None)
+
+
 class SiddhiManager:
     """io.siddhi.core.SiddhiManager (C/SiddhiManager.java:84-96)."""
 
     def __init__(self, engine_factory: Optional[Callable] = None):
         self._engine_factory = engine_factory
         self._runtimes: List[SiddhiAppRuntime] = []
+        self._store = None
+
+    def setPersistenceStore(self, store):  # noqa: N802
+        """SiddhiManager.setPersistenceStore (C/SiddhiManager.java)."""
+        self._store = store
+        for r in self._runtimes:
+            r.persistence_store = store
 
     def createSiddhiAppRuntime(self, app_text: str) -> SiddhiAppRuntime:
         app = qc.parse(app_text)
@@ -400,6 +514,7 @@ class SiddhiManager:
             from .hip_engine import HipQueryEngine   # product path: MI355X only
             factory = HipQueryEngine
         rt = SiddhiAppRuntime(app, factory, app_text)
+        rt.persistence_store = self._store
         self._runtimes.append(rt)
         return rt
 

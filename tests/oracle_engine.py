@@ -69,6 +69,7 @@ class OracleQueryEngine:
             raise pl.SiddhiAppCreationException("oracle: " + self.lib.orc_last_error().decode())
         self.n_out = self.lib.orc_num_outputs(self.h)
         self.types = qp.plan.stream_types
+        self._log = []
 
     def close(self):
         if self.h:
@@ -95,12 +96,53 @@ class OracleQueryEngine:
         self.lib.orc_clear_rows(self.h)
         return split_chunks(chunk, typ, ts, vals[:, :self.n_out], nul[:, :self.n_out])
 
+    # snapshot / restore for the checker: the oracle's state is a function of
+    # its input history, so its "snapshot" is that history (replayed into a
+    # fresh oracle on restore).  Serialized with numpy (no pickle).
+    def snapshot(self) -> bytes:
+        import io
+        arrs = {}
+        for i, op in enumerate(self._log):
+            if op[0] == "t":
+                arrs["op%d_t" % i] = np.array([op[1]], np.int64)
+            else:
+                _, si, b, adv = op
+                arrs["op%d_p" % i] = np.array([si, 1 if adv else 0, len(b.cols)], np.int64)
+                arrs["op%d_ts" % i] = np.asarray(b.ts, np.int64)
+                arrs["op%d_co" % i] = np.asarray(b.call_offsets, np.int64)
+                for a, c in enumerate(b.cols):
+                    arrs["op%d_c%d" % (i, a)] = np.asarray(c)
+                    if b.nulls[a] is not None:
+                        arrs["op%d_n%d" % (i, a)] = np.asarray(b.nulls[a], np.uint8)
+        bio = io.BytesIO()
+        np.savez(bio, n_ops=np.array([len(self._log)], np.int64), **arrs)
+        return bio.getvalue()
+
+    def restore(self, image: bytes):
+        import io
+        from siddhi_amd.runtime import ColumnBatch
+        z = np.load(io.BytesIO(image), allow_pickle=False)
+        self.close()
+        words = self._ir
+        self.h = self.lib.orc_create(words.ctypes.data, len(words))
+        self._log = []
+        for i in range(int(z["n_ops"][0])):
+            if "op%d_t" % i in z:
+                self.set_time(int(z["op%d_t" % i][0]))
+                continue
+            si, adv, nc = (int(x) for x in z["op%d_p" % i])
+            cols = [z["op%d_c%d" % (i, a)] for a in range(nc)]
+            nulls = [z["op%d_n%d" % (i, a)] if ("op%d_n%d" % (i, a)) in z else None for a in range(nc)]
+            self.push(si, ColumnBatch(z["op%d_ts" % i], cols, nulls, z["op%d_co" % i]), bool(adv))
+
     def set_time(self, t):
+        self._log.append(("t", int(t)))
         if self.lib.orc_set_time(self.h, int(t)) != 0:
             raise RuntimeError("oracle: " + self.lib.orc_last_error().decode())
         return self._drain()
 
     def push(self, si, batch, advance_time=False):
+        self._log.append(("p", si, batch, advance_time))
         types = self.types[si]
         n = batch.n
         vals = np.empty((n, max(len(types), 1)), np.uint64)

@@ -1,0 +1,211 @@
+"""State persistence: SiddhiAppRuntime.snapshot()/restore(), persist()/
+restoreLastRevision() with an InMemoryPersistenceStore
+(C/SiddhiAppRuntimeImpl.java:677-745, C/util/snapshot/SnapshotService.java:90,333).
+
+* The reference's own persistence tests
+  (modules/siddhi-core/src/test/java/io/siddhi/core/managment/PersistenceTestCase.java
+  persistenceTest1 :62-143 window, persistenceTest2 :145-230 count pattern,
+  persistenceTest3 :232-293 no store) transcribed against the runtime API, on
+  the CPU oracle (checker) and on the device (libsiddhi_hip).
+* Device parity: a stream cut at a push boundary, the device state
+  snapshotted, restored into a fresh query and the rest pushed there, must give
+  exactly the rows of an uninterrupted device run and of the oracle, for the
+  pattern engine (P3), the window engine (W2 length / time) and the NFA engine
+  (S4 shapes, partitioned and not).
+"""
+import numpy as np
+import pytest
+
+from oracle_engine import OracleQueryEngine
+from parity import assert_same_rows, compile_single_query, concat_rows, run_device, run_oracle, stock_batch
+from siddhi_amd import workloads as wl
+from siddhi_amd.runtime import (InMemoryPersistenceStore, NoPersistenceStoreException, QueryCallback,
+                                SiddhiManager)
+
+
+class _Collect(QueryCallback):
+    def __init__(self):
+        self.rows = []
+
+    def receive(self, timestamp, inEvents, removeEvents):
+        for e in inEvents or []:
+            self.rows.append(list(e.getData()))
+
+
+WINDOW_APP = ("@app:name('Test') define stream StockStream ( symbol string, price float, volume int );"
+              "@info(name = 'query1') from StockStream[price>10]#window.length(10) "
+              "select symbol, price, sum(volume) as totalVol insert into OutStream ")
+COUNT_APP = ("@app:name('Test') define stream Stream1 (symbol string, price float, volume int); "
+             "define stream Stream2 (symbol string, price float, volume int); "
+             "@info(name = 'query1') from e1=Stream1[price>20] <2:5> -> e2=Stream2[price>20] "
+             "select e1[0].price as price1_0, e1[1].price as price1_1, e1[2].price as price1_2, "
+             "   e1[3].price as price1_3, e2.price as price2 insert into OutputStream ;")
+
+
+def _manager(engine):
+    return SiddhiManager(engine_factory=OracleQueryEngine) if engine == "oracle" else SiddhiManager()
+
+
+def _persistence_test1(engine):
+    """PersistenceTestCase.persistenceTest1 (:62-143): length window, persist, 2 lost events, restore."""
+    m = _manager(engine)
+    m.setPersistenceStore(InMemoryPersistenceStore())
+    cb = _Collect()
+    rt = m.createSiddhiAppRuntime(WINDOW_APP)
+    rt.addCallback("query1", cb)
+    ih = rt.getInputHandler("StockStream")
+    rt.start()
+    ih.send(["IBM", 75.6, 100])
+    ih.send(["WSO2", 75.6, 100])
+    assert cb.rows[-1][2] == 200
+    rt.persist()
+    ih.send(["IBM", 75.6, 100])
+    ih.send(["WSO2", 75.6, 100])
+    rt.shutdown()
+    rt = m.createSiddhiAppRuntime(WINDOW_APP)
+    rt.addCallback("query1", cb)
+    ih = rt.getInputHandler("StockStream")
+    rt.start()
+    assert rt.restoreLastRevision() is not None
+    ih.send(["IBM", 75.6, 100])
+    ih.send(["WSO2", 75.6, 100])
+    rt.shutdown()
+    assert len(cb.rows) <= 6
+    assert all(r[0] in ("IBM", "WSO2") for r in cb.rows)
+    assert cb.rows[-1][2] == 400
+
+
+def _persistence_test2(engine):
+    """PersistenceTestCase.persistenceTest2 (:145-230): count pattern state survives a restart."""
+    m = _manager(engine)
+    m.setPersistenceStore(InMemoryPersistenceStore())
+    cb = _Collect()
+    rt = m.createSiddhiAppRuntime(COUNT_APP)
+    rt.addCallback("query1", cb)
+    s1 = rt.getInputHandler("Stream1")
+    rt.start()
+    s1.send(["WSO2", 25.6, 100])
+    s1.send(["GOOG", 47.6, 100])
+    s1.send(["GOOG", 13.7, 100])
+    assert cb.rows == []
+    rt.persist()
+    rt.shutdown()
+    rt = m.createSiddhiAppRuntime(COUNT_APP)
+    rt.addCallback("query1", cb)
+    s1, s2 = rt.getInputHandler("Stream1"), rt.getInputHandler("Stream2")
+    rt.start()
+    rt.restoreLastRevision()
+    s2.send(["IBM", 45.7, 100])
+    s1.send(["GOOG", 47.8, 100])
+    s2.send(["IBM", 55.7, 100])
+    rt.shutdown()
+    assert len(cb.rows) == 1
+    f32 = lambda x: float(np.float32(x))   # noqa: E731  (Java float values)
+    assert cb.rows[0] == [f32(25.6), f32(47.6), None, None, f32(45.7)]
+
+
+def test_persistence_window_oracle():
+    _persistence_test1("oracle")
+
+
+def test_persistence_count_pattern_oracle():
+    _persistence_test2("oracle")
+
+
+def test_persist_without_store_raises():
+    """PersistenceTestCase.persistenceTest3 (:232-293): NoPersistenceStoreException."""
+    m = SiddhiManager(engine_factory=OracleQueryEngine)
+    rt = m.createSiddhiAppRuntime(COUNT_APP)
+    rt.start()
+    with pytest.raises(NoPersistenceStoreException):
+        rt.persist()
+
+
+def test_restore_rejects_other_app():
+    m = SiddhiManager(engine_factory=OracleQueryEngine)
+    a = m.createSiddhiAppRuntime(WINDOW_APP)
+    b = m.createSiddhiAppRuntime(COUNT_APP)
+    from siddhi_amd.runtime import CannotRestoreSiddhiAppStateException
+    with pytest.raises(CannotRestoreSiddhiAppStateException):
+        b.restore(a.snapshot())
+
+
+@pytest.mark.gpu
+def test_persistence_window_device(hip_available):
+    _persistence_test1("device")
+
+
+@pytest.mark.gpu
+def test_persistence_count_pattern_device(hip_available):
+    _persistence_test2("device")
+
+
+def _split(sym, price, vol, ts, parts, call=1024):
+    n = len(ts)
+    cuts = sorted(set([0, n] + [int(n * k / parts) // call * call for k in range(1, parts)]))
+    return [(0, stock_batch(sym[a:b], price[a:b], vol[a:b], ts[a:b], call)) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def _run_with_restore(qp, batches, cut):
+    """Device: batches[:cut] on one query, snapshot, restore into a fresh query, batches[cut:]."""
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
+    parts = []
+
+    def feed(dq, bs):
+        for si, b in bs:
+            cols = [np.ascontiguousarray(c) for c in b.cols]
+            ts = np.ascontiguousarray(b.ts, np.int64)
+            dq.push_raw(si, b.n, ts.ctypes.data, [c.ctypes.data for c in cols], [0] * len(cols), SHD_MEM_HOST,
+                        b.call_offsets if len(b.call_offsets) > 2 else None, True)
+            r = dq.poll()
+            if r is not None:
+                parts.append(r)
+
+    dq = DeviceQuery(qp.ir)
+    feed(dq, batches[:cut])
+    image = dq.snapshot()
+    dq.close()
+    dq2 = DeviceQuery(qp.ir)
+    dq2.restore(image)
+    feed(dq2, batches[cut:])
+    dq2.close()
+    return concat_rows(parts)
+
+
+RESTORE_CASES = [
+    ("P3", wl.P3_APP, 200_000, 20_000, 0.01, 4),
+    ("P3-dense", wl.P3_APP, 120_000, 3_000, 1e-4, 3),
+    ("W2-length", wl.W2_LENGTH_APP, 100_000, 1000, 0.1, 4),
+    ("W2-time", wl.W2_TIME_APP, 100_000, 1000, 0.5, 4),
+    ("S4-seq", wl.S4_APPS["seq"], 30_000, 100, 1.0, 3),
+    ("S4-and-part", wl.S4_PART_APPS["and"], 30_000, 100, 1.0, 3),
+    ("S4-not-part", wl.S4_PART_APPS["not"], 30_000, 100, 1.0, 3),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,app,n,keys,delta,parts", RESTORE_CASES, ids=[c[0] for c in RESTORE_CASES])
+def test_device_snapshot_restore_midstream(hip_available, name, app, n, keys, delta, parts):
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(n, keys, delta, seed_offset=301)
+    batches = _split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    whole, _, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(whole, ora)
+    for cut in range(1, len(batches)):
+        assert_same_rows(_run_with_restore(qp, batches, cut), ora)
+
+
+@pytest.mark.gpu
+def test_restore_rejects_other_plan(hip_available):
+    from siddhi_amd.hip_engine import DeviceQuery, SiddhiHipError
+    qa, _ = compile_single_query(wl.P3_APP)
+    qb, _ = compile_single_query(wl.W2_LENGTH_APP)
+    a, b = DeviceQuery(qa.ir), DeviceQuery(qb.ir)
+    try:
+        with pytest.raises(SiddhiHipError):
+            b.restore(a.snapshot())
+    finally:
+        a.close()
+        b.close()
