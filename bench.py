@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
     ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
                     help="roundrobin: every rank holds a round-robin share of the global stream and events are "
-                         "re-routed to their key's owner with one RCCL all-to-all per micro-batch (default for N>1)")
+                         "re-routed to their key's owner with one RCCL all-to-all per micro-batch (default: "
+                         "prepartitioned, no data-path collective)")
     return ap.parse_args()
 
 
@@ -173,7 +174,10 @@ def main():
     else:
         qp = plan_query(qa, item, StringDictionary())
 
-    mode = args.input if args.input != "auto" else ("prepartitioned" if world == 1 else "roundrobin")
+    # P3 shards by partition key with no data-path collective (each rank owns a
+    # key slice and receives its events); --input roundrobin adds the RCCL
+    # all-to-all re-route of events that arrive at the wrong rank
+    mode = args.input if args.input != "auto" else "prepartitioned"
     if mode == "roundrobin" and not pattern:
         mode = "prepartitioned"   # window configs are unpartitioned: replicas
     # inputs resident in HBM before the timed region

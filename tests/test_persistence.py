@@ -177,7 +177,8 @@ RESTORE_CASES = [
     ("P3-dense", wl.P3_APP, 120_000, 3_000, 1e-4, 3),
     ("W2-length", wl.W2_LENGTH_APP, 100_000, 1000, 0.1, 4),
     ("W2-time", wl.W2_TIME_APP, 100_000, 1000, 0.5, 4),
-    ("S4-seq", wl.S4_APPS["seq"], 30_000, 100, 1.0, 3),
+    ("S4-or", wl.S4_APPS["or"], 30_000, 100, 1.0, 3),
+    ("S4-seqplus-part", wl.S4_PART_APPS["seqplus"], 30_000, 50, 1.0, 3),
     ("S4-and-part", wl.S4_PART_APPS["and"], 30_000, 100, 1.0, 3),
     ("S4-not-part", wl.S4_PART_APPS["not"], 30_000, 100, 1.0, 3),
 ]
