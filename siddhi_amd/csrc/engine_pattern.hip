@@ -150,7 +150,8 @@ struct PrepArgs {
   DExprSet es;
   DFilters f1;
   int is_a, is_b;           // pushed stream plays A and/or B
-  int partitioned;
+  int partitioned;          // write a key per row
+  int null_skip;            // partition key semantics: null key -> event dropped (F_SKIP)
   int key64;                // key written as u64 (long / double / float keys)
   DExpr key_expr;           // key expression of the pushed stream
   int key_type;
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       }
       const bool p1 = a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx));
       f = F_NEW;
-      if (kv.null) {
+      if (kv.null && a.null_skip) {
         f |= F_SKIP;   // PartitionStreamReceiver drops null keys
       } else {
         if (a.is_b) f |= F_B;
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
           f |= F_CAND;
           created++;
         }
-        k = canon_key(kv, a.key_type);
+        k = kv.null ? 0 : canon_key(kv, a.key_type);
       }
       tmin = t < tmin ? t : tmin;
       tmax = t > tmax ? t : tmax;
@@ -830,6 +831,67 @@ int plain_load_attr(const Plan& p, int e) {
   return -1;
 }
 
+// Does one of the e2 filters hold a top-level conjunct `e2.x == e1.y` (x, y
+// attributes of the same string / int / long type, no conversion)?  Then an
+// unpartitioned partial can only complete on an event with its own x value, so
+// with time-ordered events the pattern runs grouped by that value exactly like
+// a partitioned one (SURVEY.md §8e "sharding by symbol ... provable from the
+// plan").  Returns the attribute pair (A-stream attr, B-stream attr).
+bool find_key_equality(const Plan& p, const std::vector<int>& filters, int& attr_a, int& attr_b, int& type) {
+  for (int e : filters) {
+    const auto& code = p.exprs[e];
+    // postfix -> tree (children of binary ops), then walk AND nodes from the root
+    std::vector<int> st;
+    std::vector<std::pair<int, int>> kid(code.size(), {-1, -1});
+    bool ok = true;
+    for (int i = 0; i < (int)code.size() && ok; i++) {
+      const int op = code[i].op;
+      if (op == SHD_OP_LOAD || op == SHD_OP_CONST || op == SHD_OP_NULL || op == SHD_OP_EVNULL || op == SHD_OP_TS ||
+          op == SHD_OP_AGG) {
+        st.push_back(i);
+      } else if (op == SHD_OP_CVT || op == SHD_OP_NOT || op == SHD_OP_ISNULL) {
+        if (st.empty()) ok = false;
+        else { kid[i].first = st.back(); st.back() = i; }
+      } else if (op >= SHD_OP_ADD && op <= SHD_OP_OR) {
+        if (st.size() < 2) { ok = false; break; }
+        kid[i] = {st[st.size() - 2], st.back()};
+        st.pop_back();
+        st.back() = i;
+      } else if (op != SHD_OP_END) {
+        ok = false;
+      }
+    }
+    if (!ok || st.size() != 1) continue;
+    std::vector<int> todo{st[0]};
+    while (!todo.empty()) {
+      const int n = todo.back();
+      todo.pop_back();
+      const Instr& in = code[n];
+      if (in.op == SHD_OP_AND) {
+        todo.push_back(kid[n].first);
+        todo.push_back(kid[n].second);
+        continue;
+      }
+      if (in.op != SHD_OP_EQ) continue;
+      const Instr& l = code[kid[n].first];
+      const Instr& r = code[kid[n].second];
+      if (l.op != SHD_OP_LOAD || r.op != SHD_OP_LOAD) continue;
+      auto cur = [](const Instr& x) { return x.b == 0 || x.b == SHD_IDX_CURRENT; };
+      if (!cur(l) || !cur(r)) continue;
+      const Instr& la = l.a == 0 ? l : r;
+      const Instr& lb = l.a == 0 ? r : l;
+      if (la.a != 0 || lb.a != 1) continue;
+      const int ta = la.c >> 16, tb = lb.c >> 16;
+      if (ta != tb || in.a != ta || !(ta == SHD_T_STRING || ta == SHD_T_INT || ta == SHD_T_LONG)) continue;
+      attr_a = la.c & 0xFFFF;
+      attr_b = lb.c & 0xFFFF;
+      type = ta;
+      return true;
+    }
+  }
+  return false;
+}
+
 
 }  // namespace
 
@@ -838,6 +900,9 @@ struct PatternEngine : Engine {
   std::vector<int> f1, f2;
   int64_t W = INT64_MAX;
   bool partitioned = false;
+  // unpartitioned plan whose f2 holds `e2.x == e1.y`: keys written by prepare,
+  // pushes with time-ordered events run grouped by that attribute
+  bool implicit_key = false;
   int key_expr[2] = {-1, -1}, key_col[2] = {-1, -1}, key_type[2] = {0, 0};
   std::vector<int> outs;
   std::vector<int> typesA;
@@ -953,10 +1018,11 @@ struct PatternEngine : Engine {
     SHD_HIP(hipEventRecord(ev0, s));
     stage_begin();
     const int slot = isA ? 0 : 1;
-    const bool key64 = partitioned && type_key64(key_type[slot]);
+    const bool keyed = partitioned || implicit_key;
+    const bool key64 = keyed && type_key64(key_type[slot]);
     d_pv.reserve(n_ext * 4);
     d_ts.reserve(n_ext * 4);
-    if (partitioned) {
+    if (keyed) {
       if (key64) d_k64.reserve(n_ext * 8);
       d_k32.reserve(n_ext * 4);
     }
@@ -978,10 +1044,11 @@ struct PatternEngine : Engine {
     pa.f1 = dfilters(f1);
     pa.is_a = isA;
     pa.is_b = isB;
-    pa.partitioned = partitioned;
+    pa.partitioned = keyed;
+    pa.null_skip = partitioned;
     pa.key64 = key64;
-    if (partitioned) {
-      pa.key_expr = dexpr(key_expr[slot]);
+    if (keyed) {
+      if (key_expr[slot] >= 0) pa.key_expr = dexpr(key_expr[slot]);
       pa.key_col = key_col[slot];
       pa.key_type = key_type[slot];
     } else {
@@ -1000,7 +1067,7 @@ struct PatternEngine : Engine {
     const int nblk = grid_for(n_ext, 1, 4096);
     d_blk.reserve((size_t)2 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
-    const bool fast1 = (!isA || pa.f1.fp.ok) && (!partitioned || pa.key_col >= 0);
+    const bool fast1 = (!isA || pa.f1.fp.ok) && (!keyed || pa.key_col >= 0);
     if (fast1)
       hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
                          d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
@@ -1032,8 +1099,12 @@ struct PatternEngine : Engine {
     const int64_t* sts64 = nullptr;
     bool sorted64 = false;
     const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX;
+    // implicit grouping needs the reference's global expiry order to be the
+    // per-key one: pushed rows time-ordered, carried partials before them
+    const bool grouped = partitioned || (implicit_key && !pg.unmono && (C == 0 || pg.carry_tmax <= pg.ts_min));
     uint32_t hash_mask = 0;
-    if (partitioned) {
+    counters.group_bits = 0;
+    if (grouped) {
       uint64_t kmax = pg.kmax;
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
@@ -1086,7 +1157,7 @@ struct PatternEngine : Engine {
     sa.es = dset();
     sa.f2 = dfilters(f2);
     sa.within = W;
-    sa.partitioned = partitioned;
+    sa.partitioned = grouped;
     sa.prune = prune;
     sa.hash_mask = hash_mask;
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
@@ -1198,7 +1269,7 @@ struct PatternEngine : Engine {
       GatherArgs ga{};
       ga.x = x;
       ga.ncols = (int)typesA.size();
-      ga.partitioned = partitioned;
+      ga.partitioned = keyed;
       ga.key64 = sorted64;
       for (size_t c = 0; c < typesA.size(); c++) {
         ga.types[c] = (int32_t)typesA[c];
@@ -1208,6 +1279,11 @@ struct PatternEngine : Engine {
       ga.dts = carry[nxt].ts.as<int64_t>();
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
+      if (keyed && !grouped) {   // positions are rows: the prepare output holds each row's key
+        ga.key64 = key64;
+        skey32 = d_k32.as<uint32_t>();
+        skey64 = d_k64.as<uint64_t>();
+      }
       hipLaunchKernelGGL(k_gather_carry, dim3(ntile), dim3(kBlock), 0, s, dev_args(ga),
                          (const uint8_t*)d_pst.as<uint8_t>(), (const uint32_t*)d_boff.as<uint32_t>(), spv, skey32,
                          skey64, n_ext, tile);
@@ -1266,6 +1342,16 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
   e->typesA = p.stream_types[a.stream];
   for (auto& o : p.outputs) e->outs.push_back(o.second);
   e->partitioned = !p.part_keys.empty();
+  if (!e->partitioned && !getenv("SHD_NO_IMPLICIT_KEY")) {
+    int aa, ab, t;
+    // one stream playing both roles: an event has one key, so both sides must be the same attribute
+    if (find_key_equality(p, b.filters, aa, ab, t) && (a.stream != b.stream || aa == ab)) {
+      e->implicit_key = true;
+      e->key_col[0] = aa;
+      e->key_col[1] = ab;
+      e->key_type[0] = e->key_type[1] = t;
+    }
+  }
   if (e->partitioned) {
     int cls = -1;
     for (auto& pk : p.part_keys) {

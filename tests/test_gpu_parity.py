@@ -172,3 +172,56 @@ def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
     assert counters["group_bits"] == 12   # exact: bit length of the largest key
+
+
+@pytest.mark.parametrize("implicit", [True, False])
+@pytest.mark.parametrize("parts", [1, 3])
+def test_unpartitioned_pattern_grouped_by_equality(hip_available, monkeypatch, implicit, parts):
+    """Config P1 (unpartitioned, f2 holds `symbol == e1.symbol`): with
+    time-ordered events the engine groups by symbol like a partitioned query
+    (SHD_NO_IMPLICIT_KEY turns that off); results identical to the oracle."""
+    if not implicit:
+        monkeypatch.setenv("SHD_NO_IMPLICIT_KEY", "1")
+    qp, _ = compile_single_query(wl.P1_APP)
+    sym, price, vol, ts = wl.stock_stream(100_000, 1000, 0.5, seed_offset=91)
+    batches = split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == 1 and len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+    assert (counters["group_bits"] > 0) == implicit
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_implicit_grouping_edge_cases(hip_available, reverse):
+    """Null symbols and two streams keyed by their own attribute; with
+    `reverse`, one push whose events go back in time (no grouping for it: the
+    ungrouped walk either reproduces the oracle or refuses with
+    SHD_E_UNSUPPORTED -- never a silent difference)."""
+    from siddhi_amd.hip_engine import SiddhiHipError, SHD_E_UNSUPPORTED
+    app = ("@app:playback define stream A (k string, p double); define stream B (k string, p double); "
+           "@info(name='q') from every e1=A[p>20] -> e2=B[k==e1.k and p>e1.p] within 50 milliseconds "
+           "select e1.k as k, e1.p as p1, e2.p as p2 insert into O;")
+    qp, d = compile_single_query(app)
+    rng = np.random.default_rng(8)
+    batches = []
+    t = 1000
+    for r in range(30):
+        si = r % 2
+        m = int(rng.integers(1000, 6000))
+        k = rng.integers(0, 40, m).astype(np.uint32)
+        kn = (rng.random(m) < 0.05).astype(np.uint8)   # null keys
+        p = rng.uniform(0, 100, m)
+        ts = t + np.sort(rng.integers(0, 30, m)).astype(np.int64)
+        if reverse and r == 17:
+            ts = ts[::-1].copy()   # time goes back inside this push
+        t = int(ts.max())
+        batches.append((si, ColumnBatch(ts, [k, p], [kn, None], np.array([0, m], np.int64))))
+    ora = run_oracle(qp, batches)
+    assert len(ora[2]) > 0
+    try:
+        dev, _, _ = run_device(qp, batches)
+    except SiddhiHipError as e:
+        assert reverse and e.code == SHD_E_UNSUPPORTED
+        return
+    assert_same_rows(dev, ora)
