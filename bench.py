@@ -144,6 +144,118 @@ def cpu_baseline(cfg_name, app, keys, delta, sample):
                       "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)}
 
 
+def run_multi(args, torch, dist, rank, world, local, dev):
+    """Config M5: every query of a multi-query app on one StockStream junction
+    (StreamJunction fan-out, C/stream/StreamJunction.java:146-272).
+    Query-parallel: rank r runs the queries with index % world == r over the
+    whole stream (broadcast input: each rank holds it in its own HBM);
+    value = stream events / max-over-ranks time ("strong": the total work,
+    all queries over the stream, is fixed as N grows)."""
+    from siddhi_amd import workloads as wl
+    from siddhi_amd import hip_engine as he
+    from siddhi_amd.planner import StringDictionary, plan_query
+    from siddhi_amd import query_compiler as qc
+
+    app, n_def, k_def, delta = wl.CONFIGS[args.config]
+    n = args.events or n_def
+    keys = args.keys or k_def
+    qa = qc.parse(app)
+    d = StringDictionary()
+    wl.register_symbols(d, keys)
+    plans = [plan_query(qa, item, d) for item in qa.execution_order]
+    mine = [i for i in range(len(plans)) if i % world == rank]
+    sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=0, key_base=0, dev=dev)
+    torch.cuda.synchronize()
+    he.context(local)
+    dqs = [he.DeviceQuery(plans[i].ir, device=local) for i in mine]
+    # 100 queries each keep their own scratch: 10M-event micro-batches by default
+    batch = min(args.batch if args.batch != 50_000_000 else 10_000_000, n)
+    cuts = list(range(0, n, batch)) + [n]
+    offs_all = wl.call_offsets(n)
+
+    def run_step(collect=None):
+        for dq in dqs:
+            dq.reset()
+        tot = {}
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo = np.searchsorted(offs_all, a)
+            hi = np.searchsorted(offs_all, b)
+            co = (np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a).astype(np.int64)
+            cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
+            for dq in dqs:   # junction fan-out in definition order
+                dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE, co, True)
+                dq.discard()
+                if collect is not None:
+                    for k, v in dq.stage_times().items():
+                        tot[k] = tot.get(k, 0) + v
+        if collect is not None:
+            collect.append(tot)
+
+    for _ in range(args.warmup):
+        run_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    stage_runs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step(stage_runs)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # algorithmic bytes of every owned query (pattern / window formulas of SURVEY.md §8d)
+    bytes_step, matches = 0.0, 0
+    for i, dq in zip(mine, dqs):
+        c = dq.counters()
+        matches += c["matches"]
+        if dq.engine_kind in (1, 4):
+            bytes_step += alg_bytes_pattern(c, c["events"])[0]
+        else:
+            bytes_step += alg_bytes_window(c, c["events"], 0)[0]
+    stages = {}
+    for r in stage_runs:
+        for k, v in r.items():
+            stages[k] = stages.get(k, 0) + v / len(stage_runs)
+    vals = torch.tensor([bytes_step, float(matches)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(vals)
+    bytes_all, matches_all = float(vals[0].item()), float(vals[1].item())
+    dominant = max(stages, key=stages.get) if stages else None
+    roof = None
+    if dominant:
+        launches = (len(cuts) - 1) * len(dqs)
+        ach = (bytes_step / launches) / (stages[dominant] / launches * 1e-9) / 1e9
+        path = bytes_step / (sum(stages.values()) * 1e-9) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_stage": dominant,
+                "path_achieved": round(path, 1), "path_frac": round(path / HBM_PEAK_GBS, 4)}
+    if rank == 0:
+        line = {
+            "metric": "events/sec ingested + matches/sec (partitioned pattern, 1–8 GPU); % HBM peak",
+            "value": round(n * args.steps / elapsed, 1), "unit": "events/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
+            "config": {"workload": "M5", "queries": len(plans), "events": n, "keys": keys, "delta_ms": delta,
+                       "micro_batch": batch, "call_size": 1024,
+                       "parallelism": "query-parallel x%d (broadcast input)" % world},
+            "query_events_per_s": round(n * len(plans) * args.steps / elapsed, 1),
+            "matches_per_s": round(matches_all * args.steps / elapsed, 1),
+            "algorithmic_bytes_per_step": round(bytes_all),
+            "stage_ms_per_step_rank0": {k: round(v / 1e6, 3) for k, v in stages.items()},
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line))
+    for dq in dqs:
+        dq.close()
+
+
 def main():
     args = parse()
     import torch
@@ -157,6 +269,11 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(local)
+    if args.config == "M5":
+        run_multi(args, torch, dist, rank, world, local, dev)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from siddhi_amd import workloads as wl
     from siddhi_amd import hip_engine as he

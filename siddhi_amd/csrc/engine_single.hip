@@ -356,12 +356,84 @@ struct FoldArgs {
   int64_t nkeys;
 };
 
-// One lane per group segment: the reference's sequential add/remove order.
+// One aggregator step on a CURRENT (add) or EXPIRED (remove) event: the
+// reference's incremental executors, Sum/Avg/CountAttributeAggregatorExecutor
+// (.../selector/attribute/aggregator/*.java: processAdd / processRemove).
+// ob/on: the aggregator's value after the step (on = null).  avg: ob is the
+// running sum and the count is the state c; the division value / count happens
+// at emission (k_emit) for the rows that are emitted, not in the sequential fold.
+__device__ __forceinline__ void agg_step(int kind, int type, bool add, uint64_t xb, bool xn, double& d, int64_t& l,
+                                         int64_t& c, uint64_t& ob, bool& on) {
+  ob = 0;
+  on = true;
+  switch (kind) {
+    case SHD_AGG_COUNT:
+      c += add ? 1 : -1;
+      ob = (uint64_t)c;
+      on = false;
+      break;
+    case SHD_AGG_SUM:
+      if (type == SHD_T_INT || type == SHD_T_LONG) {
+        if (xn) {
+          if (c != 0) { ob = (uint64_t)l; on = false; }
+          break;
+        }
+        int64_t x = type == SHD_T_INT ? (int64_t)v_i32(xb) : (int64_t)xb;
+        if (add) {
+          l = (int64_t)((uint64_t)l + (uint64_t)x);
+          c++;
+          ob = (uint64_t)l;
+          on = false;
+        } else {
+          l = java_d2l(__dsub_rn((double)l, (double)x));
+          c--;
+          if (c != 0) { ob = (uint64_t)l; on = false; }
+        }
+      } else {
+        if (xn) {
+          if (type == SHD_T_DOUBLE && c != 0) { ob = p_f64(d); on = false; }
+          break;
+        }
+        double x = type == SHD_T_FLOAT ? (double)v_f32(xb) : v_f64(xb);
+        if (add) {
+          d = __dadd_rn(d, x);
+          c++;
+          ob = p_f64(d);
+          on = false;
+        } else {
+          d = __dsub_rn(d, x);
+          c--;
+          if (c != 0) { ob = p_f64(d); on = false; }
+        }
+      }
+      break;
+    case SHD_AGG_AVG: {
+      if (xn) {
+        if (c != 0) { ob = p_f64(d); on = false; }
+        break;
+      }
+      double x;
+      switch (type) {
+        case SHD_T_INT: x = (double)v_i32(xb); break;
+        case SHD_T_LONG: x = (double)(int64_t)xb; break;
+        case SHD_T_FLOAT: x = (double)v_f32(xb); break;
+        default: x = v_f64(xb);
+      }
+      if (add) { c++; d = __dadd_rn(d, x); }
+      else { c--; d = __dsub_rn(d, x); }
+      if (c != 0) { ob = p_f64(d); on = false; }
+      break;
+    }
+  }
+}
+
+// One lane per group segment: the reference's sequential add/remove order
+// (short segments: many groups, few operations each).
 __global__ __launch_bounds__(kBlock) void k_fold(const FoldArgs* __restrict__ ap, const uint32_t* heads, int64_t nheads, int64_t nops,
                                                  const uint32_t* okey_sorted, const uint32_t* oref_sorted,
                                                  const uint64_t* iargv, const uint8_t* iargn, const int32_t* ievrow,
                                                  const int32_t* call_of, uint64_t* resv, uint8_t* resn,
-                                                 uint8_t* first, uint32_t* last_of) {
+                                                 int64_t* resc, uint8_t* first, uint32_t* last_of) {
   const FoldArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nheads; h += (int64_t)gridDim.x * blockDim.x) {
     int64_t q0 = heads[h];
@@ -381,72 +453,13 @@ __global__ __launch_bounds__(kBlock) void k_fold(const FoldArgs* __restrict__ ap
       bool add = ref & kAddBit;
       uint32_t t = ref & ~kAddBit;
       for (int g = 0; g < a.nagg; g++) {
-        uint64_t xb = iargv[g * a.cap + t];
-        bool xn = iargn[g * a.cap + t];
-        uint64_t ob = 0;
-        bool on = true;
-        switch (a.kind[g]) {
-          case SHD_AGG_COUNT:
-            c[g] += add ? 1 : -1;
-            ob = (uint64_t)c[g];
-            on = false;
-            break;
-          case SHD_AGG_SUM:
-            if (a.type[g] == SHD_T_INT || a.type[g] == SHD_T_LONG) {
-              if (xn) {
-                if (c[g] != 0) { ob = (uint64_t)l[g]; on = false; }
-                break;
-              }
-              int64_t x = a.type[g] == SHD_T_INT ? (int64_t)v_i32(xb) : (int64_t)xb;
-              if (add) {
-                l[g] = (int64_t)((uint64_t)l[g] + (uint64_t)x);
-                c[g]++;
-                ob = (uint64_t)l[g];
-                on = false;
-              } else {
-                l[g] = java_d2l(__dsub_rn((double)l[g], (double)x));
-                c[g]--;
-                if (c[g] != 0) { ob = (uint64_t)l[g]; on = false; }
-              }
-            } else {
-              if (xn) {
-                if (a.type[g] == SHD_T_DOUBLE && c[g] != 0) { ob = p_f64(d[g]); on = false; }
-                break;
-              }
-              double x = a.type[g] == SHD_T_FLOAT ? (double)v_f32(xb) : v_f64(xb);
-              if (add) {
-                d[g] = __dadd_rn(d[g], x);
-                c[g]++;
-                ob = p_f64(d[g]);
-                on = false;
-              } else {
-                d[g] = __dsub_rn(d[g], x);
-                c[g]--;
-                if (c[g] != 0) { ob = p_f64(d[g]); on = false; }
-              }
-            }
-            break;
-          case SHD_AGG_AVG: {
-            if (xn) {
-              if (c[g] != 0) { ob = p_f64(__ddiv_rn(d[g], (double)c[g])); on = false; }
-              break;
-            }
-            double x;
-            switch (a.type[g]) {
-              case SHD_T_INT: x = (double)v_i32(xb); break;
-              case SHD_T_LONG: x = (double)(int64_t)xb; break;
-              case SHD_T_FLOAT: x = (double)v_f32(xb); break;
-              default: x = v_f64(xb);
-            }
-            if (add) { c[g]++; d[g] = __dadd_rn(d[g], x); }
-            else { c[g]--; d[g] = __dsub_rn(d[g], x); }
-            if (c[g] != 0) { ob = p_f64(__ddiv_rn(d[g], (double)c[g])); on = false; }
-            break;
-          }
-        }
+        uint64_t ob;
+        bool on;
+        agg_step(a.kind[g], a.type[g], add, iargv[g * a.cap + t], iargn[g * a.cap + t], d[g], l[g], c[g], ob, on);
         if (add) {
           resv[g * a.cap + t] = ob;
           resn[g * a.cap + t] = (uint8_t)on;
+          if (a.kind[g] == SHD_AGG_AVG) resc[g * a.cap + t] = c[g];
         }
       }
       if (add) {
@@ -469,6 +482,298 @@ __global__ __launch_bounds__(kBlock) void k_fold(const FoldArgs* __restrict__ ap
   }
 }
 
+// One WAVE per group segment (long segments: few groups, many operations --
+// config W2 has 1000 groups and ~30k operations per group per push).  The
+// wave loads 64 consecutive operations with coalesced loads (the gathers of
+// their operands run in parallel across lanes, NCH chunks ahead of the fold),
+// then folds them in order with the running state held wave-uniform: step k
+// reads lane k's operands (readlane) and deposits the result in lane k.  Same
+// arithmetic, same order as k_fold: bit-identical results.
+template <int NA>
+__global__ __launch_bounds__(kBlock) void k_fold_wave(const FoldArgs* __restrict__ ap, const uint32_t* heads,
+                                                      int64_t nheads, int64_t nops, const uint32_t* okey_sorted,
+                                                      const uint32_t* oref_sorted, const uint64_t* iargv,
+                                                      const uint8_t* iargn, const int32_t* ievrow,
+                                                      const int32_t* call_of, uint64_t* resv, uint8_t* resn,
+                                                      int64_t* resc, uint8_t* first, uint32_t* last_of) {
+  const FoldArgs& a = *ap;
+  const int lane = threadIdx.x & 63;
+  const int64_t h = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;   // one wave per head
+  if (h >= nheads) return;
+  const int64_t q0 = heads[h];
+  const int64_t q1 = h + 1 < nheads ? (int64_t)heads[h + 1] : nops;
+  const uint32_t key = okey_sorted[q0];
+  double d[NA];
+  int64_t l[NA], c[NA];
+#pragma unroll
+  for (int g = 0; g < NA; g++) {
+    d[g] = a.dsum[g * a.nkeys + key];
+    l[g] = a.lsum[g * a.nkeys + key];
+    c[g] = a.cnt[g * a.nkeys + key];
+  }
+  int kind[NA], type[NA];
+#pragma unroll
+  for (int g = 0; g < NA; g++) {
+    kind[g] = a.kind[g];
+    type[g] = a.type[g];
+  }
+  int32_t cur_call = -1;
+  uint32_t t_first = 0, t_prev = 0;
+  // operands of one 64-operation chunk, lane k = operation base + k
+  struct Chunk {
+    uint32_t ref;
+    int32_t call;
+    uint64_t xb[NA];
+    uint8_t xn[NA];
+  };
+  auto load = [&](int64_t base, Chunk& ch) {
+    const int64_t q = base + lane;
+    ch.ref = q < q1 ? oref_sorted[q] : 0u;
+    const uint32_t t = ch.ref & ~kAddBit;
+#pragma unroll
+    for (int g = 0; g < NA; g++) {
+      ch.xb[g] = q < q1 ? iargv[g * a.cap + t] : 0ull;
+      ch.xn[g] = q < q1 ? iargn[g * a.cap + t] : (uint8_t)0;
+    }
+    ch.call = (q < q1 && (ch.ref & kAddBit)) ? call_of[ievrow[t]] : -1;
+  };
+  constexpr int NCH = 4;   // chunks in flight
+  Chunk ring[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; i++) load(q0 + (int64_t)i * 64, ring[i]);
+  for (int64_t base = q0; base < q1; base += 64 * NCH) {
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+      const int64_t cb = base + (int64_t)i * 64;
+      if (cb >= q1) break;
+      Chunk ch = ring[i];
+      load(cb + 64 * NCH, ring[i]);   // refill this slot NCH chunks ahead
+      const int nk = q1 - cb < 64 ? (int)(q1 - cb) : 64;
+      uint64_t ob_l[NA];
+      int64_t oc_l[NA];
+      uint8_t on_l[NA];
+      uint8_t first_l = 0;
+      for (int k = 0; k < nk; k++) {
+        const uint32_t ref = (uint32_t)__builtin_amdgcn_readlane((int)ch.ref, k);
+        const bool add = ref & kAddBit;
+        const uint32_t t = ref & ~kAddBit;
+#pragma unroll
+        for (int g = 0; g < NA; g++) {
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ch.xb[g], k);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ch.xb[g] >> 32), k);
+          const bool xn = __builtin_amdgcn_readlane((int)ch.xn[g], k) != 0;
+          uint64_t ob;
+          bool on;
+          agg_step(kind[g], type[g], add, ((uint64_t)hi << 32) | lo, xn, d[g], l[g], c[g], ob, on);
+          if (lane == k) {
+            ob_l[g] = ob;
+            on_l[g] = (uint8_t)on;
+            oc_l[g] = c[g];
+          }
+        }
+        if (add) {
+          const int32_t call = __builtin_amdgcn_readlane(ch.call, k);
+          if (call != cur_call) {
+            if (cur_call >= 0 && lane == 0) last_of[t_first] = t_prev;
+            if (lane == k) first_l = 1;
+            t_first = t;
+            cur_call = call;
+          }
+          t_prev = t;
+        }
+      }
+      if (lane < nk && (ch.ref & kAddBit)) {
+        const uint32_t t = ch.ref & ~kAddBit;
+#pragma unroll
+        for (int g = 0; g < NA; g++) {
+          resv[g * a.cap + t] = ob_l[g];
+          resn[g * a.cap + t] = on_l[g];
+          if (kind[g] == SHD_AGG_AVG) resc[g * a.cap + t] = oc_l[g];
+        }
+        if (first_l) first[t] = 1;
+      }
+    }
+  }
+  if (cur_call >= 0 && lane == 0) last_of[t_first] = t_prev;
+  if (lane == 0) {
+#pragma unroll
+    for (int g = 0; g < NA; g++) {
+      a.dsum[g * a.nkeys + key] = d[g];
+      a.lsum[g * a.nkeys + key] = l[g];
+      a.cnt[g * a.nkeys + key] = c[g];
+    }
+  }
+}
+
+// Wave fold specialised for the aggregators whose state is a double running
+// sum plus a count -- count(), sum(double|float), avg(any numeric); config W2
+// is avg(price), sum(price), count().  Branch-light: the counts after every
+// operation are a wave prefix sum (integers: exact in any order); only the
+// double sums run as sequential chains, one v_add_f64 per operation in
+// operation order (a - b == a + (-b) in IEEE 754: identical to the reference's
+// value -= x), with the operands read by v_readlane; the callback-run
+// bookkeeping (first / last_of) comes from ballots.  Results are bit-identical
+// to agg_step / k_fold.
+__device__ __forceinline__ int wave_incl_scan_i32(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int k) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, k);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), k);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int NA>
+__global__ __launch_bounds__(kBlock) void k_fold_wave_d(const FoldArgs* __restrict__ ap, const uint32_t* heads,
+                                                        int64_t nheads, int64_t nops, const uint32_t* okey_sorted,
+                                                        const uint32_t* oref_sorted, const uint64_t* iargv,
+                                                        const uint8_t* iargn, const int32_t* ievrow,
+                                                        const int32_t* call_of, uint64_t* resv, uint8_t* resn,
+                                                        int64_t* resc, uint8_t* first, uint32_t* last_of) {
+  const FoldArgs& a = *ap;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t h = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;   // one wave per head
+  if (h >= nheads) return;
+  const int64_t q0 = heads[h];
+  const int64_t q1 = h + 1 < nheads ? (int64_t)heads[h + 1] : nops;
+  const uint32_t key = okey_sorted[q0];
+  int kind[NA], type[NA];
+  double d[NA];
+  int64_t c[NA];
+#pragma unroll
+  for (int g = 0; g < NA; g++) {
+    kind[g] = a.kind[g];
+    type[g] = a.type[g];
+    d[g] = a.dsum[g * a.nkeys + key];
+    c[g] = a.cnt[g * a.nkeys + key];
+  }
+  int32_t cur_call = -1;
+  uint32_t t_first = 0, t_prev = 0;
+  struct Chunk {
+    uint32_t ref;
+    int32_t call;
+    uint64_t xb[NA];
+    uint8_t xn[NA];
+  };
+  auto load = [&](int64_t base, Chunk& ch) {
+    const int64_t q = base + lane;
+    ch.ref = q < q1 ? oref_sorted[q] : 0u;
+    const uint32_t t = ch.ref & ~kAddBit;
+#pragma unroll
+    for (int g = 0; g < NA; g++) {
+      ch.xb[g] = q < q1 ? iargv[g * a.cap + t] : 0ull;
+      ch.xn[g] = q < q1 ? iargn[g * a.cap + t] : (uint8_t)0;
+    }
+    ch.call = (q < q1 && (ch.ref & kAddBit)) ? call_of[ievrow[t]] : -1;
+  };
+  constexpr int NCH = 4;   // chunks in flight
+  Chunk ring[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; i++) load(q0 + (int64_t)i * 64, ring[i]);
+  for (int64_t base = q0; base < q1; base += 64 * NCH) {
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+      const int64_t cb = base + (int64_t)i * 64;
+      if (cb >= q1) break;
+      const Chunk ch = ring[i];
+      load(cb + 64 * NCH, ring[i]);   // refill this slot NCH chunks ahead
+      const int nk = q1 - cb < 64 ? (int)(q1 - cb) : 64;
+      const bool valid = lane < nk;
+      const bool add = valid && (ch.ref & kAddBit);
+      const uint32_t t = ch.ref & ~kAddBit;
+      double x[NA], dk[NA];
+      uint64_t skip[NA];
+      int64_t ck[NA];
+      bool xn[NA];
+#pragma unroll
+      for (int g = 0; g < NA; g++) {
+        xn[g] = kind[g] != SHD_AGG_COUNT && ch.xn[g];
+        const int dc = !valid || xn[g] ? 0 : (add ? 1 : -1);
+        const int inc = wave_incl_scan_i32(dc, lane);
+        ck[g] = c[g] + inc;
+        c[g] += __builtin_amdgcn_readlane(inc, 63);
+        double v;
+        switch (type[g]) {   // Number.doubleValue() of the operand
+          case SHD_T_INT: v = (double)v_i32(ch.xb[g]); break;
+          case SHD_T_LONG: v = (double)(int64_t)ch.xb[g]; break;
+          case SHD_T_FLOAT: v = (double)v_f32(ch.xb[g]); break;
+          default: v = v_f64(ch.xb[g]);
+        }
+        x[g] = add ? v : -v;
+        skip[g] = __ballot(!valid || xn[g] || kind[g] == SHD_AGG_COUNT);
+        dk[g] = d[g];
+      }
+      // the sequential double chains, in operation order (independent across aggregators)
+      for (int k = 0; k < nk; k++) {
+#pragma unroll
+        for (int g = 0; g < NA; g++) {
+          const double xk = readlane_f64(x[g], k);
+          if (!((skip[g] >> k) & 1ull)) d[g] = __dadd_rn(d[g], xk);
+          dk[g] = lane == k ? d[g] : dk[g];
+        }
+      }
+      // callback runs: consecutive add operations of one InputHandler call
+      const uint64_t A = __ballot(add);
+      const uint64_t Ab = A & below;
+      const bool has_prev = Ab != 0;
+      const int pl = has_prev ? 63 - __clzll(Ab) : lane;   // previous add lane
+      const int32_t call_p = __shfl(ch.call, pl, 64);
+      const uint32_t t_p = __shfl(t, pl, 64);
+      const bool fst = add && ch.call != (has_prev ? call_p : cur_call);
+      const uint64_t F = __ballot(fst);
+      const uint64_t Fp = has_prev ? (F & (pl == 63 ? ~0ull : ((2ull << pl) - 1ull))) : 0ull;
+      const int sl = Fp ? 63 - __clzll(Fp) : lane;          // run start at or before pl
+      const uint32_t t_s = __shfl(t, sl, 64);
+      if (fst) {
+        if (has_prev) last_of[Fp ? t_s : t_first] = t_p;    // the run that ended at pl
+        else if (cur_call >= 0) last_of[t_first] = t_prev;  // the run carried from earlier chunks
+      }
+      if (add) {
+#pragma unroll
+        for (int g = 0; g < NA; g++) {
+          uint64_t ob;
+          uint8_t on;
+          if (kind[g] == SHD_AGG_COUNT) {
+            ob = (uint64_t)ck[g];
+            on = 0;
+          } else {
+            ob = p_f64(dk[g]);
+            on = kind[g] == SHD_AGG_SUM ? (uint8_t)(xn[g] && !(type[g] == SHD_T_DOUBLE && ck[g] != 0))
+                                        : (uint8_t)(ck[g] == 0);   // avg: value / count at emission
+            if (on) ob = 0;
+          }
+          resv[g * a.cap + t] = ob;
+          resn[g * a.cap + t] = on;
+          if (kind[g] == SHD_AGG_AVG) resc[g * a.cap + t] = ck[g];
+        }
+        if (fst) first[t] = 1;
+      }
+      if (A) {
+        const int ll = 63 - __clzll(A);
+        cur_call = __builtin_amdgcn_readlane(ch.call, ll);
+        t_prev = (uint32_t)__builtin_amdgcn_readlane((int)t, ll);
+        if (F) t_first = (uint32_t)__builtin_amdgcn_readlane((int)t, 63 - __clzll(F));
+      }
+    }
+  }
+  if (cur_call >= 0 && lane == 0) last_of[t_first] = t_prev;
+  if (lane == 0) {
+#pragma unroll
+    for (int g = 0; g < NA; g++) {
+      a.dsum[g * a.nkeys + key] = d[g];
+      a.cnt[g * a.nkeys + key] = c[g];
+    }
+  }
+}
+
 __global__ void k_first_counts(const uint8_t* first, int64_t C, int64_t total, uint32_t* cnt) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total - C; t += (int64_t)gridDim.x * blockDim.x)
     cnt[t] = first[C + t] ? 1u : 0u;
@@ -480,6 +785,7 @@ struct EmitArgs {
   DExpr outs[kMaxCols];
   int nout;
   int nagg;
+  int kind[kMaxAggs];
   int64_t cap;
   int64_t C;
   int64_t row0;
@@ -488,8 +794,9 @@ struct EmitArgs {
 
 __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
-                                                 const uint64_t* resv, const uint8_t* resn, int64_t* o_chunk,
-                                                 int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+                                                 const uint64_t* resv, const uint8_t* resn, const int64_t* resc,
+                                                 int64_t* o_chunk, int32_t* o_type, int64_t* o_ts, uint64_t* o_vals,
+                                                 uint8_t* o_nul) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -504,6 +811,8 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
     for (int g = 0; g < a.nagg; g++) {
       av[g] = resv[g * a.cap + tl];
       an[g] = resn[g * a.cap + tl];
+      // avg = value / count (AvgAttributeAggregatorExecutor: value / count as double)
+      if (a.kind[g] == SHD_AGG_AVG && !an[g]) av[g] = p_f64(__ddiv_rn(v_f64(av[g]), (double)resc[g * a.cap + tl]));
     }
     RowCtx cx{&cs, ev, av, an};
     int64_t row = a.row0 + foff[t0];
@@ -545,7 +854,7 @@ struct SingleEngine : Engine {
   int cur = 0;
   DevBuf ikey[2], its[2], iargv[2], iargn[2];
   int64_t icap[2] = {0, 0};
-  DevBuf ievrow, inow, e_exp, okey, oref, okey32, okey32_alt, oref_alt, heads, hoff, hlist, resv, resn, first,
+  DevBuf ievrow, inow, e_exp, okey, oref, okey32, okey32_alt, oref_alt, heads, hoff, hlist, resv, resc, resn, first,
       last_of, fcnt, foff;
   // group state (dense by key)
   DevBuf g_dsum, g_lsum, g_cnt;
@@ -926,6 +1235,7 @@ struct SingleEngine : Engine {
                          (const uint32_t*)hoff.as<uint32_t>(), nops, hlist.as<uint32_t>());
       SHD_CHECK_LAUNCH();
       resv.reserve(std::max(nagg, 1) * cap * 8);
+      resc.reserve(std::max(nagg, 1) * cap * 8);
       resn.reserve(std::max(nagg, 1) * cap);
       first.reserve(cap);
       last_of.reserve(cap * 4);
@@ -941,11 +1251,44 @@ struct SingleEngine : Engine {
       fo.lsum = g_lsum.as<int64_t>();
       fo.cnt = g_cnt.as<int64_t>();
       fo.nkeys = g_nkeys;
-      hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, dev_args(fo), (const uint32_t*)hlist.as<uint32_t>(),
-                         nheads, nops, sk, sr, (const uint64_t*)iargv[cur].as<uint64_t>(),
-                         (const uint8_t*)iargn[cur].as<uint8_t>(), (const int32_t*)ievrow.as<int32_t>(),
-                         (const int32_t*)d_call_of.as<int32_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(),
-                         first.as<uint8_t>(), last_of.as<uint32_t>());
+      const FoldArgs* d_fo = dev_args(fo);
+      // long group segments: one wave per group (coalesced operand loads,
+      // wave-uniform fold); short ones: one lane per group
+      const bool wave = nops >= 256 * nheads && !getenv("SHD_FOLD_LANE");
+#define SHD_FOLD_ARGS                                                                                           \
+  d_fo, (const uint32_t*)hlist.as<uint32_t>(), nheads, nops, sk, sr, (const uint64_t*)iargv[cur].as<uint64_t>(), \
+      (const uint8_t*)iargn[cur].as<uint8_t>(), (const int32_t*)ievrow.as<int32_t>(),                            \
+      (const int32_t*)d_call_of.as<int32_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(), resc.as<int64_t>(),     \
+      first.as<uint8_t>(), last_of.as<uint32_t>()
+      // aggregators with a double running sum + count only: the branch-light fold
+      bool dfam = nagg >= 1 && nagg <= 4 && !getenv("SHD_FOLD_GENERIC");
+      for (int g = 0; g < nagg; g++) {
+        const int k = plan.aggs[g].kind, t = plan.aggs[g].type;
+        dfam = dfam && (k == SHD_AGG_COUNT || k == SHD_AGG_AVG ||
+                        (k == SHD_AGG_SUM && (t == SHD_T_DOUBLE || t == SHD_T_FLOAT)));
+      }
+      if (wave && dfam) {
+        const dim3 gw((unsigned)ceil_div(nheads * 64, kBlock));
+        switch (nagg) {
+          case 1: hipLaunchKernelGGL(k_fold_wave_d<1>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          case 2: hipLaunchKernelGGL(k_fold_wave_d<2>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          case 3: hipLaunchKernelGGL(k_fold_wave_d<3>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          default: hipLaunchKernelGGL(k_fold_wave_d<4>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+        }
+      } else if (wave) {
+        const dim3 gw((unsigned)ceil_div(nheads * 64, kBlock));
+        switch (nagg) {
+          case 1: hipLaunchKernelGGL(k_fold_wave<1>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          case 2: hipLaunchKernelGGL(k_fold_wave<2>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          case 3: hipLaunchKernelGGL(k_fold_wave<3>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          case 4: hipLaunchKernelGGL(k_fold_wave<4>, gw, dim3(kBlock), 0, s, SHD_FOLD_ARGS); break;
+          default:
+            hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, SHD_FOLD_ARGS);
+        }
+      } else {
+        hipLaunchKernelGGL(k_fold, dim3(grid_for(nheads)), dim3(kBlock), 0, s, SHD_FOLD_ARGS);
+      }
+#undef SHD_FOLD_ARGS
       SHD_CHECK_LAUNCH();
       mark("group_fold");
       // emission: first-seen (call, group) rows in event order
@@ -968,6 +1311,7 @@ struct SingleEngine : Engine {
           ea.nout = (int)outs.size();
           for (size_t c = 0; c < outs.size(); c++) ea.outs[c] = dexpr(outs[c]);
           ea.nagg = nagg;
+          for (int g = 0; g < nagg; g++) ea.kind[g] = plan.aggs[g].kind;
           ea.cap = cap;
           ea.C = C;
           ea.row0 = out.count;
@@ -975,7 +1319,8 @@ struct SingleEngine : Engine {
           hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
                              (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
                              (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
-                             (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(), out.d_chunk(),
+                             (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(),
+                             (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
                              out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
           SHD_CHECK_LAUNCH();
           out.count += nrows;

@@ -53,6 +53,28 @@ S4_PART_APPS = {k: "@app:playback " + STOCK_DEF + " partition with (symbol of St
                 for k, q in (("seq", S4_SEQ_QUERY), ("seqplus", S4_SEQPLUS_QUERY), ("or", S4_OR_QUERY), ("and", S4_AND_QUERY),
                              ("not", S4_NOT_QUERY))}
 
+# config M5: 100 queries on one StockStream junction -- 50
+# variants of P1 (e1 threshold 60..84.5, step 0.5) and 50 of W2-length
+# (length 100..5000, step 100)
+M5_PATTERN_THRESHOLDS = [60.0 + 0.5 * i for i in range(50)]
+M5_WINDOW_LENGTHS = [100 * (i + 1) for i in range(50)]
+
+
+def m5_app(n_pattern: int = 50, n_window: int = 50) -> str:
+    qs = []
+    for i, th in enumerate(M5_PATTERN_THRESHOLDS[:n_pattern]):
+        qs.append("@info(name='p%02d') from every e1=StockStream[price>%s] -> "
+                  "e2=StockStream[symbol==e1.symbol and price>e1.price*1.05] within 1 sec "
+                  "select e1.symbol as symbol, e1.price as p1, e2.price as p2 insert into AlertP%02d;" % (i, repr(th), i))
+    for i, ln in enumerate(M5_WINDOW_LENGTHS[:n_window]):
+        qs.append("@info(name='w%02d') from StockStream[price>60]#window.length(%d) "
+                  "select symbol, avg(price) as a, sum(price) as s, count() as c group by symbol "
+                  "insert into OutW%02d;" % (i, ln, i))
+    return "@app:playback " + STOCK_DEF + " " + " ".join(qs)
+
+
+M5_APP = m5_app()
+
 CONFIGS = {
     # name: (app, n_events, n_keys, delta_ms)
     "P1": (P1_APP, 1_000_000, 1_000, 1.0),
@@ -66,6 +88,8 @@ CONFIGS = {
     "S4-not": (S4_APPS["not"], 1_000_000, 1_000, 1.0),
     "S4-seqplus": (S4_APPS["seqplus"], 1_000_000, 1_000, 1.0),
     "S4P-seqplus": (S4_PART_APPS["seqplus"], 10_000_000, 100_000, 0.01),
+    # 1B events in SURVEY.md §8d; the bench default is a bounded 100M-event pass
+    "M5": (M5_APP, 100_000_000, 1_000, 0.001),
 }
 
 

@@ -225,3 +225,49 @@ def test_implicit_grouping_edge_cases(hip_available, reverse):
         assert reverse and e.code == SHD_E_UNSUPPORTED
         return
     assert_same_rows(dev, ora)
+
+
+TYPED_WINDOW_APPS = [
+    ("length-sum-avg-count", "define stream S (k int, i int, l long, f float, d double); @info(name='q') "
+     "from S[d > -1.0]#window.length(300) select k, sum(i) as si, sum(l) as sl, avg(f) as af, count() as c "
+     "group by k insert into O;"),
+    ("time-sum-avg", "define stream S (k int, i int, l long, f float, d double); @info(name='q') "
+     "from S#window.time(40 milliseconds) select k, sum(d) as sd, avg(d) as ad, sum(f) as sf "
+     "group by k insert into O;"),
+    ("length-w2-shape", "define stream S (k int, i int, l long, f float, d double); @info(name='q') "
+     "from S[d > 20.0]#window.length(700) select k, avg(d) as a, sum(d) as s, count() as c, avg(i) as ai "
+     "group by k insert into O;"),
+]
+
+
+@pytest.mark.parametrize("fold", ["wave", "wave-generic", "lane"])
+@pytest.mark.parametrize("name,app", TYPED_WINDOW_APPS, ids=[a[0] for a in TYPED_WINDOW_APPS])
+def test_group_fold_long_segments(hip_available, monkeypatch, fold, name, app):
+    """Few groups, long operation segments per push: the one-wave-per-group
+    fold (coalesced operand loads, wave-uniform sequential state) and the
+    one-lane-per-group fold must both give the oracle's rows bit for bit,
+    typed aggregates and null arguments included."""
+    if fold == "lane":
+        monkeypatch.setenv("SHD_FOLD_LANE", "1")
+    if fold == "wave-generic":
+        monkeypatch.setenv("SHD_FOLD_GENERIC", "1")
+    qp, _ = compile_single_query("@app:playback " + app)
+    rng = np.random.default_rng(31)
+    batches = []
+    t = 10_000
+    for r in range(4):
+        m = 30_000
+        k = rng.integers(0, 6, m).astype(np.int32)
+        i = rng.integers(-1000, 1000, m).astype(np.int32)
+        lv = rng.integers(-10 ** 12, 10 ** 12, m).astype(np.int64)
+        f = rng.uniform(-50, 50, m).astype(np.float32)
+        d = rng.uniform(0, 100, m)
+        nulls = [None, (rng.random(m) < 0.03).astype(np.uint8), None, (rng.random(m) < 0.03).astype(np.uint8),
+                 (rng.random(m) < 0.03).astype(np.uint8)]
+        ts = t + np.sort(rng.integers(0, 3000, m)).astype(np.int64)
+        t = int(ts[-1])
+        batches.append((0, ColumnBatch(ts, [k, i, lv, f, d], nulls, np.arange(0, m + 1, 500, dtype=np.int64))))
+    ora = run_oracle(qp, batches)
+    dev, _, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
