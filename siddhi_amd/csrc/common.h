@@ -196,12 +196,13 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& result_in_alt);
 // Device-wide max of u64 keys (result to dev ptr).
 // Same, carrying a second 32-bit payload word per key.
+// kbase: digits of (key - kbase) (keys of the sort span [kbase, kbase + 2^bits)).
 // hashed: digits are taken from key_bucket_mix(key) instead of the key, so
 // bits < 32 groups equal keys into 2^bits buckets (stable: input order inside
 // a bucket) while the array still carries the raw keys.
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
-                            bool hashed = false);
+                            bool hashed = false, uint32_t kbase = 0);
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
 void reduce_max_u64(const uint64_t* in, int64_t n, uint64_t* out_dev, hipStream_t s);

@@ -143,6 +143,7 @@ struct PrepAgg {
   unsigned long long ovf;   // some row's ts - batch.ts[0] does not fit in int32
   unsigned long long unmono;   // some batch row's ts is below its predecessor's
   long long carry_tmax;        // latest carried partial (LLONG_MIN: none)
+  unsigned long long kmin;     // smallest key (rows with a key)
 };
 
 struct PrepArgs {
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
   const ExtRows& x = a.x;
-  unsigned long long created = 0, kmax = 0, ovf = 0, unmono = 0;
+  unsigned long long created = 0, kmax = 0, ovf = 0, unmono = 0, kmin = ULLONG_MAX;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctmax = LLONG_MIN;
   // timestamps travel with the key sort as 32-bit offsets from the batch's
   // first event (ovf: the push falls back to a 64-bit gather after the sort)
@@ -237,7 +238,10 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
       if (a.key64) k64[r] = k;
       else k32[r] = (uint32_t)k;
-      kmax = k > kmax ? k : kmax;
+      if (!(f & F_SKIP)) {
+        kmax = k > kmax ? k : kmax;
+        kmin = k < kmin ? k : kmin;
+      }
     }
     pv[r] = (f << kRowBits) | (uint32_t)r;
     const int64_t dt = (int64_t)t - tbase;
@@ -252,11 +256,12 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
     unmono |= __shfl_xor(unmono, o, 64);
   }
   kmax = wave_max(kmax);
+  kmin = wave_min(kmin);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
   ctmax = wave_max(ctmax);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf, unmono, ctmax};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf, unmono, ctmax, kmin};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
@@ -264,6 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       r.ovf |= wpart[w].ovf;
       r.unmono |= wpart[w].unmono;
       r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
+      r.kmin = wpart[w].kmin < r.kmin ? wpart[w].kmin : r.kmin;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -274,12 +280,13 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
 }
 
 __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
-  unsigned long long c = 0, km = 0, ov = 0, um = 0;
+  unsigned long long c = 0, km = 0, ov = 0, um = 0, kn = ULLONG_MAX;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctm = LLONG_MIN;
 #pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
     ov |= blk[b].ovf;
     um |= blk[b].unmono;
+    kn = blk[b].kmin < kn ? blk[b].kmin : kn;
     ctm = blk[b].carry_tmax > ctm ? blk[b].carry_tmax : ctm;
     c += blk[b].n_cand;
     km = blk[b].kmax > km ? blk[b].kmax : km;
@@ -292,11 +299,12 @@ __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int 
     um |= __shfl_xor(um, o, 64);
   }
   km = wave_max(km);
+  kn = wave_min(kn);
   tmin = wave_min(tmin);
   tmax = wave_max(tmax);
   ctm = wave_max(ctm);
   __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax, ov, um, ctm};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{c, km, tmin, tmax, ov, um, ctm, kn};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
@@ -304,6 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int 
       r.ovf |= wpart[w].ovf;
       r.unmono |= wpart[w].unmono;
       r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
+      r.kmin = wpart[w].kmin < r.kmin ? wpart[w].kmin : r.kmin;
       r.n_cand += wpart[w].n_cand;
       r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
@@ -414,7 +423,8 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       pq = wp[i];
       tq = wt[i];
       kq = wk[i];
-      if (!f2_now && a.partitioned && kq != k) {
+      // rows of dropped (null-key) events carry no usable key: passed over
+    if (!f2_now && a.partitioned && kq != k && !(pv_flags(pq) & F_SKIP)) {
         stop = true;
         if (!a.hash_mask) break;   // end of the key's run
         if ((key_bucket_mix((uint32_t)kq) ^ key_bucket_mix((uint32_t)k)) & a.hash_mask) break;   // end of the bucket
@@ -1055,7 +1065,7 @@ struct PatternEngine : Engine {
       pa.key_col = -1;
     }
     pa.carry_key = carry[cur].key.as<uint64_t>();
-    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN};
+    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN, ULLONG_MAX};
     PrepAgg* d_pa = d_agg.as<PrepAgg>();
     ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
     std::memcpy(h_agg.p, &init, sizeof(init));
@@ -1105,9 +1115,21 @@ struct PatternEngine : Engine {
     uint32_t hash_mask = 0;
     counters.group_bits = 0;
     if (grouped) {
+      // keys of this push span [kmin, kmax]: sort the offsets from kmin (a
+      // rank owning one key slice sorts as many bits as rank 0)
+      const uint64_t kmin = pg.kmin <= pg.kmax ? pg.kmin : 0;
       uint64_t kmax = pg.kmax;
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
+      uint32_t kbase = 0;
+      if (bits <= 32 && !type_key64(key_type[slot])) {
+        int rb = 0;
+        while (rb < 64 && ((kmax - kmin) >> rb)) rb++;
+        if (rb < bits) {
+          bits = rb > 0 ? rb : 1;
+          kbase = (uint32_t)kmin;
+        }
+      }
       if (bits <= 32) {
         const int hb = hashed_bucket_bits(pg, n_ext, bits, prune);
         if (hb > 0) {
@@ -1127,7 +1149,7 @@ struct PatternEngine : Engine {
         d_k32_alt.reserve(n_ext * 4);
         radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
                                d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
-                               bits, d_sort, s, in_alt, hash_mask != 0);
+                               bits, d_sort, s, in_alt, hash_mask != 0, hash_mask ? 0u : kbase);
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);

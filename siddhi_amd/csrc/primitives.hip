@@ -154,16 +154,17 @@ __device__ __forceinline__ int rs_tile_of(int b, int nb) {
 
 template <class K>
 __device__ __forceinline__ uint32_t rs_digit(K k, int shift) { return (uint32_t)((k >> shift) & 255u); }
-// H: digits of key_bucket_mix(key) (hashed bucket sort; 32-bit keys only)
+// H: digits of key_bucket_mix(key) (hashed bucket sort; 32-bit keys only).
+// kb: key base subtracted first (the keys of a push span [kb, kb + 2^bits)).
 template <bool H, class K>
-__device__ __forceinline__ uint32_t rs_hdigit(K k, int shift) {
+__device__ __forceinline__ uint32_t rs_hdigit(K k, int shift, K kb) {
   if constexpr (H) return (key_bucket_mix((uint32_t)k) >> shift) & 255u;
-  else return rs_digit(k, shift);
+  else return rs_digit((K)(k - kb), shift);
 }
 
 template <class K, int R, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys, int64_t n, int shift,
-                                                      uint32_t* __restrict__ hist, int nb, int xcd) {
+                                                      uint32_t* __restrict__ hist, int nb, int xcd, K kb) {
   __shared__ uint32_t h[kRsWaves][256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
@@ -180,10 +181,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < R / 4; i++) {
-        atomicAdd(&h[w][rs_hdigit<H>(q[i].x, shift)], 1u);
-        atomicAdd(&h[w][rs_hdigit<H>(q[i].y, shift)], 1u);
-        atomicAdd(&h[w][rs_hdigit<H>(q[i].z, shift)], 1u);
-        atomicAdd(&h[w][rs_hdigit<H>(q[i].w, shift)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>((K)q[i].x, shift, kb)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>((K)q[i].y, shift, kb)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>((K)q[i].z, shift, kb)], 1u);
+        atomicAdd(&h[w][rs_hdigit<H>((K)q[i].w, shift, kb)], 1u);
       }
       done = true;
     }
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; r++)
-      if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_hdigit<H>(k[r], shift)], 1u);
+      if (wb + r * 64 + lane < n) atomicAdd(&h[w][rs_hdigit<H>(k[r], shift, kb)], 1u);
   }
   __syncthreads();
   if (tid < 256) {
@@ -258,7 +259,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
                                                          uint32_t* __restrict__ vout, uint32_t* __restrict__ wout,
                                                          int64_t n, int shift, const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ offs,
-                                                         const uint32_t* __restrict__ dtotal, int nb, int xcd) {
+                                                         const uint32_t* __restrict__ dtotal, int nb, int xcd,
+                                                         K kb) {
   constexpr int T = rs_tile(R);
   __shared__ K sk[T];
   __shared__ uint32_t sv[T];
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool ok = wb + r * 64 + lane < n;
-    const uint32_t d = rs_hdigit<H>(k[r], shift);
+    const uint32_t d = rs_hdigit<H>(k[r], shift, kb);
     uint64_t peers = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (wb + r * 64 + lane < n) {
-      const uint32_t pos = wcnt[w][rs_hdigit<H>(k[r], shift)] + lr[r];
+      const uint32_t pos = wcnt[w][rs_hdigit<H>(k[r], shift, kb)] + lr[r];
       sk[pos] = k[r];
       sv[pos] = v[r];
       if (P2) sw[pos] = x[r];
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 #pragma unroll 4
   for (int i = tid; i < tile_n; i += kRsBlock) {
     const K kk = sk[i];
-    const uint32_t d = rs_hdigit<H>(kk, shift);
+    const uint32_t d = rs_hdigit<H>(kk, shift, kb);
 #if defined(SHD_RS_EXP) && SHD_RS_EXP == 1   // timing experiment: coalesced identity write-out
     const uint32_t o = (uint32_t)(t0 + i) + 0 * (gbase[d] - lpre[d]);
 #elif defined(SHD_RS_EXP) && SHD_RS_EXP == 2   // timing experiment: no write-out
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 
 template <class K, int R, bool P2, bool H = false>
 static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, uint32_t* vals_alt, uint32_t* w_alt,
-                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt) {
+                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt, K kb = 0) {
   in_alt = false;
   if (n <= 1 || bits <= 0) return;
   // k_rs_hist reads full tiles of 32-bit keys with 16-byte loads
@@ -397,13 +399,13 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
   K* ki = keys; uint32_t* vi = vals; uint32_t* wi = w;
   K* ko = keys_alt; uint32_t* vo = vals_alt; uint32_t* wo = w_alt;
   for (int shift = 0; shift < bits; shift += 8) {
-    hipLaunchKernelGGL((k_rs_hist<K, R, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd);
+    hipLaunchKernelGGL((k_rs_hist<K, R, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd, kb);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_rs_digit_scan, dim3(256), dim3(kRsBlock), 0, s, (const uint32_t*)hist, nb, offs, dtot);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_rs_scatter<K, R, P2, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, (const uint32_t*)vi,
                        (const uint32_t*)wi, ko, vo, wo, n, shift, (const uint32_t*)hist, (const uint32_t*)offs,
-                       (const uint32_t*)dtot, nb, xcd);
+                       (const uint32_t*)dtot, nb, xcd, kb);
     SHD_CHECK_LAUNCH();
     std::swap(ki, ko);
     std::swap(vi, vo);
@@ -426,12 +428,13 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
 
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
-                            bool hashed) {
+                            bool hashed, uint32_t kbase) {
   if (hashed)
     radix_sort_run<uint32_t, kRsRounds, true, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s,
                                                     in_alt);
   else
-    radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt);
+    radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt,
+                                              kbase);
 }
 
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,

@@ -271,3 +271,30 @@ def test_group_fold_long_segments(hip_available, monkeypatch, fold, name, app):
     dev, _, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_partition_keys_far_from_zero(hip_available, parts):
+    """Keys of a push span [kmin, kmax] far from 0 (one rank's key slice):
+    the sort covers only the bits of kmax - kmin; rows of null-key events
+    (dropped by PartitionStreamReceiver) sit anywhere in the sorted order and
+    are passed over by the walks."""
+    app = ("define stream S (k int, p double); partition with (k of S) begin "
+           "@info(name='q') from every e1=S[p>40] -> e2=S[p>e1.p*1.02] within 30 milliseconds "
+           "select e1.k as k, e1.p as p1, e2.p as p2 insert into O; end;")
+    qp, _ = compile_single_query(app)
+    rng = np.random.default_rng(12)
+    n = 120_000
+    k = (70_000_000 + rng.integers(0, 20_000, n)).astype(np.int32)
+    kn = (rng.random(n) < 0.05).astype(np.uint8)
+    k[kn.astype(bool)] = 0
+    p = rng.uniform(0, 100, n)
+    ts = 5_000 + np.arange(n, dtype=np.int64) // 20
+    cuts = [int(n * j / parts) for j in range(parts + 1)]
+    batches = [(0, ColumnBatch(ts[a:b], [k[a:b], p[a:b]], [kn[a:b], None], np.arange(a, b + 1, 1000) - a))
+               for a, b in zip(cuts[:-1], cuts[1:])]
+    ora = run_oracle(qp, batches)
+    dev, counters, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+    assert counters["group_bits"] <= 15
