@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=50_000_000, help="micro-batch size (events)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
+    ap.add_argument("--key-base", type=int, default=-1,
+                    help="first key id of this rank's slice (default rank * keys; diagnostics)")
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
     ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
                     help="roundrobin: every rank holds a round-robin share of the global stream and events are "
@@ -300,7 +302,8 @@ def main():
     # inputs resident in HBM before the timed region
     if mode == "prepartitioned":
         # rank r owns key slice r and its own events (no data-path collective)
-        sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=rank * keys, dev=dev)
+        kb = args.key_base if args.key_base >= 0 else rank * keys
+        sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=kb, dev=dev)
         seqs = None
     else:
         # one global stream over world*keys keys, held round-robin; re-routed per micro-batch

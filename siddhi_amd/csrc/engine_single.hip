@@ -282,6 +282,94 @@ __global__ __launch_bounds__(kBlock) void k_prefix_max_u32(uint32_t* e, int64_t 
   }
 }
 
+// Parallel form of k_prefix_max_u32 for large item counts: per-tile maxima,
+// one-block exclusive prefix max over the tiles, then per-tile inclusive
+// prefix max with the carry-in.  Tiles of kPmaxTile items (4 per thread).
+constexpr int kPmaxTile = kBlock * 4;
+
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t* wm) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int k = 0; k < kBlock / 64; k++) r = wm[k] > r ? wm[k] : r;
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pmax_tiles(const uint32_t* e, int64_t n, uint32_t* tmax) {
+  __shared__ uint32_t wm[kBlock / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kPmaxTile + threadIdx.x * 4;
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (b0 + i < n) v = e[b0 + i] > v ? e[b0 + i] : v;
+  const uint32_t r = block_max_u32(v, wm);
+  if (threadIdx.x == 0) tmax[blockIdx.x] = r;
+}
+
+// exclusive prefix max over the tile maxima (in place), one block
+__global__ __launch_bounds__(kBlock) void k_pmax_scan(uint32_t* tmax, int64_t nt) {
+  __shared__ uint32_t wm[kBlock / 64];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t base = 0; base < nt; base += kBlock) {
+    const int64_t i = base + threadIdx.x;
+    const uint32_t x = i < nt ? tmax[i] : 0;
+    uint32_t v = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(v, o, 64);
+      if (lane >= o) v = t > v ? t : v;
+    }
+    if (lane == 63) wm[w] = v;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (int k = 0; k < w; k++) pre = wm[k] > pre ? wm[k] : pre;
+    // exclusive: max of everything before i
+    uint32_t ex = __shfl_up(v, 1, 64);
+    ex = lane == 0 ? pre : (ex > pre ? ex : pre);
+    const uint32_t inc = v > pre ? v : pre;
+    __syncthreads();
+    if (i < nt) tmax[i] = ex;
+    if (threadIdx.x == kBlock - 1) carry = inc;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pmax_apply(uint32_t* e, int64_t n, const uint32_t* tpre) {
+  __shared__ uint32_t wm[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * kPmaxTile + threadIdx.x * 4;
+  uint32_t x[4];
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    x[i] = b0 + i < n ? e[b0 + i] : 0;
+    v = x[i] > v ? x[i] : v;
+  }
+  // exclusive prefix max of the per-thread maxima within the block
+  uint32_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = t > inc ? t : inc;
+  }
+  if (lane == 63) wm[w] = inc;
+  __syncthreads();
+  uint32_t pre = tpre[blockIdx.x];
+  for (int k = 0; k < w; k++) pre = wm[k] > pre ? wm[k] : pre;
+  uint32_t ex = __shfl_up(inc, 1, 64);
+  if (lane != 0) pre = ex > pre ? ex : pre;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pre = x[i] > pre ? x[i] : pre;
+    if (b0 + i < n) e[b0 + i] = pre;
+  }
+}
+
 __global__ void k_count_expired(const uint32_t* e, int64_t n, unsigned long long* cnt) {
   uint64_t c = 0;
   for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
@@ -847,7 +935,8 @@ struct SingleEngine : Engine {
   std::vector<int> types;
   int nagg = 0;
   // per-batch scratch
-  DevBuf d_offs, d_call_of, d_last_ts, d_now, d_flags, d_cnt, d_off, d_pkey, d_start, d_run, d_tot, d_scan, d_sort;
+  DevBuf d_offs, d_call_of, d_last_ts, d_now, d_flags, d_cnt, d_off, d_pkey, d_start, d_run, d_tot, d_scan, d_sort,
+      d_pmax;
   PinnedBuf h_tot;
   // window items: carry [0, C) + new; double-buffered
   int64_t C = 0;
@@ -1180,8 +1269,21 @@ struct SingleEngine : Engine {
                        (const int64_t*)its[cur].as<int64_t>(), (const int64_t*)inow.as<int64_t>(), e_exp.as<uint32_t>());
     SHD_CHECK_LAUNCH();
     if (wkind == SHD_W_TIME) {
-      hipLaunchKernelGGL(k_prefix_max_u32, dim3(1), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total);
-      SHD_CHECK_LAUNCH();
+      if (total <= (int64_t)kPmaxTile * 8) {
+        hipLaunchKernelGGL(k_prefix_max_u32, dim3(1), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total);
+        SHD_CHECK_LAUNCH();
+      } else {
+        const int64_t nt = ceil_div(total, kPmaxTile);
+        d_pmax.reserve(nt * 4);
+        hipLaunchKernelGGL(k_pmax_tiles, dim3((unsigned)nt), dim3(kBlock), 0, s, (const uint32_t*)e_exp.as<uint32_t>(),
+                           total, d_pmax.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_pmax_scan, dim3(1), dim3(kBlock), 0, s, d_pmax.as<uint32_t>(), nt);
+        SHD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_pmax_apply, dim3((unsigned)nt), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total,
+                           (const uint32_t*)d_pmax.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+      }
     }
     unsigned long long* d_x = (unsigned long long*)(d_tot.as<uint64_t>() + 1);
     uint64_t* d_kmax = d_tot.as<uint64_t>() + 2;
