@@ -175,6 +175,7 @@ struct Engine {
 };
 
 std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);
+std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why);
 

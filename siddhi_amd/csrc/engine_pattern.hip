@@ -66,12 +66,16 @@ struct ExtRows {
   __device__ __forceinline__ int64_t seq(int64_t r) const { return r < C ? carry_seq[r] : seq0 + (r - C); }
 };
 
-// Expression context over (e1 row, e2 row); stream-state chains hold one event.
+// Expression context over (e1 row, second-state row); stream-state chains
+// hold one event.  s2: the state id r2 fills (1 for e1 -> e2; for the logical
+// OR form the branch that matched -- the partner slot is always empty then).
 struct PairCtx {
   const ExtRows* x;
-  int64_t r1, r2;   // ext rows of state 0 / state 1 (-1 = empty slot)
+  int64_t r1, r2;   // ext rows of state 0 / state s2 (-1 = empty slot)
+  int s2 = 1;
+  bool matched = false;   // projection of a completed partial
   __device__ __forceinline__ int64_t slot(int st, int idx) const {
-    int64_t r = st == 0 ? r1 : (st == 1 ? r2 : -1);
+    int64_t r = st == 0 ? r1 : (st == s2 ? r2 : -1);
     if (r < 0) return -1;
     // StateEvent.getStreamEvent(int[]) on a one-event chain: index 0 / CURRENT hit it
     return (idx == 0 || idx == SHD_IDX_CURRENT) ? r : -1;
@@ -90,10 +94,10 @@ struct PairCtx {
     return col_load(x->batch, r - x->C, attr);
   }
   __device__ __forceinline__ bool evnull(int st, int idx) const { return slot(st, idx) < 0; }
-  __device__ __forceinline__ int64_t ts(int st, int idx) const {
-    int64_t r = slot(st, idx);
-    return r < 0 ? 0 : x->ts(r);
-  }
+  // eventTimestamp() reads the StateEvent's timestamp: e1's while the e2 filters
+  // run, the completing event's once matched (StreamPostStateProcessor.java:64-83
+  // sets it before the selector)
+  __device__ __forceinline__ int64_t ts(int, int) const { return x->ts(matched ? r2 : r1); }
   __device__ __forceinline__ Val agg(int) const {
     Val v;
     v.b = 0;
@@ -340,6 +344,11 @@ struct ScanArgs {
   ExtRows x;
   DExprSet es;
   DFilters f2;
+  // logical OR second state `(e2=B[f2] or e3=B[f3])`: f2 = the filters of the
+  // processor that sees an event first (state s_first), f3 = its partner's
+  DFilters f3;
+  int logical;
+  int s_first, s_second;
   int64_t within;
   int partitioned;
   int prune;            // drop partials that can no longer match (horizon guard on later pushes)
@@ -464,10 +473,19 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
         if (f2_now) {
           f2_now = false;
           const int64_t r2 = pv_row(pq);
-          PairCtx cx{&a.x, r, r2};
-          if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+          PairCtx cx{&a.x, r, r2, a.s_first};
+          bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+          int32_t br = 0;
+          if (!hit && a.logical) {
+            // LogicalPreStateProcessor (OR): the partner processor sees the
+            // same event next (LogicalPreStateProcessor.java:113-154)
+            cx.s2 = a.s_second;
+            hit = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
+            br = 1;
+          }
+          if (hit) {
             st = ST_MATCH;
-            j = (int32_t)r2;
+            j = (int32_t)r2 | (br << kRowBits);   // matched branch above the row bits
             stop = true;
             break;
           }
@@ -720,11 +738,13 @@ __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int 
 
 __global__ __launch_bounds__(kBlock) void k_emit_pairs(const uint8_t* pst, const uint32_t* boff,
                                                        const int32_t* match_row, const uint32_t* spv, int64_t n,
-                                                       int64_t tile, uint32_t* pj, uint32_t* pi) {
+                                                       int64_t tile, int logical, uint32_t* pj, uint32_t* pi) {
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n ? t0 + tile : n;
   tile_compact(pst, t0, t1, PS_MATCH, boff[blockIdx.x], [&](int64_t p, uint32_t o) {
-    pj[o] = (uint32_t)match_row[p];
+    const uint32_t mr = (uint32_t)match_row[p];
+    // logical: sort key (e2 event, processor order) = row * 2 + branch
+    pj[o] = logical ? ((mr & kRowMask) << 1) | (mr >> kRowBits) : mr;
     pi[o] = pv_row(spv[p]);
   });
 }
@@ -735,6 +755,8 @@ struct ProjArgs {
   DExpr outs[kMaxCols];
   int nout;
   int multi;            // chunk per e2 event (same stream) vs per match
+  int logical;          // pj = row * 2 + branch; chunk per (event, processor)
+  int s_first, s_second;
   int64_t chunk0;
   int64_t row0;         // output buffer offset
 };
@@ -748,7 +770,12 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
   const ExtRows& x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < m; k = m) {
     int64_t j = pj[k], i = pi[k];
-    PairCtx cx{&x, i, j};
+    int br = 0;
+    if (a.logical) {
+      br = (int)(j & 1);
+      j >>= 1;
+    }
+    PairCtx cx{&x, i, j, br ? a.s_second : a.s_first, true};
     int64_t row = a.row0 + k;
     for (int c = 0; c < a.nout; c++) {
       Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
@@ -757,7 +784,8 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
     }
     o_ts[row] = x.ts(j);
     o_type[row] = 0;
-    o_chunk[row] = a.multi ? x.seq(j) : a.chunk0 + k;
+    // MultiProcessStreamReceiver: one callback chunk per (event, processor)
+    o_chunk[row] = a.logical ? 2 * x.seq(j) + br : (a.multi ? x.seq(j) : a.chunk0 + k);
   }
 }
 
@@ -908,6 +936,11 @@ bool find_key_equality(const Plan& p, const std::vector<int>& filters, int& attr
 struct PatternEngine : Engine {
   int sA = 0, sB = 0;
   std::vector<int> f1, f2;
+  // `every e1 -> (e2 or e3)`: f3 = the partner's filters, s_first / s_second =
+  // state ids in the order the two processors see an event
+  bool logical = false;
+  std::vector<int> f3;
+  int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
   bool partitioned = false;
   // unpartitioned plan whose f2 holds `e2.x == e1.y`: keys written by prepare,
@@ -1178,6 +1211,10 @@ struct PatternEngine : Engine {
     sa.x = x;
     sa.es = dset();
     sa.f2 = dfilters(f2);
+    sa.logical = logical;
+    sa.s_first = s_first;
+    sa.s_second = s_second;
+    if (logical) sa.f3 = dfilters(f3);
     sa.within = W;
     sa.partitioned = grouped;
     sa.prune = prune;
@@ -1185,7 +1222,7 @@ struct PatternEngine : Engine {
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     const ScanArgs* d_sa = dev_args(sa);
-    const bool fast2 = sa.f2.fp.ok != 0;
+    const bool fast2 = sa.f2.fp.ok != 0 && (!logical || sa.f3.fp.ok != 0);
     // contiguous tiles of positions per block (compaction offsets per block)
     const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
     const int ntile = (int)ceil_div(n_ext, tile);
@@ -1256,10 +1293,11 @@ struct PatternEngine : Engine {
       d_pi_alt.reserve((int64_t)m * 4);
       hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
                          (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
-                         tile, d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
+                         tile, (int)logical, d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
       SHD_CHECK_LAUNCH();
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
+      if (logical) bits++;   // + processor order
       bool in_alt = false;
       // pairs come out in (key, creation) order; the stable sort by j leaves the
       // partials of one e2 event in creation order (pending-list order)
@@ -1274,13 +1312,16 @@ struct PatternEngine : Engine {
       pr.nout = (int)outs.size();
       for (size_t c = 0; c < outs.size(); c++) pr.outs[c] = dexpr(outs[c]);
       pr.multi = (sA == sB);
+      pr.logical = logical;
+      pr.s_first = s_first;
+      pr.s_second = s_second;
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
       hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
                          out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
       SHD_CHECK_LAUNCH();
       out.count += m;
-      if (sA != sB) chunk_seq += m;
+      if (sA != sB && !logical) chunk_seq += m;
       mark("order_project");
     }
 
@@ -1329,6 +1370,9 @@ struct PatternEngine : Engine {
   }
 };
 
+std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, const PNode& b, const PNode* c,
+                                              std::string& why);
+
 std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
   // shape: NEXT(EVERY(STREAM a), STREAM b), pattern type, plain stream states
   if (p.kind != SHD_KIND_STATE || p.state_type != 0) { why = "not a pattern"; return nullptr; }
@@ -1343,9 +1387,45 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
   }
   const PNode& a = ev.kids[0];
   if (a.absent || b.absent || a.state_id != 0 || b.state_id != 1) { why = "absent / unexpected state ids"; return nullptr; }
+  return finish_pattern_engine(p, a, b, nullptr, why);
+}
+
+// `every e1=A[f1] -> (e2=B[f2] or e3=B[f3]) (within W)`: a partial completes at
+// the first B event that passes the filters of one of the two logical
+// processors, tried in the order MultiProcessStreamReceiver hands them an event
+// (reverse setup order: the first logical operand first,
+// StateInputStreamParser.java:349-361 + LogicalInnerStateRuntime.setup); the
+// partner slot stays empty (LogicalPreStateProcessor.java:113-154 drops the
+// partial from the partner's pending list).  AND keeps a half-filled partial
+// across events (and pushes), which this engine does not carry: generic engine.
+std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& why) {
+  if (p.kind != SHD_KIND_STATE || p.state_type != 0) { why = "not a pattern"; return nullptr; }
+  const PNode& r = p.root;
+  if (r.kind != SHD_NODE_NEXT || r.kids.size() != 2) { why = "not a two-state chain"; return nullptr; }
+  const PNode& ev = r.kids[0];
+  const PNode& lg = r.kids[1];
+  if (ev.kind != SHD_NODE_EVERY || ev.kids.size() != 1 || ev.kids[0].kind != SHD_NODE_STREAM ||
+      lg.kind != SHD_NODE_LOGICAL || lg.ltype != 1 || lg.kids.size() != 2) {
+    why = "not every e1 -> (e2 or e3)";
+    return nullptr;
+  }
+  const PNode& a = ev.kids[0];
+  const PNode& b = lg.kids[0];
+  const PNode& c = lg.kids[1];
+  if (b.kind != SHD_NODE_STREAM || c.kind != SHD_NODE_STREAM || a.absent || b.absent || c.absent ||
+      a.state_id != 0 || b.stream != c.stream) {
+    why = "logical operands: absent / different streams";
+    return nullptr;
+  }
+  return finish_pattern_engine(p, a, b, &c, why);
+}
+
+std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, const PNode& b, const PNode* c,
+                                              std::string& why) {
   if (!p.aggs.empty() || !p.group_by.empty() || p.having >= 0) { why = "aggregating selector"; return nullptr; }
   if (!p.current_on) { why = "pattern without current events output"; return nullptr; }
-  if (p.outputs.size() > (size_t)kMaxCols || a.filters.size() > 4 || b.filters.size() > 4) {
+  if (p.outputs.size() > (size_t)kMaxCols || a.filters.size() > 4 || b.filters.size() > 4 ||
+      (c && c->filters.size() > 4)) {
     why = "too many outputs / filters";
     return nullptr;
   }
@@ -1360,11 +1440,17 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
   e->sB = b.stream;
   e->f1 = a.filters;
   e->f2 = b.filters;
+  if (c) {
+    e->logical = true;
+    e->f3 = c->filters;
+    e->s_first = b.state_id;
+    e->s_second = c->state_id;
+  }
   e->W = p.within >= 0 ? p.within : INT64_MAX;
   e->typesA = p.stream_types[a.stream];
   for (auto& o : p.outputs) e->outs.push_back(o.second);
   e->partitioned = !p.part_keys.empty();
-  if (!e->partitioned && !getenv("SHD_NO_IMPLICIT_KEY")) {
+  if (!e->partitioned && !c && !getenv("SHD_NO_IMPLICIT_KEY")) {
     int aa, ab, t;
     // one stream playing both roles: an event has one key, so both sides must be the same attribute
     if (find_key_equality(p, b.filters, aa, ab, t) && (a.stream != b.stream || aa == ab)) {

@@ -518,6 +518,8 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
       // the 2-state every-pattern shape (P1/P3) has a dedicated forward-scan
       // engine; every other state plan runs on the generic per-key NFA
       e = make_pattern_engine(p, why1);
+      // SHD_NO_LOGICAL_SCAN: leave `every e1 -> (e2 or e3)` to the generic NFA engine (tests)
+      if (!e && !getenv("SHD_NO_LOGICAL_SCAN")) e = make_logical_pattern_engine(p, why1);
       if (!e) e = make_nfa_engine(p, why2);
       if (!e) why1 += "; ";
     } else {

@@ -14,7 +14,10 @@ from siddhi_amd import workloads as wl
 
 pytestmark = pytest.mark.gpu
 
-ENGINE_NFA = 4
+ENGINE_PATTERN, ENGINE_NFA = 1, 4
+# `every e1 -> (e2 or e3)` runs on the forward-scan pattern engine
+# (tests/test_gpu_logical.py); every other S4 shape on the generic NFA engine
+EXPECT_ENGINE = {"or": ENGINE_PATTERN, "Por": ENGINE_PATTERN}
 
 
 def split(sym, price, vol, ts, parts, call=1024):
@@ -36,7 +39,7 @@ def test_s4_unpartitioned_equals_oracle(hip_available, name, app, parts):
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
     dev, counters, kind = run_device(qp, batches)
-    assert kind == ENGINE_NFA
+    assert kind == EXPECT_ENGINE.get(name, ENGINE_NFA)
     assert_same_rows(dev, ora)
     assert counters["events"] == len(ts)
 
@@ -49,7 +52,7 @@ def test_s4_partitioned_equals_oracle(hip_available, name, app, parts):
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
     dev, counters, kind = run_device(qp, batches)
-    assert kind == ENGINE_NFA
+    assert kind == EXPECT_ENGINE.get(name, ENGINE_NFA)
     if name != "Pseq":
         assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
