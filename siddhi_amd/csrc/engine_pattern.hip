@@ -52,8 +52,12 @@ struct ExtRows {
   int64_t C;
   int64_t seq0;           // global seq of batch row 0
   const int64_t* carry_seq;
-  __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : batch; }
-  __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : r - C; }
+  // logical AND: rows [C + n, 2C + n) are the operand events the carried
+  // half-filled partials hold (stream B schema; row C + n + i for carry row i)
+  ColSet half;
+  const int64_t* half_seq;
+  __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : (r < C + batch.n ? batch : half); }
+  __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : (r < C + batch.n ? r - C : r - C - batch.n); }
   __device__ __forceinline__ int64_t ts(int64_t r) const {
 #ifdef SHD_DEBUG
     if (r < 0 || r >= C + batch.n) {
@@ -61,9 +65,13 @@ struct ExtRows {
       return 0;
     }
 #endif
-    return r < C ? gld(carry.ts, r) : gld(batch.ts, r - C);
+    if (r < C) return gld(carry.ts, r);
+    if (r < C + batch.n) return gld(batch.ts, r - C);
+    return gld(half.ts, r - C - batch.n);
   }
-  __device__ __forceinline__ int64_t seq(int64_t r) const { return r < C ? carry_seq[r] : seq0 + (r - C); }
+  __device__ __forceinline__ int64_t seq(int64_t r) const {
+    return r < C ? carry_seq[r] : (r < C + batch.n ? seq0 + (r - C) : half_seq[r - C - batch.n]);
+  }
 };
 
 // Expression context over (e1 row, second-state row); stream-state chains
@@ -74,8 +82,10 @@ struct PairCtx {
   int64_t r1, r2;   // ext rows of state 0 / state s2 (-1 = empty slot)
   int s2 = 1;
   bool matched = false;   // projection of a completed partial
+  int64_t r3 = -1;        // logical AND: the partner operand's row (state s3)
+  int s3 = -1;
   __device__ __forceinline__ int64_t slot(int st, int idx) const {
-    int64_t r = st == 0 ? r1 : (st == s2 ? r2 : -1);
+    int64_t r = st == 0 ? r1 : (st == s2 ? r2 : (st == s3 ? r3 : -1));
     if (r < 0) return -1;
     // StateEvent.getStreamEvent(int[]) on a one-event chain: index 0 / CURRENT hit it
     return (idx == 0 || idx == SHD_IDX_CURRENT) ? r : -1;
@@ -91,7 +101,8 @@ struct PairCtx {
     // branch on the row's table instead of selecting a per-lane ColSet
     // pointer: each branch reads a wave-uniform column table (scalar loads)
     if (r < x->C) return col_load(x->carry, r, attr);
-    return col_load(x->batch, r - x->C, attr);
+    if (r < x->C + x->batch.n) return col_load(x->batch, r - x->C, attr);
+    return col_load(x->half, r - x->C - x->batch.n, attr);
   }
   __device__ __forceinline__ bool evnull(int st, int idx) const { return slot(st, idx) < 0; }
   // eventTimestamp() reads the StateEvent's timestamp: e1's while the e2 filters
@@ -347,8 +358,9 @@ struct ScanArgs {
   // logical OR second state `(e2=B[f2] or e3=B[f3])`: f2 = the filters of the
   // processor that sees an event first (state s_first), f3 = its partner's
   DFilters f3;
-  int logical;
+  int logical;          // 0: e1 -> e2, 1: OR, 2: AND
   int s_first, s_second;
+  const uint8_t* carry_half;   // AND: operands already filled per carried partial (bit 0 first, bit 1 second)
   int64_t within;
   int partitioned;
   int prune;            // drop partials that can no longer match (horizon guard on later pushes)
@@ -403,7 +415,8 @@ template <bool DEFER, bool FAST, int WIN, class Ld>
 __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
                                                 int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
                                                 int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
-                                                uint64_t& steps, uint32_t& viol) {
+                                                uint64_t& steps, uint32_t& viol, uint32_t& fm, int64_t& ra,
+                                                int64_t& rb) {
   uint8_t st = ST_OPEN;
   bool stop = false, first = true;
   while (!stop && q < n_ext) {
@@ -473,6 +486,37 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
         if (f2_now) {
           f2_now = false;
           const int64_t r2 = pv_row(pq);
+          if (a.logical == 2) {
+            // LogicalPre/PostStateProcessor (AND): an operand that passes fills
+            // its slot and leaves its processor's pending list; the partial
+            // completes when the partner slot is filled too -- possibly by the
+            // partner processor on this same event (LogicalPostStateProcessor.java:59-86)
+            int32_t br = -1;
+            if (!(fm & 1u)) {
+              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second};
+              if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+                fm |= 1u;
+                ra = r2;
+                if (fm == 3u) br = 0;
+              }
+            }
+            if (br < 0 && !(fm & 2u)) {
+              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first};
+              if (FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx)) {
+                fm |= 2u;
+                rb = r2;
+                if (fm == 3u) br = 1;
+              }
+            }
+            if (br >= 0) {
+              st = ST_MATCH;
+              j = (int32_t)r2 | (br << kRowBits);
+              stop = true;
+              break;
+            }
+            q++;
+            continue;
+          }
           PairCtx cx{&a.x, r, r2, a.s_first};
           bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
           int32_t br = 0;
@@ -539,6 +583,29 @@ __device__ __forceinline__ void scan_block_reduce(uint64_t steps, uint64_t prune
   }
 }
 
+// AND: a partial's filled-operand state as the carry stores it, match_row =
+// filled operand row | fm << kRowBits (0 when no operand is filled).  A carried
+// half-filled partial holds its operand event at ext row C + n + (carry row).
+__device__ __forceinline__ void and_carried(const ScanArgs& a, int64_t r, uint32_t& fm, int64_t& ra, int64_t& rb) {
+  fm = 0;
+  ra = rb = -1;
+  if (r < a.x.C) {
+    fm = a.carry_half[r];
+    const int64_t hr = a.x.C + a.x.batch.n + r;
+    if (fm & 1u) ra = hr;
+    if (fm & 2u) rb = hr;
+  }
+}
+__device__ __forceinline__ int32_t and_code(uint32_t fm, int64_t ra, int64_t rb) {
+  return fm == 0 ? 0 : (int32_t)((fm & 1u ? ra : rb) | ((int64_t)fm << kRowBits));
+}
+__device__ __forceinline__ int32_t and_open_code(const ScanArgs& a, int64_t r) {
+  uint32_t fm;
+  int64_t ra, rb;
+  and_carried(a, r, fm, ra, rb);
+  return and_code(fm, ra, rb);
+}
+
 // One lane per position; candidates walk forward over the later events of
 // their key (sorted positions when partitioned, ext rows otherwise).  Keys,
 // flags and timestamps are read at sorted positions (timestamps travel with
@@ -579,14 +646,17 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
     if (pv_flags(pvp) & F_CAND) {
       int64_t q = p + 1;
       int32_t j = -1;
+      uint32_t fm = 0;
+      int64_t ra = -1, rb = -1;
       const uint8_t st = walk_partial<true, false, HASH ? 4 : 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq,
-                                                                 kq, tsi, false, j, steps, viol);
+                                                                 kq, tsi, false, j, steps, viol, fm, ra, rb);
       if (st == ST_DEFER) {
         out = PS_DEFER;
         match_row[p] = (int32_t)q;   // resume position (< 2^28)
       } else if (st == ST_OPEN) {
         out = PS_OPEN;
         no++;
+        if (a.logical == 2) match_row[p] = and_open_code(a, pv_row(pvp));   // carried half state unchanged
       } else if (st == ST_PRUNED) {
         pruned++;   // every later event is at or after t_end: it would expire this partial
       }
@@ -600,8 +670,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
 
 // Deferred walks: positions whose walk reached a B event inside `within`
 // evaluate f2 there (FAST: pre-decoded predicate, else the interpreter) and
-// continue.  Same tiles as k_forward_scan; 16 outcome bytes per thread.
-template <bool K64, bool FAST, bool TS64>
+// continue.  Same tiles as k_forward_scan.  DENSE: one position per lane per
+// round; else each thread scans 16 outcome bytes and resumes its hits in turn.
+template <bool K64, bool FAST, bool TS64, bool DENSE>
 __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                            int64_t tile, const uint32_t* __restrict__ skey32,
                                                            const uint64_t* __restrict__ skey64,
@@ -609,6 +680,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
                                                            const int32_t* __restrict__ sts32,
                                                            const int64_t* __restrict__ sts64,
                                                            int32_t* __restrict__ match_row,
+                                                           int32_t* __restrict__ match_other,
                                                            uint8_t* __restrict__ pst, uint32_t* __restrict__ bcnt,
                                                            ScanOut* __restrict__ blk) {
   const ScanArgs& a = *ap;
@@ -620,18 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
   const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
   const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
   const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
-  for (int64_t c0 = t0; c0 < t1; c0 += kBlock * 16) {
-    const int64_t pb = c0 + (int64_t)threadIdx.x * 16;
-    if (pb >= t1) continue;
-    const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
-    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
-    uint32_t hit = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-      if (((wv[i >> 2] >> ((i & 3) * 8)) & 255u) == PS_DEFER && pb + i < t1) hit |= 1u << i;
-    while (hit) {
-      const int64_t p = pb + __ffs(hit) - 1;
-      hit &= hit - 1;
+  auto resume_one = [&](int64_t p) {
       int64_t q = match_row[p];
       uint32_t pvp, pq;
       int64_t tsi, tq;
@@ -639,20 +700,49 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       ld(p, pvp, tsi, k);
       ld(q, pq, tq, kq);
       int32_t j = -1;
+      uint32_t fm = 0;
+      int64_t ra = -1, rb = -1;
+      if (a.logical == 2) and_carried(a, pv_row(pvp), fm, ra, rb);
       const uint8_t st = walk_partial<false, FAST, 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true,
-                                                      j, steps, viol);
+                                                      j, steps, viol, fm, ra, rb);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
         out = PS_MATCH;
         match_row[p] = j;
+        // AND: the partner operand's row (the completing processor is bit kRowBits)
+        if (a.logical == 2) match_other[p] = (int32_t)((j >> kRowBits) ? ra : rb);
         nm++;
       } else if (st == ST_OPEN) {
         out = PS_OPEN;
         no++;
+        if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
       } else if (st == ST_PRUNED) {
         pruned++;
       }
       pst[p] = out;
+  };
+  if constexpr (DENSE) {
+    // one position per lane per round: when most candidates defer (walks over
+    // every event of a busy key or of the whole stream) the walks of
+    // neighbouring positions run side by side, not one after another in a lane
+    for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock)
+      if (pst[p] == PS_DEFER) resume_one(p);
+  } else {
+    // few deferrals (sparse keys): 16 outcome bytes per thread per 16-byte load
+    for (int64_t c0 = t0; c0 < t1; c0 += kBlock * 16) {
+      const int64_t pb = c0 + (int64_t)threadIdx.x * 16;
+      if (pb >= t1) continue;
+      const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
+      const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+      uint32_t hit = 0;
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        if (((wv[i >> 2] >> ((i & 3) * 8)) & 255u) == PS_DEFER && pb + i < t1) hit |= 1u << i;
+      while (hit) {
+        const int64_t p = pb + __ffs(hit) - 1;
+        hit &= hit - 1;
+        resume_one(p);
+      }
     }
   }
   scan_block_reduce(steps, pruned, viol, nm, no, blk, gridDim.x + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
@@ -738,13 +828,21 @@ __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int 
 
 __global__ __launch_bounds__(kBlock) void k_emit_pairs(const uint8_t* pst, const uint32_t* boff,
                                                        const int32_t* match_row, const uint32_t* spv, int64_t n,
-                                                       int64_t tile, int logical, uint32_t* pj, uint32_t* pi) {
+                                                       int64_t tile, int logical, const int32_t* match_other,
+                                                       uint32_t* pj, uint32_t* pi, uint32_t* se1, int32_t* sot) {
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n ? t0 + tile : n;
   tile_compact(pst, t0, t1, PS_MATCH, boff[blockIdx.x], [&](int64_t p, uint32_t o) {
     const uint32_t mr = (uint32_t)match_row[p];
     // logical: sort key (e2 event, processor order) = row * 2 + branch
     pj[o] = logical ? ((mr & kRowMask) << 1) | (mr >> kRowBits) : mr;
+    if (logical == 2) {
+      // AND: the pair sort carries the match index; e1 / partner rows stay put
+      pi[o] = o;
+      se1[o] = pv_row(spv[p]);
+      sot[o] = match_other[p];
+      return;
+    }
     pi[o] = pv_row(spv[p]);
   });
 }
@@ -757,6 +855,8 @@ struct ProjArgs {
   int multi;            // chunk per e2 event (same stream) vs per match
   int logical;          // pj = row * 2 + branch; chunk per (event, processor)
   int s_first, s_second;
+  const uint32_t* se1;  // AND: pi = match index -> e1 row / partner operand row
+  const int32_t* sot;
   int64_t chunk0;
   int64_t row0;         // output buffer offset
 };
@@ -775,7 +875,12 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
       br = (int)(j & 1);
       j >>= 1;
     }
-    PairCtx cx{&x, i, j, br ? a.s_second : a.s_first, true};
+    int64_t other = -1;
+    if (a.logical == 2) {
+      other = a.sot[i];
+      i = a.se1[i];
+    }
+    PairCtx cx{&x, i, j, br ? a.s_second : a.s_first, true, other, br ? a.s_first : a.s_second};
     int64_t row = a.row0 + k;
     for (int c = 0; c < a.nout; c++) {
       Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
@@ -800,7 +905,25 @@ struct GatherArgs {
   int64_t* dts;
   uint64_t* dkey;
   int64_t* dseq;
+  // logical AND: filled-operand bits + the held operand event (stream B)
+  int and_mode;
+  const int32_t* match_row;
+  uint8_t* dhalf;
+  int ncolsB;
+  int32_t typesB[kMaxCols];
+  void* dcolB[kMaxCols];
+  uint8_t* dnulB[kMaxCols];
+  int64_t* dtsB;
+  int64_t* dseqB;
 };
+
+__device__ __forceinline__ void store_col(void* dst, int type, int64_t o, uint64_t b) {
+  switch (type) {
+    case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)dst)[o] = (uint32_t)b; break;
+    case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)dst)[o] = b; break;
+    case SHD_T_BOOL: ((uint8_t*)dst)[o] = (uint8_t)b; break;
+  }
+}
 
 // Still-open partials -> next push's carry rows (position order: per key in
 // creation order, which is all the stable key sort of the next push needs).
@@ -829,11 +952,52 @@ __global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __res
     a.dts[o] = x.ts(r);
     a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
     a.dseq[o] = x.seq(r);
+    if (a.and_mode) {
+      const uint32_t mr = (uint32_t)a.match_row[p];
+      const uint32_t fm = mr >> kRowBits;
+      a.dhalf[o] = (uint8_t)fm;
+      if (fm) {
+        const int64_t hr = mr & kRowMask;
+        const ColSet& hc = x.cs(hr);
+        const int64_t hrow = x.row(hr);
+        for (int c = 0; c < a.ncolsB; c++) {
+          const Val v = col_load(hc, hrow, c);
+          store_col(a.dcolB[c], a.typesB[c], o, v.b);
+          a.dnulB[c][o] = (uint8_t)v.null;
+        }
+        a.dtsB[o] = x.ts(hr);
+        a.dseqB[o] = x.seq(hr);
+      }
+    }
   });
 }
 
 struct CarryTable {
   DevBuf col[kMaxCols], nul[kMaxCols], ts, key, seq;
+  // logical AND: filled-operand bits and the held operand event (stream B)
+  DevBuf half, bcol[kMaxCols], bnul[kMaxCols], bts, bseq;
+  void reserve_b(int64_t n, const std::vector<int>& types) {
+    n = std::max<int64_t>(n, 1);
+    half.reserve(n);
+    for (size_t c = 0; c < types.size(); c++) {
+      bcol[c].reserve(n * type_size(types[c]));
+      bnul[c].reserve(n);
+    }
+    bts.reserve(n * 8);
+    bseq.reserve(n * 8);
+  }
+  ColSet colset_b(const std::vector<int>& types, int64_t n) const {
+    ColSet cs{};
+    cs.ncols = (int)types.size();
+    for (size_t c = 0; c < types.size(); c++) {
+      cs.col[c] = bcol[c].p;
+      cs.nul[c] = bnul[c].as<uint8_t>();
+      cs.type[c] = (int32_t)types[c];
+    }
+    cs.ts = bts.as<int64_t>();
+    cs.n = n;
+    return cs;
+  }
   void reserve(int64_t n, const std::vector<int>& types) {
     for (size_t c = 0; c < types.size(); c++) {
       col[c].reserve(std::max<int64_t>(n, 1) * type_size(types[c]));
@@ -936,10 +1100,12 @@ bool find_key_equality(const Plan& p, const std::vector<int>& filters, int& attr
 struct PatternEngine : Engine {
   int sA = 0, sB = 0;
   std::vector<int> f1, f2;
-  // `every e1 -> (e2 or e3)`: f3 = the partner's filters, s_first / s_second =
-  // state ids in the order the two processors see an event
-  bool logical = false;
+  // `every e1 -> (e2 or|and e3)`: logical 1 = OR, 2 = AND; f3 = the partner's
+  // filters, s_first / s_second = state ids in the order the two processors see
+  // an event
+  int logical = 0;
   std::vector<int> f3;
+  std::vector<int> typesB;   // AND: schema of the operand events carried with half-filled partials
   int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
   bool partitioned = false;
@@ -959,7 +1125,7 @@ struct PatternEngine : Engine {
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
-      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk;
+      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot;
   PinnedBuf h_agg;
 
   int kind() const override { return ENG_PATTERN; }
@@ -989,6 +1155,15 @@ struct PatternEngine : Engine {
     w.dev(t.ts.p, (size_t)C * 8);
     w.dev(t.key.p, (size_t)C * 8);
     w.dev(t.seq.p, (size_t)C * 8);
+    if (logical == 2) {
+      w.dev(t.half.p, (size_t)C);
+      for (size_t c = 0; c < typesB.size(); c++) {
+        w.dev(t.bcol[c].p, (size_t)C * type_size(typesB[c]));
+        w.dev(t.bnul[c].p, (size_t)C);
+      }
+      w.dev(t.bts.p, (size_t)C * 8);
+      w.dev(t.bseq.p, (size_t)C * 8);
+    }
   }
   void load_state(SnapR& r) override {
     const int64_t c0 = r.get<int64_t>();
@@ -1005,6 +1180,16 @@ struct PatternEngine : Engine {
     r.dev_into(t.ts.p, (size_t)c0 * 8);
     r.dev_into(t.key.p, (size_t)c0 * 8);
     r.dev_into(t.seq.p, (size_t)c0 * 8);
+    if (logical == 2) {
+      t.reserve_b(c0, typesB);
+      r.dev_into(t.half.p, (size_t)c0);
+      for (size_t c = 0; c < typesB.size(); c++) {
+        r.dev_into(t.bcol[c].p, (size_t)c0 * type_size(typesB[c]));
+        r.dev_into(t.bnul[c].p, (size_t)c0);
+      }
+      r.dev_into(t.bts.p, (size_t)c0 * 8);
+      r.dev_into(t.bseq.p, (size_t)c0 * 8);
+    }
     C = c0;
     counters.carry = C;
   }
@@ -1056,7 +1241,8 @@ struct PatternEngine : Engine {
     if (n <= 0) return;
     const bool isA = b.stream == sA, isB = b.stream == sB;
     const int64_t n_ext = C + n;
-    if (n_ext > (int64_t)kRowMask) throw Error(SHD_E_CAPACITY, "pattern batch + carried partials exceed 2^28 rows");
+    if (n_ext + (logical == 2 ? C : 0) > (int64_t)kRowMask)
+      throw Error(SHD_E_CAPACITY, "pattern batch + carried partials exceed 2^28 rows");
     hipStream_t s = stream;
     SHD_HIP(hipEventRecord(ev0, s));
     stage_begin();
@@ -1080,6 +1266,12 @@ struct PatternEngine : Engine {
     x.C = C;
     x.seq0 = seq;
     x.carry_seq = carry[cur].seq.as<int64_t>();
+    if (logical == 2) {
+      carry[cur].reserve_b(C, typesB);
+      x.half = carry[cur].colset_b(typesB, C);
+      x.half_seq = carry[cur].bseq.as<int64_t>();
+      d_mother.reserve(n_ext * 4);
+    }
 
     PrepArgs pa{};
     pa.x = x;
@@ -1215,6 +1407,7 @@ struct PatternEngine : Engine {
     sa.s_first = s_first;
     sa.s_second = s_second;
     if (logical) sa.f3 = dfilters(f3);
+    if (logical == 2) sa.carry_half = carry[cur].half.as<uint8_t>();
     sa.within = W;
     sa.partitioned = grouped;
     sa.prune = prune;
@@ -1229,15 +1422,29 @@ struct PatternEngine : Engine {
     d_bcnt.reserve((size_t)2 * ntile * 4);
     d_boff.reserve((size_t)2 * ntile * 4);
     const bool ts64 = sts64 != nullptr;
+    // deferred walks are dense when a partial expects another event of its key
+    // inside `within` (every event, ungrouped): E = events per `within` span / keys
+    bool dense = !grouped;
+    if (grouped) {
+      const double span = (double)(pg.ts_max - pg.ts_min) + 1.0;
+      const double per_w = W == INT64_MAX ? (double)n_ext : std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span);
+      const double nkeys = hash_mask ? (double)hash_mask + 1.0 : (double)(pg.kmax - std::min(pg.kmin, pg.kmax)) + 1.0;
+      dense = per_w / nkeys >= 0.25;
+    }
     // hot walk without f2 (deferrals), then the deferred walks with f2
 #define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
   hipLaunchKernelGGL((k_forward_scan<K64, TS64, H>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
                      skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), \
                      d_blk.as<ScanOut>())
+#define SHD_LAUNCH_RESUME_D(K64, FAST, TS64, D)                                                                 \
+  hipLaunchKernelGGL((k_forward_resume<K64, FAST, TS64, D>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, \
+                     skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_mother.as<int32_t>(),           \
+                     d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>())
 #define SHD_LAUNCH_RESUME(K64, FAST, TS64)                                                                      \
-  hipLaunchKernelGGL((k_forward_resume<K64, FAST, TS64>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile,    \
-                     skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(),              \
-                     d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>())
+  do {                                                                                                          \
+    if (dense) SHD_LAUNCH_RESUME_D(K64, FAST, TS64, true);                                                      \
+    else SHD_LAUNCH_RESUME_D(K64, FAST, TS64, false);                                                           \
+  } while (0)
 #define SHD_LAUNCH_RESUME2(K64, FAST) \
   if (ts64) SHD_LAUNCH_RESUME(K64, FAST, true); else SHD_LAUNCH_RESUME(K64, FAST, false)
     if (sorted64) {
@@ -1256,6 +1463,7 @@ struct PatternEngine : Engine {
       else { SHD_LAUNCH_RESUME2(false, false); }
     }
 #undef SHD_LAUNCH_RESUME2
+#undef SHD_LAUNCH_RESUME_D
 #undef SHD_LAUNCH_RESUME
 #undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
@@ -1291,9 +1499,14 @@ struct PatternEngine : Engine {
       d_pi.reserve((int64_t)m * 4);
       d_pj_alt.reserve((int64_t)m * 4);
       d_pi_alt.reserve((int64_t)m * 4);
+      if (logical == 2) {
+        d_se1.reserve((int64_t)m * 4);
+        d_sot.reserve((int64_t)m * 4);
+      }
       hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
                          (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
-                         tile, (int)logical, d_pj.as<uint32_t>(), d_pi.as<uint32_t>());
+                         tile, logical, (const int32_t*)d_mother.as<int32_t>(), d_pj.as<uint32_t>(),
+                         d_pi.as<uint32_t>(), d_se1.as<uint32_t>(), d_sot.as<int32_t>());
       SHD_CHECK_LAUNCH();
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
@@ -1315,6 +1528,8 @@ struct PatternEngine : Engine {
       pr.logical = logical;
       pr.s_first = s_first;
       pr.s_second = s_second;
+      pr.se1 = d_se1.as<uint32_t>();
+      pr.sot = d_sot.as<int32_t>();
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
       hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
@@ -1342,6 +1557,20 @@ struct PatternEngine : Engine {
       ga.dts = carry[nxt].ts.as<int64_t>();
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
+      if (logical == 2) {
+        carry[nxt].reserve_b(n_open, typesB);
+        ga.and_mode = 1;
+        ga.match_row = d_match.as<int32_t>();
+        ga.dhalf = carry[nxt].half.as<uint8_t>();
+        ga.ncolsB = (int)typesB.size();
+        for (size_t c = 0; c < typesB.size(); c++) {
+          ga.typesB[c] = (int32_t)typesB[c];
+          ga.dcolB[c] = carry[nxt].bcol[c].p;
+          ga.dnulB[c] = carry[nxt].bnul[c].as<uint8_t>();
+        }
+        ga.dtsB = carry[nxt].bts.as<int64_t>();
+        ga.dseqB = carry[nxt].bseq.as<int64_t>();
+      }
       if (keyed && !grouped) {   // positions are rows: the prepare output holds each row's key
         ga.key64 = key64;
         skey32 = d_k32.as<uint32_t>();
@@ -1396,8 +1625,12 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why) {
 // (reverse setup order: the first logical operand first,
 // StateInputStreamParser.java:349-361 + LogicalInnerStateRuntime.setup); the
 // partner slot stays empty (LogicalPreStateProcessor.java:113-154 drops the
-// partial from the partner's pending list).  AND keeps a half-filled partial
-// across events (and pushes), which this engine does not carry: generic engine.
+// partial from the partner's pending list).
+// `... -> (e2=B[f2] and e3=B[f3])`: each operand fills at the first B event
+// that passes its filter (tried in the same order, the partner slot visible to
+// the filter); the partial completes when both are filled, emitted by the
+// processor that filled last.  A half-filled open partial carries its operand
+// event to the next push (CarryTable::half / bcol, ext rows C + n + i).
 std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& why) {
   if (p.kind != SHD_KIND_STATE || p.state_type != 0) { why = "not a pattern"; return nullptr; }
   const PNode& r = p.root;
@@ -1405,8 +1638,8 @@ std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& 
   const PNode& ev = r.kids[0];
   const PNode& lg = r.kids[1];
   if (ev.kind != SHD_NODE_EVERY || ev.kids.size() != 1 || ev.kids[0].kind != SHD_NODE_STREAM ||
-      lg.kind != SHD_NODE_LOGICAL || lg.ltype != 1 || lg.kids.size() != 2) {
-    why = "not every e1 -> (e2 or e3)";
+      lg.kind != SHD_NODE_LOGICAL || (lg.ltype != 0 && lg.ltype != 1) || lg.kids.size() != 2) {
+    why = "not every e1 -> (e2 or|and e3)";
     return nullptr;
   }
   const PNode& a = ev.kids[0];
@@ -1441,8 +1674,9 @@ std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, con
   e->f1 = a.filters;
   e->f2 = b.filters;
   if (c) {
-    e->logical = true;
+    e->logical = p.root.kids[1].ltype == 1 ? 1 : 2;
     e->f3 = c->filters;
+    e->typesB = p.stream_types[b.stream];
     e->s_first = b.state_id;
     e->s_second = c->state_id;
   }

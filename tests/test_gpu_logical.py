@@ -1,4 +1,4 @@
-"""`every e1=A[f1] -> (e2=B[f2] or e3=B[f3]) [within W]` on the forward-scan
+"""`every e1=A[f1] -> (e2=B[f2] or|and e3=B[f3]) [within W]` on the forward-scan
 pattern engine (engine 1) vs the CPU oracle, and vs the generic NFA engine
 (engine 4, forced with SHD_NO_LOGICAL_SCAN) on the same device.
 
@@ -6,7 +6,11 @@ Reference: LogicalPreStateProcessor.java:113-154 / LogicalPostStateProcessor.jav
 (OR: the first operand whose filter passes fills its slot, the partner slot
 stays empty), MultiProcessStreamReceiver (processors in reverse setup order,
 one callback chunk per (event, processor)), StateInputStreamParser.java:349-361.
-Overlapping filters pin which operand wins when both pass on one event."""
+Overlapping filters pin which operand wins when both pass on one event.
+AND: both operands fill at their first passing event (possibly the same one);
+half-filled partials carry their operand event across pushes."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -52,12 +56,62 @@ OR_CASES = [
 ]
 
 
+AND_CASES = [
+    ("s4-and", wl.S4_APPS["and"]),
+    # one event often passes both operands: it fills both and completes at once
+    ("and-overlap", HEAD + q("e2=StockStream[price>e1.price] and e3=StockStream[price>e1.price*1.01]",
+                             " within 20 milliseconds")),
+    # the first operand's filter reads the partner's slot (null until filled; the
+    # parser compiles the second operand first, so only this direction resolves)
+    ("and-partner-ref", HEAD + q("e2=StockStream[price>e1.price and not (e3.price is null)] and "
+                                 "e3=StockStream[price<e1.price*0.95]", " within 30 milliseconds")),
+    ("and-long-carry", HEAD + q("e2=StockStream[price>e1.price*1.3] and e3=StockStream[price<e1.price*0.75]",
+                                " within 3 sec")),
+    ("and-partitioned", HEAD + "partition with (symbol of StockStream) begin " +
+     q("e2=StockStream[price>e1.price*1.1] and e3=StockStream[price<e1.price*0.9]", " within 1 sec",
+       "e1.symbol as s, e1.price as p1, e2.price as p2, e3.price as p3, eventTimestamp() as t") + " end;"),
+]
+
+
+@pytest.mark.parametrize("name,app", AND_CASES, ids=[c[0] for c in AND_CASES])
+@pytest.mark.parametrize("parts", [1, 5])
+def test_logical_and_equals_oracle(hip_available, name, app, parts):
+    qp, _ = compile_single_query(app)
+    keys = 40 if name == "and-partitioned" else 1000
+    sym, price, vol, ts = wl.stock_stream(20000, keys, 1.0, seed_offset=zlib.crc32(name.encode()) % 1000)
+    batches = split(sym, price, vol, ts, parts)
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == ENGINE_PATTERN
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+
+
+@pytest.mark.parametrize("name,app", AND_CASES[:3], ids=[c[0] for c in AND_CASES[:3]])
+def test_logical_and_scan_equals_generic_nfa(hip_available, monkeypatch, name, app):
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(30000, 1000, 1.0, seed_offset=17)
+    batches = split(sym, price, vol, ts, 4)
+    scan, _, k1 = run_device(qp, batches)
+    monkeypatch.setenv("SHD_NO_LOGICAL_SCAN", "1")
+    nfa, _, k2 = run_device(qp, batches)
+    assert (k1, k2) == (ENGINE_PATTERN, ENGINE_NFA)
+    assert_same_rows(scan, nfa)
+
+
+def test_logical_and_single_event_calls(hip_available):
+    qp, _ = compile_single_query(AND_CASES[1][1])
+    sym, price, vol, ts = wl.stock_stream(3000, 20, 3.0, seed_offset=13)
+    batches = [(0, stock_batch(sym, price, vol, ts, call_size=1))]
+    assert_same_rows(run_device(qp, batches)[0], run_oracle(qp, batches))
+
+
 @pytest.mark.parametrize("name,app", OR_CASES, ids=[c[0] for c in OR_CASES])
 @pytest.mark.parametrize("parts", [1, 4])
 def test_logical_or_equals_oracle(hip_available, name, app, parts):
     qp, _ = compile_single_query(app)
     keys = 40 if name == "partitioned" else 1000
-    sym, price, vol, ts = wl.stock_stream(20000, keys, 1.0, seed_offset=hash(name) % 1000)
+    sym, price, vol, ts = wl.stock_stream(20000, keys, 1.0, seed_offset=zlib.crc32(name.encode()) % 1000)
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
     dev, counters, kind = run_device(qp, batches)
@@ -86,12 +140,13 @@ def test_logical_or_single_event_calls(hip_available):
     assert_same_rows(run_device(qp, batches)[0], run_oracle(qp, batches))
 
 
-def test_logical_or_two_streams(hip_available):
+@pytest.mark.parametrize("op", ["or", "and"])
+def test_logical_two_streams(hip_available, op):
     """e1 on A, both operands on B: B has two processors, so every B event
     with matches gives one chunk per operand (MultiProcessStreamReceiver)."""
     app = ("define stream A (k int, p double); define stream B (k int, p double); "
-           "@info(name='q') from every e1=A[p>20] -> (e2=B[p>e1.p] or e3=B[p<e1.p*0.5]) within 40 milliseconds "
-           "select e1.k as k, e1.p as p1, e2.p as p2, e3.p as p3 insert into O;")
+           "@info(name='q') from every e1=A[p>20] -> (e2=B[p>e1.p] %s e3=B[p<e1.p*0.5]) within 40 milliseconds "
+           "select e1.k as k, e1.p as p1, e2.p as p2, e3.p as p3 insert into O;" % op)
     qp, _ = compile_single_query(app)
     rng = np.random.default_rng(9)
     batches = []

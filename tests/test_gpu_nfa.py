@@ -15,9 +15,9 @@ from siddhi_amd import workloads as wl
 pytestmark = pytest.mark.gpu
 
 ENGINE_PATTERN, ENGINE_NFA = 1, 4
-# `every e1 -> (e2 or e3)` runs on the forward-scan pattern engine
+# `every e1 -> (e2 or|and e3)` runs on the forward-scan pattern engine
 # (tests/test_gpu_logical.py); every other S4 shape on the generic NFA engine
-EXPECT_ENGINE = {"or": ENGINE_PATTERN, "Por": ENGINE_PATTERN}
+EXPECT_ENGINE = {"or": ENGINE_PATTERN, "Por": ENGINE_PATTERN, "and": ENGINE_PATTERN, "Pand": ENGINE_PATTERN}
 
 
 def split(sym, price, vol, ts, parts, call=1024):
@@ -119,6 +119,7 @@ def test_capacity_overflow_is_reported(hip_available, monkeypatch):
     """A per-key pending list that overflows raises SHD_E_CAPACITY (never drops)."""
     from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST, SiddhiHipError, SHD_E_CAPACITY
     monkeypatch.setenv("SHD_NFA_LIST", "4")
+    monkeypatch.setenv("SHD_NO_LOGICAL_SCAN", "1")   # the generic engine's pending lists
     qp, _ = compile_single_query(wl.S4_APPS["and"])
     sym, price, vol, ts = wl.stock_stream(5000, 1000, 1.0, seed_offset=2)
     b = stock_batch(sym, price, vol, ts)

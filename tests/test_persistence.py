@@ -180,6 +180,9 @@ RESTORE_CASES = [
     ("S4-or", wl.S4_APPS["or"], 30_000, 100, 1.0, 3),
     ("S4-seqplus-part", wl.S4_PART_APPS["seqplus"], 30_000, 50, 1.0, 3),
     ("S4-and-part", wl.S4_PART_APPS["and"], 30_000, 100, 1.0, 3),
+    # half-filled AND partials carry their operand event through the snapshot
+    ("S4-and-wide", wl.S4_APPS["and"].replace("price>e1.price*1.2", "price>e1.price*1.3")
+     .replace("within 1 sec", "within 40 milliseconds"), 30_000, 100, 1.0, 3),
     ("S4-not-part", wl.S4_PART_APPS["not"], 30_000, 100, 1.0, 3),
 ]
 
