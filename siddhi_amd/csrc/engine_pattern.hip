@@ -34,9 +34,11 @@ namespace {
 
 enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
 // Per-position scan result (positions = key-sorted order when partitioned).
-enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5 };
+enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5, ST_YIELD = 6 };
 // per-position outcome stored by k_forward_scan for the compaction kernels
-enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3 };
+// PS_CONT: a capped lane walk stopped before position match_row[p] (long
+// walk, continued by the wave-cooperative pass)
+enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3, PS_CONT = 4 };
 
 // Sort payload: row index of the extended batch (28 bits) | flags (4 bits).
 constexpr int kRowBits = 28;
@@ -411,7 +413,7 @@ struct GlobalPos {
 // WIN: positions are loaded WIN at a time (one round trip for WIN steps);
 // walks over hashed buckets step over a few other keys, and a wave waits for
 // its longest walk, so they fetch ahead.
-template <bool DEFER, bool FAST, int WIN, class Ld>
+template <bool DEFER, bool FAST, int WIN, class Ld, int CAP = 0>
 __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
                                                 int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
                                                 int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
@@ -419,7 +421,16 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
                                                 int64_t& rb) {
   uint8_t st = ST_OPEN;
   bool stop = false, first = true;
+  int it = 0;
   while (!stop && q < n_ext) {
+    if constexpr (CAP > 0) {
+      // CAP positions walked: yield before position q (nothing of it processed)
+      if (!f2_now && it >= CAP) {
+        st = ST_YIELD;
+        break;
+      }
+      it += WIN;
+    }
     uint32_t wp[WIN];
     int64_t wt[WIN];
     uint64_t wk[WIN];
@@ -668,11 +679,123 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
 }
 
+// Cooperative walk (resume MODE 2): the 64 lanes of a wave scan ONE deferred
+// partial's later positions 64 at a time (coalesced loads, f2 evaluated for all
+// of them at once) and ballot the first terminating position -- the same
+// outcome as walk_partial's sequential walk: the first of {f2 match, expiry
+// (ts - tsi > within), end of the key's run, end of the push, timestamp
+// decrease} in position order.  A lane-per-partial walk keeps a wave busy for
+// its longest walk; here a partial that completes early costs one round and
+// one that never matches ceil(window / 64) rounds.  Plain and OR forms only
+// (an AND partial's operand state is sequential).
+template <bool FAST, class Ld>
+__device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
+                                            int64_t p, bool cont, int32_t* __restrict__ match_row,
+                                            uint8_t* __restrict__ pst, uint64_t& steps, uint64_t& pruned,
+                                            uint32_t& viol, uint32_t& nm, uint32_t& no) {
+  const int lane = threadIdx.x & 63;
+  uint32_t pvp, pd;
+  int64_t tsi, td;
+  uint64_t k = 0, kd = 0;
+  ld(p, pvp, tsi, k);
+  int64_t q0 = match_row[p];
+  // deferred (PS_DEFER): q0 is the B event where f2 comes first, its step
+  // already counted; continued (PS_CONT): q0 is unprocessed, the last walked
+  // position precedes it
+  ld(cont ? q0 - 1 : q0, pd, td, kd);
+  const int64_t r = pv_row(pvp);
+  int64_t prev = td;   // time of the last step taken (running-order check)
+  if (cont && (!(pv_flags(pd) & F_NEW) || (pv_flags(pd) & F_SKIP) || (a.partitioned && kd != k))) prev = tsi;
+  bool first = !cont;
+  uint8_t st = ST_OPEN;
+  int32_t j = -1;
+  uint64_t wsteps = 0;
+  bool wviol = false;
+  while (q0 < n_ext) {
+    const int64_t q = q0 + lane;
+    const bool inb = q < n_ext;
+    uint32_t pq = 0;
+    int64_t tq = 0;
+    uint64_t kq = 0;
+    if (inb) ld(q, pq, tq, kq);
+    const uint32_t fq = pv_flags(pq);
+    const bool f0 = first && lane == 0;   // the deferred B event: f2 is evaluated there directly
+    const bool skip = (fq & F_SKIP) != 0;
+    const bool endkey = inb && !f0 && a.partitioned && kq != k && !skip;
+    const bool isnew = inb && !f0 && !endkey && (fq & F_NEW) && !skip;
+    // running maximum of the earlier steps' times (a decrease is a violation)
+    int64_t m = isnew ? tq : INT64_MIN;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(m, o, 64);
+      if (lane >= o) m = t > m ? t : m;
+    }
+    int64_t before = __shfl_up(m, 1, 64);
+    if (lane == 0) before = INT64_MIN;
+    before = before > prev ? before : prev;
+    const bool vio = isnew && tq < before;
+    const bool expire = isnew && !vio && tq - tsi > a.within;
+    const uint64_t stopm = __ballot(!inb || endkey || vio || expire);
+    const int sidx = stopm ? __ffsll((unsigned long long)stopm) - 1 : 64;
+    bool hit = false;
+    int32_t code = 0;
+    if (lane < sidx && (f0 || (isnew && (fq & F_B)))) {
+      const int64_t r2 = pv_row(pq);
+      PairCtx cx{&a.x, r, r2, a.s_first};
+      hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+      int32_t br = 0;
+      if (!hit && a.logical) {
+        cx.s2 = a.s_second;
+        hit = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
+        br = 1;
+      }
+      code = (int32_t)r2 | (br << kRowBits);
+    }
+    const uint64_t hm = __ballot(hit);
+    const int fidx = hm ? __ffsll((unsigned long long)hm) - 1 : 64;
+    const int term = fidx < sidx ? fidx : sidx;
+    const uint64_t upto = term >= 63 ? ~0ull : ((2ull << term) - 1ull);
+    wsteps += (uint64_t)__popcll(__ballot(isnew && !vio) & upto);
+    if (fidx < sidx) {
+      st = ST_MATCH;
+      j = __shfl(code, fidx, 64);
+      break;
+    }
+    if (sidx < 64) {
+      const int kind = __shfl(vio ? 2 : (expire ? 1 : 0), sidx, 64);
+      if (kind == 2) wviol = true;
+      else if (kind == 1) st = ST_DEAD;
+      break;
+    }
+    prev = __shfl(m, 63, 64) > prev ? __shfl(m, 63, 64) : prev;
+    first = false;
+    q0 += 64;
+  }
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+  if (lane == 0) {
+    steps += wsteps;
+    if (wviol) viol = 1;
+    uint8_t out = PS_NONE;
+    if (st == ST_MATCH) {
+      out = PS_MATCH;
+      match_row[p] = j;
+      nm++;
+    } else if (st == ST_OPEN) {
+      out = PS_OPEN;
+      no++;
+    } else if (st == ST_PRUNED) {
+      pruned++;
+    }
+    pst[p] = out;
+  }
+}
+
 // Deferred walks: positions whose walk reached a B event inside `within`
 // evaluate f2 there (FAST: pre-decoded predicate, else the interpreter) and
-// continue.  Same tiles as k_forward_scan.  DENSE: one position per lane per
-// round; else each thread scans 16 outcome bytes and resumes its hits in turn.
-template <bool K64, bool FAST, bool TS64, bool DENSE>
+// continue.  Same tiles as k_forward_scan.  MODE 2: one wave per deferred
+// partial (coop_resume); MODE 1: one position per lane per round; MODE 0: each
+// thread scans 16 outcome bytes and resumes its hits in turn.
+template <bool K64, bool FAST, bool TS64, int MODE>
 __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                            int64_t tile, const uint32_t* __restrict__ skey32,
                                                            const uint64_t* __restrict__ skey64,
@@ -682,7 +805,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
                                                            int32_t* __restrict__ match_row,
                                                            int32_t* __restrict__ match_other,
                                                            uint8_t* __restrict__ pst, uint32_t* __restrict__ bcnt,
-                                                           ScanOut* __restrict__ blk) {
+                                                           ScanOut* __restrict__ blk, int slot0) {
   const ScanArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -721,7 +844,52 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       }
       pst[p] = out;
   };
-  if constexpr (DENSE) {
+  if constexpr (MODE == 2) {
+    // one wave per deferred / continued partial, the wave's 64-position slices in turn
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t base = t0 + (int64_t)w * 64; base < t1; base += kBlock) {
+      const int64_t pp = base + lane;
+      const uint8_t o = pp < t1 ? pst[pp] : (uint8_t)PS_NONE;
+      uint64_t dm = __ballot(o == PS_DEFER || o == PS_CONT);
+      const uint64_t cm = __ballot(o == PS_CONT);
+      while (dm) {
+        const int b = __ffsll((unsigned long long)dm) - 1;
+        dm &= dm - 1;
+        coop_resume<FAST>(a, es, n_ext, ld, base + b, (cm >> b) & 1ull, match_row, pst, steps, pruned, viol, nm, no);
+      }
+    }
+  } else if constexpr (MODE == 3) {
+    // lane walks capped at 64 positions; longer ones go on in the MODE 2 pass
+    for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
+      if (pst[p] != PS_DEFER) continue;
+      int64_t q = match_row[p];
+      uint32_t pvp, pq;
+      int64_t tsi, tq;
+      uint64_t k = 0, kq = 0;
+      ld(p, pvp, tsi, k);
+      ld(q, pq, tq, kq);
+      int32_t j = -1;
+      uint32_t fm = 0;
+      int64_t ra = -1, rb = -1;
+      const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 64>(
+          a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j, steps, viol, fm, ra, rb);
+      uint8_t out = PS_NONE;
+      if (st == ST_MATCH) {
+        out = PS_MATCH;
+        match_row[p] = j;
+        nm++;
+      } else if (st == ST_OPEN) {
+        out = PS_OPEN;
+        no++;
+      } else if (st == ST_PRUNED) {
+        pruned++;
+      } else if (st == ST_YIELD) {
+        out = PS_CONT;
+        match_row[p] = (int32_t)q;
+      }
+      pst[p] = out;
+    }
+  } else if constexpr (MODE == 1) {
     // one position per lane per round: when most candidates defer (walks over
     // every event of a busy key or of the whole stream) the walks of
     // neighbouring positions run side by side, not one after another in a lane
@@ -745,7 +913,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       }
     }
   }
-  scan_block_reduce(steps, pruned, viol, nm, no, blk, gridDim.x + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
+  scan_block_reduce(steps, pruned, viol, nm, no, blk, slot0 + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
 }
 
 // Stable compaction of one block's tile: position p with pst[p] == want gets
@@ -1300,7 +1468,7 @@ struct PatternEngine : Engine {
     // at full bandwidth, and the one-block folds of the per-block partials
     // (k_finish_prep / k_finish_scan) stay short
     const int nblk = grid_for(n_ext, 1, 4096);
-    d_blk.reserve((size_t)2 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
+    d_blk.reserve((size_t)3 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!keyed || pa.key_col >= 0);
     if (fast1)
@@ -1431,19 +1599,32 @@ struct PatternEngine : Engine {
       const double nkeys = hash_mask ? (double)hash_mask + 1.0 : (double)(pg.kmax - std::min(pg.kmin, pg.kmax)) + 1.0;
       dense = per_w / nkeys >= 0.25;
     }
+    // dense: lane walks capped at 64 positions, the longer ones continued one
+    // wave per partial (plain / OR forms, full-key grouping), else uncapped
+    // lane walks; SHD_RESUME_MODE forces 0..3 (tests)
+    int rmode = dense ? (logical != 2 && !hash_mask ? 3 : 1) : 0;
+    if (const char* f = getenv("SHD_RESUME_MODE")) {
+      const int m = atoi(f);
+      if (m >= 0 && m <= 3 && !(m >= 2 && (logical == 2 || hash_mask))) rmode = m;
+    }
     // hot walk without f2 (deferrals), then the deferred walks with f2
 #define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
   hipLaunchKernelGGL((k_forward_scan<K64, TS64, H>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
                      skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), \
                      d_blk.as<ScanOut>())
-#define SHD_LAUNCH_RESUME_D(K64, FAST, TS64, D)                                                                 \
+#define SHD_LAUNCH_RESUME_D(K64, FAST, TS64, D, SLOT)                                                           \
   hipLaunchKernelGGL((k_forward_resume<K64, FAST, TS64, D>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, \
                      skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_mother.as<int32_t>(),           \
-                     d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>())
+                     d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>(), SLOT)
 #define SHD_LAUNCH_RESUME(K64, FAST, TS64)                                                                      \
   do {                                                                                                          \
-    if (dense) SHD_LAUNCH_RESUME_D(K64, FAST, TS64, true);                                                      \
-    else SHD_LAUNCH_RESUME_D(K64, FAST, TS64, false);                                                           \
+    if (rmode == 3) {                                                                                           \
+      SHD_LAUNCH_RESUME_D(K64, FAST, TS64, 3, ntile);                                                           \
+      SHD_CHECK_LAUNCH();                                                                                       \
+      SHD_LAUNCH_RESUME_D(K64, FAST, TS64, 2, 2 * ntile);                                                       \
+    } else if (rmode == 2) SHD_LAUNCH_RESUME_D(K64, FAST, TS64, 2, ntile);                                      \
+    else if (rmode == 1) SHD_LAUNCH_RESUME_D(K64, FAST, TS64, 1, ntile);                                        \
+    else SHD_LAUNCH_RESUME_D(K64, FAST, TS64, 0, ntile);                                                        \
   } while (0)
 #define SHD_LAUNCH_RESUME2(K64, FAST) \
   if (ts64) SHD_LAUNCH_RESUME(K64, FAST, true); else SHD_LAUNCH_RESUME(K64, FAST, false)
@@ -1467,8 +1648,9 @@ struct PatternEngine : Engine {
 #undef SHD_LAUNCH_RESUME
 #undef SHD_LAUNCH_SCAN
     SHD_CHECK_LAUNCH();
-    // partials: [0, ntile) hot walk, [ntile, 2 ntile) deferred walks
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), 2 * ntile,
+    // partials: [0, ntile) hot walk, [ntile, 2 ntile) deferred walks, [2 ntile, 3 ntile) continued walks
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(),
+                       (rmode == 3 ? 3 : 2) * ntile,
                        d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");

@@ -164,3 +164,33 @@ def test_logical_two_streams(hip_available, op):
     assert kind == ENGINE_PATTERN
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
+
+
+MODE_CASES = [
+    ("p1", wl.P1_APP, 30000, 1000, 1.0),
+    ("p1-dense", wl.P1_APP, 30000, 50, 0.2),
+    ("p3-dense", wl.P3_APP, 100000, 2000, 0.05),
+    ("or-within", OR_CASES[3][1], 20000, 1000, 1.0),
+    ("or-overlap", OR_CASES[1][1], 20000, 1000, 1.0),
+    ("or-partitioned", OR_CASES[4][1], 20000, 40, 1.0),
+    # ~1000 same-key events per `within` span: walks beyond the 64-position cap
+    ("p1-long", wl.P1_APP, 40000, 20, 0.05),
+    ("or-part-long", OR_CASES[4][1], 40000, 20, 0.05),
+]
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("name,app,n,keys,delta", MODE_CASES, ids=[c[0] for c in MODE_CASES])
+def test_resume_modes_equal_oracle(hip_available, monkeypatch, mode, name, app, n, keys, delta):
+    """Deferred walks: 16 positions per thread (0), one lane per partial (1),
+    one wave per partial with ballots over 64 positions (2), lane walks capped
+    at 64 positions continued one wave per partial (3) -- same outputs."""
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(n, keys, delta, seed_offset=zlib.crc32(name.encode()) % 1000)
+    batches = split(sym, price, vol, ts, 3)
+    ora = run_oracle(qp, batches)
+    monkeypatch.setenv("SHD_RESUME_MODE", mode)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == ENGINE_PATTERN
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
