@@ -691,7 +691,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
 template <bool FAST, class Ld>
 __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
                                             int64_t p, bool cont, int32_t* __restrict__ match_row,
-                                            uint8_t* __restrict__ pst, uint64_t& steps, uint64_t& pruned,
+                                            int32_t* __restrict__ match_other, uint8_t* __restrict__ pst,
+                                            uint64_t& steps, uint64_t& pruned,
                                             uint32_t& viol, uint32_t& nm, uint32_t& no) {
   const int lane = threadIdx.x & 63;
   uint32_t pvp, pd;
@@ -709,6 +710,12 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
   bool first = !cont;
   uint8_t st = ST_OPEN;
   int32_t j = -1;
+  // AND (operand filters that do not read the partner slot): each operand
+  // fills at its first passing position; state carried between rounds
+  uint32_t fm = 0;
+  int64_t ra = -1, rb = -1;
+  int32_t other = -1;
+  if (a.logical == 2) and_carried(a, r, fm, ra, rb);
   uint64_t wsteps = 0;
   bool wviol = false;
   while (q0 < n_ext) {
@@ -739,6 +746,53 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     const int sidx = stopm ? __ffsll((unsigned long long)stopm) - 1 : 64;
     bool hit = false;
     int32_t code = 0;
+    if (a.logical == 2) {
+      const bool cand = lane < sidx && (f0 || (isnew && (fq & F_B)));
+      const int64_t r2 = pv_row(pq);
+      bool ha = false, hb = false;
+      if (cand && !(fm & 1u)) {
+        PairCtx cx{&a.x, r, r2, a.s_first};
+        ha = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+      }
+      if (cand && !(fm & 2u)) {
+        PairCtx cx{&a.x, r, r2, a.s_second};
+        hb = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
+      }
+      const uint64_t am = __ballot(ha), bm = __ballot(hb);
+      // fill positions in this round (-1: filled in an earlier round)
+      int ia = (fm & 1u) ? -1 : (am ? __ffsll((unsigned long long)am) - 1 : 64);
+      int ib = (fm & 2u) ? -1 : (bm ? __ffsll((unsigned long long)bm) - 1 : 64);
+      if (ia >= 0 && ia < 64) {
+        fm |= 1u;
+        ra = __shfl(r2, ia, 64);
+      }
+      if (ib >= 0 && ib < 64) {
+        fm |= 2u;
+        rb = __shfl(r2, ib, 64);
+      }
+      const int term2 = fm == 3u ? (ia > ib ? ia : ib) : sidx;
+      const uint64_t upto2 = term2 >= 63 ? ~0ull : ((2ull << term2) - 1ull);
+      wsteps += (uint64_t)__popcll(__ballot(isnew && !vio) & upto2);
+      if (fm == 3u) {
+        // the processor that fills last completes it; on one event the second
+        // operand's processor comes last
+        const int br = ib >= ia ? 1 : 0;
+        st = ST_MATCH;
+        j = (int32_t)__shfl(r2, term2, 64) | (br << kRowBits);
+        other = (int32_t)(br ? ra : rb);
+        break;
+      }
+      if (sidx < 64) {
+        const int kind = __shfl(vio ? 2 : (expire ? 1 : 0), sidx, 64);
+        if (kind == 2) wviol = true;
+        else if (kind == 1) st = ST_DEAD;
+        break;
+      }
+      prev = __shfl(m, 63, 64) > prev ? __shfl(m, 63, 64) : prev;
+      first = false;
+      q0 += 64;
+      continue;
+    }
     if (lane < sidx && (f0 || (isnew && (fq & F_B)))) {
       const int64_t r2 = pv_row(pq);
       PairCtx cx{&a.x, r, r2, a.s_first};
@@ -779,10 +833,12 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     if (st == ST_MATCH) {
       out = PS_MATCH;
       match_row[p] = j;
+      if (a.logical == 2) match_other[p] = other;
       nm++;
     } else if (st == ST_OPEN) {
       out = PS_OPEN;
       no++;
+      if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
     } else if (st == ST_PRUNED) {
       pruned++;
     }
@@ -855,7 +911,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       while (dm) {
         const int b = __ffsll((unsigned long long)dm) - 1;
         dm &= dm - 1;
-        coop_resume<FAST>(a, es, n_ext, ld, base + b, (cm >> b) & 1ull, match_row, pst, steps, pruned, viol, nm, no);
+        coop_resume<FAST>(a, es, n_ext, ld, base + b, (cm >> b) & 1ull, match_row, match_other, pst, steps, pruned,
+                          viol, nm, no);
       }
     }
   } else if constexpr (MODE == 3) {
@@ -1274,6 +1331,7 @@ struct PatternEngine : Engine {
   int logical = 0;
   std::vector<int> f3;
   std::vector<int> typesB;   // AND: schema of the operand events carried with half-filled partials
+  bool and_indep = false;    // AND: neither operand filter reads the partner's slot
   int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
   bool partitioned = false;
@@ -1602,10 +1660,13 @@ struct PatternEngine : Engine {
     // dense: lane walks capped at 64 positions, the longer ones continued one
     // wave per partial (plain / OR forms, full-key grouping), else uncapped
     // lane walks; SHD_RESUME_MODE forces 0..3 (tests)
-    int rmode = dense ? (logical != 2 && !hash_mask ? 3 : 1) : 0;
+    // AND with operand filters that do not read the partner slot: one wave per
+    // partial from the start (no capped lane phase: the operand state would
+    // have to travel between the two passes)
+    int rmode = dense ? (hash_mask ? 1 : (logical != 2 ? 3 : (and_indep ? 2 : 1))) : 0;
     if (const char* f = getenv("SHD_RESUME_MODE")) {
       const int m = atoi(f);
-      if (m >= 0 && m <= 3 && !(m >= 2 && (logical == 2 || hash_mask))) rmode = m;
+      if (m >= 0 && m <= 3 && !(m >= 2 && (hash_mask || (logical == 2 && (m == 3 || !and_indep))))) rmode = m;
     }
     // hot walk without f2 (deferrals), then the deferred walks with f2
 #define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
@@ -1859,6 +1920,14 @@ std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, con
     e->logical = p.root.kids[1].ltype == 1 ? 1 : 2;
     e->f3 = c->filters;
     e->typesB = p.stream_types[b.stream];
+    auto reads_only = [&](const std::vector<int>& fs, int own) {
+      for (int f : fs)
+        for (auto& in : p.exprs[f])
+          if ((in.op == SHD_OP_LOAD || in.op == SHD_OP_EVNULL || in.op == SHD_OP_TS) && in.a != 0 && in.a != own)
+            return false;
+      return true;
+    };
+    e->and_indep = reads_only(b.filters, b.state_id) && reads_only(c->filters, c->state_id);
     e->s_first = b.state_id;
     e->s_second = c->state_id;
   }

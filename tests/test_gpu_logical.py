@@ -176,6 +176,13 @@ MODE_CASES = [
     # ~1000 same-key events per `within` span: walks beyond the 64-position cap
     ("p1-long", wl.P1_APP, 40000, 20, 0.05),
     ("or-part-long", OR_CASES[4][1], 40000, 20, 0.05),
+    # AND: wave-cooperative walks keep the operand state between 64-position
+    # rounds (mode 3 is not offered for AND and falls back to the default)
+    ("and-s4", AND_CASES[0][1], 20000, 1000, 1.0),
+    ("and-overlap", AND_CASES[1][1], 20000, 1000, 1.0),
+    ("and-partner-ref", AND_CASES[2][1], 20000, 1000, 1.0),
+    ("and-long-carry", AND_CASES[3][1], 30000, 1000, 0.5),
+    ("and-part-long", AND_CASES[4][1], 40000, 20, 0.05),
 ]
 
 
