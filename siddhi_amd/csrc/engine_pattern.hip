@@ -58,6 +58,11 @@ struct ExtRows {
   // half-filled partials hold (stream B schema; row C + n + i for carry row i)
   ColSet half;
   const int64_t* half_seq;
+  // dense grouped walks: the e2-side attributes the filters read, copied into
+  // key-sorted position order (bit a of bpos_mask: attribute a is there), so
+  // the 64 positions a wave steps over load coalesced instead of one row each
+  ColSet bpos;
+  uint32_t bpos_mask;
   __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : (r < C + batch.n ? batch : half); }
   __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : (r < C + batch.n ? r - C : r - C - batch.n); }
   __device__ __forceinline__ int64_t ts(int64_t r) const {
@@ -86,6 +91,7 @@ struct PairCtx {
   bool matched = false;   // projection of a completed partial
   int64_t r3 = -1;        // logical AND: the partner operand's row (state s3)
   int s3 = -1;
+  int64_t q2 = -1;        // sorted position of r2 (walks; -1 in the projection)
   __device__ __forceinline__ int64_t slot(int st, int idx) const {
     int64_t r = st == 0 ? r1 : (st == s2 ? r2 : (st == s3 ? r3 : -1));
     if (r < 0) return -1;
@@ -102,6 +108,7 @@ struct PairCtx {
     }
     // branch on the row's table instead of selecting a per-lane ColSet
     // pointer: each branch reads a wave-uniform column table (scalar loads)
+    if (st == s2 && q2 >= 0 && ((x->bpos_mask >> attr) & 1u)) return col_load(x->bpos, q2, attr);
     if (r < x->C) return col_load(x->carry, r, attr);
     if (r < x->C + x->batch.n) return col_load(x->batch, r - x->C, attr);
     return col_load(x->half, r - x->C - x->batch.n, attr);
@@ -504,7 +511,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
             // partner processor on this same event (LogicalPostStateProcessor.java:59-86)
             int32_t br = -1;
             if (!(fm & 1u)) {
-              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second};
+              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second, q};
               if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
                 fm |= 1u;
                 ra = r2;
@@ -512,7 +519,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
               }
             }
             if (br < 0 && !(fm & 2u)) {
-              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first};
+              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first, q};
               if (FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx)) {
                 fm |= 2u;
                 rb = r2;
@@ -529,6 +536,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
             continue;
           }
           PairCtx cx{&a.x, r, r2, a.s_first};
+          cx.q2 = q;
           bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
           int32_t br = 0;
           if (!hit && a.logical) {
@@ -679,6 +687,28 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
 }
 
+// Position-major copy of the e2-side attributes the filters read (ExtRows::bpos):
+// dst column a, position p = batch row of position p (carried rows are e1
+// partials, never evaluated as e2 events).
+__global__ __launch_bounds__(kBlock) void k_gather_bpos(const ExtRows* __restrict__ xp, const uint32_t* spv,
+                                                       int64_t n_ext) {
+  const ExtRows& x = *xp;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = pv_row(spv[p]);
+    if (r < x.C) continue;
+    for (int c = 0; c < x.batch.ncols; c++) {
+      if (!((x.bpos_mask >> c) & 1u)) continue;
+      const Val v = col_load(x.batch, r - x.C, c);
+      switch (x.bpos.type[c]) {
+        case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)x.bpos.col[c])[p] = (uint32_t)v.b; break;
+        case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)x.bpos.col[c])[p] = v.b; break;
+        case SHD_T_BOOL: ((uint8_t*)x.bpos.col[c])[p] = (uint8_t)v.b; break;
+      }
+      ((uint8_t*)x.bpos.nul[c])[p] = (uint8_t)v.null;
+    }
+  }
+}
+
 // Cooperative walk (resume MODE 2): the 64 lanes of a wave scan ONE deferred
 // partial's later positions 64 at a time (coalesced loads, f2 evaluated for all
 // of them at once) and ballot the first terminating position -- the same
@@ -752,10 +782,12 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       bool ha = false, hb = false;
       if (cand && !(fm & 1u)) {
         PairCtx cx{&a.x, r, r2, a.s_first};
+        cx.q2 = q;
         ha = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
       }
       if (cand && !(fm & 2u)) {
         PairCtx cx{&a.x, r, r2, a.s_second};
+        cx.q2 = q;
         hb = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
       }
       const uint64_t am = __ballot(ha), bm = __ballot(hb);
@@ -796,6 +828,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     if (lane < sidx && (f0 || (isnew && (fq & F_B)))) {
       const int64_t r2 = pv_row(pq);
       PairCtx cx{&a.x, r, r2, a.s_first};
+      cx.q2 = q;
       hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
       int32_t br = 0;
       if (!hit && a.logical) {
@@ -1332,6 +1365,8 @@ struct PatternEngine : Engine {
   std::vector<int> f3;
   std::vector<int> typesB;   // AND: schema of the operand events carried with half-filled partials
   bool and_indep = false;    // AND: neither operand filter reads the partner's slot
+  uint32_t bpos_mask = 0;    // e2-side attributes read by the operand filters (ExtRows::bpos)
+  DevBuf d_bpos[kMaxCols], d_bpos_nul[kMaxCols];
   int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
   bool partitioned = false;
@@ -1640,7 +1675,6 @@ struct PatternEngine : Engine {
     sa.hash_mask = hash_mask;
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
-    const ScanArgs* d_sa = dev_args(sa);
     const bool fast2 = sa.f2.fp.ok != 0 && (!logical || sa.f3.fp.ok != 0);
     // contiguous tiles of positions per block (compaction offsets per block)
     const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
@@ -1651,11 +1685,13 @@ struct PatternEngine : Engine {
     // deferred walks are dense when a partial expects another event of its key
     // inside `within` (every event, ungrouped): E = events per `within` span / keys
     bool dense = !grouped;
+    double e_key = 0.0;   // expected events of a partial's key inside one `within` span
     if (grouped) {
       const double span = (double)(pg.ts_max - pg.ts_min) + 1.0;
       const double per_w = W == INT64_MAX ? (double)n_ext : std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span);
       const double nkeys = hash_mask ? (double)hash_mask + 1.0 : (double)(pg.kmax - std::min(pg.kmin, pg.kmax)) + 1.0;
-      dense = per_w / nkeys >= 0.25;
+      e_key = per_w / nkeys;
+      dense = e_key >= 0.25;
     }
     // dense: lane walks capped at 64 positions, the longer ones continued one
     // wave per partial (plain / OR forms, full-key grouping), else uncapped
@@ -1668,6 +1704,25 @@ struct PatternEngine : Engine {
       const int m = atoi(f);
       if (m >= 0 && m <= 3 && !(m >= 2 && (hash_mask || (logical == 2 && (m == 3 || !and_indep))))) rmode = m;
     }
+    // dense grouped walks revisit each position once per partial of its key
+    // inside `within`: the e2 attributes the filters read are copied into
+    // position order once, so the walks load them coalesced; worth its pass
+    // only when walks are long (SHD_NO_BPOS: off, SHD_BPOS: always when dense)
+    if (grouped && rmode != 0 && isB && bpos_mask && !getenv("SHD_NO_BPOS") && (e_key >= 8.0 || getenv("SHD_BPOS"))) {
+      sa.x.bpos = b.cs;
+      sa.x.bpos.n = n_ext;
+      for (int c = 0; c < b.cs.ncols; c++) {
+        if (!((bpos_mask >> c) & 1u)) continue;
+        d_bpos[c].reserve(n_ext * type_size(b.cs.type[c]));
+        d_bpos_nul[c].reserve(n_ext);
+        sa.x.bpos.col[c] = d_bpos[c].p;
+        sa.x.bpos.nul[c] = d_bpos_nul[c].as<uint8_t>();
+      }
+      sa.x.bpos_mask = bpos_mask;
+      hipLaunchKernelGGL(k_gather_bpos, dim3(grid_for(n_ext, 1, 4096)), dim3(kBlock), 0, s, dev_args(sa.x), spv, n_ext);
+      SHD_CHECK_LAUNCH();
+    }
+    const ScanArgs* d_sa = dev_args(sa);
     // hot walk without f2 (deferrals), then the deferred walks with f2
 #define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
   hipLaunchKernelGGL((k_forward_scan<K64, TS64, H>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \
@@ -1933,6 +1988,16 @@ std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, con
   }
   e->W = p.within >= 0 ? p.within : INT64_MAX;
   e->typesA = p.stream_types[a.stream];
+  {
+    // attributes of the e2-side state(s) that the walk filters load
+    auto scan = [&](const std::vector<int>& fs, int st) {
+      for (int f : fs)
+        for (auto& in : p.exprs[f])
+          if (in.op == SHD_OP_LOAD && in.a == st && (in.c & 0xFFFF) < kMaxCols) e->bpos_mask |= 1u << (in.c & 0xFFFF);
+    };
+    scan(b.filters, b.state_id);
+    if (c) scan(c->filters, c->state_id);
+  }
   for (auto& o : p.outputs) e->outs.push_back(o.second);
   e->partitioned = !p.part_keys.empty();
   if (!e->partitioned && !c && !getenv("SHD_NO_IMPLICIT_KEY")) {

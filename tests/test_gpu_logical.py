@@ -197,6 +197,7 @@ def test_resume_modes_equal_oracle(hip_available, monkeypatch, mode, name, app, 
     batches = split(sym, price, vol, ts, 3)
     ora = run_oracle(qp, batches)
     monkeypatch.setenv("SHD_RESUME_MODE", mode)
+    monkeypatch.setenv("SHD_BPOS", "1")   # position-major e2 attributes whenever walks are dense
     dev, counters, kind = run_device(qp, batches)
     assert kind == ENGINE_PATTERN
     assert len(ora[2]) > 0
