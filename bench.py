@@ -102,27 +102,24 @@ def alg_bytes_window(c, n, n_out):
     return (20 + 12 + 36 * o) * n, dict(o=o)
 
 
-def pmc_traffic(cfg_name, stage, events_per_launch):
-    """HBM bytes per launch of `stage` from the newest committed rocprofv3 PMC
-    summary (profiles/rNN_pmc_<config>.json, written by scripts/pmc_summary.py
-    from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 corrections),
-    scaled from its bytes per event to this run's events per launch."""
+def pmc_summary(cfg_name):
+    """Newest committed rocprofv3 PMC summary of this config (profiles/rNN_pmc_<config>.json,
+    written by scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes with the
+    gfx950 corrections): per-kernel HBM bytes and times of one push."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % cfg_name)))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    st = d.get("stages", {}).get(stage)
-    if not st:
-        return None, None
-    return round(st["hbm_bytes_per_event"] * events_per_launch), os.path.relpath(files[-1], ROOT)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % cfg_name)), reverse=True):
+        d = json.load(open(f))
+        if "push" in d and "kernels" in d:
+            return d, os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(cfg_name, app, keys, delta, sample):
-    """CPU oracle (C++ restatement, 1 core) on the first `sample` events of the same stream."""
+    """CPU oracle (C++ restatement, 1 core) on the first `sample` events of the same
+    stream; also returns its output rows (the parity_prefix check)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_engine import OracleQueryEngine
-    from parity import compile_single_query, stock_batch
+    from parity import compile_single_query, concat_rows
     from siddhi_amd import workloads as wl
     qp, _ = compile_single_query(app)
     eng = OracleQueryEngine(qp, None)
@@ -131,6 +128,8 @@ def cpu_baseline(cfg_name, app, keys, delta, sample):
     nul = np.zeros_like(vals, dtype=np.uint8)
     offs = wl.call_offsets(sample)
     lib = eng.lib
+    nout = eng.n_out
+    parts = []
     t0 = time.perf_counter()
     for c in range(len(offs) - 1):
         a, b = int(offs[c]), int(offs[c + 1])
@@ -138,12 +137,42 @@ def cpu_baseline(cfg_name, app, keys, delta, sample):
         nn = np.ascontiguousarray(nul[a:b])
         tt = np.ascontiguousarray(t[a:b])
         lib.orc_push(eng.h, 0, b - a, tt.ctypes.data, vv.ctypes.data, nn.ctypes.data, 1)
+        m = lib.orc_num_rows(eng.h)
+        if m:   # QueryCallback: the rows of this call
+            ch, ty, ts_ = np.empty(m, np.int64), np.empty(m, np.int32), np.empty(m, np.int64)
+            va, nu = np.empty((m, max(nout, 1)), np.uint64), np.empty((m, max(nout, 1)), np.uint8)
+            lib.orc_get_rows(eng.h, ch.ctypes.data, ty.ctypes.data, ts_.ctypes.data, va.ctypes.data, nu.ctypes.data)
+            parts.append((ch + 1_000_000 * c, ty, ts_, va[:, :nout], nu[:, :nout]))
         lib.orc_clear_rows(eng.h)
     dt = time.perf_counter() - t0
     eng.close()
-    return {"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": "first %d events of the %s stream (%d keys, delta %g ms), C++ restatement of the "
-                      "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)}
+    return ({"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
+             "sample": "first %d events of the %s stream (%d keys, delta %g ms), C++ restatement of the "
+                       "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)},
+            concat_rows(parts), qp)
+
+
+def parity_prefix(torch, he, qp, cols, ts, offs_all, prefix, ora_rows):
+    """The device path on the first `prefix` events of the benchmark stream (one
+    fresh query, polled, outside the timed region) against the oracle's rows."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import assert_same_rows
+    dq = he.DeviceQuery(qp.ir)
+    try:
+        co = offs_all[offs_all <= prefix]
+        if co[-1] != prefix:
+            co = np.append(co, prefix)
+        dq.push_raw(0, prefix, ts.data_ptr(), [c.data_ptr() for c in cols], [0, 0, 0], he.SHD_MEM_DEVICE,
+                    co.astype(np.int64), True)
+        r = dq.poll()
+        from parity import concat_rows
+        dev = concat_rows([r] if r is not None else [])
+        assert_same_rows(dev, ora_rows)
+        return "equal (%d events, %d rows)" % (prefix, len(dev[2]))
+    except AssertionError as e:
+        return "DIFFERENT: %s" % str(e).splitlines()[0]
+    finally:
+        dq.close()
 
 
 def run_multi(args, torch, dist, rank, world, local, dev):
@@ -367,6 +396,15 @@ def main():
                               "events_per_s": round(n * world / dt, 1), "stage_ms_per_step": st}),
                   file=sys.stderr, flush=True)
 
+    # SURVEY.md §8d algorithmic bytes need the reference's pending-scan counts
+    # (P-bar: (partial, event) pairs its pending lists visit).  The sort path's
+    # walks count exactly those; the bucketed walk skips expiry visits beyond its
+    # `within` lookahead, so the counts come from one untimed step on the sort path.
+    calib = None
+    if pattern:
+        os.environ["SHD_NO_BUCKET"] = "1"
+        calib = run_step()
+        del os.environ["SHD_NO_BUCKET"]
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()
@@ -394,31 +432,44 @@ def main():
     for r in stage_runs:
         for k, v in r.items():
             stages[k] = stages.get(k, 0) + v / len(stage_runs)
-    dominant = max(stages, key=stages.get) if stages else None
     step_dev_ns = sum(stages.values())
     if pattern:
-        bytes_step, derived = alg_bytes_pattern(counters, counters["events"])
+        bytes_step, derived = alg_bytes_pattern(calib, calib["events"])
     else:
         bytes_step, derived = alg_bytes_window(counters, counters["events"], len(qp.output_names))
-    launches = len(cuts) - 1
     roof = None
-    if dominant:
-        # achieved: the path's algorithmic bytes per launch of the dominant kernel stage / its mean launch time
-        per_launch_bytes = bytes_step / launches
-        per_launch_s = stages[dominant] / launches * 1e-9
-        ach = per_launch_bytes / per_launch_s / 1e9
-        traffic, tsrc = pmc_traffic(args.config, dominant, counters["events"] / launches)
+    if stages:
+        # frac: the path's algorithmic bytes per step / the wall time of a step
+        # (recomputable from this line: alg_bytes_per_event * events / ms_per_step);
+        # device_*: / the HIP-event time of the push pipeline; kernels: each
+        # kernel's own HBM bytes (PMC) / its rocprof duration, from profiles/
+        ach = bytes_step / (elapsed / args.steps) / 1e9
+        dev_ach = bytes_step / (step_dev_ns * 1e-9) / 1e9
+        pmc, psrc = pmc_summary(args.config)
+        traffic = None
+        kern = None
+        if pmc:
+            traffic = round(pmc["push"]["hbm_bytes_per_event"] * n)
+            top = sorted(pmc["kernels"].items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["dispatches_per_push"])[:5]
+            kern = {k: {"avg_us": v["avg_us"], "per_push": v["dispatches_per_push"],
+                        "hbm_bytes_per_event": v["hbm_bytes_per_event"], "hbm_frac": v["hbm_frac"]}
+                    for k, v in top}
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                "kernel_stage": dominant,
-                "path_achieved": round(bytes_step / (step_dev_ns * 1e-9) / 1e9, 1),
-                "path_frac": round(bytes_step / (step_dev_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_ratio": round(traffic / bytes_step, 3) if traffic else None,
+                "alg_bytes_per_event": round(bytes_step / n, 2),
+                "scope": "whole push pipeline per step (wall clock)",
+                "device_achieved": round(dev_ach, 1), "device_frac": round(dev_ach / HBM_PEAK_GBS, 4),
+                "pmc_source": psrc, "kernels": kern}
     matches_per_s = counters["matches"] * world * args.steps / elapsed
 
     cpu = None
+    prefix = None
     if rank == 0 and world == 1 and args.cpu_sample != 0:
         sample = args.cpu_sample if args.cpu_sample > 0 else (2_000_000 if pattern else 1_000_000)
-        cpu = cpu_baseline(args.config, app, keys, delta, min(sample, n))
+        cpu, ora_rows, _ = cpu_baseline(args.config, app, keys, delta, min(sample, n))
+        if pattern and mode == "prepartitioned" and kb == 0:
+            prefix = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, min(sample, n), ora_rows)
 
     if rank == 0:
         line = {
@@ -443,6 +494,7 @@ def main():
             "stage_ms_per_step": {k: round(v / 1e6, 3) for k, v in stages.items()},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity_prefix": prefix,
         }
         print(json.dumps(line))
     dq.close()

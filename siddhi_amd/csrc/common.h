@@ -205,6 +205,13 @@ void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_
                             bool hashed = false, uint32_t kbase = 0);
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
+// Digit totals (256 per pass, u32) of the last radix pass run with `scratch`
+// over n keys (radix_sort_triples_u32 / _pairs_u32): the bucket sizes of a
+// one-pass hashed bucket sort.
+const uint32_t* radix_digit_totals(const DevBuf& scratch, int64_t n);
+// Row scans of a [256][nb] per-tile digit histogram: offs[d*nb + t] = digit
+// d's count in tiles before t, dtot[d] = digit d's total (one pass's offsets).
+void radix_digit_scan(const uint32_t* hist, int nb, uint32_t* offs, uint32_t* dtot, hipStream_t s);
 void reduce_max_u64(const uint64_t* in, int64_t n, uint64_t* out_dev, hipStream_t s);
 void fill_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s);
 

@@ -104,6 +104,24 @@ struct SnapR {
   }
 };
 
+// Thrown by an engine whose formulation cannot continue on a valid input
+// (e.g. the pattern forward scan when timestamps go back inside a key) but
+// whose cross-push state the generic NFA engine can take over: shd_push then
+// replays the open partials (Engine::export_replay) into a fresh NFA engine
+// and runs the push there.  Never surfaces through the C-ABI.
+struct NeedNfa : Error {
+  explicit NeedNfa(const std::string& m) : Error(SHD_E_UNSUPPORTED, m) {}
+};
+
+// Host image of a query's open partial matches as the events that created
+// them, in arrival order (one stream, typed columns as in shd_batch).
+struct Replay {
+  int stream = 0;
+  int64_t n = 0;
+  std::vector<int64_t> ts;
+  std::vector<std::vector<uint8_t>> cols, nulls;   // [ncols] typed bytes / null bytes
+};
+
 struct Engine {
   Plan plan;
   DevExprTable ex;
@@ -141,6 +159,9 @@ struct Engine {
   // chunk ids, counters) are written by shd_snapshot itself.
   virtual void save_state(SnapW&) { throw Error(SHD_E_UNSUPPORTED, "engine has no snapshot support"); }
   virtual void load_state(SnapR&) { throw Error(SHD_E_UNSUPPORTED, "engine has no snapshot support"); }
+  // Events whose replay through the reference algorithm (from a fresh state)
+  // rebuilds exactly this engine's open partial matches (NeedNfa hand-over).
+  virtual void export_replay(Replay&) { throw Error(SHD_E_UNSUPPORTED, "engine state cannot be handed over"); }
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column
@@ -178,5 +199,11 @@ std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why);
+// list_hint: expected partials per key at once (sizes the per-key lists of an
+// unpartitioned plan; 0 = defaults)
+std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t list_hint);
+// Engine setup shared by shd_plan_load and the engine switches (expression
+// table upload, output arena, stream and events, reset).
+void init_engine(Engine& e, const Plan& p);
 
 }  // namespace shd

@@ -2109,7 +2109,9 @@ struct NfaEngine : Engine {
   }
 };
 
-std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why) {
+std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why) { return make_nfa_engine(p, why, 0); }
+
+std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t list_hint) {
   if (p.kind != SHD_KIND_STATE) {
     why = "not a state plan";
     return nullptr;
@@ -2263,10 +2265,17 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why) {
   // per-key capacities: one key (unpartitioned) gets deep lists, many keys get lean blocks
   NfaLayout& Y = e->lay;
   const bool many = e->partitioned;
-  Y.L = env_int("SHD_NFA_LIST", many ? 32 : 2048);
-  Y.SC = std::min(env_int("SHD_NFA_PARTIALS", many ? 128 : 8192), 32768);
+  // list_hint (a pattern query handing its open partials over): the one key of
+  // an unpartitioned plan must hold about that many partials at once
+  int L0 = many ? 32 : 2048, S0 = many ? 128 : 8192;
+  if (!many && list_hint > 0) {
+    while (L0 < 2 * list_hint && L0 < 32768) L0 *= 2;
+    S0 = std::max(S0, std::min(2 * L0, 32768));
+  }
+  Y.L = env_int("SHD_NFA_LIST", L0);
+  Y.SC = std::min(env_int("SHD_NFA_PARTIALS", S0), 32768);
   Y.EC = std::min(env_int("SHD_NFA_EVENTS", 2 * Y.SC), 65000);
-  Y.RC = std::min(env_int("SHD_NFA_RECORDS", many ? 128 : 8192), 65000);
+  Y.RC = std::min(env_int("SHD_NFA_RECORDS", S0), 65000);
   Y.QC = env_int("SHD_NFA_TIMERS", many ? 32 : 1024);
   Y.RETC = std::min(Y.L * std::max(npre, 1), 65000);
   Y.WK = 4 * kNP;

@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "engine.h"
+#include "radix_tile.h"
 
 namespace shd {
 
@@ -201,95 +202,92 @@ __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
-// Per extended row: key and packed (flags, row) sort payload.  One pass over
-// the pushed columns (key, f1 inputs, ts); the f1 bytecode is read from LDS.
-// FAST: the f1 chain is a pre-decoded conjunction and the key a plain column,
-// so this variant carries no interpreter (far fewer registers, more waves).
-template <bool FAST>
-__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
-                                                    uint32_t* __restrict__ k32, uint64_t* __restrict__ k64,
-                                                    uint32_t* __restrict__ pv, int32_t* __restrict__ tso,
-                                                    PrepAgg* __restrict__ blk) {
-  const PrepArgs& a = *ap;
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
-  const ExtRows& x = a.x;
+// Running per-thread aggregates of the row preparation (PrepAgg fields).
+struct PrepAcc {
   unsigned long long created = 0, kmax = 0, ovf = 0, unmono = 0, kmin = ULLONG_MAX;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctmax = LLONG_MIN;
-  // timestamps travel with the key sort as 32-bit offsets from the batch's
-  // first event (ovf: the push falls back to a 64-bit gather after the sort)
-  const int64_t tbase = x.batch.ts[0];
-  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r += stride) {
-    uint32_t f;
-    uint64_t k = 0;
-    long long t;
-    if (r < x.C) {
-      k = a.partitioned ? gld(a.carry_key, r) : 0;
-      f = F_CAND;
-      t = (long long)gld(x.carry.ts, r);
-      ctmax = t > ctmax ? t : ctmax;
-    } else {
-      // every load of the row is issued before the first use (no serial
-      // round trips): ts, key, f1 operands; the null-key test comes last
-      const int64_t br = r - x.C;
-      BatchRowCtx cx{&x.batch, br};
-      t = (long long)gld(x.batch.ts, br);
-      const long long tprev = br > 0 ? (long long)gld(x.batch.ts, br - 1) : t;
-      Val kv;
-      kv.b = 0;
-      kv.null = 0;
-      if (a.partitioned) {
-        if (FAST || a.key_col >= 0) kv = col_load(x.batch, br, a.key_col);
-        else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
-      }
-      const bool p1 = a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx));
-      f = F_NEW;
-      if (kv.null && a.null_skip) {
-        f |= F_SKIP;   // PartitionStreamReceiver drops null keys
-      } else {
-        if (a.is_b) f |= F_B;
-        if (p1) {
-          f |= F_CAND;
-          created++;
-        }
-        k = kv.null ? 0 : canon_key(kv, a.key_type);
-      }
-      tmin = t < tmin ? t : tmin;
-      tmax = t > tmax ? t : tmax;
-      unmono |= tprev > t;
-    }
+};
+
+// One extended row: key, flags (F_CAND / F_NEW / F_B / F_SKIP) and the
+// timestamp as a 32-bit offset from the batch's first event (acc.ovf when it
+// does not fit: the push then falls back to a 64-bit gather after the sort).
+// Every load of the row is issued before the first use (ts, key, f1
+// operands); the null-key test comes last.  FAST: the f1 chain is a
+// pre-decoded conjunction and the key a plain column (no interpreter).
+template <bool FAST>
+__device__ __forceinline__ void prep_row(const PrepArgs& a, const DExprSet& es, int64_t r, int64_t tbase,
+                                         bool count, uint64_t& k, uint32_t& f, int32_t& tso, PrepAcc& acc) {
+  const ExtRows& x = a.x;
+  long long t;
+  k = 0;
+  if (r < x.C) {
+    k = a.partitioned ? gld(a.carry_key, r) : 0;
+    f = F_CAND;
+    t = (long long)gld(x.carry.ts, r);
+    if (count) acc.ctmax = t > acc.ctmax ? t : acc.ctmax;
+  } else {
+    const int64_t br = r - x.C;
+    BatchRowCtx cx{&x.batch, br};
+    t = (long long)gld(x.batch.ts, br);
+    const long long tprev = br > 0 ? (long long)gld(x.batch.ts, br - 1) : t;
+    Val kv;
+    kv.b = 0;
+    kv.null = 0;
     if (a.partitioned) {
-      if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
-      if (a.key64) k64[r] = k;
-      else k32[r] = (uint32_t)k;
-      if (!(f & F_SKIP)) {
-        kmax = k > kmax ? k : kmax;
-        kmin = k < kmin ? k : kmin;
-      }
+      if (FAST || a.key_col >= 0) kv = col_load(x.batch, br, a.key_col);
+      else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
     }
-    pv[r] = (f << kRowBits) | (uint32_t)r;
-    const int64_t dt = (int64_t)t - tbase;
-    ovf |= dt != (int64_t)(int32_t)dt;
-    tso[r] = (int32_t)dt;
+    const bool p1 = a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx));
+    f = F_NEW;
+    if (kv.null && a.null_skip) {
+      f |= F_SKIP;   // PartitionStreamReceiver drops null keys
+    } else {
+      if (a.is_b) f |= F_B;
+      if (p1) {
+        f |= F_CAND;
+        acc.created += count ? 1u : 0u;
+      }
+      k = kv.null ? 0 : canon_key(kv, a.key_type);
+    }
+    if (count) {
+      acc.tmin = t < acc.tmin ? t : acc.tmin;
+      acc.tmax = t > acc.tmax ? t : acc.tmax;
+      acc.unmono |= tprev > t;
+    }
   }
-  // one partial per block (plain store; k_finish_prep folds them): no
-  // same-address atomics from every wave of a large grid
+  if (a.partitioned) {
+    if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
+    if (count && !(f & F_SKIP)) {
+      acc.kmax = k > acc.kmax ? k : acc.kmax;
+      acc.kmin = k < acc.kmin ? k : acc.kmin;
+    }
+  }
+  const int64_t dt = (int64_t)t - tbase;
+  if (count) acc.ovf |= dt != (int64_t)(int32_t)dt;
+  tso = (int32_t)dt;
+}
+
+// Per-block fold of the PrepAcc partials into blk[slot] (plain store;
+// k_finish_prep folds the blocks): no same-address atomics from every wave.
+template <int NT>
+__device__ __forceinline__ void prep_block_reduce(PrepAcc acc, PrepAgg* blk, int slot) {
   for (int o = 32; o > 0; o >>= 1) {
-    created += __shfl_xor(created, o, 64);
-    ovf |= __shfl_xor(ovf, o, 64);
-    unmono |= __shfl_xor(unmono, o, 64);
+    acc.created += __shfl_xor(acc.created, o, 64);
+    acc.ovf |= __shfl_xor(acc.ovf, o, 64);
+    acc.unmono |= __shfl_xor(acc.unmono, o, 64);
   }
-  kmax = wave_max(kmax);
-  kmin = wave_min(kmin);
-  tmin = wave_min(tmin);
-  tmax = wave_max(tmax);
-  ctmax = wave_max(ctmax);
-  __shared__ PrepAgg wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = PrepAgg{created, kmax, tmin, tmax, ovf, unmono, ctmax, kmin};
+  acc.kmax = wave_max(acc.kmax);
+  acc.kmin = wave_min(acc.kmin);
+  acc.tmin = wave_min(acc.tmin);
+  acc.tmax = wave_max(acc.tmax);
+  acc.ctmax = wave_max(acc.ctmax);
+  __shared__ PrepAgg wpart[NT / 64];
+  if ((threadIdx.x & 63) == 0)
+    wpart[threadIdx.x >> 6] = PrepAgg{acc.created, acc.kmax, acc.tmin, acc.tmax, acc.ovf, acc.unmono, acc.ctmax, acc.kmin};
   __syncthreads();
   if (threadIdx.x == 0) {
     PrepAgg r = wpart[0];
-    for (int w = 1; w < kBlock / 64; w++) {
+    for (int w = 1; w < NT / 64; w++) {
       r.ovf |= wpart[w].ovf;
       r.unmono |= wpart[w].unmono;
       r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
@@ -299,8 +297,113 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
       r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
       r.ts_max = wpart[w].ts_max > r.ts_max ? wpart[w].ts_max : r.ts_max;
     }
-    blk[blockIdx.x] = r;
+    blk[slot] = r;
   }
+}
+
+// Per extended row: key and packed (flags, row) sort payload (prep_row), for
+// the key sort of the sort path.
+template <bool FAST>
+__global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__ ap, int64_t n_ext, int64_t stride,
+                                                    uint32_t* __restrict__ k32, uint64_t* __restrict__ k64,
+                                                    uint32_t* __restrict__ pv, int32_t* __restrict__ tso,
+                                                    PrepAgg* __restrict__ blk) {
+  const PrepArgs& a = *ap;
+  const DExprSet es = a.es;
+  PrepAcc acc;
+  const int64_t tbase = a.x.batch.ts[0];
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n_ext; r += stride) {
+    uint64_t k;
+    uint32_t f;
+    int32_t t32;
+    prep_row<FAST>(a, es, r, tbase, true, k, f, t32, acc);
+    if (a.partitioned) {
+      if (a.key64) k64[r] = k;
+      else k32[r] = (uint32_t)k;
+    }
+    pv[r] = (f << kRowBits) | (uint32_t)r;
+    tso[r] = t32;
+  }
+  prep_block_reduce<kBlock>(acc, blk, blockIdx.x);
+}
+
+// Fused prepare + one stable hashed bucket pass (the bucketed walk's layout):
+// k_bkt_hist counts the 256 buckets of every tile from the key column alone
+// (plain 32-bit attribute keys), k_bkt_scatter prepares the rows in registers
+// (prep_row) and writes (key, flags|row, ts32) straight to their bucket
+// positions -- the prepared rows never make a round trip through HBM.
+constexpr int kBktRounds = 16;   // rows per lane of a scatter tile (4096 rows / tile)
+
+__device__ __forceinline__ uint32_t bkt_key32(const PrepArgs& a, int64_t r) {
+  const ExtRows& x = a.x;
+  if (r < x.C) return (uint32_t)gld(a.carry_key, r);
+  const int64_t br = r - x.C;
+  const uint8_t* nul = x.batch.nul[a.key_col];
+  if (nul && gld(nul, br)) return 0u;
+  return gld((const uint32_t*)x.batch.col[a.key_col], br);
+}
+
+__global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restrict__ ap, int64_t n_ext,
+                                                       uint32_t* __restrict__ hist, int nb) {
+  const PrepArgs& a = *ap;
+  __shared__ uint32_t h[kRsWaves][256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
+  const int tile = rs_tile_of(blockIdx.x, nb);
+  const int64_t wb = (int64_t)tile * rs_tile(kBktRounds) + (int64_t)w * 64 * kBktRounds;
+  uint32_t k[kBktRounds];
+#pragma unroll
+  for (int r = 0; r < kBktRounds; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    k[r] = bkt_key32(a, idx < n_ext ? idx : n_ext - 1);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kBktRounds; r++)
+    if (wb + r * 64 + lane < n_ext) atomicAdd(&h[w][key_bucket_mix(k[r]) & 255u], 1u);
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < kRsWaves; i++) c += h[i][tid];
+    hist[(int64_t)tid * nb + tile] = c;
+  }
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __restrict__ ap, int64_t n_ext,
+                                                          const uint32_t* __restrict__ hist,
+                                                          const uint32_t* __restrict__ offs,
+                                                          const uint32_t* __restrict__ dtotal, int nb,
+                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                          uint32_t* __restrict__ tout, PrepAgg* __restrict__ blk) {
+  const PrepArgs& a = *ap;
+  const DExprSet es = a.es;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = rs_tile_of(blockIdx.x, nb);
+  const int64_t t0 = (int64_t)tile * rs_tile(kBktRounds);
+  const int64_t wb = t0 + (int64_t)w * 64 * kBktRounds;
+  const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
+  const int64_t tbase = a.x.batch.ts[0];
+  PrepAcc acc;
+  uint32_t k[kBktRounds], v[kBktRounds], x[kBktRounds];
+#pragma unroll
+  for (int r = 0; r < kBktRounds; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    const bool ok = idx < n_ext;
+    const int64_t li = ok ? idx : n_ext - 1;
+    uint64_t kk;
+    uint32_t f;
+    int32_t t32;
+    prep_row<FAST>(a, es, li, tbase, ok, kk, f, t32, acc);
+    k[r] = (uint32_t)kk;
+    v[r] = (f << kRowBits) | (uint32_t)li;
+    x[r] = (uint32_t)t32;
+  }
+  rs_scatter_tile<uint32_t, kBktRounds, true, true>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
+  prep_block_reduce<kRsBlock>(acc, blk, tile);
 }
 
 __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
@@ -385,7 +488,7 @@ struct ScanOut {
   unsigned long long steps;   // (partial, event) pairs examined
   unsigned long long pruned;  // open partials dropped by the horizon rule
   uint32_t violation;         // per-key timestamp decrease seen
-  uint32_t pad;
+  uint32_t hbm_walks;         // bucketed walk: partials walked on in HBM (lookahead too short)
 };
 // d_agg layout: PrepAgg at 0, ScanOut at 64, match / open totals at 128
 static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
@@ -477,7 +580,9 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       } else if (!f2_now) {
         const uint32_t fq = pv_flags(pq);
         if ((fq & F_NEW) && !(fq & F_SKIP)) {
-          if (tq < prev) {
+          // a per-key time regression only matters under `within` (expiry);
+          // without it the outcome of every partial is time-independent
+          if (a.within != INT64_MAX && tq < prev) {
             viol = 1;
             stop = true;
             break;
@@ -770,7 +875,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     int64_t before = __shfl_up(m, 1, 64);
     if (lane == 0) before = INT64_MIN;
     before = before > prev ? before : prev;
-    const bool vio = isnew && tq < before;
+    const bool vio = isnew && a.within != INT64_MAX && tq < before;
     const bool expire = isnew && !vio && tq - tsi > a.within;
     const uint64_t stopm = __ballot(!inb || endkey || vio || expire);
     const int sidx = stopm ? __ffsll((unsigned long long)stopm) - 1 : 64;
@@ -1006,6 +1111,263 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
   scan_block_reduce(steps, pruned, viol, nm, no, blk, slot0 + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
 }
 
+// ---------------------------------------------------------------- bucketed time-local walk
+// Sparse keys under `within` (config P3: 10M keys, ~0.01 events of a key per
+// `within` span).  The push is split by ONE stable hashed pass into 256
+// buckets (low 8 bits of key_bucket_mix(key)); inside a bucket positions keep
+// arrival order, which is time order (checked: the push is globally
+// time-ordered and carried partials precede it).  A partial can only complete
+// or expire on an event at most `within` later, so a workgroup takes a chunk of
+// one bucket's positions plus the bucket events up to `within` past the
+// chunk's last one, stages them in LDS, groups them by key with a second hash
+// level in LDS (1024 sub-buckets), and resolves every partial of the chunk
+// against its own key's later events there:
+//   expiry  at the first same-key event with ts - tsi > within,
+//   match   at the first same-key B event inside `within` with f2 true,
+// whichever comes first (the sequential walk's outcome; a key's events are in
+// time order).  A partial whose key has no such event in the staged region is
+// open (the bucket ends there), retired (the region already reaches beyond
+// `within`: every later event would expire it, the horizon rule), or --
+// rarely, when the staged lookahead was too short -- walked on in HBM over
+// the bucket (walk_partial, hashed-bucket stepping).
+// Bytes: one read of the bucketed (key, ts32, flags|row) per position plus
+// the lookahead overlap, instead of the three LSD passes of a full key sort.
+constexpr int kBwThreads = 512;
+constexpr int kBwEntries = 4096;   // staged positions per chunk (owned + lookahead)
+constexpr int kBwSub = 1024;       // LDS sub-buckets (bits 8..17 of key_bucket_mix)
+constexpr int kBuckets = 256;
+
+struct BktArgs {
+  ScanArgs s;
+  const PrepAgg* pg;        // device: batch time range (t_end = ts_max)
+  const uint32_t* dtot;     // positions per bucket (digit totals of the hashed pass)
+  int ch;                   // owned positions per chunk
+  int la;                   // lookahead capacity (ch + la <= kBwEntries)
+  int g2;                   // workgroups per bucket
+};
+
+template <bool FAST>
+__global__ __launch_bounds__(kBwThreads) void k_bkt_walk(const BktArgs* __restrict__ ap, int64_t n_ext,
+                                                        const uint32_t* __restrict__ skey,
+                                                        const uint32_t* __restrict__ spv,
+                                                        const int32_t* __restrict__ sts,
+                                                        int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                        ScanOut* __restrict__ blk) {
+  const BktArgs& A = *ap;
+  const ScanArgs& a = A.s;
+  const DExprSet es = a.es;
+  __shared__ uint32_t lkey[kBwEntries];
+  __shared__ int32_t lts[kBwEntries];
+  __shared__ uint32_t lpv[kBwEntries];
+  __shared__ uint16_t lslot[kBwEntries];
+  __shared__ uint16_t lperm[kBwEntries];
+  __shared__ uint32_t cnt[kBwSub + 1];
+  __shared__ uint32_t wsum[kBwThreads / 64];
+  __shared__ int64_t sh_bounds[2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // XCD-aware: consecutive workgroup ids land on different XCDs; give the
+  // workgroups of one XCD neighbouring buckets
+  const int b = (int)(blockIdx.x % kBuckets);
+  const int g = (int)(blockIdx.x / kBuckets);
+  if (tid < 64) {
+    // bucket b spans [sum of the totals of buckets < b, + its own total)
+    uint64_t pre = 0;
+    for (int d = lane; d < kBuckets; d += 64) pre += d < b ? A.dtot[d] : 0u;
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0) {
+      sh_bounds[0] = (int64_t)pre;
+      sh_bounds[1] = (int64_t)pre + A.dtot[b];
+    }
+  }
+  __syncthreads();
+  const int64_t bs = sh_bounds[0], be = sh_bounds[1];
+  const int64_t tbase = a.x.batch.ts[0];
+  const int64_t t_end = (int64_t)A.pg->ts_max;
+  const int64_t W = a.within;
+  const GlobalPos<false, false> ld{skey, nullptr, spv, sts, nullptr, tbase, 1};
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0, hw = 0;
+  for (int64_t p0 = bs + (int64_t)g * A.ch; p0 < be; p0 += (int64_t)A.g2 * A.ch) {
+    const int64_t p1 = p0 + A.ch < be ? p0 + A.ch : be;
+    const int64_t pl = p1 + A.la < be ? p1 + A.la : be;
+    const int nown = (int)(p1 - p0), nreg = (int)(pl - p0);
+    __syncthreads();   // the previous chunk's LDS readers are done
+    for (int i = tid; i < nreg; i += kBwThreads) {
+      lkey[i] = skey[p0 + i];
+      lts[i] = sts[p0 + i];
+      lpv[i] = spv[p0 + i];
+    }
+    for (int i = tid; i <= kBwSub; i += kBwThreads) cnt[i] = 0;
+    __syncthreads();
+    // events (batch rows with a key) go into their sub-bucket (unordered)
+    for (int i = tid; i < nreg; i += kBwThreads) {
+      const uint32_t f = pv_flags(lpv[i]);
+      if ((f & F_NEW) && !(f & F_SKIP)) {
+        const uint32_t d2 = (key_bucket_mix(lkey[i]) >> 8) & (kBwSub - 1);
+        lslot[i] = (uint16_t)atomicAdd(&cnt[d2], 1u);
+      }
+    }
+    __syncthreads();
+    {
+      // exclusive scan of the sub-bucket counts (two per thread)
+      const uint32_t c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
+      uint32_t inc = c0 + c1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t pre = inc - c0 - c1, tot = 0;
+#pragma unroll
+      for (int k = 0; k < kBwThreads / 64; k++) {
+        if (k < w) pre += wsum[k];
+        tot += wsum[k];
+      }
+      __syncthreads();
+      cnt[2 * tid] = pre;
+      cnt[2 * tid + 1] = pre + c0;
+      if (tid == 0) cnt[kBwSub] = tot;
+    }
+    __syncthreads();
+    for (int i = tid; i < nreg; i += kBwThreads) {
+      const uint32_t f = pv_flags(lpv[i]);
+      if ((f & F_NEW) && !(f & F_SKIP)) {
+        const uint32_t d2 = (key_bucket_mix(lkey[i]) >> 8) & (kBwSub - 1);
+        lperm[cnt[d2] + lslot[i]] = (uint16_t)i;
+      }
+    }
+    __syncthreads();
+    const int64_t treg = tbase + (int64_t)lts[nreg - 1];   // time of the last staged position
+    for (int li = tid; li < nown; li += kBwThreads) {
+      const uint32_t pv = lpv[li];
+      uint8_t out = PS_NONE;
+      if (pv_flags(pv) & F_CAND) {
+        const uint32_t k = lkey[li];
+        const int64_t tsi = tbase + (int64_t)lts[li];
+        const int64_t r = pv_row(pv);
+        const uint32_t d2 = (key_bucket_mix(k) >> 8) & (kBwSub - 1);
+        const int q0 = (int)cnt[d2], q1 = (int)cnt[d2 + 1];
+        int jd = kBwEntries, jm = kBwEntries;
+        for (int q = q0; q < q1; q++) {
+          const int e = lperm[q];
+          if (e <= li || lkey[e] != k) continue;
+          if (tbase + (int64_t)lts[e] - tsi > W) {
+            jd = e < jd ? e : jd;
+          } else if (e < jm && (pv_flags(lpv[e]) & F_B)) {
+            PairCtx cx{&a.x, r, (int64_t)pv_row(lpv[e]), a.s_first};
+            if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) jm = e;
+          }
+        }
+        const int term = jm < jd ? jm : jd;
+        for (int q = q0; q < q1; q++) {   // (partial, event) pairs the reference examines
+          const int e = lperm[q];
+          steps += (e > li && e <= term && lkey[e] == k) ? 1u : 0u;
+        }
+        if (jm < jd) {
+          out = PS_MATCH;
+          match_row[p0 + li] = (int32_t)pv_row(lpv[jm]);
+        } else if (jd < kBwEntries) {
+          out = PS_NONE;   // expired by a later event of its key
+        } else if (pl >= be) {
+          // no later event of its key in this push
+          if (a.prune && t_end - tsi > W) {
+            pruned++;
+          } else {
+            out = PS_OPEN;
+          }
+        } else if (treg - tsi > W) {
+          pruned++;   // every later event of the push is beyond `within` (t_end >= treg)
+        } else {
+          // lookahead too short: walk on over the bucket in HBM from pl
+          hw++;
+          int64_t q = pl;
+          uint32_t pq;
+          int64_t tq;
+          uint64_t kq;
+          ld(q, pq, tq, kq);
+          int32_t j = -1;
+          uint32_t fm = 0;
+          int64_t ra = -1, rb = -1;
+          uint64_t st2 = 0;
+          const uint8_t st = walk_partial<false, FAST, 4>(a, es, n_ext, ld, r, (uint64_t)k, tsi, q, pq, tq, kq, tsi,
+                                                          false, j, st2, viol, fm, ra, rb);
+          steps += st2;
+          if (st == ST_MATCH) {
+            out = PS_MATCH;
+            match_row[p0 + li] = j;
+          } else if (st == ST_OPEN) {
+            out = PS_OPEN;
+          } else if (st == ST_PRUNED) {
+            pruned++;
+          }
+        }
+      }
+      pst[p0 + li] = out;
+    }
+  }
+  // block partials of the scan counters (match / open counts: k_tile_count)
+  for (int o = 32; o > 0; o >>= 1) {
+    steps += __shfl_xor(steps, o, 64);
+    pruned += __shfl_xor(pruned, o, 64);
+    viol |= __shfl_xor(viol, o, 64);
+    hw += __shfl_xor(hw, o, 64);
+  }
+  __shared__ ScanOut wpart[kBwThreads / 64];
+  if (lane == 0) wpart[w] = ScanOut{steps, pruned, viol, hw};
+  __syncthreads();
+  if (tid == 0) {
+    ScanOut r = wpart[0];
+    for (int k = 1; k < kBwThreads / 64; k++) {
+      r.steps += wpart[k].steps;
+      r.pruned += wpart[k].pruned;
+      r.violation |= wpart[k].violation;
+      r.hbm_walks += wpart[k].hbm_walks;
+    }
+    blk[blockIdx.x] = r;
+  }
+}
+
+// Per-tile match / open counts of the outcome bytes (the compaction tiles of
+// k_emit_pairs / k_gather_carry): 16 bytes per thread per round.
+__global__ __launch_bounds__(kBlock) void k_tile_count(const uint8_t* __restrict__ pst, int64_t n, int64_t tile,
+                                                       uint32_t* __restrict__ bcnt) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  uint32_t nm = 0, no = 0;
+  for (int64_t pb = t0 + (int64_t)threadIdx.x * 16; pb < t1; pb += kBlock * 16) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
+    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t o = (wv[i >> 2] >> ((i & 3) * 8)) & 255u;
+      const bool in = pb + i < t1;
+      nm += (in && o == PS_MATCH) ? 1u : 0u;
+      no += (in && o == PS_OPEN) ? 1u : 0u;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    nm += __shfl_xor(nm, o, 64);
+    no += __shfl_xor(no, o, 64);
+  }
+  __shared__ uint32_t ws[2][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    ws[0][threadIdx.x >> 6] = nm;
+    ws[1][threadIdx.x >> 6] = no;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, b = 0;
+    for (int k = 0; k < kBlock / 64; k++) {
+      a += ws[0][k];
+      b += ws[1][k];
+    }
+    bcnt[blockIdx.x] = a;
+    bcnt[gridDim.x + blockIdx.x] = b;
+  }
+}
+
 // Stable compaction of one block's tile: position p with pst[p] == want gets
 // output index base + (# such positions before p in the tile).  Each thread
 // takes 16 consecutive outcome bytes per round (one 16-byte load; tiles start
@@ -1058,20 +1420,22 @@ __device__ __forceinline__ void tile_compact(const uint8_t* __restrict__ pst, in
 
 __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int nblk, ScanOut* out) {
   unsigned long long st = 0, pr = 0;
-  uint32_t v = 0;
+  uint32_t v = 0, hw = 0;
 #pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
     st += blk[b].steps;
     pr += blk[b].pruned;
     v |= blk[b].violation;
+    hw += blk[b].hbm_walks;
   }
   for (int o = 32; o > 0; o >>= 1) {
     st += __shfl_xor(st, o, 64);
     pr += __shfl_xor(pr, o, 64);
     v |= __shfl_xor(v, o, 64);
+    hw += __shfl_xor(hw, o, 64);
   }
   __shared__ ScanOut wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{st, pr, v, 0};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{st, pr, v, hw};
   __syncthreads();
   if (threadIdx.x == 0) {
     ScanOut r = wpart[0];
@@ -1079,6 +1443,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int 
       r.steps += wpart[w].steps;
       r.pruned += wpart[w].pruned;
       r.violation |= wpart[w].violation;
+      r.hbm_walks += wpart[w].hbm_walks;
     }
     *out = r;
   }
@@ -1383,6 +1748,7 @@ struct PatternEngine : Engine {
   // (time >= horizon) would expire them, later pushes must not go back before it
   bool have_horizon = false;
   int64_t horizon = INT64_MIN;
+  int64_t t_last = INT64_MIN;   // time of the last event (arrival order) of the committed pushes
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
@@ -1400,6 +1766,65 @@ struct PatternEngine : Engine {
     counters = shd_counters{};
     have_horizon = false;
     horizon = INT64_MIN;
+    t_last = INT64_MIN;
+  }
+
+  // Open partials as the A events that created them, in arrival order.  Each
+  // was processed by the reference against every later event without
+  // completing or expiring, so replaying just these events from a fresh state
+  // rebuilds the same pending lists (a replayed event j meets an earlier
+  // replayed partial i exactly as it did the first time: f2(i, j) false,
+  // |ts_j - ts_i| <= within).  Unpartitioned plans expire globally: partials
+  // further than `within` behind the latest event are already gone there.
+  void export_replay(Replay& r) override {
+    SHD_HIP(hipStreamSynchronize(stream));
+    const CarryTable& t = carry[cur];
+    r.stream = sA;
+    std::vector<int64_t> ts(C), sq(C);
+    if (C > 0) {
+      SHD_HIP(hipMemcpy(ts.data(), t.ts.p, C * 8, hipMemcpyDeviceToHost));
+      SHD_HIP(hipMemcpy(sq.data(), t.seq.p, C * 8, hipMemcpyDeviceToHost));
+    }
+    std::vector<std::vector<uint8_t>> col(typesA.size()), nul(typesA.size());
+    for (size_t c = 0; c < typesA.size(); c++) {
+      col[c].resize((size_t)C * type_size(typesA[c]));
+      nul[c].resize((size_t)C);
+      if (C > 0) {
+        SHD_HIP(hipMemcpy(col[c].data(), t.col[c].p, col[c].size(), hipMemcpyDeviceToHost));
+        SHD_HIP(hipMemcpy(nul[c].data(), t.nul[c].p, (size_t)C, hipMemcpyDeviceToHost));
+      }
+    }
+    if (logical == 2 && C > 0) {
+      std::vector<uint8_t> half(C);
+      SHD_HIP(hipMemcpy(half.data(), t.half.p, C, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < C; i++)
+        if (half[i])
+          throw Error(SHD_E_UNSUPPORTED,
+                      "pattern engine (and): timestamps go back while a partial holds one operand; the generic "
+                      "NFA engine cannot be seeded with half-filled partials");
+    }
+    std::vector<int64_t> idx;
+    for (int64_t i = 0; i < C; i++)
+      if (partitioned || W == INT64_MAX || t_last == INT64_MIN || !(t_last - ts[i] > W)) idx.push_back(i);
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return sq[a] < sq[b]; });
+    r.n = (int64_t)idx.size();
+    r.ts.resize(r.n);
+    r.cols.assign(typesA.size(), {});
+    r.nulls.assign(typesA.size(), {});
+    for (size_t c = 0; c < typesA.size(); c++) {
+      const int w = type_size(typesA[c]);
+      r.cols[c].resize((size_t)r.n * w);
+      r.nulls[c].resize((size_t)r.n);
+    }
+    for (int64_t k = 0; k < r.n; k++) {
+      const int64_t i = idx[k];
+      r.ts[k] = ts[i];
+      for (size_t c = 0; c < typesA.size(); c++) {
+        const int w = type_size(typesA[c]);
+        std::memcpy(r.cols[c].data() + k * w, col[c].data() + i * w, w);
+        r.nulls[c][k] = nul[c][i];
+      }
+    }
   }
 
   // open partials (carry table) + horizon guard
@@ -1498,6 +1923,224 @@ struct PatternEngine : Engine {
   }
 
   void push(const Staged& b) override {
+    if (b.n <= 0) return;
+    int la = 0;
+    int64_t t_last_probe = 0;
+    if (bucket_candidate(b, la, t_last_probe) && bucket_push(b, la, t_last_probe)) return;
+    sort_push(b);
+  }
+
+  // The bucketed time-local walk (k_bkt_walk) fits pushes whose keys are
+  // sparse inside one `within` span: the bucket events of one span (E_b =
+  // events per span / 256 buckets) must fit the LDS lookahead next to a chunk.
+  // Decided from the batch's first / last timestamps (one 16-byte probe);
+  // whether the push really is time-ordered (and carried partials precede it)
+  // is checked on the device and the push is redone on the sort path if not.
+  // SHD_NO_BUCKET (or a forced SHD_HASH_BITS sort): off; SHD_BUCKET: on
+  // whenever legal (tests).
+  bool bucket_candidate(const Staged& b, int& la, int64_t& t_last_probe) {
+    const int slot = b.stream == sA ? 0 : 1;
+    if (getenv("SHD_NO_BUCKET") || getenv("SHD_HASH_BITS") || logical != 0 || W == INT64_MAX || !(partitioned || implicit_key) ||
+        type_key64(key_type[slot]) || sA != sB)
+      return false;
+    const int64_t n_ext = C + b.n;
+    const bool forced = getenv("SHD_BUCKET") != nullptr;
+    if (!forced && n_ext < kPruneMinRows) return false;
+    h_agg.reserve(256);
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 208, b.cs.ts, 8, hipMemcpyDeviceToHost, stream));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 216, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, stream));
+    SHD_HIP(hipStreamSynchronize(stream));
+    int64_t t0, t1;
+    std::memcpy(&t0, h_agg.as<char>() + 208, 8);
+    std::memcpy(&t1, h_agg.as<char>() + 216, 8);
+    if (t1 < t0) return false;
+    const double span = (double)(t1 - t0) + 1.0;
+    const double eb = std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span) / kBuckets;
+    const double need = eb + 4.0 * std::sqrt(eb) + 64.0;
+    if (need > kBwEntries / 2) return false;
+    la = (int)std::min<double>(kBwEntries / 2, std::ceil(need / 64.0) * 64.0);
+    t_last_probe = t1;
+    return true;
+  }
+
+  bool bucket_push(const Staged& b, int la, int64_t t_last_probe) {
+    const int64_t n = b.n;
+    const bool isA = b.stream == sA, isB = b.stream == sB;
+    const int64_t n_ext = C + n;
+    if (n_ext > (int64_t)kRowMask) throw Error(SHD_E_CAPACITY, "pattern batch + carried partials exceed 2^28 rows");
+    hipStream_t s = stream;
+    SHD_HIP(hipEventRecord(ev0, s));
+    stage_begin();
+    const int slot = isA ? 0 : 1;
+    d_pv.reserve(n_ext * 4);
+    d_ts.reserve(n_ext * 4);
+    d_k32.reserve(n_ext * 4);
+    d_match.reserve(n_ext * 4);
+    d_pst.reserve(n_ext + kCompactPad);
+    d_agg.reserve(256);
+    h_agg.reserve(256);
+    ExtRows x{};
+    x.carry = carry_cs();
+    x.batch = b.cs;
+    x.C = C;
+    x.seq0 = seq;
+    x.carry_seq = carry[cur].seq.as<int64_t>();
+    PrepArgs pa{};
+    pa.x = x;
+    pa.es = dset();
+    pa.f1 = dfilters(f1);
+    pa.is_a = isA;
+    pa.is_b = isB;
+    pa.partitioned = 1;
+    pa.null_skip = partitioned;
+    pa.key64 = 0;
+    if (key_expr[slot] >= 0) pa.key_expr = dexpr(key_expr[slot]);
+    pa.key_col = key_col[slot];
+    pa.key_type = key_type[slot];
+    pa.carry_key = carry[cur].key.as<uint64_t>();
+    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN, ULLONG_MAX};
+    PrepAgg* d_pa = d_agg.as<PrepAgg>();
+    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
+    std::memcpy(h_agg.p, &init, sizeof(init));
+    std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
+    SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
+    const int nblk = grid_for(n_ext, 1, 4096);
+    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
+    const int ntile = (int)ceil_div(n_ext, tile);
+    const int g2 = (int)std::max<int64_t>(1, ceil_div(ceil_div(n_ext, kBuckets), kBwEntries - la));
+    const int nwalk = kBuckets * g2;
+    const int nbt = (int)ceil_div(n_ext, rs_tile(kBktRounds));   // fused scatter tiles
+    d_blk.reserve((size_t)std::max<int64_t>(std::max(3 * nblk, nbt), nwalk) *
+                  std::max(sizeof(PrepAgg), sizeof(ScanOut)));
+    const PrepArgs* d_pa_args = dev_args(pa);
+    const bool fast1 = (!isA || pa.f1.fp.ok) && pa.key_col >= 0;
+    const uint32_t* skey32;
+    const uint32_t* spv;
+    const int32_t* sts32;
+    const uint32_t* dtot;
+    if (pa.key_col >= 0 && !getenv("SHD_BUCKET_UNFUSED")) {
+      // fused: hist of the key column, then prepare + scatter in one pass
+      d_k32_alt.reserve(n_ext * 4);
+      d_pv_alt.reserve(n_ext * 4);
+      d_ts_alt.reserve(n_ext * 4);
+      d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
+      uint32_t* hist = d_sort.as<uint32_t>();
+      uint32_t* offs = hist + (int64_t)nbt * 256;
+      uint32_t* tot = offs + (int64_t)nbt * 256;
+      hipLaunchKernelGGL(k_bkt_hist, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
+      SHD_CHECK_LAUNCH();
+      radix_digit_scan(hist, nbt, offs, tot, s);
+      if (fast1)
+        hipLaunchKernelGGL(k_bkt_scatter<true>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
+                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                           d_blk.as<PrepAgg>());
+      else
+        hipLaunchKernelGGL(k_bkt_scatter<false>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
+                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                           d_blk.as<PrepAgg>());
+      SHD_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
+      SHD_CHECK_LAUNCH();
+      skey32 = d_k32_alt.as<uint32_t>();
+      spv = d_pv_alt.as<uint32_t>();
+      sts32 = d_ts_alt.as<int32_t>();
+      dtot = tot;
+      mark("bucket_scatter");
+    } else {
+    if (fast1)
+      hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
+    else
+      hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
+    SHD_CHECK_LAUNCH();
+    mark("prepare");
+    // one stable hashed pass: 256 buckets, arrival order inside a bucket
+    d_k32_alt.reserve(n_ext * 4);
+    d_pv_alt.reserve(n_ext * 4);
+    d_ts_alt.reserve(n_ext * 4);
+    bool in_alt = false;
+    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
+                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, 8, d_sort, s, in_alt, true, 0);
+    skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
+    spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
+    sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
+    dtot = radix_digit_totals(d_sort, n_ext);
+    mark("bucket_sort");
+    }
+    ScanArgs sa{};
+    sa.x = x;
+    sa.es = dset();
+    sa.f2 = dfilters(f2);
+    sa.logical = 0;
+    sa.s_first = s_first;
+    sa.s_second = s_second;
+    sa.within = W;
+    sa.partitioned = 1;
+    sa.prune = 1;
+    sa.hash_mask = kBuckets - 1;
+    sa.t_end = t_last_probe;   // the push is time-ordered (else redone): its last event is its latest
+    BktArgs ba{};
+    ba.s = sa;
+    ba.pg = d_pa;
+    ba.dtot = dtot;
+    ba.ch = kBwEntries - la;
+    ba.la = la;
+    ba.g2 = g2;
+    const BktArgs* d_ba = dev_args(ba);
+    if (sa.f2.fp.ok)
+      hipLaunchKernelGGL(k_bkt_walk<true>, dim3(nwalk), dim3(kBwThreads), 0, s, d_ba, n_ext, skey32, spv, sts32,
+                         d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>());
+    else
+      hipLaunchKernelGGL(k_bkt_walk<false>, dim3(nwalk), dim3(kBwThreads), 0, s, d_ba, n_ext, skey32, spv, sts32,
+                         d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>());
+    SHD_CHECK_LAUNCH();
+    d_bcnt.reserve((size_t)2 * ntile * 4);
+    d_boff.reserve((size_t)2 * ntile * 4);
+    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
+                       d_bcnt.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
+    SHD_CHECK_LAUNCH();
+    mark("bucket_walk");
+    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    mark("compact");
+    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 144, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    PrepAgg pg;
+    ScanOut so;
+    std::memcpy(&pg, h_agg.p, sizeof(pg));
+    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
+    const uint32_t m = h_agg.as<uint32_t>()[32];
+    const uint32_t n_open = h_agg.as<uint32_t>()[33];
+    // the walk assumed a time-ordered push after its carried partials, 32-bit
+    // time offsets and no retirement horizon behind it: else redo on the sort path
+    if (pg.unmono || pg.ovf || (C > 0 && pg.carry_tmax > pg.ts_min) || (have_horizon && pg.ts_min < horizon) ||
+        so.violation)
+      return false;
+    const int64_t t_end = (int64_t)pg.ts_max;
+    if (so.pruned) {
+      have_horizon = true;
+      horizon = std::max(horizon, t_end);
+    }
+    counters.group_bits = 8;
+    if (getenv("SHD_DEBUG_BUCKET"))
+      fprintf(stderr, "bucket push: n_ext %lld la %d ch %d g2 %d hbm_walks %u pruned %llu steps %llu\n",
+              (long long)n_ext, la, kBwEntries - la, g2, so.hbm_walks, so.pruned, so.steps);
+    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
+    return true;
+  }
+
+  void sort_push(const Staged& b) {
     const int64_t n = b.n;
     if (n <= 0) return;
     const bool isA = b.stream == sA, isB = b.stream == sB;
@@ -1584,7 +2227,6 @@ struct PatternEngine : Engine {
       throw Error(SHD_E_UNSUPPORTED,
                   "pattern engine: an event precedes the pruning horizon of an earlier push (timestamps must not "
                   "go back across pushes once partials were retired)");
-    counters.partials += (int64_t)pg.n_cand;
 
     // ---- key-sort the extended batch (stable: creation order within a key),
     //      carrying the packed (flags, row) payload and the event timestamp
@@ -1777,20 +2419,30 @@ struct PatternEngine : Engine {
     scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
     mark("compact");
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
+    // time of the push's last event in arrival order (NeedNfa hand-over: global expiry of unpartitioned plans)
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     ScanOut so;
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];
     const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    if (so.violation)
-      throw Error(SHD_E_UNSUPPORTED,
-                  "pattern engine: event timestamps decrease within a key; the forward-scan formulation "
-                  "requires per-key non-decreasing timestamps");
+    if (so.violation)   // the generic NFA engine takes over (shd_push replays the open partials)
+      throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
     if (so.pruned) {
       have_horizon = true;
       horizon = std::max(horizon, t_end);
     }
+    finish(b, x, n_ext, tile, ntile, spv, skey32, skey64, sorted64, keyed, grouped, key64, m, n_open, so, t_end,
+           pg.n_cand);
+  }
 
+  // Shared tail of a push: matches in (e2 event, creation) order -> projected
+  // output rows; still-open partials -> the next push's carry; commit.
+  void finish(const Staged& b, const ExtRows& x, int64_t n_ext, int64_t tile, int ntile, const uint32_t* spv,
+              const uint32_t* skey32, const uint64_t* skey64, bool sorted64, bool keyed, bool grouped, bool key64,
+              uint32_t m, uint32_t n_open, const ScanOut& so, int64_t t_end, uint64_t n_cand) {
+    hipStream_t s = stream;
+    const int64_t n = b.n;
     // ---- matches ordered by (e2 event, creation) -> projected output rows
     if (m > 0) {
       d_pj.reserve((int64_t)m * 4);
@@ -1889,12 +2541,15 @@ struct PatternEngine : Engine {
     C = n_open;
     seq += n;
     if (b.advance_time && t_end > now) now = t_end;
+    std::memcpy(&t_last, h_agg.as<char>() + 192, 8);
     counters.events += n;
     counters.matches += m;
     counters.partial_scans += (int64_t)so.steps;
     counters.carry = C;
     counters.kernel_ns = (int64_t)(ms * 1e6);
+      counters.partials += (int64_t)n_cand;
   }
+
 };
 
 std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, const PNode& b, const PNode* c,

@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "radix_tile.h"
 
 namespace shd {
 
@@ -120,47 +121,7 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* 
 }
 
 // ============================================================ radix sort
-// One workgroup (kRsBlock threads, kRsWaves waves) sorts a tile of
-// R*kRsBlock keys per pass.  Wave w owns the contiguous slice
-// [t0 + w*64R, t0 + (w+1)*64R) and holds its R keys per lane in registers
-// (all loads issued up front).  Stable in-wave ranking from eight 64-bit
-// ballots per round and a per-wave running count per digit in LDS (the wave
-// executes in order, so no barrier between rounds); a tile needs four
-// workgroup barriers.  The tile is reordered by digit in LDS and written out
-// in per-digit runs, so consecutive lanes store consecutive addresses.
-// Optional second payload: a 32-bit word per key.
-#ifndef SHD_RS_ROUNDS
-#define SHD_RS_ROUNDS 24
-#endif
-#ifndef SHD_RS_BLOCK
-#define SHD_RS_BLOCK 256
-#endif
-constexpr int kRsRounds = SHD_RS_ROUNDS;
-constexpr int kRsBlock = SHD_RS_BLOCK;
-constexpr int kRsWaves = kRsBlock / 64;
-static_assert(kRsBlock >= 256 && kRsBlock % 64 == 0, "one thread per digit in the digit phases");
-
-__host__ __device__ constexpr int rs_tile(int rounds) { return kRsBlock * rounds; }
-
-// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
-// (blocks b and b+8 share one), so block b takes tile (b%8)*per + b/8: the
-// tiles of one XCD are consecutive, and the per-digit runs that neighbouring
-// tiles write next to each other meet in the same L2 (fewer partial-line
-// write-backs).  Any bijection is correct; this one is for speed only.
-__device__ __forceinline__ int rs_tile_of(int b, int nb) {
-  const int per = nb >> 3, rem = nb & 7, x = b & 7, i = b >> 3;
-  return x * per + (x < rem ? x : rem) + i;
-}
-
-template <class K>
-__device__ __forceinline__ uint32_t rs_digit(K k, int shift) { return (uint32_t)((k >> shift) & 255u); }
-// H: digits of key_bucket_mix(key) (hashed bucket sort; 32-bit keys only).
-// kb: key base subtracted first (the keys of a push span [kb, kb + 2^bits)).
-template <bool H, class K>
-__device__ __forceinline__ uint32_t rs_hdigit(K k, int shift, K kb) {
-  if constexpr (H) return (key_bucket_mix((uint32_t)k) >> shift) & 255u;
-  else return rs_digit((K)(k - kb), shift);
-}
+// (tile constants, digit helpers and the in-tile scatter: radix_tile.h)
 
 template <class K, int R, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const K* __restrict__ keys, int64_t n, int shift,
@@ -261,21 +222,13 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
                                                          const uint32_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ dtotal, int nb, int xcd,
                                                          K kb) {
-  constexpr int T = rs_tile(R);
-  __shared__ K sk[T];
-  __shared__ uint32_t sv[T];
-  __shared__ uint32_t sw[P2 ? T : 1];
-  __shared__ uint32_t lpre[256];             // tile-local first position of each digit
-  __shared__ uint32_t gbase[256];            // global first position of this tile's digit run
-  __shared__ uint32_t wcnt[kRsWaves][256];   // per-wave running digit counts, then per-wave digit bases
-  __shared__ uint32_t wsum[4], dsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = xcd ? rs_tile_of(blockIdx.x, nb) : (int)blockIdx.x;
-  const int64_t t0 = (int64_t)tile * T;
+  const int64_t t0 = (int64_t)tile * rs_tile(R);
   const int64_t wb = t0 + (int64_t)w * 64 * R;
   // this tile's histogram column and global digit offsets are loaded first:
-  // the digit prefix below then waits only for them, while the key loads
-  // issued after them are still in flight (in-order vmcnt)
+  // the digit prefix then waits only for them, while the key loads issued
+  // after them are still in flight (in-order vmcnt)
   const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
   const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
   const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
@@ -290,93 +243,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
     v[r] = vin[li];
     if (P2) x[r] = win[li];
   }
-  for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&wcnt[0][0])[i] = 0;
-  {
-    // tile-local exclusive prefix over digits (threads 0..255, one digit
-    // each), and the global base of each digit (prefix of the digit totals)
-    uint32_t inc = c, dinc = dt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      const uint32_t u = __shfl_up(dinc, o, 64);
-      if (lane >= o) {
-        inc += t;
-        dinc += u;
-      }
-    }
-    if (lane == 63 && w < 4) {
-      wsum[w] = inc;
-      dsum[w] = dinc;
-    }
-    __syncthreads();
-    if (tid < 256) {
-      uint32_t pre = 0, dpre = 0;
-      for (int i = 0; i < w; i++) {
-        pre += wsum[i];
-        dpre += dsum[i];
-      }
-      lpre[tid] = pre + inc - c;
-      gbase[tid] = dpre + dinc - dt + gr;
-    }
-  }
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint32_t lr[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const bool ok = wb + r * 64 + lane < n;
-    const uint32_t d = rs_hdigit<H>(k[r], shift, kb);
-    uint64_t peers = __ballot(ok);
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    const uint64_t below = peers & lt;
-    const uint32_t c = wcnt[w][d];
-    lr[r] = c + (uint32_t)__popcll(below);
-    __builtin_amdgcn_wave_barrier();
-    if (ok && below == 0) wcnt[w][d] = c + (uint32_t)__popcll(peers);
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (tid < 256) {
-    uint32_t acc = lpre[tid];
-#pragma unroll
-    for (int i = 0; i < kRsWaves; i++) {
-      const uint32_t c = wcnt[i][tid];
-      wcnt[i][tid] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    if (wb + r * 64 + lane < n) {
-      const uint32_t pos = wcnt[w][rs_hdigit<H>(k[r], shift, kb)] + lr[r];
-      sk[pos] = k[r];
-      sv[pos] = v[r];
-      if (P2) sw[pos] = x[r];
-    }
-  }
-  __syncthreads();
-  const int tile_n = n - t0 < T ? (int)(n - t0) : T;
-#pragma unroll 4
-  for (int i = tid; i < tile_n; i += kRsBlock) {
-    const K kk = sk[i];
-    const uint32_t d = rs_hdigit<H>(kk, shift, kb);
-#if defined(SHD_RS_EXP) && SHD_RS_EXP == 1   // timing experiment: coalesced identity write-out
-    const uint32_t o = (uint32_t)(t0 + i) + 0 * (gbase[d] - lpre[d]);
-#elif defined(SHD_RS_EXP) && SHD_RS_EXP == 2   // timing experiment: no write-out
-    const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
-    if (i != 0) continue;
-#else
-    const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
-#endif
-    kout[o] = kk;
-    vout[o] = sv[i];
-    if (P2) wout[o] = sw[i];
-  }
+  rs_scatter_tile<K, R, P2, H>(k, v, x, n, t0, wb, shift, c, gr, dt, kb, kout, vout, wout);
 }
 
 template <class K, int R, bool P2, bool H = false>
@@ -412,6 +279,16 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
     std::swap(wi, wo);
     in_alt = !in_alt;
   }
+}
+
+void radix_digit_scan(const uint32_t* hist, int nb, uint32_t* offs, uint32_t* dtot, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_digit_scan, dim3(256), dim3(kRsBlock), 0, s, hist, nb, offs, dtot);
+  SHD_CHECK_LAUNCH();
+}
+
+const uint32_t* radix_digit_totals(const DevBuf& scratch, int64_t n) {
+  const int64_t nh = ceil_div(n, rs_tile(kRsRounds)) * 256;   // scratch layout of radix_sort_run
+  return scratch.as<uint32_t>() + 2 * nh;
 }
 
 void radix_sort_pairs_u32(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int64_t n,

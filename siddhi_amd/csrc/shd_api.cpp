@@ -414,6 +414,17 @@ bool compile_fast_pred(const Plan& p, const std::vector<int>& ids, FPred& out) {
   return true;
 }
 
+void init_engine(Engine& e, const Plan& p) {
+  e.plan = p;
+  e.ex.upload(p);
+  e.out.init((int)p.outputs.size());
+  e.on_loaded();
+  SHD_HIP(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+  SHD_HIP(hipEventCreate(&e.ev0));
+  SHD_HIP(hipEventCreate(&e.ev1));
+  e.reset();
+}
+
 DFilters Engine::dfilters(const std::vector<int>& ids) const {
   DFilters f{};
   f.n = (int)ids.size();
@@ -471,6 +482,107 @@ int guarded(F&& f) {
 }
 }  // namespace
 
+namespace {
+
+// Copy host columns of one stream into device buffers (stream ordered, through
+// pinned memory); the caller's buffers may be pageable and are only valid for
+// the duration of the call.
+void stage_host(hipStream_t s, PinnedBuf& pin, DevBuf& dts, DevBuf* dcol, DevBuf* dnul, const shd_batch* b,
+                const std::vector<int>& types, Staged& st) {
+  SHD_HIP(hipStreamSynchronize(s));   // the previous use of the pinned area has drained
+  size_t total = (size_t)b->n * 8;
+  for (int c = 0; c < b->ncols; c++) {
+    total += (size_t)b->n * type_size(types[c]) + 64;
+    if (b->nulls && b->nulls[c]) total += (size_t)b->n + 64;
+  }
+  pin.reserve(total + 64);
+  char* hp = pin.as<char>();
+  size_t used = 0;
+  auto stage = [&](DevBuf& dst, const void* src, size_t bytes) -> void* {
+    dst.reserve(bytes);
+    std::memcpy(hp + used, src, bytes);
+    SHD_HIP(hipMemcpyAsync(dst.p, hp + used, bytes, hipMemcpyHostToDevice, s));
+    used += (bytes + 63) & ~size_t(63);
+    return dst.p;
+  };
+  st.cs.ts = (const int64_t*)stage(dts, b->ts, (size_t)b->n * 8);
+  for (int c = 0; c < b->ncols; c++) {
+    st.cs.col[c] = stage(dcol[c], b->cols[c], (size_t)b->n * type_size(types[c]));
+    st.cs.type[c] = (int8_t)types[c];
+    st.cs.nul[c] = (b->nulls && b->nulls[c]) ? (const uint8_t*)stage(dnul[c], b->nulls[c], (size_t)b->n) : nullptr;
+  }
+}
+
+// The running engine hit a valid input its formulation cannot process
+// (NeedNfa): rebuild its open partial matches in a fresh generic NFA engine
+// by replaying the events that created them, carry over unpolled output and
+// the query's counters, then run the push there.  The query stays on the NFA
+// engine from then on.
+void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, const std::string& why) {
+  Engine& old = *q->eng;
+  Replay r;
+  old.export_replay(r);
+  std::string w2;
+  std::unique_ptr<Engine> ne = make_nfa_engine(old.plan, w2, r.n + st.n);
+  if (!ne) throw Error(SHD_E_UNSUPPORTED, why + "; the generic NFA engine does not take this plan: " + w2);
+  init_engine(*ne, old.plan);
+  if (r.n > 0) {
+    const auto& types = old.plan.stream_types[r.stream];
+    std::vector<const void*> cp(types.size());
+    std::vector<const uint8_t*> np(types.size());
+    for (size_t c = 0; c < types.size(); c++) {
+      cp[c] = r.cols[c].data();
+      np[c] = r.nulls[c].data();
+    }
+    shd_batch rb{};
+    rb.stream = r.stream;
+    rb.mem = SHD_MEM_HOST;
+    rb.n = r.n;
+    rb.ts = r.ts.data();
+    rb.ncols = (int32_t)types.size();
+    rb.cols = cp.data();
+    rb.nulls = np.data();
+    Staged rs;
+    rs.stream = r.stream;
+    rs.n = r.n;
+    rs.call_offsets = {0, r.n};
+    rs.advance_time = false;
+    rs.cs.ncols = rb.ncols;
+    rs.cs.n = r.n;
+    PinnedBuf pin;
+    DevBuf dts, dcol[kMaxCols], dnul[kMaxCols];
+    stage_host(ne->stream, pin, dts, dcol, dnul, &rb, types, rs);
+    ne->args_begin();
+    ne->push(rs);
+    SHD_HIP(hipStreamSynchronize(ne->stream));
+    if (ne->out.count != 0) throw Error(SHD_E_DEVICE, "internal: replaying the open partials produced output");
+  }
+  // unpolled rows of earlier pushes stay ahead of this push's rows
+  if (old.out.count > 0) {
+    const int64_t m = old.out.count;
+    const int w = std::max(old.out.ncols, 1);
+    ne->out.ensure(m, ne->stream);
+    SHD_HIP(hipMemcpyAsync(ne->out.chunk.p, old.out.chunk.p, m * 8, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.type.p, old.out.type.p, m * 4, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.ts.p, old.out.ts.p, m * 8, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.vals.p, old.out.vals.p, m * w * 8, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.nulls.p, old.out.nulls.p, m * w, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipStreamSynchronize(ne->stream));
+    ne->out.count = m;
+  }
+  ne->seq = old.seq;
+  ne->now = old.now;
+  ne->chunk_seq = old.chunk_seq;
+  const int64_t carry = ne->counters.carry;
+  ne->counters = before;
+  ne->counters.carry = carry;
+  q->eng = std::move(ne);
+  q->eng->args_begin();
+  q->eng->push(st);
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* shd_last_error(void) { return g_err.c_str(); }
@@ -526,14 +638,7 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
       e = make_single_engine(p, why2);
     }
     if (!e) return fail(SHD_E_UNSUPPORTED, "plan outside the device path: " + why1 + why2);
-    e->plan = p;
-    e->ex.upload(p);
-    e->out.init((int)p.outputs.size());
-    e->on_loaded();
-    SHD_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    SHD_HIP(hipEventCreate(&e->ev0));
-    SHD_HIP(hipEventCreate(&e->ev1));
-    e->reset();
+    init_engine(*e, p);
     auto* q = new shd_query();
     q->ctx = ctx;
     q->eng = std::move(e);
@@ -609,41 +714,17 @@ int shd_push(shd_query* q, const shd_batch* b) {
         st.cs.type[c] = (int8_t)types[c];
       }
     } else {
-      // Host batches: copy into library-owned pinned memory (the caller's
-      // buffers may be pageable and are only valid until we return), then
-      // H2D on the query's stream.  The previous push's copies must have
-      // drained before the pinned area is reused.
-      hipStream_t s = e.stream;
-      SHD_HIP(hipStreamSynchronize(s));
-      size_t total = (size_t)b->n * 8;
-      for (int c = 0; c < b->ncols; c++) {
-        total += (size_t)b->n * type_size(types[c]) + 64;
-        if (b->nulls && b->nulls[c]) total += (size_t)b->n + 64;
-      }
-      q->pin.reserve(total + 64);
-      char* hp = q->pin.as<char>();
-      size_t used = 0;
-      auto stage = [&](DevBuf& dst, const void* src, size_t bytes) -> void* {
-        dst.reserve(bytes);
-        std::memcpy(hp + used, src, bytes);
-        SHD_HIP(hipMemcpyAsync(dst.p, hp + used, bytes, hipMemcpyHostToDevice, s));
-        used += (bytes + 63) & ~size_t(63);
-        return dst.p;
-      };
-      st.cs.ts = (const int64_t*)stage(q->stage_ts, b->ts, (size_t)b->n * 8);
-      for (int c = 0; c < b->ncols; c++) {
-        size_t bytes = (size_t)b->n * type_size(types[c]);
-        st.cs.col[c] = stage(q->stage_col[c], b->cols[c], bytes);
-        st.cs.type[c] = (int8_t)types[c];
-        if (b->nulls && b->nulls[c]) {
-          st.cs.nul[c] = (const uint8_t*)stage(q->stage_nul[c], b->nulls[c], (size_t)b->n);
-        } else {
-          st.cs.nul[c] = nullptr;
-        }
-      }
+      // Host batches: copy into library-owned pinned memory, then H2D on the
+      // query's stream.
+      stage_host(e.stream, q->pin, q->stage_ts, q->stage_col, q->stage_nul, b, types, st);
     }
+    const shd_counters before = e.counters;
     e.args_begin();
-    e.push(st);
+    try {
+      e.push(st);
+    } catch (NeedNfa& nf) {
+      switch_to_nfa(q, st, before, nf.what());
+    }
     return SHD_OK;
   });
 }
@@ -748,29 +829,70 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
   });
 }
 
+// Common fields + engine section of an image, from after the header.
+static void load_image(Engine& e, SnapR& r) {
+  e.reset();
+  const int64_t seq = r.get<int64_t>(), now = r.get<int64_t>(), chunk = r.get<int64_t>();
+  const shd_counters c = r.get<shd_counters>();
+  e.load_state(r);
+  if (r.at != r.n) throw Error(SHD_E_ARG, "trailing bytes in snapshot");
+  e.seq = seq;
+  e.now = now;
+  e.chunk_seq = chunk;
+  e.counters = c;
+  e.out.count = 0;
+}
+
 int shd_restore(shd_query* q, const void* data, size_t len) {
   return guarded([&]() -> int {
     if (!q || (!data && len)) return fail(SHD_E_ARG, "null argument");
-    Engine& e = *q->eng;
-    SHD_HIP(hipStreamSynchronize(e.stream));
+    Engine& cur = *q->eng;
+    SHD_HIP(hipStreamSynchronize(cur.stream));
     SnapR r;
     r.p = (const uint8_t*)data;
     r.n = len;
-    r.s = e.stream;
+    r.s = cur.stream;
     if (r.get<uint32_t>() != kSnapMagic || r.get<uint32_t>() != kSnapVersion)
       return fail(SHD_E_ARG, "not a libsiddhi_hip snapshot (or another version)");
-    if (r.get<int32_t>() != e.kind() || r.get<uint64_t>() != q->plan_hash)
-      return fail(SHD_E_ARG, "snapshot was taken from a different plan");
-    e.reset();
-    const int64_t seq = r.get<int64_t>(), now = r.get<int64_t>(), chunk = r.get<int64_t>();
-    const shd_counters c = r.get<shd_counters>();
-    e.load_state(r);
-    if (r.at != r.n) return fail(SHD_E_ARG, "trailing bytes in snapshot");
-    e.seq = seq;
-    e.now = now;
-    e.chunk_seq = chunk;
-    e.counters = c;
-    e.out.count = 0;
+    const int kind = r.get<int32_t>();
+    if (r.get<uint64_t>() != q->plan_hash) return fail(SHD_E_ARG, "snapshot was taken from a different plan");
+    if (kind != cur.kind()) {
+      // the image comes from the other engine of this plan (a pattern query
+      // that switched to the generic NFA engine, or the reverse): restore
+      // into a fresh engine of that kind; a bad image leaves q untouched
+      std::string why;
+      std::unique_ptr<Engine> fresh;
+      if (kind == ENG_NFA) fresh = make_nfa_engine(cur.plan, why);
+      else if (kind == ENG_PATTERN) {
+        fresh = make_pattern_engine(cur.plan, why);
+        if (!fresh) fresh = make_logical_pattern_engine(cur.plan, why);
+      }
+      if (!fresh || fresh->kind() != kind) return fail(SHD_E_ARG, "snapshot of an engine this plan cannot run on");
+      init_engine(*fresh, cur.plan);
+      r.s = fresh->stream;
+      load_image(*fresh, r);
+      q->eng = std::move(fresh);
+      return SHD_OK;
+    }
+    // in place: keep an image of the current state, so that a truncated or
+    // mismatched snapshot leaves the query as it was
+    SnapW bk;
+    bk.s = cur.stream;
+    bk.put<int64_t>(cur.seq);
+    bk.put<int64_t>(cur.now);
+    bk.put<int64_t>(cur.chunk_seq);
+    bk.put<shd_counters>(cur.counters);
+    cur.save_state(bk);
+    try {
+      load_image(cur, r);
+    } catch (...) {
+      SnapR br;
+      br.p = bk.b.data();
+      br.n = bk.b.size();
+      br.s = cur.stream;
+      load_image(cur, br);
+      throw;
+    }
     return SHD_OK;
   });
 }

@@ -121,9 +121,14 @@ class DeviceQuery:
         q = ctypes.c_void_p()
         _check(self.lib.shd_plan_load(ctx, self._ir, len(ir), ctypes.byref(q)))
         self.q = q
+
+    @property
+    def engine_kind(self) -> int:
+        """Engine the query runs on now (a pattern query moves to the generic
+        NFA engine when its input leaves the forward scan's formulation)."""
         e = ctypes.c_int()
-        _check(self.lib.shd_plan_engine(q, ctypes.byref(e)))
-        self.engine_kind = e.value
+        _check(self.lib.shd_plan_engine(self.q, ctypes.byref(e)))
+        return e.value
 
     def close(self):
         if self.q:

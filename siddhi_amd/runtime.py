@@ -213,6 +213,8 @@ class InputHandler:
 
     def send_batch(self, batch: ColumnBatch):
         """Columnar fast path: one pre-built SoA batch (call boundaries in batch.call_offsets)."""
+        if not self._rt.started:
+            raise RuntimeError("Siddhi app '%s' is not running, cannot send events" % self._rt.name)
         self._rt._send_columns(self.stream_id, batch)
 
 
@@ -312,12 +314,19 @@ class SiddhiAppRuntime:
             raise CannotRestoreSiddhiAppStateException("snapshot was taken from a different Siddhi app")
         strings = head["dictionary"]
         cur = self.dictionary.strings
-        if strings[:len(cur)] != cur:
-            raise CannotRestoreSiddhiAppStateException("string dictionary of the snapshot does not extend this app's")
+        # the device state holds dictionary ids: they keep their meaning when
+        # either dictionary is a prefix of the other (strings interned after
+        # persist(), or before a restore into a fresh runtime, only append)
+        k = min(len(strings), len(cur))
+        if strings[:k] != cur[:k]:
+            raise CannotRestoreSiddhiAppStateException("string dictionary of the snapshot conflicts with this app's")
+        sizes = head["sizes"]
+        if len(sizes) != len(self.queries) or at + sum(sizes) != len(snapshot):
+            raise CannotRestoreSiddhiAppStateException("snapshot is truncated or has trailing bytes")
         for x in strings[len(cur):]:
             self.dictionary.id(x)
         self._last_wall = max(self._last_wall, int(head["last_wall"]))
-        for q, n in zip(self.queries, head["sizes"]):
+        for q, n in zip(self.queries, sizes):
             q.engine.restore(snapshot[at:at + n])
             at += n
 

@@ -137,7 +137,8 @@ def test_hashed_bucket_grouping(hip_available, monkeypatch, bits, parts):
     """Partitioned pattern with the key sort replaced by a sort on the low bits
     of a key hash (several keys per bucket, walks step over the other keys of
     their bucket).  bits=2 puts ~1/4 of all keys in one bucket: results must
-    still equal the oracle's row for row.  'auto' on 2^20 keys must choose it."""
+    still equal the oracle's row for row.  'auto' on 2^20 keys with sparse keys
+    per `within` span takes the one-pass bucketed walk (8-bit buckets)."""
     if bits != "auto":
         monkeypatch.setenv("SHD_HASH_BITS", bits)
     qp, _ = compile_single_query(wl.P3_APP)
@@ -149,7 +150,7 @@ def test_hashed_bucket_grouping(hip_available, monkeypatch, bits, parts):
     dev, counters, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert counters["group_bits"] == (16 if bits == "auto" else int(bits))
+    assert counters["group_bits"] == (8 if bits == "auto" else int(bits))
 
 
 def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
@@ -195,10 +196,8 @@ def test_unpartitioned_pattern_grouped_by_equality(hip_available, monkeypatch, i
 @pytest.mark.parametrize("reverse", [False, True])
 def test_implicit_grouping_edge_cases(hip_available, reverse):
     """Null symbols and two streams keyed by their own attribute; with
-    `reverse`, one push whose events go back in time (no grouping for it: the
-    ungrouped walk either reproduces the oracle or refuses with
-    SHD_E_UNSUPPORTED -- never a silent difference)."""
-    from siddhi_amd.hip_engine import SiddhiHipError, SHD_E_UNSUPPORTED
+    `reverse`, one push whose events go back in time inside a key (the query
+    hands over to the generic NFA engine and still equals the oracle)."""
     app = ("@app:playback define stream A (k string, p double); define stream B (k string, p double); "
            "@info(name='q') from every e1=A[p>20] -> e2=B[k==e1.k and p>e1.p] within 50 milliseconds "
            "select e1.k as k, e1.p as p1, e2.p as p2 insert into O;")
@@ -219,12 +218,9 @@ def test_implicit_grouping_edge_cases(hip_available, reverse):
         batches.append((si, ColumnBatch(ts, [k, p], [kn, None], np.array([0, m], np.int64))))
     ora = run_oracle(qp, batches)
     assert len(ora[2]) > 0
-    try:
-        dev, _, _ = run_device(qp, batches)
-    except SiddhiHipError as e:
-        assert reverse and e.code == SHD_E_UNSUPPORTED
-        return
+    dev, _, kind = run_device(qp, batches)
     assert_same_rows(dev, ora)
+    assert kind == (4 if reverse else 1)
 
 
 TYPED_WINDOW_APPS = [

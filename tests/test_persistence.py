@@ -104,6 +104,47 @@ def _persistence_test2(engine):
     assert cb.rows[0] == [f32(25.6), f32(47.6), None, None, f32(45.7)]
 
 
+def _restore_after_new_symbol(engine):
+    """a symbol interned between persist() and restoreLastRevision()
+    on the same runtime (the live dictionary outgrew the snapshot's) must not
+    make the restore fail; the window then holds the persisted events only."""
+    m = _manager(engine)
+    m.setPersistenceStore(InMemoryPersistenceStore())
+    cb = _Collect()
+    rt = m.createSiddhiAppRuntime(WINDOW_APP)
+    rt.addCallback("query1", cb)
+    ih = rt.getInputHandler("StockStream")
+    rt.start()
+    ih.send(["IBM", 75.6, 100])
+    rt.persist()
+    ih.send(["ORCL", 75.6, 100])    # new string after the snapshot
+    assert cb.rows[-1][2] == 200
+    assert rt.restoreLastRevision() is not None
+    ih.send(["ORCL", 75.6, 100])
+    assert cb.rows[-1] == ["ORCL", float(np.float32(75.6)), 200]
+    rt.shutdown()
+
+
+def test_restore_after_new_symbol_oracle():
+    _restore_after_new_symbol("oracle")
+
+
+@pytest.mark.gpu
+def test_restore_after_new_symbol_device(hip_available):
+    _restore_after_new_symbol("device")
+
+
+def test_send_batch_requires_start():
+    """the columnar path refuses events before start(), like send()."""
+    from siddhi_amd.runtime import ColumnBatch
+    m = SiddhiManager(engine_factory=OracleQueryEngine)
+    rt = m.createSiddhiAppRuntime(WINDOW_APP)
+    b = ColumnBatch(np.array([1], np.int64), [np.array([0], np.uint32), np.array([11.0], np.float32),
+                                              np.array([1], np.int32)], [None, None, None])
+    with pytest.raises(RuntimeError):
+        rt.getInputHandler("StockStream").send_batch(b)
+
+
 def test_persistence_window_oracle():
     _persistence_test1("oracle")
 
