@@ -110,6 +110,12 @@ int shd_plan_free(shd_query* q);
 int shd_plan_engine(shd_query* q, int* engine);
 
 int shd_set_time(shd_query* q, int64_t ts);
+/* Named per-query options (SHD_E_ARG for an unknown name):
+ *   "exact_aggregates" (window/aggregate engine): 1 = the bit-exact sequential
+ *     per-group fold (Java's `sum += v; sum -= v` order, AttributeAggregator
+ *     executors); 0 (default) = segmented scans, double aggregates within 1e-9
+ *     relative of that fold (BASELINE.json north_star). */
+int shd_set_option(shd_query* q, const char* key, int64_t value);
 int shd_push(shd_query* q, const shd_batch* batch);
 int shd_flush(shd_query* q);                  /* wait for queued device work      */
 int shd_poll(shd_query* q, shd_out* out);      /* buffers valid until next call    */

@@ -149,6 +149,10 @@ struct Engine {
     if (t >= now) now = t;
   }
   virtual void reset() = 0;
+  // shd_set_option: named engine options (unknown names -> SHD_E_ARG)
+  virtual void set_option(const std::string& key, int64_t) {
+    throw Error(SHD_E_ARG, "unknown option '" + key + "' for this query");
+  }
   // called once the plan's expression table is on the device
   virtual void on_loaded() {}
   // Cross-push state (partial-match tables, window contents, aggregates) for

@@ -201,7 +201,7 @@ struct ItemArgs {
 __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restrict__ ap, int64_t n, const uint32_t* cnt, const uint32_t* off,
                                                        const int32_t* call_of, const int64_t* call_now,
                                                        uint64_t* ikey, int64_t* its, uint64_t* iargv, uint8_t* iargn,
-                                                       int32_t* ievrow, int64_t* inow, int64_t cap,
+                                                       int32_t* ievrow, int32_t* icall, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
@@ -229,6 +229,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
       iargn[g * cap + t] = (uint8_t)v.null;
     }
     ievrow[t] = (int32_t)i;
+    icall[t] = call_of[i];
     inow[t] = call_now[call_of[i]];
   }
 }
@@ -862,6 +863,340 @@ __global__ __launch_bounds__(kBlock) void k_fold_wave_d(const FoldArgs* __restri
   }
 }
 
+// ------------------------------------------------ segmented-scan aggregation
+// Default mode for count / sum(double|float) / avg(any numeric) (north_star:
+// "sliding-window sum/avg/count use segmented scans"; the exact sequential
+// fold above stays behind the `exact_aggregates` option).  Window items are
+// stably sorted by group, so a group's items are one segment in arrival order.
+// A segmented inclusive scan gives every position p the group prefix S(p) of
+// its channel values (double-double: hi + lo, so the prefix itself carries
+// no rounding error worth the name) and of its non-null counts.  The window
+// of a group right after the add of item x (sorted position p) is the
+// positions [k, p] of its segment whose expiry e > x (FIFO expiry makes e
+// non-decreasing along a segment, so k comes from a galloping search), and
+// its aggregate is S(p) - S(k-1): the reference's running value (Java
+// `sum += v; sum -= v`, SumAttributeAggregatorExecutor.java:184-198,
+// AvgAttributeAggregatorExecutor.java:148-166) up to that running value's
+// own rounding residue -- checked at rtol 1e-9 (tests/test_gpu_segscan.py).
+// Counts are exact integers.
+constexpr int kSegPer = 8;                    // positions per thread
+constexpr int kSegTile = kBlock * kSegPer;    // positions per tile (workgroup)
+constexpr int kMaxChan = 4;                   // distinct aggregated expressions
+
+struct DD {
+  double hi, lo;
+};
+// error-free sum of two double-doubles (Knuth two-sum + renormalisation);
+// the build has -ffp-contract=off, so no step is fused
+__device__ __forceinline__ DD dd_add(DD a, DD b) {
+  const double s = a.hi + b.hi;
+  const double bb = s - a.hi;
+  const double err = (a.hi - (s - bb)) + (b.hi - bb);
+  const double lo = (a.lo + b.lo) + err;
+  const double hi = s + lo;
+  return DD{hi, lo - (hi - s)};
+}
+__device__ __forceinline__ double dd_diff(DD a, DD b) {   // round(a - b)
+  const double s = a.hi - b.hi;
+  const double bb = s - a.hi;
+  const double err = (a.hi - (s - bb)) + (-b.hi - bb);
+  return s + (err + (a.lo - b.lo));
+}
+
+template <int NC>
+struct SegAcc {
+  int flag;            // a segment head lies in the range
+  DD s[NC];            // channel sums since the range's last head (whole range if none)
+  int32_t nn[NC];      // non-null counts, likewise
+};
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_identity() {
+  SegAcc<NC> r;
+  r.flag = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    r.s[c] = DD{0.0, 0.0};
+    r.nn[c] = 0;
+  }
+  return r;
+}
+// a (earlier range) then b (later range)
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_combine(const SegAcc<NC>& a, const SegAcc<NC>& b) {
+  if (b.flag) return b;
+  SegAcc<NC> r;
+  r.flag = a.flag;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    r.s[c] = dd_add(a.s[c], b.s[c]);
+    r.nn[c] = a.nn[c] + b.nn[c];
+  }
+  return r;
+}
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_shfl_up(const SegAcc<NC>& a, int o) {
+  SegAcc<NC> r;
+  r.flag = __shfl_up(a.flag, o, 64);
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    r.s[c].hi = __shfl_up(a.s[c].hi, o, 64);
+    r.s[c].lo = __shfl_up(a.s[c].lo, o, 64);
+    r.nn[c] = __shfl_up(a.nn[c], o, 64);
+  }
+  return r;
+}
+// inclusive segmented scan over the 64 lanes of a wave
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_wave_scan(SegAcc<NC> v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const SegAcc<NC> t = seg_shfl_up(v, o);
+    if (lane >= o) v = seg_combine(t, v);
+  }
+  return v;
+}
+
+struct SegArgs {
+  int nch;
+  int ch_agg[kMaxChan];      // first aggregator of each channel (its argument column)
+  int ch_type[kMaxChan];
+  int nagg;
+  int kind[kMaxAggs];
+  int type[kMaxAggs];
+  int chan[kMaxAggs];        // channel of each aggregator (-1: count())
+  int64_t cap;               // item capacity (stride of per-agg item arrays)
+  int64_t C;                 // carried items [0, C)
+  int64_t total;             // items [0, total)
+  double* dsum;              // group tables [nagg][nkeys] (window state after the push)
+  int64_t* cnt;
+  int64_t nkeys;
+};
+
+// sorted-order copies of what the scan and the window search read
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_gather(const SegArgs* __restrict__ ap, const uint32_t* sp,
+                                                       const uint64_t* iargv, const uint8_t* iargn,
+                                                       const uint32_t* e, const int32_t* icall, double* sval,
+                                                       uint8_t* snn, uint32_t* se, int32_t* scall) {
+  const SegArgs& a = *ap;
+  const int64_t total = a.total;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total; p = total) {
+    const uint32_t x = sp[p];
+    uint8_t m = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const int g = a.ch_agg[c];
+      const uint64_t b = iargv[g * a.cap + x];
+      const bool nul = iargn[g * a.cap + x] != 0;
+      double v;
+      switch (a.ch_type[c]) {   // Number.doubleValue() of the operand
+        case SHD_T_INT: v = (double)v_i32(b); break;
+        case SHD_T_LONG: v = (double)(int64_t)b; break;
+        case SHD_T_FLOAT: v = (double)v_f32(b); break;
+        default: v = v_f64(b);
+      }
+      sval[c * total + p] = nul ? 0.0 : v;
+      m |= nul ? 0 : (uint8_t)(1u << c);
+    }
+    snn[p] = m;
+    se[p] = e[x];
+    scall[p] = (int64_t)x >= a.C ? icall[x] : -1;
+  }
+}
+
+// this thread's kSegPer consecutive positions as one segmented range
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_thread_range(int64_t p0, int64_t total, const uint32_t* sk,
+                                                       const double* sval, const uint8_t* snn) {
+  SegAcc<NC> acc = seg_identity<NC>();
+  uint32_t prev = p0 > 0 && p0 <= total ? sk[p0 - 1] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < kSegPer; i++) {
+    const int64_t p = p0 + i;
+    if (p >= total) break;
+    const uint32_t k = sk[p];
+    const uint8_t m = snn[p];
+    const bool head = p == 0 || k != prev;
+    prev = k;
+    if (head) acc = seg_identity<NC>(), acc.flag = 1;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      acc.s[c] = dd_add(acc.s[c], DD{sval[c * total + p], 0.0});
+      acc.nn[c] += (m >> c) & 1;
+    }
+  }
+  return acc;
+}
+
+// block-wide exclusive segmented prefix of the threads' ranges (+ carry-in);
+// returns this thread's exclusive prefix, *tile_total the block's inclusive total
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_block_exclusive(const SegAcc<NC>& mine, const SegAcc<NC>& carry,
+                                                          SegAcc<NC>* wagg, SegAcc<NC>* tile_total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const SegAcc<NC> inc = seg_wave_scan(mine, lane);
+  if (lane == 63) wagg[w] = inc;
+  __syncthreads();
+  SegAcc<NC> pre = carry;
+  for (int k = 0; k < w; k++) pre = seg_combine(pre, wagg[k]);
+  const SegAcc<NC> ex_w = seg_shfl_up(inc, 1);
+  const SegAcc<NC> ex = lane == 0 ? pre : seg_combine(pre, ex_w);
+  if (tile_total) {
+    SegAcc<NC> t = carry;
+    for (int k = 0; k < kBlock / 64; k++) t = seg_combine(t, wagg[k]);
+    *tile_total = t;
+  }
+  return ex;
+}
+
+// phase 1: per-tile segmented totals
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_tiles(int64_t total, const uint32_t* sk, const double* sval,
+                                                      const uint8_t* snn, SegAcc<NC>* tagg) {
+  __shared__ SegAcc<NC> wagg[kBlock / 64];
+  const int64_t p0 = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegPer;
+  const SegAcc<NC> mine = seg_thread_range<NC>(p0, total, sk, sval, snn);
+  SegAcc<NC> tot;
+  seg_block_exclusive<NC>(mine, seg_identity<NC>(), wagg, &tot);
+  if (threadIdx.x == 0) tagg[blockIdx.x] = tot;
+}
+
+// phase 2: exclusive segmented prefix over the tile totals (one workgroup;
+// each thread folds a contiguous run of tiles)
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_tilescan(SegAcc<NC>* tagg, int64_t nt) {
+  __shared__ SegAcc<NC> wagg[kBlock / 64];
+  const int64_t per = (nt + kBlock - 1) / kBlock;
+  const int64_t t0 = (int64_t)threadIdx.x * per;
+  const int64_t t1 = t0 + per < nt ? t0 + per : nt;
+  SegAcc<NC> mine = seg_identity<NC>();
+  for (int64_t t = t0; t < t1; t++) mine = seg_combine(mine, tagg[t]);
+  SegAcc<NC> run = seg_block_exclusive<NC>(mine, seg_identity<NC>(), wagg, nullptr);
+  for (int64_t t = t0; t < t1; t++) {
+    const SegAcc<NC> v = tagg[t];
+    tagg[t] = run;
+    run = seg_combine(run, v);
+  }
+}
+
+// phase 3: inclusive segmented prefix at every position (S, NN)
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_apply(int64_t total, const uint32_t* sk, const double* sval,
+                                                      const uint8_t* snn, const SegAcc<NC>* tcarry, DD* S,
+                                                      int32_t* NN) {
+  __shared__ SegAcc<NC> wagg[kBlock / 64];
+  const int64_t p0 = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegPer;
+  const SegAcc<NC> mine = seg_thread_range<NC>(p0, total, sk, sval, snn);
+  SegAcc<NC> run = seg_block_exclusive<NC>(mine, tcarry[blockIdx.x], wagg, nullptr);
+  uint32_t prev = p0 > 0 && p0 <= total ? sk[p0 - 1] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < kSegPer; i++) {
+    const int64_t p = p0 + i;
+    if (p >= total) break;
+    const uint32_t k = sk[p];
+    const uint8_t m = snn[p];
+    if (p == 0 || k != prev) run = seg_identity<NC>(), run.flag = 1;
+    prev = k;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      run.s[c] = dd_add(run.s[c], DD{sval[c * total + p], 0.0});
+      run.nn[c] += (m >> c) & 1;
+      S[c * total + p] = run.s[c];
+      NN[c * total + p] = run.nn[c];
+    }
+  }
+}
+
+// smallest q in [0, p] with pred(q), where pred holds on a suffix ending at p
+template <class Pred>
+__device__ __forceinline__ int64_t gallop_first(int64_t p, Pred pred) {
+  int64_t in = p, out = -1, step = 1;
+  for (;;) {
+    const int64_t q = p - step;
+    if (q < 0 || !pred(q)) { out = q < 0 ? -1 : q; break; }
+    in = q;
+    step <<= 1;
+  }
+  while (in - out > 1) {
+    const int64_t mid = out + ((in - out) >> 1);
+    if (pred(mid)) in = mid;
+    else out = mid;
+  }
+  return in;
+}
+
+// phase 4: window aggregates at the last add of every (group, call) run ->
+// the emission inputs of k_emit (first / last_of / resv / resn / resc); the
+// group tables get the window state after the push at every segment end
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__ ap, const uint32_t* sk,
+                                                     const uint32_t* sp, const uint32_t* se, const int32_t* scall,
+                                                     const DD* S, const int32_t* NN, const uint8_t* iargn,
+                                                     uint64_t* resv, uint8_t* resn, int64_t* resc, uint8_t* first,
+                                                     uint32_t* last_of) {
+  const SegArgs& a = *ap;
+  const int64_t total = a.total;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total; p = total) {
+    const uint32_t g = sk[p];
+    const uint32_t x = sp[p];
+    const bool seg_end = p + 1 == total || sk[p + 1] != g;
+    const int32_t call = scall[p];
+    const bool run_end = (int64_t)x >= a.C && (seg_end || scall[p + 1] != call);
+    if (!seg_end && !run_end) continue;
+    auto window = [&](uint32_t thr, int64_t& k, int64_t& kin) {
+      // first position of the segment still in the window (expiry after thr)
+      k = gallop_first(p, [&](int64_t q) { return sk[q] == g && se[q] > thr; });
+      kin = k - 1 >= 0 && sk[k - 1] == g ? k - 1 : -1;   // prefix before the window, in this segment
+    };
+    auto chan_val = [&](int c, int64_t kin, int32_t& nnw) -> double {
+      const DD sp_ = S[c * total + p];
+      const DD sk_ = kin >= 0 ? S[c * total + kin] : DD{0.0, 0.0};
+      nnw = NN[c * total + p] - (kin >= 0 ? NN[c * total + kin] : 0);
+      return dd_diff(sp_, sk_);
+    };
+    if (seg_end) {   // window contents after the push (items never expired: e == kInf)
+      int64_t k, kin;
+      window((uint32_t)(total - 1), k, kin);
+      for (int j = 0; j < a.nagg; j++) {
+        const int c = a.chan[j];
+        int32_t nnw = 0;
+        const double v = c >= 0 ? chan_val(c, kin, nnw) : 0.0;
+        a.dsum[j * a.nkeys + g] = nnw ? v : 0.0;
+        a.cnt[j * a.nkeys + g] = c >= 0 ? (int64_t)nnw : p - k + 1;
+      }
+    }
+    if (!run_end) continue;
+    int64_t k, kin;
+    window(x, k, kin);
+    const int64_t rs = gallop_first(p, [&](int64_t q) { return sk[q] == g && scall[q] == call; });
+    const uint32_t xf = sp[rs];
+    first[xf] = 1;
+    last_of[xf] = x;
+    for (int j = 0; j < a.nagg; j++) {
+      const int c = a.chan[j];
+      uint64_t ob = 0;
+      uint8_t on = 0;
+      if (a.kind[j] == SHD_AGG_COUNT) {
+        ob = (uint64_t)(p - k + 1);
+      } else {
+        int32_t nnw = 0;
+        const double v = chan_val(c, kin, nnw);
+        if (a.kind[j] == SHD_AGG_SUM) {
+          // a null operand leaves the sum (null once nothing is left; float sums: null)
+          const bool xn = iargn[j * a.cap + x] != 0;
+          on = (uint8_t)(xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0));
+        } else {
+          on = (uint8_t)(nnw == 0);   // avg: value / count at emission
+          resc[j * a.cap + x] = nnw;
+        }
+        ob = on ? 0ull : p_f64(v);
+      }
+      resv[j * a.cap + x] = ob;
+      resn[j * a.cap + x] = on;
+    }
+  }
+}
+
 __global__ void k_first_counts(const uint8_t* first, int64_t C, int64_t total, uint32_t* cnt) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total - C; t += (int64_t)gridDim.x * blockDim.x)
     cnt[t] = first[C + t] ? 1u : 0u;
@@ -943,13 +1278,26 @@ struct SingleEngine : Engine {
   int cur = 0;
   DevBuf ikey[2], its[2], iargv[2], iargn[2];
   int64_t icap[2] = {0, 0};
-  DevBuf ievrow, inow, e_exp, okey, oref, okey32, okey32_alt, oref_alt, heads, hoff, hlist, resv, resc, resn, first,
+  DevBuf ievrow, icall, inow, e_exp, okey, oref, okey32, okey32_alt, oref_alt, heads, hoff, hlist, resv, resc, resn, first,
       last_of, fcnt, foff;
+  // segmented-scan mode (default for count / sum(double|float) / avg)
+  bool seg_ok = false, seg_mode = false;
+  int nch = 0;                       // distinct aggregated expressions (channels)
+  int ch_agg[kMaxChan] = {}, ch_type[kMaxChan] = {};
+  int chan_of[kMaxAggs] = {};
+  DevBuf sval, snn, se, scall, tagg, segS, segNN;
   // group state (dense by key)
   DevBuf g_dsum, g_lsum, g_cnt;
   int64_t g_nkeys = 0;
 
   int kind() const override { return agg_mode ? ENG_WINDOW : ENG_FILTER; }
+
+  // "exact_aggregates" = 1: the bit-exact sequential fold instead of the
+  // segmented scans (any time; both keep the group tables current)
+  void set_option(const std::string& key, int64_t v) override {
+    if (key == "exact_aggregates") seg_mode = seg_ok && v == 0;
+    else Engine::set_option(key, v);
+  }
 
   void reset() override {
     C = 0;
@@ -1212,6 +1560,131 @@ struct SingleEngine : Engine {
     g_nkeys = nk;
   }
 
+  // Emission: one row per (call, group) with a CURRENT event, in first-seen
+  // order, with the group's values after its last event of the call
+  // (QuerySelector.processInBatchGroupBy, QuerySelector.java:315-373).
+  void emit_rows(const Staged& b, int64_t m, int64_t cap) {
+    hipStream_t s = stream;
+    const int64_t total = C + m;
+    fcnt.reserve(m * 4);
+    foff.reserve(m * 4);
+    hipLaunchKernelGGL(k_first_counts, dim3(grid_for(m)), dim3(kBlock), 0, s, (const uint8_t*)first.as<uint8_t>(), C,
+                       total, fcnt.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    uint32_t* d_f = (uint32_t*)(d_tot.as<uint64_t>() + 4);
+    scan_exclusive_u32(fcnt.as<uint32_t>(), foff.as<uint32_t>(), m, d_f, d_scan, s);
+    SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 4, d_f, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t nrows = h_tot.as<uint32_t>()[8];
+    if (nrows <= 0) return;
+    out.ensure(nrows, s);
+    EmitArgs ea{};
+    ea.cs = b.cs;
+    ea.es = dset();
+    ea.nout = (int)outs.size();
+    for (size_t c = 0; c < outs.size(); c++) ea.outs[c] = dexpr(outs[c]);
+    ea.nagg = nagg;
+    for (int g = 0; g < nagg; g++) ea.kind[g] = plan.aggs[g].kind;
+    ea.cap = cap;
+    ea.C = C;
+    ea.row0 = out.count;
+    ea.chunk0 = chunk_seq;
+    hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m,
+                       (const uint32_t*)fcnt.as<uint32_t>(), (const uint32_t*)foff.as<uint32_t>(),
+                       (const uint32_t*)last_of.as<uint32_t>(), (const int32_t*)ievrow.as<int32_t>(),
+                       (const int32_t*)d_call_of.as<int32_t>(), (const uint64_t*)resv.as<uint64_t>(),
+                       (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
+                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+    SHD_CHECK_LAUNCH();
+    out.count += nrows;
+    counters.matches += nrows;
+    mark("emit");
+  }
+
+  // Segmented-scan window aggregates (see k_seg_gather .. k_seg_emit): stable
+  // group sort of the window items, sorted copies, 3-phase segmented scan,
+  // windowed differences at the (call, group) run ends.
+  template <int NC>
+  void segscan_kernels(int64_t total, const uint32_t* sk, const uint32_t* sp, const SegArgs* d_sa, int64_t cap) {
+    hipStream_t s = stream;
+    sval.reserve((size_t)NC * total * 8);
+    snn.reserve(total);
+    se.reserve(total * 4);
+    scall.reserve(total * 4);
+    hipLaunchKernelGGL(k_seg_gather<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sp,
+                       (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(),
+                       (const uint32_t*)e_exp.as<uint32_t>(), (const int32_t*)icall.as<int32_t>(), sval.as<double>(),
+                       snn.as<uint8_t>(), se.as<uint32_t>(), scall.as<int32_t>());
+    SHD_CHECK_LAUNCH();
+    mark("seg_gather");
+    const int64_t nt = ceil_div(total, kSegTile);
+    tagg.reserve(nt * sizeof(SegAcc<NC>));
+    segS.reserve((size_t)NC * total * sizeof(DD));
+    segNN.reserve((size_t)NC * total * 4);
+    hipLaunchKernelGGL(k_seg_tiles<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                       (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(), tagg.as<SegAcc<NC>>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_seg_tilescan<NC>, dim3(1), dim3(kBlock), 0, s, tagg.as<SegAcc<NC>>(), nt);
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_seg_apply<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                       (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(),
+                       (const SegAcc<NC>*)tagg.as<SegAcc<NC>>(), segS.as<DD>(), segNN.as<int32_t>());
+    SHD_CHECK_LAUNCH();
+    mark("seg_scan");
+    hipLaunchKernelGGL(k_seg_emit<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sk, sp,
+                       (const uint32_t*)se.as<uint32_t>(), (const int32_t*)scall.as<int32_t>(),
+                       (const DD*)segS.as<DD>(), (const int32_t*)segNN.as<int32_t>(),
+                       (const uint8_t*)iargn[cur].as<uint8_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(),
+                       resc.as<int64_t>(), first.as<uint8_t>(), last_of.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    mark("seg_window");
+  }
+
+  void agg_segscan(int64_t total, uint64_t kmax, int64_t cap) {
+    hipStream_t s = stream;
+    okey32.reserve(total * 4);
+    okey32_alt.reserve(total * 4);
+    oref.reserve(total * 4);
+    oref_alt.reserve(total * 4);
+    hipLaunchKernelGGL(k_narrow, dim3(grid_for(total)), dim3(kBlock), 0, s, (const uint64_t*)ikey[cur].as<uint64_t>(),
+                       okey32.as<uint32_t>(), total);
+    SHD_CHECK_LAUNCH();
+    fill_iota_u32(oref.as<uint32_t>(), total, 0, s);
+    int bits = 0;
+    while (bits < 32 && (kmax >> bits)) bits++;
+    bool in_alt = false;
+    radix_sort_pairs_u32(okey32.as<uint32_t>(), oref.as<uint32_t>(), okey32_alt.as<uint32_t>(),
+                         oref_alt.as<uint32_t>(), total, bits, d_sort, s, in_alt);
+    const uint32_t* sk = in_alt ? okey32_alt.as<uint32_t>() : okey32.as<uint32_t>();
+    const uint32_t* sp = in_alt ? oref_alt.as<uint32_t>() : oref.as<uint32_t>();
+    mark("group_sort");
+    SegArgs sa{};
+    sa.nch = std::max(nch, 1);
+    for (int c = 0; c < sa.nch; c++) {
+      sa.ch_agg[c] = nch ? ch_agg[c] : 0;
+      sa.ch_type[c] = nch ? ch_type[c] : SHD_T_DOUBLE;
+    }
+    sa.nagg = nagg;
+    for (int g = 0; g < nagg; g++) {
+      sa.kind[g] = plan.aggs[g].kind;
+      sa.type[g] = plan.aggs[g].type;
+      sa.chan[g] = chan_of[g];
+    }
+    sa.cap = cap;
+    sa.C = C;
+    sa.total = total;
+    sa.dsum = g_dsum.as<double>();
+    sa.cnt = g_cnt.as<int64_t>();
+    sa.nkeys = g_nkeys;
+    const SegArgs* d_sa = dev_args(sa);
+    switch (sa.nch) {
+      case 1: segscan_kernels<1>(total, sk, sp, d_sa, cap); break;
+      case 2: segscan_kernels<2>(total, sk, sp, d_sa, cap); break;
+      case 3: segscan_kernels<3>(total, sk, sp, d_sa, cap); break;
+      default: segscan_kernels<4>(total, sk, sp, d_sa, cap); break;
+    }
+  }
+
   void push_agg(const Staged& b, int64_t ncalls, int64_t n) {
     hipStream_t s = stream;
     SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 4, hipMemcpyDeviceToHost, s));
@@ -1239,6 +1712,7 @@ struct SingleEngine : Engine {
     }
     const int64_t cap = icap[cur];
     ievrow.reserve(cap * 4);
+    icall.reserve(cap * 4);
     inow.reserve(cap * 8);
     ItemArgs ia{};
     ia.cs = b.cs;
@@ -1259,7 +1733,7 @@ struct SingleEngine : Engine {
                        (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
                        ikey[cur].as<uint64_t>(), its[cur].as<int64_t>(), iargv[cur].as<uint64_t>(),
-                       iargn[cur].as<uint8_t>(), ievrow.as<int32_t>(), inow.as<int64_t>(), cap,
+                       iargn[cur].as<uint8_t>(), ievrow.as<int32_t>(), icall.as<int32_t>(), inow.as<int64_t>(), cap,
                        (uint32_t*)(d_tot.as<uint64_t>() + 5));
     SHD_CHECK_LAUNCH();
     mark("window_items");
@@ -1301,7 +1775,15 @@ struct SingleEngine : Engine {
       throw Error(SHD_E_UNSUPPORTED, "group-by key outside the dense device range");
     ensure_groups((int64_t)kmax + 1);
     const int64_t nops = m + X;
-    if (nops > 0) {
+    resv.reserve(std::max(nagg, 1) * cap * 8);
+    resc.reserve(std::max(nagg, 1) * cap * 8);
+    resn.reserve(std::max(nagg, 1) * cap);
+    first.reserve(cap);
+    last_of.reserve(cap * 4);
+    if (total > 0) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
+    if (seg_mode && total > 0) {
+      agg_segscan(total, kmax, cap);
+    } else if (nops > 0) {
       okey.reserve(nops * 8);
       oref.reserve(nops * 4);
       hipLaunchKernelGGL(k_make_ops, dim3(grid_for(total)), dim3(kBlock), 0, s, C, total,
@@ -1336,12 +1818,6 @@ struct SingleEngine : Engine {
       hipLaunchKernelGGL(k_head_list, dim3(grid_for(nops)), dim3(kBlock), 0, s, (const uint32_t*)heads.as<uint32_t>(),
                          (const uint32_t*)hoff.as<uint32_t>(), nops, hlist.as<uint32_t>());
       SHD_CHECK_LAUNCH();
-      resv.reserve(std::max(nagg, 1) * cap * 8);
-      resc.reserve(std::max(nagg, 1) * cap * 8);
-      resn.reserve(std::max(nagg, 1) * cap);
-      first.reserve(cap);
-      last_of.reserve(cap * 4);
-      SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
       FoldArgs fo{};
       fo.nagg = nagg;
       for (int g = 0; g < nagg; g++) {
@@ -1393,44 +1869,9 @@ struct SingleEngine : Engine {
 #undef SHD_FOLD_ARGS
       SHD_CHECK_LAUNCH();
       mark("group_fold");
-      // emission: first-seen (call, group) rows in event order
-      if (m > 0) {
-        fcnt.reserve(m * 4);
-        foff.reserve(m * 4);
-        hipLaunchKernelGGL(k_first_counts, dim3(grid_for(m)), dim3(kBlock), 0, s, (const uint8_t*)first.as<uint8_t>(),
-                           C, total, fcnt.as<uint32_t>());
-        SHD_CHECK_LAUNCH();
-        uint32_t* d_f = (uint32_t*)(d_tot.as<uint64_t>() + 4);
-        scan_exclusive_u32(fcnt.as<uint32_t>(), foff.as<uint32_t>(), m, d_f, d_scan, s);
-        SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 4, d_f, 4, hipMemcpyDeviceToHost, s));
-        SHD_HIP(hipStreamSynchronize(s));
-        const int64_t nrows = h_tot.as<uint32_t>()[8];
-        if (nrows > 0) {
-          out.ensure(nrows, s);
-          EmitArgs ea{};
-          ea.cs = b.cs;
-          ea.es = dset();
-          ea.nout = (int)outs.size();
-          for (size_t c = 0; c < outs.size(); c++) ea.outs[c] = dexpr(outs[c]);
-          ea.nagg = nagg;
-          for (int g = 0; g < nagg; g++) ea.kind[g] = plan.aggs[g].kind;
-          ea.cap = cap;
-          ea.C = C;
-          ea.row0 = out.count;
-          ea.chunk0 = chunk_seq;
-          hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m, (const uint32_t*)fcnt.as<uint32_t>(),
-                             (const uint32_t*)foff.as<uint32_t>(), (const uint32_t*)last_of.as<uint32_t>(),
-                             (const int32_t*)ievrow.as<int32_t>(), (const int32_t*)d_call_of.as<int32_t>(),
-                             (const uint64_t*)resv.as<uint64_t>(), (const uint8_t*)resn.as<uint8_t>(),
-                             (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
-                             out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
-          SHD_CHECK_LAUNCH();
-          out.count += nrows;
-          counters.matches += nrows;
-          mark("emit");
-        }
-      }
     }
+    // emission: first-seen (call, group) rows in event order
+    if (m > 0) emit_rows(b, m, cap);
     // carry: the unexpired suffix [X, total) becomes the new window contents
     int64_t keep = wkind == 0 ? 0 : total - X;
     if (keep > 0 && X > 0) {
@@ -1480,6 +1921,34 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
   if (p.expired_on && (needs_agg || e->wkind != 0)) { why = "expired-event output from a window"; return nullptr; }
   if (e->wkind != 0 && e->wparam <= 0 && e->wkind == SHD_W_LENGTH) { why = "length(0) window"; return nullptr; }
   e->agg_mode = needs_agg;
+  // segmented-scan aggregation: count(), sum(double|float), avg(numeric); one
+  // channel per distinct argument expression (avg(price) and sum(price) share one)
+  bool seg = e->agg_mode && e->nagg >= 1;
+  for (int g = 0; g < e->nagg && seg; g++) {
+    const auto& a = p.aggs[g];
+    if (a.kind == SHD_AGG_COUNT) { e->chan_of[g] = -1; continue; }
+    if (a.kind == SHD_AGG_SUM && a.type != SHD_T_DOUBLE && a.type != SHD_T_FLOAT) { seg = false; break; }
+    if (a.kind != SHD_AGG_SUM && a.kind != SHD_AGG_AVG) { seg = false; break; }
+    if (a.expr < 0) { seg = false; break; }
+    int c = -1;
+    for (int k = 0; k < e->nch && c < 0; k++) {
+      const auto& x = p.exprs[p.aggs[e->ch_agg[k]].expr];
+      const auto& y = p.exprs[a.expr];
+      bool same = x.size() == y.size() && e->ch_type[k] == a.type;
+      for (size_t i = 0; same && i < x.size(); i++)
+        same = x[i].op == y[i].op && x[i].a == y[i].a && x[i].b == y[i].b && x[i].c == y[i].c;
+      if (same) c = k;
+    }
+    if (c < 0) {
+      if (e->nch == kMaxChan) { seg = false; break; }
+      c = e->nch++;
+      e->ch_agg[c] = g;
+      e->ch_type[c] = a.type;
+    }
+    e->chan_of[g] = c;
+  }
+  e->seg_ok = seg;
+  e->seg_mode = seg && !getenv("SHD_EXACT_AGGREGATES");
   if (e->partitioned) {
     if (e->agg_mode) { why = "partitioned window/aggregation"; return nullptr; }
     e->key_expr = p.part_keys[0].second;

@@ -729,6 +729,15 @@ int shd_push(shd_query* q, const shd_batch* b) {
   });
 }
 
+int shd_set_option(shd_query* q, const char* key, int64_t value) {
+  return guarded([&]() -> int {
+    if (!q || !key) return fail(SHD_E_ARG, "null argument");
+    SHD_HIP(hipStreamSynchronize(q->eng->stream));
+    q->eng->set_option(key, value);
+    return SHD_OK;
+  });
+}
+
 int shd_flush(shd_query* q) {
   return guarded([&]() -> int {
     if (!q) return fail(SHD_E_ARG, "null query");

@@ -27,7 +27,7 @@ ENGINE_NAMES = {1: "pattern-forward-scan", 2: "window-aggregate", 3: "filter-pro
 EXPORTED = ["shd_device_count", "shd_ctx_create", "shd_ctx_destroy", "shd_plan_load", "shd_plan_free",
             "shd_plan_engine", "shd_set_time", "shd_push", "shd_flush", "shd_poll", "shd_discard_output",
             "shd_reset", "shd_get_counters", "shd_query_stream", "shd_stage_times", "shd_snapshot", "shd_restore",
-            "shd_last_error"]
+            "shd_set_option", "shd_last_error"]
 
 
 class SiddhiHipError(RuntimeError):
@@ -76,6 +76,7 @@ def load_library(path: str = LIB_PATH):
         lib.shd_plan_free.argtypes = [P]
         lib.shd_plan_engine.argtypes = [P, ctypes.POINTER(I)]
         lib.shd_set_time.argtypes = [P, I64]
+        lib.shd_set_option.argtypes = [P, ctypes.c_char_p, I64]
         lib.shd_push.argtypes = [P, ctypes.POINTER(ShdBatch)]
         lib.shd_flush.argtypes = [P]
         lib.shd_poll.argtypes = [P, ctypes.POINTER(ShdOut)]
@@ -168,6 +169,11 @@ class DeviceQuery:
     def set_time(self, t):
         _check(self.lib.shd_set_time(self.q, int(t)))
 
+    def set_option(self, key: str, value: int):
+        """shd_set_option: e.g. ("exact_aggregates", 1) = bit-exact sequential
+        window folds instead of the default segmented scans."""
+        _check(self.lib.shd_set_option(self.q, key.encode(), int(value)))
+
     def flush(self):
         _check(self.lib.shd_flush(self.q))
 
@@ -227,7 +233,7 @@ class DeviceQuery:
 class HipQueryEngine:
     """Query engine of SiddhiAppRuntime backed by libsiddhi_hip (MI355X)."""
 
-    def __init__(self, qp: pl.QueryPlan, dictionary):
+    def __init__(self, qp: pl.QueryPlan, dictionary, exact_aggregates: bool = False):
         self.qp = qp
         try:
             self.dq = DeviceQuery(qp.ir)
@@ -235,6 +241,8 @@ class HipQueryEngine:
             if e.code == SHD_E_UNSUPPORTED:
                 raise pl.UnsupportedPlanException(str(e))
             raise
+        if exact_aggregates and self.dq.engine_kind == 2:
+            self.dq.set_option("exact_aggregates", 1)
         self.types = qp.plan.stream_types
 
     @property

@@ -505,8 +505,12 @@ class InMemoryPersistenceStore:
 class SiddhiManager:
     """io.siddhi.core.SiddhiManager (C/SiddhiManager.java:84-96)."""
 
-    def __init__(self, engine_factory: Optional[Callable] = None):
+    def __init__(self, engine_factory: Optional[Callable] = None, exact_aggregates: bool = False):
+        """exact_aggregates: window sum/avg run as the bit-exact sequential
+        per-group fold (the reference's add/remove order) instead of the
+        default segmented scans (within 1e-9 relative of it)."""
         self._engine_factory = engine_factory
+        self._exact_aggregates = exact_aggregates
         self._runtimes: List[SiddhiAppRuntime] = []
         self._store = None
 
@@ -521,7 +525,10 @@ class SiddhiManager:
         factory = self._engine_factory
         if factory is None:
             from .hip_engine import HipQueryEngine   # product path: MI355X only
-            factory = HipQueryEngine
+            exact = self._exact_aggregates
+
+            def factory(qp, dictionary):
+                return HipQueryEngine(qp, dictionary, exact_aggregates=exact)
         rt = SiddhiAppRuntime(app, factory, app_text)
         rt.persistence_store = self._store
         self._runtimes.append(rt)

@@ -30,7 +30,9 @@ def _py(v):
     return ("v", v)
 
 
-def values_equal(expected, actual):
+def values_equal(expected, actual, rtol=0.0):
+    """rtol: relative tolerance for double results (the device's default
+    segmented-scan window aggregates, BASELINE.json: within 1e-9 relative)."""
     kind, e = _py(expected)
     if e is None or actual is None:
         return e is None and actual is None
@@ -38,7 +40,9 @@ def values_equal(expected, actual):
         return e == actual
     if kind == "f":
         return float(np.float32(actual)) == e
-    return float(e) == float(actual) or (isinstance(e, int) and isinstance(actual, int) and e == actual)
+    if float(e) == float(actual) or (isinstance(e, int) and isinstance(actual, int) and e == actual):
+        return True
+    return rtol > 0 and isinstance(actual, float) and abs(float(e) - actual) <= rtol * abs(float(e))
 
 
 class Collector:
@@ -79,7 +83,7 @@ def run_case(case, engine_factory):
     return col
 
 
-def check_case(case, col):
+def check_case(case, col, rtol=0.0):
     errs = []
     if case.get("expected_count") is not None and len(col.in_events) != case["expected_count"]:
         errs.append("count %d != expected %d" % (len(col.in_events), case["expected_count"]))
@@ -99,6 +103,6 @@ def check_case(case, col):
             targets = [col.in_events[n - 1]]
         for ev in targets:
             d = ev.getData()
-            if len(d) != len(exp["data"]) or not all(values_equal(e, a) for e, a in zip(exp["data"], d)):
+            if len(d) != len(exp["data"]) or not all(values_equal(e, a, rtol) for e, a in zip(exp["data"], d)):
                 errs.append("event %s: %r != expected %r" % (n, d, [_py(v)[1] for v in exp["data"]]))
     return errs

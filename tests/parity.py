@@ -53,9 +53,13 @@ def run_oracle(qp, batches):
     return concat_rows(parts)
 
 
-def run_device(qp, batches):
+def run_device(qp, batches, exact=False):
+    """exact: window aggregates as the bit-exact sequential fold (shd_set_option
+    "exact_aggregates"); default: the product's segmented scans."""
     from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
     dq = DeviceQuery(qp.ir)
+    if exact and dq.engine_kind == 2:
+        dq.set_option("exact_aggregates", 1)
     parts = []
     for si, b in batches:
         cols = [np.ascontiguousarray(c) for c in b.cols]
@@ -100,3 +104,21 @@ def assert_same_rows(dev, ora, float_cols=(), rtol=0.0):
                 np.testing.assert_allclose(a, b, rtol=rtol, atol=0)
             else:
                 np.testing.assert_array_equal(dv[:, k], ov[:, k])
+
+
+AGG_RTOL = 1e-9   # BASELINE.json north_star: double aggregates within 1e-9 relative
+
+
+def float_cols(qp):
+    """Output columns of double / float type (window aggregates)."""
+    return tuple(i for i, t in enumerate(qp.output_types) if t in (3, 4))
+
+
+def assert_rows_agg(dev, ora, qp, exact):
+    """Window-aggregate outputs: bit-exact in exact mode; in segmented-scan mode
+    every non-floating column, timestamp, null flag and callback boundary
+    exact and floating columns within AGG_RTOL."""
+    if exact:
+        assert_same_rows(dev, ora)
+    else:
+        assert_same_rows(dev, ora, float_cols=float_cols(qp), rtol=AGG_RTOL)

@@ -13,9 +13,29 @@ CASES = load_cases()
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_device_matches_reference_kat(hip_available, case):
+    """Default product path (window aggregates as segmented scans: doubles
+    within 1e-9 relative of the reference's printed values)."""
     from siddhi_amd.hip_engine import HipQueryEngine
     try:
         col = run_case(case, HipQueryEngine)
+    except (UnsupportedPlanException, OutOfScopeSyntax) as e:
+        pytest.skip("device path: %s" % str(e)[:120])
+    errs = check_case(case, col, rtol=1e-9)
+    assert not errs, "%s (%s): %s" % (case["name"], case["source"], errs)
+
+
+AGG_CASES = [c for c in CASES if "window" in c["app"] and any(a in c["app"] for a in ("sum(", "avg(", "count("))]
+
+
+@pytest.mark.parametrize("case", AGG_CASES, ids=[c["name"] for c in AGG_CASES])
+def test_device_exact_aggregates_kat(hip_available, case):
+    """exact_aggregates mode: window aggregates bit-identical to the reference's."""
+    from siddhi_amd.hip_engine import HipQueryEngine
+
+    def factory(qp, d):
+        return HipQueryEngine(qp, d, exact_aggregates=True)
+    try:
+        col = run_case(case, factory)
     except (UnsupportedPlanException, OutOfScopeSyntax) as e:
         pytest.skip("device path: %s" % str(e)[:120])
     errs = check_case(case, col)

@@ -2,11 +2,12 @@
 workloads (configs P1, P3, W2 at oracle-sized scale), including micro-batch
 splits that exercise the carried partial-match / window state.
 Integer/index/string/timestamp outputs must be bit-exact; double aggregates
-are also compared bit-exactly (the device folds each group sequentially)."""
+are bit-exact in the `exact_aggregates` mode (sequential per-group fold) and
+within 1e-9 relative in the default segmented-scan mode."""
 import numpy as np
 import pytest
 
-from parity import assert_same_rows, compile_single_query, run_device, run_oracle, stock_batch
+from parity import assert_rows_agg, assert_same_rows, compile_single_query, run_device, run_oracle, stock_batch
 from siddhi_amd import workloads as wl
 from siddhi_amd.runtime import ColumnBatch
 
@@ -36,23 +37,28 @@ CASES = [
 
 @pytest.mark.parametrize("name,app,n,keys,delta", CASES, ids=[c[0] for c in CASES])
 @pytest.mark.parametrize("parts", [1, 3])
-def test_device_equals_oracle(hip_available, name, app, n, keys, delta, parts):
+@pytest.mark.parametrize("mode", ["scan", "exact"])
+def test_device_equals_oracle(hip_available, name, app, n, keys, delta, parts, mode):
+    if mode == "exact" and not name.startswith("W2"):
+        pytest.skip("exact_aggregates only concerns window aggregates")
     qp, _ = compile_single_query(app)
     sym, price, vol, ts = wl.stock_stream(n, keys, delta, seed_offset=hash(name) % 1000)
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
-    dev, counters, kind = run_device(qp, batches)
+    dev, counters, kind = run_device(qp, batches, exact=mode == "exact")
     assert len(ora[2]) > 0
-    assert_same_rows(dev, ora)
+    assert_rows_agg(dev, ora, qp, mode == "exact")
     assert counters["events"] == n
 
 
-def test_single_event_calls_match_oracle(hip_available):
+@pytest.mark.parametrize("mode", ["scan", "exact"])
+def test_single_event_calls_match_oracle(hip_available, mode):
     # B = 1 variant: every InputHandler call carries one event
     qp, _ = compile_single_query(wl.W2_LENGTH_APP.replace("length(1000)", "length(7)"))
     sym, price, vol, ts = wl.stock_stream(3000, 13, 1.0, seed_offset=3)
     batches = [(0, stock_batch(sym, price, vol, ts, call_size=1))]
-    assert_same_rows(run_device(qp, batches)[0], run_oracle(qp, batches))
+    assert_rows_agg(run_device(qp, batches, exact=mode == "exact")[0], run_oracle(qp, batches), qp,
+                    mode == "exact")
 
 
 def test_two_stream_pattern_matches_oracle(hip_available):
@@ -236,13 +242,14 @@ TYPED_WINDOW_APPS = [
 ]
 
 
-@pytest.mark.parametrize("fold", ["wave", "wave-generic", "lane"])
+@pytest.mark.parametrize("fold", ["wave", "wave-generic", "lane", "scan"])
 @pytest.mark.parametrize("name,app", TYPED_WINDOW_APPS, ids=[a[0] for a in TYPED_WINDOW_APPS])
 def test_group_fold_long_segments(hip_available, monkeypatch, fold, name, app):
     """Few groups, long operation segments per push: the one-wave-per-group
     fold (coalesced operand loads, wave-uniform sequential state) and the
     one-lane-per-group fold must both give the oracle's rows bit for bit,
-    typed aggregates and null arguments included."""
+    typed aggregates and null arguments included; the segmented-scan mode
+    (default; integer sums stay on the fold) within 1e-9 relative."""
     if fold == "lane":
         monkeypatch.setenv("SHD_FOLD_LANE", "1")
     if fold == "wave-generic":
@@ -264,9 +271,9 @@ def test_group_fold_long_segments(hip_available, monkeypatch, fold, name, app):
         t = int(ts[-1])
         batches.append((0, ColumnBatch(ts, [k, i, lv, f, d], nulls, np.arange(0, m + 1, 500, dtype=np.int64))))
     ora = run_oracle(qp, batches)
-    dev, _, _ = run_device(qp, batches)
+    dev, _, _ = run_device(qp, batches, exact=fold != "scan")
     assert len(ora[2]) > 0
-    assert_same_rows(dev, ora)
+    assert_rows_agg(dev, ora, qp, fold != "scan")
 
 
 @pytest.mark.parametrize("parts", [1, 3])

@@ -42,6 +42,16 @@ def run_app(app, factory, n, keys, delta, seed=5, call=256):
     return outs
 
 
+def _same(a, b, rtol=1e-9):
+    """Callback-for-callback equality; floating values (the window queries'
+    segmented-scan averages) within 1e-9 relative, everything else exact."""
+    if isinstance(a, float) and isinstance(b, float):
+        return a == b or abs(a - b) <= rtol * max(abs(a), abs(b))
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        return len(a) == len(b) and all(_same(x, y, rtol) for x, y in zip(a, b))
+    return type(a) == type(b) and a == b
+
+
 def test_m5_app_runs_on_oracle():
     """All 100 queries plan and run (checker side, small sample)."""
     outs = run_app(wl.M5_APP, OracleQueryEngine, 4000, 50, 0.05)
@@ -56,5 +66,5 @@ def test_m5_device_equals_oracle(hip_available):
     dev = run_app(app, None, 12000, 100, 0.02)
     assert set(ora) == set(dev) and len(ora) == 100
     for name in ora:
-        assert dev[name] == ora[name], "query %s differs" % name
+        assert _same(dev[name], ora[name]), "query %s differs" % name
     assert sum(len(v) for v in ora.values()) > 0

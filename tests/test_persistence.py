@@ -17,7 +17,8 @@ import numpy as np
 import pytest
 
 from oracle_engine import OracleQueryEngine
-from parity import assert_same_rows, compile_single_query, concat_rows, run_device, run_oracle, stock_batch
+from parity import (assert_rows_agg, assert_same_rows, compile_single_query, concat_rows, run_device, run_oracle,
+                    stock_batch)
 from siddhi_amd import workloads as wl
 from siddhi_amd.runtime import (InMemoryPersistenceStore, NoPersistenceStoreException, QueryCallback,
                                 SiddhiManager)
@@ -237,9 +238,13 @@ def test_device_snapshot_restore_midstream(hip_available, name, app, n, keys, de
     ora = run_oracle(qp, batches)
     whole, _, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
-    assert_same_rows(whole, ora)
+    exact = not name.startswith("W2")   # W2: segmented-scan aggregates (1e-9 relative)
+    assert_rows_agg(whole, ora, qp, exact)
     for cut in range(1, len(batches)):
-        assert_same_rows(_run_with_restore(qp, batches, cut), ora)
+        restored = _run_with_restore(qp, batches, cut)
+        assert_rows_agg(restored, ora, qp, exact)
+        if not exact:   # restoring mid-stream changes nothing in the device's own results
+            assert_same_rows(restored, whole)
 
 
 @pytest.mark.gpu
