@@ -576,6 +576,7 @@ struct PreState {
   bool successCondition = false, startStateReset = false;   // count
   int64_t lastScheduledTime = 0;                              // absent
   bool active = true;                                         // absent
+  int64_t lastArrivalTime = 0;                                // absent logical (LogicalStreamPreState)
 };
 
 // Runtime tree (query/input/stream/state/runtime/*InnerStateRuntime.java)
@@ -913,7 +914,12 @@ struct Engine {
         }
         break;
       }
-      case PK_LOGICAL: case PK_ABSENT_LOGICAL:
+      case PK_LOGICAL:
+        logicalAddState(pre, s);
+        break;
+      case PK_ABSENT_LOGICAL:
+        // AbsentLogicalPreStateProcessor.addState (:77-99): inactive -> dropped
+        if (!S(pre).active) break;
         logicalAddState(pre, s);
         break;
       case PK_ABSENT:
@@ -926,7 +932,17 @@ struct Engine {
     Pre& pr = pres[pre];
     SE* c = clone_se(s);
     c->type = CURRENT;
-    if (pr.kind == PK_LOGICAL || pr.kind == PK_ABSENT_LOGICAL) {
+    if (pr.kind == PK_ABSENT_LOGICAL) {
+      // AbsentLogicalPreStateProcessor.addEveryState (:101-119): the clone takes
+      // the time of the event this processor saw; only the pair's slots clear
+      if (c->ev[pr.stateId] != nullptr) c->ts = c->ev[pr.stateId]->ts;
+      c->ev[pr.stateId] = nullptr;
+      c->ev[pres[pr.partner].stateId] = nullptr;
+      S(pre).newEvery.push_back(c);
+      S(pr.partner).newEvery.push_back(c);
+      return;
+    }
+    if (pr.kind == PK_LOGICAL) {
       c->ev[pr.stateId] = nullptr;
       for (int i = pr.stateId; i < (int)c->ev.size(); i++) c->ev[i] = nullptr;
       S(pre).newEvery.push_back(c);
@@ -934,7 +950,6 @@ struct Engine {
         c->ev[pres[pr.partner].stateId] = nullptr;
         S(pr.partner).newEvery.push_back(c);
       }
-      if (pr.kind == PK_ABSENT_LOGICAL) absentLogicalEveryHook(pre, s);
       return;
     }
     for (int i = pr.stateId; i < (int)c->ev.size(); i++) c->ev[i] = nullptr;
@@ -1060,7 +1075,8 @@ struct Engine {
     switch (ps.kind) {
       case PK_STREAM: streamPost(post, s); break;
       case PK_COUNT: countPost(post, s); break;
-      case PK_LOGICAL: case PK_ABSENT_LOGICAL: logicalPost(post, s); break;
+      case PK_LOGICAL: logicalPost(post, s); break;
+      case PK_ABSENT_LOGICAL: absentLogicalPost(post, s); break;
       case PK_ABSENT: absentPost(post, s); break;
     }
   }
@@ -1114,7 +1130,8 @@ struct Engine {
   }
 
   void logicalPost(int post, SE* s) {
-    // LogicalPostStateProcessor.process (LogicalPostStateProcessor.java:59-86)
+    // LogicalPostStateProcessor.process (LogicalPostStateProcessor.java:59-86);
+    // the post of an absent operand is absentLogicalPost
     Post& ps = posts[post];
     if (ps.ltype == 0) {
       bool proceed = false;
@@ -1124,14 +1141,12 @@ struct Engine {
         proceed = true;
       }
       if (proceed) {
-        if (ps.kind == PK_ABSENT_LOGICAL) absentLogicalPostSuper(post, s);
-        else streamPost(post, s);
+        streamPost(post, s);
       } else {
         stateChanged(ps.pre);
       }
     } else {
-      if (ps.kind == PK_ABSENT_LOGICAL) absentLogicalPostSuper(post, s);
-      else streamPost(post, s);
+      streamPost(post, s);
       Post& pp = posts[ps.partnerPost];
       if (pp.hasSelector && pres[ps.pre].thisLast == ps.partnerPost) pp.isEventReturned = true;
     }
@@ -1252,7 +1267,13 @@ struct Engine {
       st.newEvery.push_back(s);
       if (pr.partner >= 0) S(pr.partner).newEvery.push_back(s);
     }
-    if (pr.kind == PK_ABSENT_LOGICAL) absentLogicalAddStateHook(pre, s);
+    if (pr.kind == PK_ABSENT_LOGICAL && !pr.isStart && pr.waiting != -1) {
+      // AbsentLogicalPreStateProcessor.addState: schedule this processor (and an
+      // absent partner) at the partial's time + waiting
+      notifyAt(pr.sched, s->ts + pr.waiting);
+      const Pre& pp = pres[pr.partner];
+      if (pp.kind == PK_ABSENT_LOGICAL) notifyAt(pp.sched, s->ts + pp.waiting);
+    }
   }
 
   std::vector<SE*> logicalProcessAndReturn(int pre, Ev* ev) {
@@ -1388,14 +1409,174 @@ struct Engine {
     }
   }
 
-  // Absent logical processors (not X and Y / not X for t or Y) are outside the
-  // round-1 oracle; plans containing them are rejected at construction.
-  void absentLogicalEveryHook(int, SE*) { throw std::runtime_error("absent logical unsupported"); }
-  void absentLogicalAddStateHook(int, SE*) { throw std::runtime_error("absent logical unsupported"); }
-  bool absentPartnerCanProceed(int, SE*) { throw std::runtime_error("absent logical unsupported"); }
-  void absentLogicalPostSuper(int, SE*) { throw std::runtime_error("absent logical unsupported"); }
-  void absentLogicalPartitionCreated(int) { throw std::runtime_error("absent logical unsupported"); }
-  std::vector<SE*> absentLogicalProcessAndReturn(int, Ev*) { throw std::runtime_error("absent logical unsupported"); }
+  // ---------------- Absent logical (not X [for t] and|or Y) ----------------
+  // AbsentLogicalPreStateProcessor (ST/AbsentLogicalPreStateProcessor.java:65-388)
+  // and AbsentLogicalPostStateProcessor.
+
+  // a fresh StreamEvent (streamEventFactory.newInstance(): ts -1, no data)
+  Ev* empty_ev() {
+    static const uint64_t zeros[64] = {0};
+    static const uint8_t ones[64] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                     1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                     1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+    Ev* e = ev_arena.get();
+    *e = Ev();
+    e->ts = -1;
+    e->data = zeros;
+    e->nul = ones;
+    return e;
+  }
+
+  static void add_event(SE* s, int sid, Ev* e) {   // StateEvent.addEvent
+    if (s->ev[sid] == nullptr) { s->ev[sid] = e; return; }
+    Ev* x = s->ev[sid];
+    while (x->next) x = x->next;
+    x->next = e;
+  }
+
+  void absentLogicalPost(int post, SE* s) {
+    // AbsentLogicalPostStateProcessor.process: state changed, event returned,
+    // updateLastArrivalTime (:36-50) -- no partner check
+    Post& ps = posts[post];
+    stateChanged(ps.pre);
+    ps.isEventReturned = true;
+    S(ps.pre).lastArrivalTime = s->ev[ps.stateId]->ts;
+  }
+
+  std::vector<SE*> absentLogicalProcessAndReturn(int pre, Ev* ev) {
+    // AbsentLogicalPreStateProcessor.processAndReturn (:243-296): an X arrival
+    // takes the partials it passes out of this processor's pending list; never
+    // returns events itself
+    Pre& pr = pres[pre];
+    PreState& st = S(pre);
+    if (!st.active) return {};
+    Post& last = posts[pr.thisLast];
+    Post& tp = posts[pr.thisPost];
+    const int psid = pres[pr.partner].stateId;
+    for (auto it = st.pending.begin(); it != st.pending.end();) {
+      SE* s = *it;
+      if (pr.ltype == 1 && s->ev[psid] != nullptr) {
+        it = st.pending.erase(it);
+        continue;
+      }
+      Ev* curEv = s->ev[pr.stateId];
+      s->ev[pr.stateId] = clone_ev(ev);
+      processChain(pre, s);
+      if (pr.waiting != -1 || (p.state_type == 1 && pr.ltype == 0 && tp.nextEvery >= 0)) s->ev[pr.stateId] = curEv;
+      bool erased = false;
+      if (last.isEventReturned) {
+        last.isEventReturned = false;
+        it = st.pending.erase(it);
+        erased = true;
+        if (p.state_type == 1) S(pr.partner).pending.remove(s);
+      }
+      if (!st.stateChanged) {
+        s->ev[pr.stateId] = curEv;
+        if (p.state_type == 1 && !erased) {
+          it = st.pending.erase(it);
+          erased = true;
+        }
+      }
+      if (!erased) ++it;
+    }
+    return {};
+  }
+
+  bool absentPartnerCanProceed(int pre, SE* s) {
+    // AbsentLogicalPreStateProcessor.partnerCanProceed (:353-388)
+    Pre& pr = pres[pre];
+    PreState& st = S(pre);
+    Post& tp = posts[pr.thisPost];
+    if (p.state_type == 1 && tp.nextEvery < 0 && st.lastArrivalTime > 0) return false;
+    if (pr.waiting == -1) {
+      if (tp.nextEvery < 0) return s->ev[pr.stateId] == nullptr;
+      if (st.lastArrivalTime > 0) {
+        st.lastArrivalTime = 0;
+        init_pre(pre);
+        return false;
+      }
+      return true;
+    }
+    return s->ev[pr.stateId] != nullptr;
+  }
+
+  void absentLogicalSendEvent(int pre, SE* s) {
+    // AbsentLogicalPreStateProcessor.sendEvent (:231-253)
+    Pre& pr = pres[pre];
+    Post& tp = posts[pr.thisPost];
+    if (tp.hasSelector) selectorEmitImmediate(s);
+    if (tp.nextPre >= 0) addState(tp.nextPre, s);
+    if (tp.nextEvery >= 0) {
+      addEveryState(tp.nextEvery, s);
+    } else if (pr.isStart) {
+      S(pre).active = false;
+      if (pr.ltype == 1 && pres[pr.partner].kind == PK_ABSENT_LOGICAL) S(pr.partner).active = false;
+    }
+    if (tp.callbackPre >= 0) countStartStateReset(tp.callbackPre);
+  }
+
+  void absentLogicalTimer(int pre, int64_t currentTime) {
+    // AbsentLogicalPreStateProcessor.process(ComplexEventChunk) on a TIMER (:122-218)
+    Pre& pr = pres[pre];
+    PreState& st = S(pre);
+    if (!st.active) return;
+    Post& tp = posts[pr.thisPost];
+    const int psid = pres[pr.partner].stateId;
+    bool notProcessed = true;
+    if (currentTime >= st.lastArrivalTime + pr.waiting) {
+      if (pr.isStart && p.state_type == 1 && st.newEvery.empty() && st.pending.empty()) {
+        addState(pre, new_se());
+      } else if (p.state_type == 1 && !st.newEvery.empty()) {
+        resetState(pre);
+      }
+      updateState(pre);
+      SE* expired = nullptr;
+      std::vector<SE*> ret;
+      for (auto it = st.pending.begin(); it != st.pending.end();) {
+        SE* s = *it;
+        if (isExpired(pre, s, currentTime)) {
+          expired = s;
+          it = st.pending.erase(it);
+          continue;
+        }
+        Ev* own = s->ev[pr.stateId];
+        const bool passed = own == nullptr ? currentTime >= s->ts + pr.waiting : currentTime >= own->ts + pr.waiting;
+        if (passed) {
+          it = st.pending.erase(it);
+          if (pr.ltype == 1 && s->ev[psid] == nullptr) {          // OR: partner not received
+            add_event(s, pr.stateId, empty_ev());
+            ret.push_back(s);
+          } else if (pr.ltype == 0 && s->ev[psid] != nullptr) {   // AND: partner received, not sent
+            ret.push_back(s);
+          } else if (pr.ltype == 0) {                              // AND: let the partner proceed
+            add_event(s, pr.stateId, empty_ev());
+          }
+          continue;
+        }
+        ++it;
+      }
+      if (expired && pr.withinEvery >= 0) {
+        addEveryState(pr.withinEvery, expired);
+        updateState(pr.withinEvery);
+      }
+      notProcessed = ret.empty();
+      for (SE* s : ret) {
+        s->ts = currentTime;
+        absentLogicalSendEvent(pre, s);
+      }
+      st.lastArrivalTime = 0;
+    }
+    if (tp.nextEvery >= 0 || (notProcessed && pr.isStart)) {
+      const int64_t nextBreak = st.lastArrivalTime == 0 ? now + pr.waiting : st.lastArrivalTime + pr.waiting;
+      notifyAt(pr.sched, nextBreak);
+    }
+  }
+
+  void absentLogicalPartitionCreated(int pre) {
+    // AbsentLogicalPreStateProcessor.partitionCreated (:318-335)
+    Pre& pr = pres[pre];
+    if (pr.isStart && pr.waiting != -1 && S(pre).active) notifyAt(pr.sched, now + pr.waiting);
+  }
 
   // ---------------- runtimes ----------------
   void rt_init(Rt* r) {
@@ -1560,7 +1741,8 @@ struct Engine {
           while (!q.empty() && *q.begin() - now <= 0) {
             int64_t nt = *q.begin();
             q.erase(q.begin());
-            absentTimer(sched_pre[sc], nt);
+            if (pres[sched_pre[sc]].kind == PK_ABSENT_LOGICAL) absentLogicalTimer(sched_pre[sc], nt);
+            else absentTimer(sched_pre[sc], nt);
           }
         }
       }
@@ -1987,6 +2169,21 @@ int orc_push(void* h, int32_t stream, int64_t n, const int64_t* ts, const uint64
              int32_t advance_time) {
   try {
     ((Engine*)h)->push(stream, n, ts, vals, nulls, advance_time != 0);
+    return 0;
+  } catch (std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// SiddhiAppRuntime.start() at app time t (wall-clock apps: the clock at start;
+// playback: 0): unpartitioned state queries are (re)initialised at t
+// (QueryRuntimeImpl.start -> initPartition, AbsentStreamPreStateProcessor.partitionCreated :291-303).
+int orc_start(void* h, int64_t t) {
+  try {
+    Engine* e = (Engine*)h;
+    if (t > e->now) e->now = t;
+    if (!e->partitioned && e->p.kind == SHD_KIND_STATE) e->start_partition();
     return 0;
   } catch (std::exception& ex) {
     g_err = ex.what();

@@ -258,6 +258,10 @@ class HipQueryEngine:
             return []
         return split_chunks(*r)
 
+    def start(self, t):
+        """SiddhiAppRuntime.start() at app time t (shd_set_option "start_time")."""
+        self.dq.set_option("start_time", int(t))
+
     def set_time(self, t):
         self.dq.set_time(t)
         return self._drain()

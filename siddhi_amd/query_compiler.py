@@ -582,6 +582,10 @@ class Parser:
         if self.at_kw("and", "or"):
             kind = self.name().lower()
             b = self.stateful_or_absent()
+            if b.absent and not a.absent:
+                # the absent operand of a mixed pair is element 1 (SiddhiQLBaseVisitorImpl.
+                # visitLogical_absent_stateful_source -> State.logicalNotAnd / logicalOr(absent, present))
+                a, b = b, a
             return LogicalSE(kind, a, b)
         if isinstance(a, StreamSE) and not a.absent:
             if self.at("<"):

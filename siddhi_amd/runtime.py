@@ -238,6 +238,7 @@ class SiddhiAppRuntime:
         self.started = False
         self.persistence_store = None
         self._last_wall = 0
+        self.clock = None   # wall-clock source (ms); None = time.time() (tests replay a recorded clock)
         extra = {}
         anon = 0
         for item in app.execution_order:
@@ -284,6 +285,14 @@ class SiddhiAppRuntime:
         return InputHandler(self, stream_id)
 
     def start(self):
+        """SiddhiAppRuntime.start(): queries start at the app's current time --
+        0 for playback apps (TimestampGeneratorImpl.lastEventTimestamp before
+        any event), the wall clock otherwise (C/util/timestamp/TimestampGeneratorImpl.java)."""
+        t0 = 0 if self.playback else self._wall_clock()
+        for q in self.queries:
+            st = getattr(q.engine, "start", None)
+            if st:
+                st(t0)
         self.started = True
 
     # -- state persistence (C/SiddhiAppRuntimeImpl.java:677-745)
@@ -366,9 +375,22 @@ class SiddhiAppRuntime:
         self.queries = []
         self.started = False
 
+    def advanceTime(self, ts: int):  # noqa: N802
+        """Move the app clock to `ts` and fire every query's due timers (absent
+        `not ... for` states, time windows): what the reference's Scheduler does
+        when wall-clock time passes (C/util/Scheduler.java:113-209) or a playback
+        heartbeat advances TimestampGeneratorImpl (C/util/timestamp/
+        TimestampGeneratorImpl.java:58-76)."""
+        if not self.started:
+            raise RuntimeError("Siddhi app '%s' is not running" % self.name)
+        t = int(ts)
+        self._last_wall = max(self._last_wall, t)
+        for q in self.queries:
+            self._deliver(q, q.engine.set_time(t))
+
     # -- internals
     def _wall_clock(self):
-        t = int(time.time() * 1000)
+        t = int(self.clock()) if self.clock else int(time.time() * 1000)
         self._last_wall = max(self._last_wall, t)
         return self._last_wall
 

@@ -40,6 +40,8 @@ FILES = [
     "query/FilterTestCase2.java",
     "query/pattern/absent/AbsentPatternTestCase.java",
     "query/pattern/absent/AbsentWithEveryPatternTestCase.java",
+    "query/pattern/absent/EveryAbsentPatternTestCase.java",
+    "query/pattern/absent/LogicalAbsentPatternTestCase.java",
     "managment/PlaybackTestCase.java",
 ]
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat")
@@ -153,6 +155,168 @@ def strip_comments(body):
     return "".join(out)
 
 
+# ---- query-API tests (FilterTestCase1/2): the Java builder calls restated as SiddhiQL
+_JTOK = re.compile(r'\s*(?:(?P<str>"(?:[^"\\]|\\.)*")|(?P<num>-?\d+(?:\.\d*)?(?:[eE][-+]?\d+)?[fFdDlL]?)|'
+                   r'(?P<id>[A-Za-z_]\w*)|(?P<p>[().,]))')
+
+
+def _jtokens(text):
+    out, i = [], 0
+    while i < len(text):
+        m = _JTOK.match(text, i)
+        if not m or m.end() == i:
+            if text[i:].strip() == "":
+                break
+            raise ValueError("java token at %r" % text[i:i + 20])
+        i = m.end()
+        kind = m.lastgroup
+        out.append((kind, m.group(kind)))
+    return out
+
+
+def _jparse(toks, i=0):
+    """primary ('.' name ['(' args ')'])* -> nested ('call', path, args) / ('str'|'num'|'id', v)."""
+    kind, v = toks[i]
+    i += 1
+    if kind == "str":
+        node = ("str", java_str(v))
+    elif kind == "num":
+        node = ("num", v)
+    elif kind == "id":
+        path = [v]
+        while i + 1 < len(toks) and toks[i] == ("p", ".") and toks[i + 1][0] == "id":
+            if i + 2 < len(toks) and toks[i + 2] == ("p", "("):
+                break
+            path.append(toks[i + 1][1])
+            i += 2
+        if i < len(toks) and toks[i] == ("p", ".") and i + 2 < len(toks) and toks[i + 2] == ("p", "("):
+            path.append(toks[i + 1][1])
+            i += 2
+        if i < len(toks) and toks[i] == ("p", "("):
+            args, i = _jargs(toks, i)
+            node = ("call", ".".join(path), args)
+        else:
+            node = ("id", ".".join(path))
+    else:
+        raise ValueError("java expr at %r" % (v,))
+    while i + 2 < len(toks) and toks[i] == ("p", ".") and toks[i + 1][0] == "id" and toks[i + 2] == ("p", "("):
+        name = toks[i + 1][1]
+        args, i = _jargs(toks, i + 2)
+        node = ("meth", node, name, args)
+    return node, i
+
+
+def _jargs(toks, i):
+    assert toks[i] == ("p", "(")
+    i += 1
+    args = []
+    if toks[i] == ("p", ")"):
+        return args, i + 1
+    while True:
+        a, i = _jparse(toks, i)
+        args.append(a)
+        if toks[i] == ("p", ")"):
+            return args, i + 1
+        if toks[i] != ("p", ","):
+            raise ValueError("java args")
+        i += 1
+
+
+_CMP = {"EQUAL": "==", "NOT_EQUAL": "!=", "GREATER_THAN": ">", "GREATER_THAN_EQUAL": ">=",
+        "LESS_THAN": "<", "LESS_THAN_EQUAL": "<="}
+_MATH = {"add": "+", "subtract": "-", "multiply": "*", "divide": "/", "mod": "%"}
+
+
+def _jexpr(n):
+    """io.siddhi.query.api.expression.Expression builders -> SiddhiQL text."""
+    if n[0] == "call":
+        f, a = n[1].split(".")[-1], n[2]
+        if f == "variable":
+            return a[0][1]
+        if f == "value":
+            k, v = a[0]
+            if k == "str":
+                return "'%s'" % v
+            if k == "id" and v in ("true", "false"):
+                return v
+            return v
+        if f == "compare":
+            return "(%s %s %s)" % (_jexpr(a[0]), _CMP[a[1][1].split(".")[-1]], _jexpr(a[2]))
+        if f in _MATH:
+            return "(%s %s %s)" % (_jexpr(a[0]), _MATH[f], _jexpr(a[1]))
+        if f in ("and", "or"):
+            return "(%s %s %s)" % (_jexpr(a[0]), f, _jexpr(a[1]))
+        if f == "not":
+            return "(not %s)" % _jexpr(a[0])
+        if f == "isNull":
+            return "(%s is null)" % _jexpr(a[0])
+    raise ValueError("query-API expression %r" % (n,))
+
+
+def _chain(n):
+    """Flatten a builder chain: root call + [(method, args)]."""
+    calls = []
+    while n[0] == "meth":
+        calls.append((n[2], n[3]))
+        n = n[1]
+    return n, calls[::-1]
+
+
+def query_api_app(body):
+    """SiddhiQL text of a test that builds its app with the query API
+    (StreamDefinition.id(..).attribute(..), new Query().from/select/insertInto)."""
+    types = {"STRING": "string", "INT": "int", "LONG": "long", "FLOAT": "float", "DOUBLE": "double", "BOOL": "bool"}
+    defs = {}
+    for m in re.finditer(r"StreamDefinition (\w+)\s*=\s*(StreamDefinition\.id\(.*?\));", body, re.S):
+        root, calls = _chain(_jparse(_jtokens(m.group(2)))[0])
+        attrs = ["%s %s" % (a[0][1], types[a[1][1].split(".")[-1]]) for name, a in calls if name == "attribute"]
+        defs[m.group(1)] = "define stream %s (%s);" % (root[2][0][1], ", ".join(attrs))
+    order = re.findall(r"siddhiApp\.defineStream\((\w+)\)", body)
+    text = " ".join(defs[d] for d in order) + " "
+    nq = len(re.findall(r"siddhiApp\.addQuery\(", body))
+    if nq != 1:
+        raise ValueError("query-API app with %d queries" % nq)
+    ann = re.search(r'query\.annotation\(Annotation\.annotation\("info"\)\.element\("name",\s*"(\w+)"\)\);', body)
+    fm = re.search(r"query\.from\((.*?)\);\s*query\.", body, re.S)
+    sm = re.search(r"query\.select\((.*?)\);\s*query\.", body, re.S)
+    im = re.search(r'query\.insertInto\("(\w+)"\);', body)
+    if not (fm and sm and im):
+        raise ValueError("query-API shape")
+    root, calls = _chain(_jparse(_jtokens(fm.group(1)))[0])
+    src = root[2][0][1]
+    for name, a in calls:
+        if name != "filter":
+            raise ValueError("query-API input %s" % name)
+        src += "[%s]" % _jexpr(a[0])
+    root, calls = _chain(_jparse(_jtokens(sm.group(1)))[0])
+    outs = []
+    for name, a in calls:
+        if name != "select":
+            raise ValueError("query-API selector %s" % name)
+        outs.append("%s as %s" % (_jexpr(a[1]), a[0][1]))
+    q = "%sfrom %s select %s insert into %s;" % ("@info(name='%s') " % ann.group(1) if ann else "", src,
+                                                 ", ".join(outs), im.group(1))
+    return text + q
+
+
+def _callback_bodies(body):
+    """(name, QueryCallback|StreamCallback, body text) of each anonymous callback."""
+    out = []
+    for m in re.finditer(r'addCallback\("(\w+)",\s*new (QueryCallback|StreamCallback)\(\)\s*\{', body):
+        depth, i = 1, m.end()
+        while depth and i < len(body):
+            depth += {"{": 1, "}": -1}.get(body[i], 0)
+            i += 1
+        out.append((m.group(1), m.group(2), body[m.start():i]))
+    return out
+
+
+def _count_mult(cbody):
+    """Events counted per in-event by a callback body (count.addAndGet(inEvents.length) k times)."""
+    return (len(re.findall(r"count\.addAndGet\(inEvents\.length\)", cbody)) +
+            len(re.findall(r"count\s*=\s*count\s*\+\s*inEvents\.length", cbody)))
+
+
 def extract(name, body, line, fname):
     body = strip_comments(body)
     if re.search(r"executorService|Thread\(|persist\(|restore|setExtension", body):
@@ -164,13 +328,37 @@ def extract(name, body, line, fname):
     if not m:
         return None, "no app"
     try:
-        app = eval_concat(m.group(1).replace("(", " ").replace(")", " "), strings)
-    except ValueError as e:
-        return None, str(e)
+        if m.group(1).strip() == "siddhiApp" and "new SiddhiApp(" in body:
+            app = query_api_app(body)
+        else:
+            app = eval_concat(m.group(1).replace("(", " ").replace(")", " "), strings)
+    except (ValueError, KeyError, IndexError, AssertionError) as e:
+        return None, "app: %s" % e
     cbs = re.findall(r'addCallback\("(\w+)",\s*new (QueryCallback|StreamCallback)', body)
-    if len(cbs) != 1:
-        return None, "callbacks=%d" % len(cbs)
-    cb_name, cb_kind = cbs[0]
+    # TestUtil.addQueryCallback(runtime, "q", new Object[]{..}, ...) (T/TestUtil.java:45-66):
+    # expected rows in arrival order, counts read back through the TestCallback
+    tu = list(re.finditer(r'TestUtil\.add(Query|Stream)Callback\(\s*\w+\s*,\s*"(\w+)"\s*(,(?:[^;])*?)?\)\s*;', body))
+    tu_expected = []
+    if tu:
+        if cbs or len(tu) != 1:
+            return None, "callbacks=%d" % (len(cbs) + len(tu))
+        cb_kind = "QueryCallback" if tu[0].group(1) == "Query" else "StreamCallback"
+        cb_name = tu[0].group(2)
+        for k, em in enumerate(re.finditer(r"new\s+Object\[\]\s*\{(.*?)\}", tu[0].group(3) or "", re.S)):
+            try:
+                # TestQueryCallback checks expected[i] only for events that arrive
+                tu_expected.append({"n": k + 1, "data": parse_values(em.group(1)), "if_arrived": True})
+            except ValueError as e:
+                return None, str(e)
+    elif len(cbs) != 1:
+        # several callbacks: the one that counts (FilterTestCase1: query1 counts, query2 only asserts)
+        counting = [c for c in _callback_bodies(body) if _count_mult(c[2])]
+        if len(counting) != 1:
+            return None, "callbacks=%d" % len(cbs)
+        cb_name, cb_kind = counting[0][0], counting[0][1]
+    else:
+        cb_name, cb_kind = cbs[0]
+    playback = "@app:playback" in app.replace(" ", "").lower()
     handlers = dict(re.findall(r'InputHandler (\w+)\s*=\s*\w+\.getInputHandler\("(\w+)"\)', body))
     # statement stream: sends, sleeps, clock updates
     clock = T0
@@ -178,20 +366,39 @@ def extract(name, body, line, fname):
     now_var = None
     events_ok = True
     stmt_re = re.compile(
-        r"(?P<sleep>Thread\.sleep\((?P<ms>\d+)\))"
+        r"(?P<wait>TestUtil\.waitForInEvents\((?P<wms>\d+),\s*\w+,\s*(?P<wn>\d+)\))"
+        r"|(?P<sleep>Thread\.sleep\((?P<ms>\d+)\))"
         r"|(?P<nowdecl>long (?P<nv>\w+) = (?P<nval>System\.currentTimeMillis\(\)|\d+L?);)"
         r"|(?P<nowadd>(?P<nv2>\w+) \+= (?P<addexpr>[\d *]+);)"
         r"|(?P<send>(?P<h>\w+)\.send\((?P<args>(?:[^;]|\n)*?)\);)")
-    cb_start = body.find("addCallback")
-    cb_end = body.find("});", cb_start)
-    scan = body[cb_end:] if cb_start >= 0 else body
+    if tu:
+        scan = body[tu[0].end():]
+        # the expectations are read at the first assertion: later sleeps (after
+        # shutdown) must not fire more timers
+        cut = [i for i in (scan.find("AssertJUnit."), scan.find("throwAssertionErrors"), scan.find(".shutdown()"))
+               if i >= 0]
+        if cut:
+            scan = scan[:min(cut)]
+    else:
+        cb_start = body.find("addCallback")
+        cb_end = body.find("});", cb_start)
+        scan = body[cb_end:] if cb_start >= 0 else body
     if re.search(r"\bfor\s*\(|\bwhile\s*\(|new Event\[|\.send\(new Event", scan):
         return None, "loop in sends"
     last_ts = None
     nv_value = None
     for sm in stmt_re.finditer(scan):
-        if sm.group("sleep"):
+        if sm.group("wait"):
+            # TestUtil.waitForInEvents (T/TestUtil.java:69-79): sleep, up to n times,
+            # until exactly one event arrived; wall-clock timers fire meanwhile
+            if not playback:
+                sends.append({"wait": int(sm.group("wms")), "retry": int(sm.group("wn"))})
+            clock += int(sm.group("wms"))
+        elif sm.group("sleep"):
             clock += int(sm.group("ms"))
+            if not playback and tu:
+                # wall clock: the scheduler fires due timers during the sleep
+                sends.append({"time": clock})
         elif sm.group("nowdecl"):
             now_var = sm.group("nv")
             v = sm.group("nval")
@@ -233,8 +440,18 @@ def extract(name, body, line, fname):
         return None, "no sends"
     # expectations
     cbm = re.search(r"addCallback\(.*?\}\s*\);", body, re.S)
-    cbody = cbm.group(0) if cbm else ""
-    expected = []
+    cbody = cbm.group(0) if cbm and not tu else ""
+    if not tu:
+        for name_, kind_, b_ in _callback_bodies(body):
+            if name_ == cb_name:
+                cbody = b_
+    expected = list(tu_expected)
+    cells = []
+    # per-callback cell checks: "X".equals(inEvents[0].getData(k)) / assertEquals("X", inEvents[0].getData(k).toString())
+    for cm_ in re.finditer(r'assertTrue\("([^"]*)"\.equals\(inEvents\[0\]\.getData\((\d+)\)\)\)', cbody):
+        cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
+    for cm_ in re.finditer(r'assertEquals\("([^"]*)",\s*inEvents\[0\]\.getData\((\d+)\)\.toString\(\)\)', cbody):
+        cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
     cases = re.split(r"case (\d+):", cbody)
     if len(cases) > 1:
         for k in range(1, len(cases), 2):
@@ -252,7 +469,13 @@ def extract(name, body, line, fname):
             except ValueError as e:
                 return None, str(e)
     count = None
-    for pat in [r'assertEquals\("Number of success events",\s*(\d+),\s*inEventCount\)',
+    if tu:
+        # the first count assertion after the callback (later ones follow more sends)
+        cm = re.search(r'assertEquals\("[^"]*",\s*(\d+),\s*\w+\.getInEventCount\(\)\)', body[tu[0].end():])
+        if cm:
+            count = int(cm.group(1))
+    for pat in [] if tu else [r'assertEquals\("Number of success events",\s*(\d+),\s*\w+\.getInEventCount\(\)\)',
+                r'assertEquals\("Number of success events",\s*(\d+),\s*inEventCount\)',
                 r"assertEquals\(inEventCount,\s*(\d+)\)",
                 r'assertEquals\("[^"]*[Ee]vent count[^"]*",\s*(\d+),\s*inEventCount\)',
                 r"assertEquals\((\d+),\s*inEventCount\)",
@@ -261,11 +484,25 @@ def extract(name, body, line, fname):
         if cm:
             count = int(cm.group(1))
             break
+    mult = _count_mult(cbody) if not tu else 0
+    if count is None and mult:
+        # `count.addAndGet(inEvents.length)` (k times per callback) checked with
+        # assertEquals(N, count[.get()]) or, lacking an assertion, the count the
+        # test waits for (SiddhiTestHelper.waitForEvents(sleep, N, count, timeout))
+        after = body[body.find(cbody) + len(cbody):] if cbody else body
+        cm = (re.search(r"assertEquals\((?:\"[^\"]*\",\s*)?(\d+)L?,\s*count(?:\.get\(\))?\)", after) or
+              re.search(r"SiddhiTestHelper\.waitForEvents\(\d+,\s*(\d+),\s*count,", after))
+        if cm:
+            n_ = int(cm.group(1))
+            if n_ % mult:
+                return None, "count %d not a multiple of %d" % (n_, mult)
+            count = n_ // mult
     removes = None
-    rm = re.search(r'assertEquals\("Number of remove events",\s*(\d+),\s*removeEventCount\)', body)
+    rm = re.search(r'assertEquals\("Number of remove events",\s*(\d+),\s*(?:removeEventCount|\w+\.getRemoveEventCount\(\))\)',
+                   body)
     if rm:
         removes = int(rm.group(1))
-    if count is None and not expected:
+    if count is None and not expected and not cells:
         return None, "no expectations"
     return {
         "name": "%s.%s" % (os.path.basename(fname)[:-5], name),
@@ -276,7 +513,9 @@ def extract(name, body, line, fname):
         "expected_rows": expected,
         "expected_count": count,
         "expected_remove_count": removes,
+        "expected_cells": cells,
         "playback": "@app:playback" in app.replace(" ", "").lower() or "@app:playback" in app.lower(),
+        "start_time": None if playback else T0,
     }, None
 
 

@@ -45,6 +45,9 @@ def values_equal(expected, actual, rtol=0.0):
     return rtol > 0 and isinstance(actual, float) and abs(float(e) - actual) <= rtol * abs(float(e))
 
 
+TICK_MS = 10   # granularity of the emulated wall clock during sleeps / waits
+
+
 class Collector:
     def __init__(self):
         self.in_events = []
@@ -73,8 +76,31 @@ def run_case(case, engine_factory):
                 col.in_events.extend(events)
         app.addCallback(cb["name"], SC())
     handlers = {}
+    # wall-clock apps: replay the recorded clock (the first step's time is the
+    # clock at start(); TestUtil / Thread.sleep steps advance it)
+    first = case["sends"][0]
+    clock = case.get("start_time") or first.get("ts", first.get("time", 0))
+    app.clock = lambda: clock
     app.start()
+    def tick_to(target):
+        # wall-clock time passes continuously: due timers fire (close to) on
+        # time, with the app clock at their due time (Scheduler on a wall clock)
+        nonlocal clock
+        while clock < target:
+            clock = min(target, clock + TICK_MS)
+            app.advanceTime(clock)
+
     for s in case["sends"]:
+        if "time" in s:          # Thread.sleep on a wall-clock app
+            tick_to(s["time"])
+            continue
+        if "wait" in s:          # TestUtil.waitForInEvents(sleep, cb, retry) (T/TestUtil.java:69-79)
+            for _ in range(s["retry"]):
+                tick_to(clock + s["wait"])
+                if len(col.in_events) == 1:
+                    break
+            continue
+        clock = max(clock, s["ts"])
         h = handlers.get(s["stream"]) or app.getInputHandler(s["stream"])
         handlers[s["stream"]] = h
         data = [_py(v)[1] for v in s["data"]]
@@ -98,11 +124,19 @@ def check_case(case, col, rtol=0.0):
             targets = [c[0][0] for c in col.chunks if c[0]]
         else:
             if n - 1 >= len(col.in_events):
-                errs.append("missing event #%d" % n)
+                if not exp.get("if_arrived"):
+                    errs.append("missing event #%d" % n)
                 continue
             targets = [col.in_events[n - 1]]
         for ev in targets:
             d = ev.getData()
             if len(d) != len(exp["data"]) or not all(values_equal(e, a, rtol) for e, a in zip(exp["data"], d)):
                 errs.append("event %s: %r != expected %r" % (n, d, [_py(v)[1] for v in exp["data"]]))
+    for cell in case.get("expected_cells", []):
+        targets = [c[0][0] for c in col.chunks if c[0]] if cell["which"] == "first_of_each" else col.in_events
+        for ev in targets:
+            d = ev.getData()
+            if cell["col"] >= len(d) or d[cell["col"]] != cell["value"]:
+                errs.append("cell %d of %r != %r" % (cell["col"], d, cell["value"]))
+                break
     return errs

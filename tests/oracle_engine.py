@@ -34,6 +34,8 @@ def load_oracle():
     lib.orc_push.argtypes = [P, ctypes.c_int32, ctypes.c_int64, P, P, P, ctypes.c_int32]
     lib.orc_set_time.restype = ctypes.c_int
     lib.orc_set_time.argtypes = [P, ctypes.c_int64]
+    lib.orc_start.restype = ctypes.c_int
+    lib.orc_start.argtypes = [P, ctypes.c_int64]
     lib.orc_num_rows.restype = ctypes.c_int64
     lib.orc_num_rows.argtypes = [P]
     lib.orc_num_outputs.restype = ctypes.c_int32
@@ -105,6 +107,8 @@ class OracleQueryEngine:
         for i, op in enumerate(self._log):
             if op[0] == "t":
                 arrs["op%d_t" % i] = np.array([op[1]], np.int64)
+            elif op[0] == "s":
+                arrs["op%d_s" % i] = np.array([op[1]], np.int64)
             else:
                 _, si, b, adv = op
                 arrs["op%d_p" % i] = np.array([si, 1 if adv else 0, len(b.cols)], np.int64)
@@ -130,10 +134,19 @@ class OracleQueryEngine:
             if "op%d_t" % i in z:
                 self.set_time(int(z["op%d_t" % i][0]))
                 continue
+            if "op%d_s" % i in z:
+                self.start(int(z["op%d_s" % i][0]))
+                continue
             si, adv, nc = (int(x) for x in z["op%d_p" % i])
             cols = [z["op%d_c%d" % (i, a)] for a in range(nc)]
             nulls = [z["op%d_n%d" % (i, a)] if ("op%d_n%d" % (i, a)) in z else None for a in range(nc)]
             self.push(si, ColumnBatch(z["op%d_ts" % i], cols, nulls, z["op%d_co" % i]), bool(adv))
+
+    def start(self, t):
+        """SiddhiAppRuntime.start() at app time t."""
+        self._log.append(("s", int(t)))
+        if self.lib.orc_start(self.h, int(t)) != 0:
+            raise RuntimeError("oracle: " + self.lib.orc_last_error().decode())
 
     def set_time(self, t):
         self._log.append(("t", int(t)))
