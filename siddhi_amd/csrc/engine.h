@@ -149,8 +149,19 @@ struct Engine {
     if (t >= now) now = t;
   }
   virtual void reset() = 0;
-  // shd_set_option: named engine options (unknown names -> SHD_E_ARG)
-  virtual void set_option(const std::string& key, int64_t) {
+  // shd_set_option: named engine options (unknown names -> SHD_E_ARG).
+  // "start_time": the app's clock when SiddhiAppRuntime.start() ran (wall-clock
+  // apps: System.currentTimeMillis(); playback: 0, TimestampGeneratorImpl's
+  // initial lastEventTimestamp) -- unpartitioned state queries seed their
+  // absent start states with it (AbsentStreamPreStateProcessor.partitionCreated
+  // :291-303 reads currentTime()).
+  int64_t start_time = 0;
+  virtual void set_option(const std::string& key, int64_t v) {
+    if (key == "start_time") {
+      start_time = v;
+      if (v > now) now = v;
+      return;
+    }
     throw Error(SHD_E_ARG, "unknown option '" + key + "' for this query");
   }
   // called once the plan's expression table is on the device

@@ -118,6 +118,7 @@ struct NfaRunArgs {
   int64_t n_keyed;      // events handed to lanes (rows[] length)
   int64_t nlanes;
   int64_t seq0;
+  int64_t start_time;   // app start (seed of unpartitioned plans)
   const int32_t* call_of;
   const int64_t* call_now;
   const uint8_t* call_changed;
@@ -471,13 +472,22 @@ struct Lane {
           }
           break;
         }
-        case PK_LOGICAL: {   // LogicalPreStateProcessor.addState :43-63
+        case PK_LOGICAL:
+        case PK_ABSENT_LOGICAL: {   // LogicalPreStateProcessor.addState :43-63
+          // AbsentLogicalPreStateProcessor.addState (:77-99): inactive -> dropped;
+          // a non-start absent operand (and an absent partner) is scheduled
+          if (pr.kind == PK_ABSENT_LOGICAL && (fl(p) & FL_INACTIVE)) break;
           if (pr.isStart || P.seq) {
             if (nn(p) == 0) push_new(p, s);
             if (pr.partner >= 0 && nn(pr.partner) == 0) push_new(pr.partner, s);
           } else {
             push_new(p, s);
             if (pr.partner >= 0) push_new(pr.partner, s);
+          }
+          if (pr.kind == PK_ABSENT_LOGICAL && !pr.isStart && pr.waiting != -1) {
+            notifyAt(pr.sched, sts(s) + pr.waiting);
+            const DPre& pp = P.pre[pr.partner];
+            if (pp.kind == PK_ABSENT_LOGICAL) notifyAt(pp.sched, sts(s) + pp.waiting);
           }
           break;
         }
@@ -503,6 +513,16 @@ struct Lane {
     const DPre& pr = P.pre[p];
     uint16_t c = clone_se(s);
     stype(c) = SHD_EV_CURRENT;
+    if (pr.kind == PK_ABSENT_LOGICAL) {
+      // AbsentLogicalPreStateProcessor.addEveryState (:101-119): the clone takes the
+      // time of the event this processor saw; only the pair's slots clear
+      if (sev(c, pr.stateId) != NIL) sts(c) = ev_ts(sev(c, pr.stateId));
+      sev(c, pr.stateId) = NIL;
+      sev(c, P.pre[pr.partner].stateId) = NIL;
+      push_new(p, c);
+      push_new(pr.partner, c);
+      return;
+    }
     for (int i = pr.stateId; i < Y.nstates; i++) sev(c, i) = NIL;
     if (pr.kind == PK_LOGICAL) {
       push_new(p, c);
@@ -537,6 +557,7 @@ struct Lane {
         }
         break;
       case PK_LOGICAL:
+      case PK_ABSENT_LOGICAL:
         if (pr.ltype == 1 || pn(p) == pn(pr.partner)) {
           pn(p) = 0;
           pn(pr.partner) = 0;
@@ -593,7 +614,7 @@ struct Lane {
       init_pre(p);
     }
     merge_new(p);
-    if (pr.kind == PK_LOGICAL) merge_new(pr.partner);
+    if (pr.kind == PK_LOGICAL || pr.kind == PK_ABSENT_LOGICAL) merge_new(pr.partner);
   }
 
   __device__ void expireEvents(int p, int64_t t) {   // :326-361
@@ -685,7 +706,10 @@ struct Lane {
   __device__ void logicalPost(int post, uint16_t s) {   // LogicalPostStateProcessor.process :59-86
     const DPost& ps = P.post[post];
     if (ps.ltype == 0) {
-      if (sev(s, P.pre[ps.partnerPre].stateId) != NIL) streamPost(post, s);
+      const bool proceed = P.pre[ps.partnerPre].kind == PK_ABSENT_LOGICAL
+                               ? partnerCanProceed(ps.partnerPre, s)
+                               : sev(s, P.pre[ps.partnerPre].stateId) != NIL;
+      if (proceed) streamPost(post, s);
       else fl(ps.pre) |= FL_CHANGED;
     } else {
       streamPost(post, s);
@@ -706,12 +730,39 @@ struct Lane {
     notifyAt(pr.sched, lst(ps.pre));
   }
 
+  // AbsentLogicalPostStateProcessor.process: state changed, event returned,
+  // updateLastArrivalTime (lst = LogicalStreamPreState.lastArrivalTime) -- no partner check
+  __device__ void absentLogicalPost(int post, uint16_t s) {
+    const DPost& ps = P.post[post];
+    fl(ps.pre) |= FL_CHANGED;
+    evret |= 1u << post;
+    lst(ps.pre) = ev_ts(sev(s, ps.stateId));
+  }
+
+  // AbsentLogicalPreStateProcessor.partnerCanProceed (:353-388), p = the absent operand
+  __device__ bool partnerCanProceed(int p, uint16_t s) {
+    const DPre& pr = P.pre[p];
+    const DPost& tp = P.post[pr.thisPost];
+    if (P.seq && tp.nextEvery < 0 && lst(p) > 0) return false;
+    if (pr.waiting == -1) {
+      if (tp.nextEvery < 0) return sev(s, pr.stateId) == NIL;
+      if (lst(p) > 0) {
+        lst(p) = 0;
+        init_pre(p);
+        return false;
+      }
+      return true;
+    }
+    return sev(s, pr.stateId) != NIL;
+  }
+
   __device__ void postProcess(int post, uint16_t s) {
     switch (P.post[post].kind) {
       case PK_STREAM: streamPost(post, s); break;
       case PK_COUNT: countPost(post, s); break;
       case PK_LOGICAL: logicalPost(post, s); break;
       case PK_ABSENT: absentPost(post, s); break;
+      case PK_ABSENT_LOGICAL: absentLogicalPost(post, s); break;
     }
   }
 
@@ -825,8 +876,48 @@ struct Lane {
     pn(p) = (uint16_t)w;
   }
 
+  // AbsentLogicalPreStateProcessor.processAndReturn (:243-296): an X arrival
+  // takes the partials it passes out of this processor's pending list; never
+  // returns events itself
+  __device__ void absentLogicalPAR(int p, uint16_t rec) {
+    const DPre& pr = P.pre[p];
+    if (fl(p) & FL_INACTIVE) return;
+    const DPost& tp = P.post[pr.thisPost];
+    const int psid = P.pre[pr.partner].stateId;
+    const bool restore = pr.waiting != -1 || (P.seq && pr.ltype == 0 && tp.nextEvery >= 0);
+    int n = pn(p), w = 0;
+    for (int r = 0; r < n; r++) {
+      uint16_t s = pend(p, r);
+      if (pr.ltype == 1 && sev(s, psid) != NIL) continue;
+      const uint16_t cur = sev(s, pr.stateId);
+      const uint16_t c = new_ev(rec);
+      sev(s, pr.stateId) = c;
+      processChain(p, s);
+      if (restore) sev(s, pr.stateId) = cur;
+      bool erased = false;
+      if (take_ret(pr.thisLast)) {
+        erased = true;
+        if (P.seq) {   // also out of the partner's pending list
+          const int q = pr.partner;
+          int m = pn(q), k = 0;
+          for (int i = 0; i < m; i++)
+            if (pend(q, i) != s) pend(q, k++) = pend(q, i);
+          pn(q) = (uint16_t)k;
+        }
+      }
+      if (!(fl(p) & FL_CHANGED)) {
+        sev(s, pr.stateId) = cur;
+        if (P.seq) erased = true;
+      }
+      if (sev(s, pr.stateId) != c) free_ev(c);
+      if (!erased) pend(p, w++) = s;
+    }
+    pn(p) = (uint16_t)w;
+  }
+
   __device__ void processAndReturn(int p, uint16_t rec) {
     switch (P.pre[p].kind) {
+      case PK_ABSENT_LOGICAL: absentLogicalPAR(p, rec); break;
       case PK_STREAM: streamPAR(p, rec, true, true); break;
       case PK_COUNT: countPAR(p, rec); break;
       case PK_LOGICAL: logicalPAR(p, rec); break;
@@ -889,6 +980,92 @@ struct Lane {
     }
   }
 
+  // a fresh StreamEvent (streamEventFactory.newInstance(): ts -1, no data)
+  __device__ uint16_t empty_ev() {
+    const int r = alloc_bit(Y.o_rec_free, Y.recw, Y.RC, OV_REC, MISC_FREE_REC, MISC_HINT_REC);
+    rts(r) = -1;
+    for (int c = 0; c < Y.ncols; c++) rval(r, c) = 0;
+    rnul(r) = 0xFFFFFFFFu;
+    return new_ev((uint16_t)r);
+  }
+  __device__ void add_event(uint16_t s, int sid, uint16_t e) {   // StateEvent.addEvent
+    uint16_t h = sev(s, sid);
+    if (h == NIL) {
+      sev(s, sid) = e;
+      return;
+    }
+    while (enext(h) != NIL) h = enext(h);
+    enext(h) = e;
+  }
+
+  __device__ void absentLogicalSendEvent(int p, uint16_t s) {   // AbsentLogicalPreStateProcessor.sendEvent
+    const DPre& pr = P.pre[p];
+    const DPost& tp = P.post[pr.thisPost];
+    if (tp.hasSelector && accepts(s)) emit(s, new_tag());
+    if (tp.nextPre >= 0) addState(tp.nextPre, s);
+    if (tp.nextEvery >= 0) {
+      addEveryState(tp.nextEvery, s);
+    } else if (pr.isStart) {
+      fl(p) |= FL_INACTIVE;
+      if (pr.ltype == 1 && P.pre[pr.partner].kind == PK_ABSENT_LOGICAL) fl(pr.partner) |= FL_INACTIVE;
+    }
+    if (tp.callbackPre >= 0) countStartStateReset(tp.callbackPre);
+  }
+
+  // AbsentLogicalPreStateProcessor.process(ComplexEventChunk) on a TIMER (:122-218)
+  __device__ void absentLogicalTimer(int p, int64_t currentTime, int64_t nowt) {
+    const DPre& pr = P.pre[p];
+    if (fl(p) & FL_INACTIVE) return;
+    const DPost& tp = P.post[pr.thisPost];
+    const int psid = P.pre[pr.partner].stateId;
+    bool notProcessed = true;
+    if (currentTime >= lst(p) + pr.waiting) {
+      if (pr.isStart && P.seq && nn(p) == 0 && pn(p) == 0) addState(p, new_se());
+      else if (P.seq && nn(p) != 0) resetState(p);
+      updateState(p);
+      uint16_t expired = NIL;
+      misc(MISC_TMPN) = 0;
+      int n = pn(p), w = 0;
+      for (int r = 0; r < n; r++) {
+        uint16_t s = pend(p, r);
+        if (isExpired(s, currentTime)) {
+          expired = s;
+          continue;
+        }
+        const uint16_t own = sev(s, pr.stateId);
+        const bool passed = own == NIL ? currentTime >= sts(s) + pr.waiting : currentTime >= ev_ts(own) + pr.waiting;
+        if (passed) {
+          if (pr.ltype == 1 && sev(s, psid) == NIL) {          // OR: partner not received
+            add_event(s, pr.stateId, empty_ev());
+            push_tmp(s);
+          } else if (pr.ltype == 0 && sev(s, psid) != NIL) {   // AND: partner received, not sent
+            push_tmp(s);
+          } else if (pr.ltype == 0) {                          // AND: let the partner proceed
+            add_event(s, pr.stateId, empty_ev());
+          }
+          continue;
+        }
+        pend(p, w++) = s;
+      }
+      pn(p) = (uint16_t)w;
+      if (expired != NIL && pr.withinEvery >= 0) {
+        addEveryState(pr.withinEvery, expired);
+        updateState(pr.withinEvery);
+      }
+      const int nret = misc(MISC_TMPN);
+      notProcessed = nret == 0;
+      for (int i = 0; i < nret; i++) {
+        const uint16_t s = tmpl(i);
+        sts(s) = currentTime;
+        absentLogicalSendEvent(p, s);
+      }
+      misc(MISC_TMPN) = 0;
+      lst(p) = 0;
+    }
+    if (tp.nextEvery >= 0 || (notProcessed && pr.isStart))
+      notifyAt(pr.sched, (lst(p) == 0 ? nowt : lst(p)) + pr.waiting);
+  }
+
   // ---------------------------------------------------------------- selector / output
   __device__ bool accepts(uint16_t s) {   // QuerySelector.processNoGroupBy event-type filter
     uint8_t t = stype(s);
@@ -937,11 +1114,15 @@ struct Lane {
     for (int i = 0; i < P.ninit; i++) init_pre(P.initSeq[i]);
     for (int p = 0; p < P.npre; p++) {   // partitionCreated for absent processors
       const DPre& pr = P.pre[p];
-      if (pr.kind != PK_ABSENT || (fl(p) & FL_STARTED)) continue;
+      if ((pr.kind != PK_ABSENT && pr.kind != PK_ABSENT_LOGICAL) || (fl(p) & FL_STARTED)) continue;
       fl(p) |= FL_STARTED;
       if (pr.isStart && pr.waiting != -1 && !(fl(p) & FL_INACTIVE)) {
-        lst(p) = now_seed + pr.waiting;
-        notifyAt(pr.sched, lst(p));
+        if (pr.kind == PK_ABSENT) {
+          lst(p) = now_seed + pr.waiting;
+          notifyAt(pr.sched, lst(p));
+        } else {   // AbsentLogicalPreStateProcessor.partitionCreated (:318-335)
+          notifyAt(pr.sched, now_seed + pr.waiting);
+        }
       }
     }
     misc(MISC_SEEDED) = 1;
@@ -1047,7 +1228,8 @@ struct Lane {
         for (int i = 1; i < n; i++) sq(sc, i - 1) = sq(sc, i);
         sqn(sc) = (uint16_t)(n - 1);
         maybe_gc();
-        absentTimer(P.schedPre[sc], nt, tnow);
+        if (P.pre[P.schedPre[sc]].kind == PK_ABSENT_LOGICAL) absentLogicalTimer(P.schedPre[sc], nt, tnow);
+        else absentTimer(P.schedPre[sc], nt, tnow);
         if (ovf) return;
       }
     }
@@ -1140,8 +1322,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     b = a.seg_start[seg];
     e = seg + 1 < a.nseg ? (int64_t)a.seg_start[seg + 1] : a.n_keyed;
   }
-  if (!seeded && !a.partitioned) {   // unpartitioned queries start with the app (now = 0)
-    L.seed(0);
+  if (!seeded && !a.partitioned) {   // unpartitioned queries start with the app
+    L.seed(a.start_time);
     seeded = true;
   }
   uint32_t cur_run = 0xFFFFFFFFu;
@@ -1507,23 +1689,25 @@ struct GraphBuilder {
         }
         const PNode& s1 = n.kids[0];
         const PNode& s2 = n.kids[1];
-        if (s1.absent || s2.absent) {
-          err = "absent logical states (not X and Y) are outside the device path";
-          return {-1, -1, HRt()};
-        }
-        auto mk = [&]() {
+        // absent operands: AbsentLogicalPre/PostStateProcessor, with a scheduler each
+        auto mk = [&](const PNode& sn) {
           HPre pr;
-          pr.kind = PK_LOGICAL;
+          pr.kind = sn.absent ? PK_ABSENT_LOGICAL : PK_LOGICAL;
           pr.ltype = n.ltype;
+          if (sn.absent) {
+            pr.waiting = sn.waiting;
+            pr.sched = n_sched++;
+            sched_pre.push_back((int)pres.size());
+          }
           pres.push_back(pr);
           HPost ps;
-          ps.kind = PK_LOGICAL;
+          ps.kind = sn.absent ? PK_ABSENT_LOGICAL : PK_LOGICAL;
           ps.ltype = n.ltype;
           posts.push_back(ps);
           return std::make_pair((int)pres.size() - 1, (int)posts.size() - 1);
         };
-        auto p1 = mk();
-        auto p2 = mk();
+        auto p1 = mk(s1);
+        auto p2 = mk(s2);
         posts[p1.second].partnerPre = p2.first;
         posts[p2.second].partnerPre = p1.first;
         posts[p1.second].partnerPost = p2.second;
@@ -1571,7 +1755,7 @@ struct GraphBuilder {
     if (post < 0 || pre < 0) return;
     HPost& ps = posts[post];
     ps.nextPre = pre;
-    if (ps.kind == PK_LOGICAL) posts[ps.partnerPost].nextPre = pre;
+    if (ps.kind == PK_LOGICAL || ps.kind == PK_ABSENT_LOGICAL) posts[ps.partnerPost].nextPre = pre;
     if (ps.kind == PK_COUNT) {   // CountPostStateProcessor.java:79-87
       if (pres[ps.pre].isStart && p.state_type == 1 && ps.minC == 0) posts[pres[pre].thisPost].callbackPre = ps.pre;
     }
@@ -1580,7 +1764,7 @@ struct GraphBuilder {
     if (post < 0 || pre < 0) return;
     HPost& ps = posts[post];
     ps.nextEvery = pre;
-    if (ps.kind == PK_LOGICAL) posts[ps.partnerPost].nextEvery = pre;
+    if (ps.kind == PK_LOGICAL || ps.kind == PK_ABSENT_LOGICAL) posts[ps.partnerPost].nextEvery = pre;
   }
 
   void setup(const HRt& r, std::vector<std::vector<int>>& streamPres) {
@@ -1951,6 +2135,7 @@ struct NfaEngine : Engine {
     ra.partitioned = partitioned;
     ra.ncalls = ncalls;
     ra.seq0 = seq;
+    ra.start_time = start_time;
     ra.call_of = d_call_of.as<int32_t>();
     ra.call_now = d_now.as<int64_t>();
     ra.call_changed = d_changed.as<uint8_t>();
