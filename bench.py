@@ -402,9 +402,13 @@ def main():
     # `within` lookahead, so the counts come from one untimed step on the sort path.
     calib = None
     if pattern:
+        prev = os.environ.get("SHD_NO_BUCKET")
         os.environ["SHD_NO_BUCKET"] = "1"
         calib = run_step()
-        del os.environ["SHD_NO_BUCKET"]
+        if prev is None:
+            del os.environ["SHD_NO_BUCKET"]
+        else:
+            os.environ["SHD_NO_BUCKET"] = prev
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()

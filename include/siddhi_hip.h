@@ -84,6 +84,15 @@ typedef struct shd_out {
   const int64_t* ts;            /* [n_rows]                                      */
   const uint64_t* values;       /* [n_rows * n_cols] 64-bit payloads (row-major)  */
   const uint8_t* nulls;         /* [n_rows * n_cols]                             */
+  const int64_t* in_seq;        /* [n_rows] arrival index (0-based, over every event
+                                   pushed to this query) of the input event whose
+                                   processing emitted the row -- the completing
+                                   event of a match, the last event of a group-by
+                                   row, the first event of the call whose time
+                                   change fired a timer row.  Rows are in
+                                   (in_seq, processor, pending-list) order, so the
+                                   outputs of key-sharded queries merge by the
+                                   global sequence of in_seq. */
 } shd_out;
 
 typedef struct shd_counters {

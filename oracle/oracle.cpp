@@ -532,6 +532,7 @@ struct OutRow {
   int64_t chunk;
   int type;
   int64_t ts;
+  int64_t seq = -1;   // arrival index of the emitting input event (shd_out.in_seq)
   std::vector<uint64_t> vals;
   std::vector<uint8_t> nul;
 };
@@ -1643,6 +1644,7 @@ struct Engine {
       std::vector<std::vector<OutRow>> holders;
       for (Ev* e : evs) {
         counters[0]++;
+        cur_seq = e->seq;
         stabilize(stream, e->ts);
         for (int k = (int)procs.size() - 1; k >= 0; k--) {
           Ev* ce = clone_ev(e);
@@ -1664,6 +1666,7 @@ struct Engine {
       std::vector<SE*> ret;
       for (Ev* e : evs) {
         counters[0]++;
+        cur_seq = e->seq;
         stabilize(stream, e->ts);
         Ev* ce = clone_ev(e);
         std::vector<SE*> r = processAndReturn(procs[0], ce);
@@ -1682,8 +1685,11 @@ struct Engine {
     return false;
   }
 
+  int64_t cur_seq = 0;   // the event being processed (timers: the next event's index)
+
   OutRow make_row(SE* s) {
     OutRow r;
+    r.seq = cur_seq;
     r.chunk = -1;
     r.type = s->type;
     r.ts = s->ts;
@@ -1753,6 +1759,7 @@ struct Engine {
 
   void set_time(int64_t t) {
     // TimestampGeneratorImpl.setCurrentTimestamp: only moves forward.
+    cur_seq = seq;   // timer rows: before the next event
     if (t >= now) {
       now = t;
       onTimeChange(t);
@@ -1971,6 +1978,7 @@ struct Engine {
       OutRow r;
       r.type = e->type;
       r.ts = e->ts;
+      r.seq = e->seq;
       EvalCtx cx;
       cx.ev = e;
       cx.aggs = &agg_vals;
@@ -2218,6 +2226,11 @@ void orc_get_rows(void* h, int64_t* chunk, int32_t* type, int64_t* ts, uint64_t*
       nulls[i * no + k] = r.nul[k];
     }
   }
+}
+
+void orc_get_rows_seq(void* h, int64_t* seq) {
+  Engine* e = (Engine*)h;
+  for (size_t i = 0; i < e->rows.size(); i++) seq[i] = e->rows[i].seq;
 }
 
 void orc_clear_rows(void* h) { ((Engine*)h)->rows.clear(); }

@@ -16,7 +16,7 @@ enum EngineKind { ENG_PATTERN = 1, ENG_WINDOW = 2, ENG_FILTER = 3, ENG_NFA = 4 }
 struct OutputBuffer {
   int ncols = 0;
   int64_t count = 0, cap = 0;
-  DevBuf chunk, type, ts, vals, nulls;
+  DevBuf chunk, type, ts, vals, nulls, seq;
   void init(int nc) { ncols = nc; }
   // Make room for `extra` more rows (copies existing rows on growth).
   void ensure(int64_t extra, hipStream_t s);
@@ -25,6 +25,7 @@ struct OutputBuffer {
   int64_t* d_ts() { return ts.as<int64_t>(); }
   uint64_t* d_vals() { return vals.as<uint64_t>(); }
   uint8_t* d_nulls() { return nulls.as<uint8_t>(); }
+  int64_t* d_seq() { return seq.as<int64_t>(); }   // shd_out.in_seq
 };
 
 // A batch staged on the device (columns either borrowed device pointers or

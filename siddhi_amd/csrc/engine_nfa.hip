@@ -32,6 +32,7 @@
 // with (event seq, timer time, key) ordering tags and sorted into the
 // reference's callback order on the device.
 #include <algorithm>
+#include <functional>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -96,7 +97,13 @@ struct NfaLayout {
   int64_t o_ev_rec, o_ev_next, o_ev_free, o_ev_mark;
   int64_t o_rec_ts, o_rec_val, o_rec_nul, o_rec_free, o_rec_mark;
   int64_t o_ret, o_tmp, o_wk, o_key, o_misc;
+  int64_t o_cse, o_cev;              // canonical ids (window-lane state hashes)
   int64_t blk;
+  // field table (one key's state = these fields, lane-interleaved): lane copies
+  static constexpr int kMaxFields = 40;
+  int nf;
+  int f_sz[kMaxFields];
+  int64_t f_off[kMaxFields], f_cnt[kMaxFields];
 };
 
 struct NfaCtl {
@@ -119,6 +126,16 @@ struct NfaRunArgs {
   int64_t nlanes;
   int64_t seq0;
   int64_t start_time;   // app start (seed of unpartitioned plans)
+  // window-lane mode (unpartitioned bounded-span sequences): lane c owns the
+  // events [c*chunk_len, (c+1)*chunk_len) and first replays the `warm` events
+  // before them from a fresh state, output suppressed; rows < 0 are the last
+  // n_pre events of the previous push (prefix)
+  int64_t chunk_len;
+  int64_t warm;
+  int64_t n_pre;
+  ColSet prefix;
+  uint64_t* hash_w;   // per lane: state hash after the warm-up (= before the first owned event)
+  uint64_t* hash_e;   // per lane: state hash after the last owned event
   const int32_t* call_of;
   const int64_t* call_now;
   const uint8_t* call_changed;
@@ -182,6 +199,7 @@ struct Lane {
   uint32_t tagc;
   uint64_t t_prim, t_sec, t_ter;
   int64_t last_seq;
+  int64_t own_from;   // window lanes: rows of events before this seq are warm-up (no output)
   int cdone;
 
   __device__ Lane(const NfaProg& p, const NfaLayout& y, const NfaRunArgs& a, DExprSet e)
@@ -209,6 +227,73 @@ struct Lane {
   __device__ __forceinline__ uint32_t& wk(int i) { return ks.at<uint32_t>(Y.o_wk, i); }
   __device__ __forceinline__ uint32_t& misc(int i) { return ks.at<uint32_t>(Y.o_misc, i); }
   __device__ __forceinline__ uint64_t& bits(int64_t off, int w) { return ks.at<uint64_t>(off, w); }
+
+  // ---------------------------------------------------------------- window lanes
+  // copy every field of another key's state into this one (lane copy)
+  __device__ void copy_lane_from(const KS& src) {
+    for (int f = 0; f < Y.nf; f++) {
+      const int sz = Y.f_sz[f];
+      for (int64_t e = 0; e < Y.f_cnt[f]; e++) {
+        const char* sp = src.b + Y.f_off[f] + (e * kLaneBlock + src.l) * sz;
+        char* dp = ks.b + Y.f_off[f] + (e * kLaneBlock + ks.l) * sz;
+        for (int k = 0; k < sz; k++) dp[k] = sp[k];
+      }
+    }
+  }
+  // Canonical hash of the key's NFA state (pending / new lists in order, each
+  // StateEvent by content -- timestamp, type, event chains by event record --
+  // with object identity kept: a StateEvent or StreamEvent seen before hashes
+  // as its first-visit index, so shared objects (count-state aliasing) and
+  // equal copies differ).  Two lanes whose states hash equal continue equally.
+  __device__ uint16_t& cse(int i) { return ks.at<uint16_t>(Y.o_cse, i); }
+  __device__ uint16_t& cev(int i) { return ks.at<uint16_t>(Y.o_cev, i); }
+  __device__ uint64_t state_hash() {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) {
+      h ^= x;
+      h *= 1099511628211ull;
+      h ^= h >> 29;
+    };
+    for (int i = 0; i <= Y.SC; i++) cse(i) = NIL;
+    for (int i = 0; i <= Y.EC; i++) cev(i) = NIL;
+    uint16_t nse = 0, nev = 0;
+    auto hse = [&](uint16_t s) {
+      if (s > Y.SC) return;
+      if (cse(s) != NIL) {
+        mix(0xA0000ull + cse(s));
+        return;
+      }
+      cse(s) = nse++;
+      mix(0xB0000ull);
+      mix((uint64_t)sts(s));
+      mix(stype(s));
+      for (int st = 0; st < Y.nstates; st++) {
+        mix(0xC0000ull + st);
+        for (uint16_t e = sev(s, st); e != NIL && e < Y.EC; e = enext(e)) {
+          if (cev(e) != NIL) {
+            mix(0xD0000ull + cev(e));
+            break;
+          }
+          cev(e) = nev++;
+          const uint16_t r = erec(e);
+          if (r >= Y.RC) continue;
+          mix((uint64_t)rts(r));
+          for (int c = 0; c < Y.ncols; c++) mix(rval(r, c));
+          mix(rnul(r));
+        }
+      }
+    };
+    for (int p = 0; p < P.npre; p++) {
+      mix(fl(p) & (FL_INIT | FL_STARTED | FL_SSRESET | FL_INACTIVE));
+      const int a = pn(p), b = nn(p);
+      mix(0xE0000ull + a);
+      for (int i = 0; i < a; i++) hse(pend(p, i));
+      mix(0xF0000ull + b);
+      for (int i = 0; i < b; i++) hse(nw(p, i));
+    }
+    mix(evret);
+    return h;
+  }
 
   // ---------------------------------------------------------------- pools
   // first free handle at or after the hint word (wrapping); cap = sink on exhaustion
@@ -837,6 +922,7 @@ struct Lane {
           (pr.stateId + 2 < Y.nstates && sev(s, pr.stateId + 2) != NIL))
         continue;   // the next state already took this partial
       uint16_t c = new_ev(rec);
+      if (ovf) return;   // pool exhausted: never link the sink element into a chain
       uint16_t h = sev(s, pr.stateId);
       if (h == NIL) {
         sev(s, pr.stateId) = c;
@@ -916,6 +1002,7 @@ struct Lane {
   }
 
   __device__ void processAndReturn(int p, uint16_t rec) {
+    if (ovf) return;   // capacity exceeded: the push fails with SHD_E_CAPACITY
     switch (P.pre[p].kind) {
       case PK_ABSENT_LOGICAL: absentLogicalPAR(p, rec); break;
       case PK_STREAM: streamPAR(p, rec, true, true); break;
@@ -989,6 +1076,7 @@ struct Lane {
     return new_ev((uint16_t)r);
   }
   __device__ void add_event(uint16_t s, int sid, uint16_t e) {   // StateEvent.addEvent
+    if (ovf) return;
     uint16_t h = sev(s, sid);
     if (h == NIL) {
       sev(s, sid) = e;
@@ -1075,6 +1163,7 @@ struct Lane {
   }
   __device__ uint64_t new_tag() { return ((uint64_t)slot << 24) | (uint64_t)(tagc++ & 0xFFFFFF); }
   __device__ void emit(uint16_t s, uint64_t tag) {
+    if (last_seq < own_from) return;   // warm-up event of a window lane
     unsigned long long idx = atomicAdd(&A.ctl->rows, 1ull);
     if ((int64_t)idx >= A.R) {
       ovf |= OV_ROWS;
@@ -1147,8 +1236,10 @@ struct Lane {
     int r = alloc_bit(Y.o_rec_free, Y.recw, Y.RC, OV_REC, MISC_FREE_REC, MISC_HINT_REC);
     rts(r) = ts;
     uint32_t nm = 0;
-    for (int c = 0; c < A.batch.ncols; c++) {
-      Val v = col_load(A.batch, row, c);
+    const ColSet& cs = row < 0 ? A.prefix : A.batch;   // rows < 0: the previous push's tail
+    const int64_t cr = row < 0 ? row + A.n_pre : row;
+    for (int c = 0; c < cs.ncols; c++) {
+      Val v = col_load(cs, cr, c);
       rval(r, c) = v.b;
       if (v.null) nm |= 1u << c;
     }
@@ -1159,7 +1250,7 @@ struct Lane {
   __device__ void process_event(int64_t row) {
     maybe_gc();
     const int si = A.stream;
-    const int64_t ts = A.batch.ts[row];
+    const int64_t ts = row < 0 ? A.prefix.ts[row + A.n_pre] : A.batch.ts[row];
     const uint16_t rec = make_rec(row, ts);
     stabilize(si, ts);
     const int np = P.nsp[si];
@@ -1299,7 +1390,9 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     seg = a.slot_seg ? (int64_t)a.slot_seg[slot] : -1;
   } else {
     seg = lane_id;
-    slot = a.seg_slot ? (int64_t)a.seg_slot[seg] : 0;
+    // window lane c works in slot c + 1 (slot 0 holds the carried state, read
+    // by lane 0); the unpartitioned one-lane plan runs in slot 0
+    slot = a.seg_slot ? (int64_t)a.seg_slot[seg] : (a.chunk_len > 0 ? lane_id + 1 : 0);
   }
   Lane L(sprog, slay, a, es);
   L.slot = slot;
@@ -1312,6 +1405,42 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   L.t_prim = L.t_sec = L.t_ter = 0;
   L.cdone = -1;
   L.last_seq = a.seq0;
+  L.own_from = INT64_MIN;
+  if (a.chunk_len > 0) {
+    // Window lane.  Lane 0 continues the exact carried state (slot 0, the
+    // previous push's end state); lane c > 0 starts fresh `warm` events before
+    // its chunk (output suppressed) and is valid when its state after the
+    // warm-up equals lane c-1's state at its end (hash_w[c] == hash_e[c-1],
+    // checked by k_win_check; on any mismatch the host reruns the push on one
+    // lane from slot 0).
+    const int64_t ob = lane_id * a.chunk_len;
+    const int64_t oe = ob + a.chunk_len < a.n_keyed ? ob + a.chunk_len : a.n_keyed;
+    L.key = 0;
+    L.cdone = a.ncalls - 1;   // no timers in this mode
+    if (lane_id == 0) {
+      KS carry;
+      carry.b = a.state;
+      carry.l = 0;
+      L.copy_lane_from(carry);
+      if (L.misc(MISC_SEEDED) == 0) L.seed(a.start_time);
+      L.evret = L.misc(MISC_EVRET);
+    } else {
+      L.evret = 0;
+      L.seed(a.start_time);
+      int64_t wb = ob - a.warm;
+      if (wb < -a.n_pre) wb = -a.n_pre;
+      L.own_from = a.seq0 + ob;
+      for (int64_t row = wb; row < ob && !L.ovf; row++) L.process_event(row);
+      a.hash_w[lane_id] = L.state_hash();
+    }
+    for (int64_t row = ob; row < oe && !L.ovf; row++) L.process_event(row);
+    L.misc(MISC_EVRET) = L.evret;
+    a.hash_e[lane_id] = L.state_hash();
+    if (L.ovf) atomicOr(&a.ctl->overflow, L.ovf);
+    if (L.partials) atomicAdd(&a.ctl->partials, L.partials);
+    if (L.scans) atomicAdd(&a.ctl->scans, L.scans);
+    return;
+  }
   bool seeded = L.misc(MISC_SEEDED) != 0;
   L.key = L.ks.at<uint64_t>(slay.o_key, 0);   // written by k_store_keys (0 when unpartitioned)
   L.evret = seeded ? L.misc(MISC_EVRET) : 0;
@@ -1353,6 +1482,25 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   if (L.partials) atomicAdd(&a.ctl->partials, L.partials);
   if (L.scans) atomicAdd(&a.ctl->scans, L.scans);
   if (live) atomicAdd(&a.ctl->live, live);
+}
+
+// window lanes: lane c > 0 is valid iff its warm-up state equals lane c-1's end state
+__global__ void k_win_check(const uint64_t* hw, const uint64_t* he, int64_t nl, unsigned int* bad) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; c < nl; c += (int64_t)gridDim.x * blockDim.x)
+    if (hw[c] != he[c - 1]) atomicAdd(bad, 1u);
+}
+
+// the last lane's end state becomes the carried state (slot 0)
+__global__ void k_win_carry(const NfaProg* __restrict__ gprog, const NfaLayout* __restrict__ glay,
+                            const NfaRunArgs* __restrict__ ap, int64_t src_slot) {
+  const NfaRunArgs& a = *ap;
+  Lane L(*gprog, *glay, a, a.es);
+  L.ks.b = a.state;
+  L.ks.l = 0;
+  KS src;
+  src.b = a.state + (src_slot / kLaneBlock) * glay->blk;
+  src.l = (int)(src_slot % kLaneBlock);
+  L.copy_lane_from(src);
 }
 
 // ---------------------------------------------------------------- batch preparation
@@ -1574,14 +1722,16 @@ __global__ void k_tag_heads(const uint64_t* tag, const uint32_t* perm, int64_t n
 }
 __global__ void k_out_rows(const uint32_t* perm, const uint32_t* hpos, const uint32_t* head, int64_t n, int nout,
                            int64_t chunk0, int64_t row0, const int64_t* sts, const int32_t* stype,
-                           const uint64_t* svals, const uint8_t* snul, int64_t* o_chunk, int32_t* o_type,
-                           int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+                           const uint64_t* svals, const uint8_t* snul, const uint64_t* sprim, int64_t* o_chunk,
+                           int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = perm[i];
     const int64_t r = row0 + i;
     o_chunk[r] = chunk0 + (int64_t)hpos[i] + (int64_t)head[i] - 1;
     o_type[r] = stype[j];
     o_ts[r] = sts[j];
+    // primary tag: 2 * seq + 1 for an event's rows, 2 * (first seq of the call) for timer rows
+    o_seq[r] = (int64_t)(sprim[j] >> 1);
     for (int c = 0; c < nout; c++) {
       o_vals[r * nout + c] = svals[j * nout + c];
       o_nul[r * nout + c] = snul[j * nout + c];
@@ -1827,6 +1977,21 @@ struct NfaEngine : Engine {
   NfaProg prog{};
   NfaLayout lay{};
   std::vector<std::vector<int>> pre_filters;
+  // Window lanes (unpartitioned sequences whose partials span at most `span`
+  // events, every-started, one stream): a sequence partial survives an event
+  // only by advancing on it (StateStreamRuntime.resetAndUpdate clears every
+  // non-start pending list, ST/StateStreamRuntime.java:81-84), so the state
+  // after event j depends on events (j-span, j] alone.  The push is cut into
+  // chunks, one lane each, every lane replaying `warm` >= span events before
+  // its chunk from a fresh state (output suppressed); the last `warm` events
+  // carry to the next push (prefix) instead of key blocks.
+  bool windowed = false;
+  int64_t win_warm = 0;
+  int win_stream = 0;
+  DevBuf pre_ts[2], pre_col[2][kMaxCols], pre_nul[2][kMaxCols], d_hash;
+  int64_t win_fallbacks = 0;   // pushes rerun on one lane (a lane's warm-up state disagreed)
+  int pre_cur = 0;
+  int64_t n_pre = 0;
   bool partitioned = false;
   int key_expr[kNStream], key_col[kNStream], key_type[kNStream];
   // key blocks
@@ -1864,6 +2029,7 @@ struct NfaEngine : Engine {
     counters = shd_counters{};
     nslots = 0;
     epoch = 0;
+    n_pre = 0;
     if (state.p && slot_cap > 0) SHD_HIP(hipMemset(state.p, 0, (size_t)(slot_cap / kLaneBlock) * lay.blk));
     if (ht_state.p && ht_cap > 0) SHD_HIP(hipMemset(ht_state.p, 0, (size_t)ht_cap * 4));
     SHD_HIP(hipDeviceSynchronize());
@@ -1871,6 +2037,19 @@ struct NfaEngine : Engine {
 
   // key blocks (all per-key NFA state) + key directory, byte for byte
   void save_state(SnapW& w) override {
+    if (windowed) {   // carried state (slot 0's block) + the carried tail events
+      const auto& types = plan.stream_types[win_stream];
+      w.put<int64_t>(win_warm);
+      w.put<int64_t>(slot_cap > 0 ? 1 : 0);
+      if (slot_cap > 0) w.dev(state.p, (size_t)lay.blk);
+      w.put<int64_t>(n_pre);
+      w.dev(pre_ts[pre_cur].p, (size_t)n_pre * 8);
+      for (size_t c = 0; c < types.size(); c++) {
+        w.dev(pre_col[pre_cur][c].p, (size_t)n_pre * type_size(types[c]));
+        w.dev(pre_nul[pre_cur][c].p, (size_t)n_pre);
+      }
+      return;
+    }
     w.put<int64_t>(slot_cap);
     w.put<int64_t>(nslots);
     w.put<int64_t>(ht_cap);
@@ -1882,6 +2061,27 @@ struct NfaEngine : Engine {
     w.dev(ht_slot.p, (size_t)ht_cap * 4);
   }
   void load_state(SnapR& r) override {
+    if (windowed) {
+      const auto& types = plan.stream_types[win_stream];
+      const int64_t ww = r.get<int64_t>();
+      if (ww < 1 || ww > (1 << 16)) throw Error(SHD_E_ARG, "snapshot of a different plan");
+      if (r.get<int64_t>() != 0) {
+        ensure_slots(kLaneBlock);
+        r.dev_into(state.p, (size_t)lay.blk);
+      }
+      win_warm = ww;
+      const int64_t np = r.get<int64_t>();
+      if (np < 0 || np > win_warm) throw Error(SHD_E_ARG, "snapshot of a different plan");
+      reserve_prefix(0, std::max<int64_t>(np, 1));
+      r.dev_into(pre_ts[0].p, (size_t)np * 8);
+      for (size_t c = 0; c < types.size(); c++) {
+        r.dev_into(pre_col[0][c].p, (size_t)np * type_size(types[c]));
+        r.dev_into(pre_nul[0][c].p, (size_t)np);
+      }
+      pre_cur = 0;
+      n_pre = np;
+      return;
+    }
     const int64_t sc = r.get<int64_t>(), ns = r.get<int64_t>(), hc = r.get<int64_t>();
     const uint32_t ep = r.get<uint32_t>();
     if (r.get<int64_t>() != (int64_t)lay.blk || sc < 0 || ns < 0 || ns > sc || hc < 0 || sc % kLaneBlock)
@@ -2094,6 +2294,54 @@ struct NfaEngine : Engine {
     return nseg;
   }
 
+  void reserve_prefix(int k, int64_t n) {
+    const auto& types = plan.stream_types[win_stream];
+    pre_ts[k].reserve(n * 8);
+    for (size_t c = 0; c < types.size(); c++) {
+      pre_col[k][c].reserve(n * type_size(types[c]));
+      pre_nul[k][c].reserve(n);
+    }
+  }
+
+  ColSet prefix_cs() {
+    const auto& types = plan.stream_types[win_stream];
+    ColSet cs{};
+    cs.ncols = (int)types.size();
+    cs.ts = pre_ts[pre_cur].as<int64_t>();
+    cs.n = n_pre;
+    for (size_t c = 0; c < types.size(); c++) {
+      cs.col[c] = pre_col[pre_cur][c].p;
+      cs.nul[c] = pre_nul[pre_cur][c].as<uint8_t>();
+      cs.type[c] = types[c];
+    }
+    return cs;
+  }
+
+  // the last `warm` events of (prefix ++ batch) become the next prefix
+  void roll_prefix(const Staged& b) {
+    const auto& types = plan.stream_types[win_stream];
+    const int64_t keep = std::min<int64_t>(win_warm, n_pre + b.n);
+    const int64_t from_b = std::min<int64_t>(keep, b.n), from_p = keep - from_b;
+    const int nx = pre_cur ^ 1;
+    reserve_prefix(nx, std::max<int64_t>(win_warm, 1));
+    hipStream_t s = stream;
+    auto cp = [&](void* dst, const void* src, size_t bytes) {
+      if (bytes) SHD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    };
+    cp(pre_ts[nx].p, pre_ts[pre_cur].as<int64_t>() + (n_pre - from_p), from_p * 8);
+    cp(pre_ts[nx].as<int64_t>() + from_p, b.cs.ts + (b.n - from_b), from_b * 8);
+    for (size_t c = 0; c < types.size(); c++) {
+      const int64_t sz = type_size(types[c]);
+      cp(pre_col[nx][c].p, pre_col[pre_cur][c].as<char>() + (n_pre - from_p) * sz, from_p * sz);
+      cp(pre_col[nx][c].as<char>() + from_p * sz, (const char*)b.cs.col[c] + (b.n - from_b) * sz, from_b * sz);
+      cp(pre_nul[nx][c].p, pre_nul[pre_cur][c].as<uint8_t>() + (n_pre - from_p), from_p);
+      if (b.cs.nul[c]) cp(pre_nul[nx][c].as<uint8_t>() + from_p, b.cs.nul[c] + (b.n - from_b), from_b);
+      else if (from_b) SHD_HIP(hipMemsetAsync(pre_nul[nx][c].as<uint8_t>() + from_p, 0, from_b, s));
+    }
+    pre_cur = nx;
+    n_pre = keep;
+  }
+
   // One push (b != nullptr) or one time change (b == nullptr, time t).
   void run_push(const Staged* b, int64_t t_only) {
     hipStream_t s = stream;
@@ -2143,8 +2391,31 @@ struct NfaEngine : Engine {
     ra.es = dset();
     const bool timers = prog.nsched > 0;
     int64_t nseg = 0, n_keyed = n;
+    const bool win = windowed && b && n > 0;
+    bool win_one = false;   // window push rerun on one lane
 
-    if (!partitioned) {
+    if (win) {
+      // lanes of ~64 events, enough lanes to fill the chip
+      int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(1024, n / 16384));
+      if (const char* e = getenv("SHD_NFA_CHUNK")) chunk = std::max(1, atoi(e));
+      const int64_t nl = ceil_div(n, chunk);
+      ensure_slots(nl + 1);
+      d_hash.reserve(2 * nl * 8);
+      ra.hash_w = d_hash.as<uint64_t>();
+      ra.hash_e = d_hash.as<uint64_t>() + nl;
+      ra.chunk_len = chunk;
+      ra.warm = win_warm;
+      ra.n_pre = n_pre;
+      if (n_pre > 0) ra.prefix = prefix_cs();
+      ra.lanes_over_slots = 0;
+      ra.nlanes = nl;
+      ra.nseg = nl;
+      if (n > 0) {
+        hipLaunchKernelGGL(k_call_run, dim3(grid_for(n)), dim3(kBlock), 0, s, (const int32_t*)d_call_of.as<int32_t>(),
+                           n, d_run.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+      }
+    } else if (!partitioned) {
       ensure_slots(1);
       nslots = 1;
       if (n > 0) {
@@ -2192,10 +2463,35 @@ struct NfaEngine : Engine {
       SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
       const NfaProg* dp = dev_args(prog);
       const NfaLayout* dl = dev_args(lay);
+      const NfaRunArgs* dra = dev_args(ra);
       hipLaunchKernelGGL(k_nfa_run, dim3((unsigned)ceil_div(ra.nlanes, kLaneBlock)), dim3(kLaneBlock), 0, s, dp, dl,
-                         dev_args(ra));
+                         dra);
       SHD_CHECK_LAUNCH();
+      if (win && ra.nlanes > 1)
+        hipLaunchKernelGGL(k_win_check, dim3(grid_for(ra.nlanes)), dim3(kBlock), 0, s,
+                           (const uint64_t*)ra.hash_w, (const uint64_t*)ra.hash_e, ra.nlanes, &d_ctl.as<NfaCtl>()->count);
       hc = read_ctl();
+      if (win && !hc.overflow) {
+        if (hc.count == 0) {
+          // every lane verified: the last lane's end state is the carried state
+          hipLaunchKernelGGL(k_win_carry, dim3(1), dim3(1), 0, s, dp, dl, dra, ra.nlanes);
+          SHD_CHECK_LAUNCH();
+        } else {
+          // a lane's warm-up did not reach its predecessor's state: rerun the
+          // push on one lane from the carried state (exact), longer warm-ups next
+          win_fallbacks++;
+          win_warm = std::min<int64_t>(win_warm * 2, 1 << 16);
+          SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
+          ra.chunk_len = 0;
+          ra.lanes_over_slots = 0;
+          ra.nlanes = 1;
+          ra.nseg = 1;
+          win_one = true;
+          hipLaunchKernelGGL(k_nfa_run, dim3(1), dim3(kLaneBlock), 0, s, dp, dl, dev_args(ra));
+          SHD_CHECK_LAUNCH();
+          hc = read_ctl();
+        }
+      }
     }
     mark("nfa");
     if (hc.overflow || (int64_t)hc.rows > R) {
@@ -2208,7 +2504,8 @@ struct NfaEngine : Engine {
       throw Error(SHD_E_CAPACITY, msg);
     }
     const int64_t m = (int64_t)hc.rows;
-    if (m > 0) order_rows(m, partitioned, timers, n);
+    if (m > 0) order_rows(m, partitioned || (win && !win_one), timers, n);   // window lanes: merge by event order
+    if (win) roll_prefix(*b);
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -2227,7 +2524,7 @@ struct NfaEngine : Engine {
     counters.matches += m;
     counters.partials += (int64_t)hc.partials;
     counters.partial_scans += (int64_t)hc.scans;
-    counters.carry = (int64_t)hc.live;
+    counters.carry = windowed ? n_pre : (int64_t)hc.live;
     counters.kernel_ns = (int64_t)(ms * 1e6);
   }
 
@@ -2278,8 +2575,8 @@ struct NfaEngine : Engine {
                        (const uint32_t*)d_thpos.as<uint32_t>(), (const uint32_t*)d_thead.as<uint32_t>(), m, prog.nout,
                        chunk_seq, out.count, (const int64_t*)st_ts.as<int64_t>(),
                        (const int32_t*)st_type.as<int32_t>(), (const uint64_t*)st_vals.as<uint64_t>(),
-                       (const uint8_t*)st_nul.as<uint8_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(),
-                       out.d_nulls());
+                       (const uint8_t*)st_nul.as<uint8_t>(), (const uint64_t*)st_p.as<uint64_t>(), out.d_chunk(),
+                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
     SHD_CHECK_LAUNCH();
     // chunk ids consumed = number of distinct tags
     SHD_HIP(hipMemcpyAsync(h_ctl.as<char>() + 64, d_thpos.as<uint32_t>() + (m - 1), 4, hipMemcpyDeviceToHost, s));
@@ -2447,9 +2744,44 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
       }
   }
 
+  // window lanes: unpartitioned sequence, every-started, one stream, multi
+  // receiver (per (event, state) callbacks), no absent states, bounded span
+  {
+    std::function<int64_t(const PNode&)> span = [&](const PNode& n) -> int64_t {
+      switch (n.kind) {
+        case SHD_NODE_STREAM: return n.absent ? -1 : 1;
+        case SHD_NODE_NEXT: {
+          const int64_t x = span(n.kids[0]), y = span(n.kids[1]);
+          return x < 0 || y < 0 ? -1 : x + y;
+        }
+        case SHD_NODE_EVERY: return span(n.kids[0]);
+        case SHD_NODE_LOGICAL: return n.kids[0].absent || n.kids[1].absent ? -1 : 2;
+        case SHD_NODE_COUNT: return n.max < 0 ? -1 : n.max;
+      }
+      return -1;
+    };
+    int used = 0, ws = -1;
+    for (size_t st = 0; st < streamPres.size(); st++)
+      if (!streamPres[st].empty()) {
+        used++;
+        ws = (int)st;
+      }
+    bool every_start = false;
+    for (int i = 0; i < npre; i++)
+      if (g.pres[i].isStart && g.posts[g.pres[i].thisPost].nextEvery >= 0) every_start = true;
+    const int64_t sp = span(p.root);
+    const char* wenv = getenv("SHD_NFA_WINDOW");
+    if (!e->partitioned && p.state_type == 1 && g.n_sched == 0 && sp > 0 && sp <= 256 && used == 1 &&
+        streamPres[ws].size() > 1 && every_start && !(wenv && wenv[0] == '0') && list_hint == 0) {
+      e->windowed = true;
+      e->win_stream = ws;
+      e->win_warm = 2 * sp + 2;
+    }
+  }
+
   // per-key capacities: one key (unpartitioned) gets deep lists, many keys get lean blocks
   NfaLayout& Y = e->lay;
-  const bool many = e->partitioned;
+  const bool many = e->partitioned || e->windowed;
   // list_hint (a pattern query handing its open partials over): the one key of
   // an unpartitioned plan must hold about that many partials at once
   int L0 = many ? 32 : 2048, S0 = many ? 128 : 8192;
@@ -2477,9 +2809,14 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.evw = (Y.EC + 1 + 63) / 64;
   Y.recw = (Y.RC + 1 + 63) / 64;
   int64_t off = 0;
+  Y.nf = 0;
   auto field = [&](int64_t count, int sz) {
     int64_t o = off;
     off += (count * kLaneBlock * sz + 255) & ~int64_t(255);
+    Y.f_off[Y.nf] = o;
+    Y.f_cnt[Y.nf] = count;
+    Y.f_sz[Y.nf] = sz;
+    Y.nf++;
     return o;
   };
   Y.o_pend = field((int64_t)npre * (Y.L + 1), 2);
@@ -2509,6 +2846,8 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.o_wk = field(Y.WK + 1, 4);
   Y.o_key = field(1, 8);
   Y.o_misc = field(MISC_N, 4);
+  Y.o_cse = field(Y.SC + 1, 2);
+  Y.o_cev = field(Y.EC + 1, 2);
   Y.blk = off;
   return e;
 }

@@ -1486,7 +1486,7 @@ struct ProjArgs {
 
 __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj,
                                                     const uint32_t* pi, int64_t m, int64_t* o_chunk, int32_t* o_type,
-                                                    int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+                                                    int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq) {
   const ProjArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -1512,6 +1512,7 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
     }
     o_ts[row] = x.ts(j);
     o_type[row] = 0;
+    o_seq[row] = x.seq(j);
     // MultiProcessStreamReceiver: one callback chunk per (event, processor)
     o_chunk[row] = a.logical ? 2 * x.seq(j) + br : (a.multi ? x.seq(j) : a.chunk0 + k);
   }
@@ -1944,8 +1945,11 @@ struct PatternEngine : Engine {
         type_key64(key_type[slot]) || sA != sB)
       return false;
     const int64_t n_ext = C + b.n;
+    // measured on MI355X (P3, 50M-event pushes, profiles/r02a_*): the bucketed
+    // walk (1.26 ms) plus its pass (0.82 ms) lose to the exact key sort and
+    // forward scan (1.9 ms per push in all), so it runs only when forced
     const bool forced = getenv("SHD_BUCKET") != nullptr;
-    if (!forced && n_ext < kPruneMinRows) return false;
+    if (!forced) return false;
     h_agg.reserve(256);
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 208, b.cs.ts, 8, hipMemcpyDeviceToHost, stream));
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 216, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, stream));
@@ -2483,7 +2487,7 @@ struct PatternEngine : Engine {
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
       hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
-                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
       SHD_CHECK_LAUNCH();
       out.count += m;
       if (sA != sB && !logical) chunk_seq += m;

@@ -155,6 +155,7 @@ struct ProjArgs {
   int nout;
   int64_t row0;
   int64_t chunk0;
+  int64_t seq0;   // arrival index of the batch's first event (shd_out.in_seq)
   int partitioned;
 };
 
@@ -162,7 +163,8 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
                                                          const uint32_t* off, const int32_t* call_of,
                                                          const uint32_t* run_excl, const uint32_t* run_start,
                                                          int64_t* o_chunk, int32_t* o_type,
-                                                         int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul) {
+                                                         int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul,
+                                                         int64_t* o_seq) {
   const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -178,6 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
     }
     o_ts[row] = cs.ts[i];
     o_type[row] = 0;
+    o_seq[row] = a.seq0 + i;
     // run of event i = inclusive start count - 1
     o_chunk[row] = a.chunk0 + (a.partitioned ? (int64_t)run_excl[i] + run_start[i] - 1 : (int64_t)call_of[i]);
   }
@@ -1213,13 +1216,14 @@ struct EmitArgs {
   int64_t C;
   int64_t row0;
   int64_t chunk0;
+  int64_t seq0;
 };
 
 __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
                                                  const uint64_t* resv, const uint8_t* resn, const int64_t* resc,
                                                  int64_t* o_chunk, int32_t* o_type, int64_t* o_ts, uint64_t* o_vals,
-                                                 uint8_t* o_nul) {
+                                                 uint8_t* o_nul, int64_t* o_seq) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -1246,6 +1250,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
     }
     o_ts[row] = cs.ts[ev];
     o_type[row] = 0;
+    o_seq[row] = a.seq0 + ev;   // the group's last event of the call
     o_chunk[row] = a.chunk0 + call_of[ev];
   }
 }
@@ -1505,11 +1510,13 @@ struct SingleEngine : Engine {
       pa.row0 = out.count;
       // exclusive run ids: the run of event i is start-scan[i] (+0 if i is a start it is its own index)
       pa.chunk0 = chunk_seq;
+      pa.seq0 = seq;
       pa.partitioned = partitioned;
       hipLaunchKernelGGL(k_project_rows, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(pa), n,
                          (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                          (const int32_t*)d_call_of.as<int32_t>(), (const uint32_t*)d_run.as<uint32_t>(),
-                         (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+                         (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(),
+                         out.d_seq());
       SHD_CHECK_LAUNCH();
       out.count += m;
     }
@@ -1589,12 +1596,13 @@ struct SingleEngine : Engine {
     ea.C = C;
     ea.row0 = out.count;
     ea.chunk0 = chunk_seq;
+    ea.seq0 = seq;
     hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m,
                        (const uint32_t*)fcnt.as<uint32_t>(), (const uint32_t*)foff.as<uint32_t>(),
                        (const uint32_t*)last_of.as<uint32_t>(), (const int32_t*)ievrow.as<int32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const uint64_t*)resv.as<uint64_t>(),
                        (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
-                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls());
+                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
     SHD_CHECK_LAUNCH();
     out.count += nrows;
     counters.matches += nrows;

@@ -240,7 +240,8 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
   if (need <= cap) return;
   int64_t nc = std::max<int64_t>(need, std::max<int64_t>(cap * 2, 4096));
   int w = std::max(ncols, 1);
-  DevBuf c2, t2, ts2, v2, n2;
+  DevBuf c2, t2, ts2, v2, n2, q2;
+  q2.reserve(nc * 8);
   c2.reserve(nc * 8);
   t2.reserve(nc * 4);
   ts2.reserve(nc * 8);
@@ -252,6 +253,7 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
     SHD_HIP(hipMemcpyAsync(ts2.p, ts.p, count * 8, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipMemcpyAsync(v2.p, vals.p, count * w * 8, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipMemcpyAsync(n2.p, nulls.p, count * w, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(q2.p, seq.p, count * 8, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipStreamSynchronize(s));
   }
   std::swap(chunk.p, c2.p); std::swap(chunk.cap, c2.cap);
@@ -259,6 +261,7 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
   std::swap(ts.p, ts2.p); std::swap(ts.cap, ts2.cap);
   std::swap(vals.p, v2.p); std::swap(vals.cap, v2.cap);
   std::swap(nulls.p, n2.p); std::swap(nulls.cap, n2.cap);
+  std::swap(seq.p, q2.p); std::swap(seq.cap, q2.cap);
   cap = nc;
 }
 
@@ -452,7 +455,7 @@ struct shd_query {
   DevBuf stage_ts, stage_col[kMaxCols], stage_nul[kMaxCols];
   PinnedBuf pin;   // host staging for SHD_MEM_HOST batches
   // poll buffers (host)
-  std::vector<int64_t> h_chunk, h_ts;
+  std::vector<int64_t> h_chunk, h_ts, h_seq;
   std::vector<int32_t> h_type;
   std::vector<uint64_t> h_vals;
   std::vector<uint8_t> h_nulls;
@@ -567,6 +570,7 @@ void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, c
     SHD_HIP(hipMemcpyAsync(ne->out.ts.p, old.out.ts.p, m * 8, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipMemcpyAsync(ne->out.vals.p, old.out.vals.p, m * w * 8, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipMemcpyAsync(ne->out.nulls.p, old.out.nulls.p, m * w, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.seq.p, old.out.seq.p, m * 8, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipStreamSynchronize(ne->stream));
     ne->out.count = m;
   }
@@ -756,12 +760,14 @@ int shd_poll(shd_query* q, shd_out* out) {
     q->h_chunk.resize(std::max<int64_t>(n, 1));
     q->h_type.resize(std::max<int64_t>(n, 1));
     q->h_ts.resize(std::max<int64_t>(n, 1));
+    q->h_seq.resize(std::max<int64_t>(n, 1));
     q->h_vals.resize(std::max<int64_t>(n * nc, 1));
     q->h_nulls.resize(std::max<int64_t>(n * nc, 1));
     if (n > 0) {
       SHD_HIP(hipMemcpyAsync(q->h_chunk.data(), e.out.chunk.p, n * 8, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipMemcpyAsync(q->h_type.data(), e.out.type.p, n * 4, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipMemcpyAsync(q->h_ts.data(), e.out.ts.p, n * 8, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(q->h_seq.data(), e.out.seq.p, n * 8, hipMemcpyDeviceToHost, s));
       if (nc > 0) {
         SHD_HIP(hipMemcpyAsync(q->h_vals.data(), e.out.vals.p, n * nc * 8, hipMemcpyDeviceToHost, s));
         SHD_HIP(hipMemcpyAsync(q->h_nulls.data(), e.out.nulls.p, n * nc, hipMemcpyDeviceToHost, s));
@@ -776,6 +782,7 @@ int shd_poll(shd_query* q, shd_out* out) {
     out->ts = q->h_ts.data();
     out->values = q->h_vals.data();
     out->nulls = q->h_nulls.data();
+    out->in_seq = q->h_seq.data();
     return SHD_OK;
   });
 }

@@ -103,6 +103,36 @@ def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world:
     return out, recv[:, k - 1].contiguous(), stats
 
 
+def merge_outputs(parts):
+    """k-way merge of key-sharded query outputs into the single-engine order.
+
+    parts: per rank (rows, global_seq) where rows = (chunk, type, ts, values,
+    nulls) as polled from the rank's query (DeviceQuery.poll) and global_seq[i]
+    is the global arrival sequence of the input event that emitted row i (the
+    rank's routed `seq` indexed by shd_out.in_seq).  A partitioned query's
+    output for one input event comes from the rank owning its key, and each
+    rank's rows are in (event, processor, pending-list) order, so a stable
+    merge on the global sequence reproduces the order one engine over the
+    whole stream emits (MultiProcessStreamReceiver: one callback chunk per
+    (event, processor), C/query/input/MultiProcessStreamReceiver.java:94-124).
+    Chunk ids are renumbered: a new chunk starts where the rank or the rank's
+    chunk id changes.  Returns the merged (chunk, type, ts, values, nulls, seq).
+    """
+    import numpy as np
+    live = [(r, rows, np.asarray(g, np.int64)) for r, (rows, g) in enumerate(parts) if rows is not None and len(g)]
+    if not live:
+        return None
+    seq = np.concatenate([g for _, _, g in live])
+    rank = np.concatenate([np.full(len(g), r, np.int64) for r, _, g in live])
+    local = np.concatenate([np.arange(len(g), dtype=np.int64) for _, _, g in live])
+    order = np.lexsort((local, rank, seq))   # seq, then rank, then the rank's own order
+    cols = [np.concatenate([rows[k] for _, rows, _ in live])[order] for k in range(5)]
+    ch, rk = cols[0], rank[order]
+    new = np.r_[True, (ch[1:] != ch[:-1]) | (rk[1:] != rk[:-1])] if len(ch) else np.zeros(0, bool)
+    cols[0] = np.cumsum(new) - 1
+    return tuple(cols) + (seq[order],)
+
+
 def call_offsets_from_seq(seq: torch.Tensor, call_size: int) -> torch.Tensor:
     """InputHandler-call boundaries of a seq-sorted event slice: calls of the
     global stream are consecutive runs of `call_size` sequence numbers."""

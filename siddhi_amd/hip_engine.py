@@ -46,7 +46,7 @@ class ShdBatch(ctypes.Structure):
 class ShdOut(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int64), ("n_cols", ctypes.c_int32), ("chunk", ctypes.c_void_p),
                 ("type", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("values", ctypes.c_void_p),
-                ("nulls", ctypes.c_void_p)]
+                ("nulls", ctypes.c_void_p), ("in_seq", ctypes.c_void_p)]
 
 
 class ShdCounters(ctypes.Structure):
@@ -183,13 +183,16 @@ class DeviceQuery:
     def reset(self):
         _check(self.lib.shd_reset(self.q))
 
-    def poll(self):
+    def poll(self, with_seq=False):
+        """Rows since the last poll: (chunk, type, ts, values, nulls), plus in_seq
+        (arrival index of the emitting input event, shd_out.in_seq) when with_seq."""
         o = ShdOut()
         _check(self.lib.shd_poll(self.q, ctypes.byref(o)))
         n, nc = o.n_rows, o.n_cols
         if n == 0:
             return None
         chunk = np.ctypeslib.as_array(ctypes.cast(o.chunk, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
+        seq = np.ctypeslib.as_array(ctypes.cast(o.in_seq, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
         typ = np.ctypeslib.as_array(ctypes.cast(o.type, ctypes.POINTER(ctypes.c_int32)), (n,)).copy()
         ts = np.ctypeslib.as_array(ctypes.cast(o.ts, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
         if nc > 0:
@@ -200,6 +203,8 @@ class DeviceQuery:
         else:
             vals = np.zeros((n, 0), np.uint64)
             nul = np.zeros((n, 0), np.uint8)
+        if with_seq:
+            return chunk, typ, ts, vals, nul, seq
         return chunk, typ, ts, vals, nul
 
     def counters(self) -> dict:

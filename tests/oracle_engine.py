@@ -42,6 +42,7 @@ def load_oracle():
     lib.orc_num_outputs.argtypes = [P]
     lib.orc_get_rows.argtypes = [P, P, P, P, P, P]
     lib.orc_clear_rows.argtypes = [P]
+    lib.orc_get_rows_seq.argtypes = [P, P]
     lib.orc_counters.argtypes = [P, P]
     lib.orc_last_error.restype = ctypes.c_char_p
     _lib = lib
@@ -72,6 +73,7 @@ class OracleQueryEngine:
         self.n_out = self.lib.orc_num_outputs(self.h)
         self.types = qp.plan.stream_types
         self._log = []
+        self.drained_seq = []
 
     def close(self):
         if self.h:
@@ -95,6 +97,9 @@ class OracleQueryEngine:
         nul = np.empty((n, max(self.n_out, 1)), np.uint8)
         self.lib.orc_get_rows(self.h, chunk.ctypes.data, typ.ctypes.data, ts.ctypes.data,
                               vals.ctypes.data, nul.ctypes.data)
+        sq = np.empty(n, np.int64)
+        self.lib.orc_get_rows_seq(self.h, sq.ctypes.data)
+        self.drained_seq.append(sq)   # shd_out.in_seq of the drained rows
         self.lib.orc_clear_rows(self.h)
         return split_chunks(chunk, typ, ts, vals[:, :self.n_out], nul[:, :self.n_out])
 

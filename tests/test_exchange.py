@@ -91,3 +91,51 @@ def test_partitioned_pattern_over_routed_ranks_matches_single_engine(routed):
         return sorted(zip(r[2].tolist(), r[3][:, 0].tolist(), r[3][:, 1].tolist(), r[3][:, 2].tolist()))
     merged = sorted(canon(rows[0]) + canon(rows[1]))
     assert merged == canon(whole)
+
+
+def _oracle_rows_with_seq(qp, batches):
+    """Oracle per InputHandler call (as run_oracle) plus each row's in_seq."""
+    from oracle_engine import OracleQueryEngine
+    from parity import concat_rows
+    from siddhi_amd.runtime import ColumnBatch
+    eng = OracleQueryEngine(qp, None)
+    parts, cid = [], 0
+    for si, b in batches:
+        offs = b.call_offsets
+        for c in range(len(offs) - 1):
+            s, e = int(offs[c]), int(offs[c + 1])
+            sub = ColumnBatch(b.ts[s:e], [x[s:e] for x in b.cols], [None] * len(b.cols))
+            for ch in eng.set_time(int(b.ts[e - 1])) + eng.push(si, sub):
+                n = len(ch.ts)
+                parts.append((np.full(n, cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+                cid += 1
+    seq = np.concatenate(eng.drained_seq) if eng.drained_seq else np.zeros(0, np.int64)
+    eng.close()
+    return concat_rows(parts), seq
+
+
+def test_merged_rank_outputs_equal_single_engine_in_order(routed):
+    """shd_out.in_seq-style merge (exchange.merge_outputs): the ranks' rows,
+    each tagged with the global sequence of its emitting event, merge into
+    exactly the rows, order and callback chunks of one engine over the whole
+    stream."""
+    from parity import assert_same_rows, compile_single_query, stock_batch
+    from siddhi_amd.runtime import ColumnBatch
+    qp, _ = compile_single_query(wl.P3_APP)
+    s, p, v, t = wl.stock_stream(N, KEYS, DELTA, seed_offset=3)
+    whole, wseq = _oracle_rows_with_seq(qp, [(0, stock_batch(s, p, v, t, CALL))])
+    parts = []
+    for z in routed:
+        batches, gseq = [], []
+        for i in range(2):
+            seq = torch.from_numpy(z["seq%d" % i])
+            offs = ex.call_offsets_from_seq(seq, CALL).numpy()
+            cols = [z["c%d_0" % i].astype(np.uint32), z["c%d_1" % i], z["c%d_2" % i]]
+            batches.append((0, ColumnBatch(z["c%d_3" % i], cols, [None] * 3, offs)))
+            gseq.append(z["seq%d" % i])
+        rows, lseq = _oracle_rows_with_seq(qp, batches)
+        parts.append((rows, np.concatenate(gseq)[lseq]))   # rank-local arrival index -> global sequence
+    merged = ex.merge_outputs(parts)
+    assert len(whole[2]) > 0
+    assert_same_rows(merged[:5], whole)
+    assert np.array_equal(merged[5], wseq)

@@ -1,0 +1,81 @@
+"""Key-sharded P3 on the device: the stream's events split by
+key owner (exchange.owner_of) over two device queries standing in for two
+ranks; each rank's rows carry shd_out.in_seq, mapped to the global sequence
+and k-way merged (exchange.merge_outputs).  The merged rows -- order, values,
+timestamps and callback chunks -- must equal one device query over the whole
+stream and the CPU oracle.  Also: in_seq of every engine equals the oracle's."""
+import numpy as np
+import pytest
+import torch
+
+from parity import assert_same_rows, compile_single_query, concat_rows, run_oracle, stock_batch
+from siddhi_amd import exchange as ex
+from siddhi_amd import workloads as wl
+from siddhi_amd.runtime import ColumnBatch
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_rows_with_seq(qp, batches):
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
+    dq = DeviceQuery(qp.ir)
+    parts, seqs = [], []
+    for si, b in batches:
+        cols = [np.ascontiguousarray(c) for c in b.cols]
+        ts = np.ascontiguousarray(b.ts, np.int64)
+        dq.push_raw(si, b.n, ts.ctypes.data, [c.ctypes.data for c in cols], [0] * len(cols), SHD_MEM_HOST,
+                    b.call_offsets if len(b.call_offsets) > 2 else None, True)
+        r = dq.poll(with_seq=True)
+        if r is not None:
+            parts.append(r[:5])
+            seqs.append(r[5])
+    dq.close()
+    return concat_rows(parts), (np.concatenate(seqs) if seqs else np.zeros(0, np.int64))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_p3_merges_to_single_engine_order(hip_available, world):
+    qp, _ = compile_single_query(wl.P3_APP)
+    n, keys, call = 120_000, 3000, 1024
+    s, p, v, t = wl.stock_stream(n, keys, 0.02, seed_offset=19)
+    whole = run_oracle(qp, [(0, stock_batch(s, p, v, t, call))])
+    one, _ = _device_rows_with_seq(qp, [(0, stock_batch(s, p, v, t, call))])
+    assert len(whole[2]) > 0
+    assert_same_rows(one, whole)
+    owner = ex.owner_of(torch.from_numpy(s.astype(np.int64)), world).numpy()
+    parts = []
+    for r in range(world):
+        gseq = np.nonzero(owner == r)[0]          # this rank's events in global arrival order
+        offs = ex.call_offsets_from_seq(torch.from_numpy(gseq), call).numpy()
+        cut = int(offs[len(offs) // 2])            # two micro-batches per rank, cut at a call boundary
+        batches = []
+        for a, b in ((0, cut), (cut, len(gseq))):
+            if b <= a:
+                continue
+            idx = gseq[a:b]
+            o = ex.call_offsets_from_seq(torch.from_numpy(idx), call).numpy()
+            batches.append((0, ColumnBatch(t[idx], [s[idx], p[idx], v[idx]], [None] * 3, o)))
+        rows, lseq = _device_rows_with_seq(qp, batches)
+        parts.append((rows, gseq[lseq]))
+    merged = ex.merge_outputs(parts)
+    assert_same_rows(merged[:5], whole)
+
+
+CASES = [("P3", wl.P3_APP, 60_000, 2000, 0.02), ("W2-length", wl.W2_LENGTH_APP, 40_000, 300, 0.1),
+         ("S4-seqplus", wl.S4_APPS["seqplus"], 8_000, 100, 1.0), ("S4-not", wl.S4_APPS["not"], 8_000, 100, 1.0)]
+
+
+@pytest.mark.parametrize("name,app,n,keys,delta", CASES, ids=[c[0] for c in CASES])
+def test_in_seq_equals_oracle(hip_available, name, app, n, keys, delta):
+    """shd_out.in_seq (the emitting event's arrival index) on every engine."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_exchange import _oracle_rows_with_seq
+    qp, _ = compile_single_query(app)
+    s, p, v, t = wl.stock_stream(n, keys, delta, seed_offset=23)
+    batches = [(0, stock_batch(s[a:b], p[a:b], v[a:b], t[a:b], 512)) for a, b in ((0, n // 2), (n // 2, n))]
+    ora, oseq = _oracle_rows_with_seq(qp, batches)
+    dev, dseq = _device_rows_with_seq(qp, batches)
+    assert len(ora[2]) > 0
+    assert len(dseq) == len(oseq)
+    assert np.array_equal(dseq, oseq)

@@ -133,3 +133,38 @@ def test_capacity_overflow_is_reported(hip_available, monkeypatch):
         assert ei.value.code == SHD_E_CAPACITY
     finally:
         dq.close()
+
+
+WINDOW_SEQS = {
+    # config S4's sequence (no match on random prices: a count below its minimum
+    # does not survive resetAndUpdate) and bounded shapes that do match
+    "seq": wl.S4_APPS["seq"],
+    "seq13": wl.S4_APPS["seq"].replace("<2:5>", "<1:3>"),
+    "seq14": wl.S4_APPS["seq"].replace("<2:5>", "<1:4>").replace("price<e2[last].price", "price<e1.price"),
+    "bare": wl.S4_APPS["bare"],
+}
+
+
+@pytest.mark.parametrize("name", list(WINDOW_SEQS))
+@pytest.mark.parametrize("chunk", ["auto", "1", "5", "64"])
+@pytest.mark.parametrize("parts", [1, 4])
+def test_sequence_window_lanes(hip_available, monkeypatch, name, chunk, parts):
+    """Unpartitioned bounded-span every-sequences run as window lanes (one
+    lane per chunk of events, each replaying the events before its chunk from a
+    fresh state; the push's tail carries to the next push): rows identical to
+    the oracle and to the one-lane NFA, for lanes of one event and micro-batch
+    cuts inside partials.  `bare` (no every) stays on one lane."""
+    if chunk != "auto":
+        monkeypatch.setenv("SHD_NFA_CHUNK", chunk)
+    qp, _ = compile_single_query(WINDOW_SEQS[name])
+    sym, price, vol, ts = wl.stock_stream(20000, 50, 1.0, seed_offset=77)
+    batches = split(sym, price, vol, ts, parts, call=700)
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert kind == ENGINE_NFA
+    assert_same_rows(dev, ora)
+    monkeypatch.setenv("SHD_NFA_WINDOW", "0")
+    one, _, _ = run_device(qp, batches)
+    assert_same_rows(dev, one)
+    if name in ("seq13", "seq14"):
+        assert len(ora[2]) > 1000

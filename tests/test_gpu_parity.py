@@ -147,6 +147,8 @@ def test_hashed_bucket_grouping(hip_available, monkeypatch, bits, parts):
     per `within` span takes the one-pass bucketed walk (8-bit buckets)."""
     if bits != "auto":
         monkeypatch.setenv("SHD_HASH_BITS", bits)
+    else:
+        monkeypatch.setenv("SHD_BUCKET", "1")   # the bucketed walk is opt-in (slower on P3)
     qp, _ = compile_single_query(wl.P3_APP)
     n, keys = 300_000, (1 << 20) if bits == "auto" else 20_000
     # auto: 2^20 keys (3 exact passes), ~10k events per `within` span -> 16-bit buckets

@@ -220,6 +220,8 @@ RESTORE_CASES = [
     ("W2-length", wl.W2_LENGTH_APP, 100_000, 1000, 0.1, 4),
     ("W2-time", wl.W2_TIME_APP, 100_000, 1000, 0.5, 4),
     ("S4-or", wl.S4_APPS["or"], 30_000, 100, 1.0, 3),
+    # window lanes: the carried tail events
+    ("S4-seq-window", wl.S4_APPS["seq"].replace("<2:5>", "<1:3>"), 30_000, 100, 1.0, 4),
     ("S4-seqplus-part", wl.S4_PART_APPS["seqplus"], 30_000, 50, 1.0, 3),
     ("S4-and-part", wl.S4_PART_APPS["and"], 30_000, 100, 1.0, 3),
     # half-filled AND partials carry their operand event through the snapshot
