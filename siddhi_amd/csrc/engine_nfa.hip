@@ -58,7 +58,7 @@ enum : uint32_t {
 enum : int {
   MISC_SEEDED = 0, MISC_EVRET = 1, MISC_WKN = 2, MISC_RETN = 3, MISC_TMPN = 4,
   MISC_FREE_SE = 5, MISC_FREE_EV = 6, MISC_FREE_REC = 7, MISC_HINT_SE = 8, MISC_HINT_EV = 9, MISC_HINT_REC = 10,
-  MISC_N = 12
+  MISC_HSTAMP = 11, MISC_N = 12
 };
 
 struct DPre {
@@ -126,14 +126,13 @@ struct NfaRunArgs {
   int64_t nlanes;
   int64_t seq0;
   int64_t start_time;   // app start (seed of unpartitioned plans)
-  // window-lane mode (unpartitioned bounded-span sequences): lane c owns the
-  // events [c*chunk_len, (c+1)*chunk_len) and first replays the `warm` events
-  // before them from a fresh state, output suppressed; rows < 0 are the last
-  // n_pre events of the previous push (prefix)
+  // window-lane mode (unpartitioned every-started plans): lane c owns the
+  // events [c*chunk_len, (c+1)*chunk_len); lanes c < c_exact start at row 0
+  // from a copy of the carried state (exact), the others replay the `warm`
+  // events before their chunk from a fresh state, output suppressed
   int64_t chunk_len;
   int64_t warm;
-  int64_t n_pre;
-  ColSet prefix;
+  int64_t c_exact;
   uint64_t* hash_w;   // per lane: state hash after the warm-up (= before the first owned event)
   uint64_t* hash_e;   // per lane: state hash after the last owned event
   const int32_t* call_of;
@@ -199,7 +198,7 @@ struct Lane {
   uint32_t tagc;
   uint64_t t_prim, t_sec, t_ter;
   int64_t last_seq;
-  int64_t own_from;   // window lanes: rows of events before this seq are warm-up (no output)
+  bool quiet;   // window lanes: warm-up events (no output)
   int cdone;
 
   __device__ Lane(const NfaProg& p, const NfaLayout& y, const NfaRunArgs& a, DExprSet e)
@@ -229,24 +228,14 @@ struct Lane {
   __device__ __forceinline__ uint64_t& bits(int64_t off, int w) { return ks.at<uint64_t>(off, w); }
 
   // ---------------------------------------------------------------- window lanes
-  // copy every field of another key's state into this one (lane copy)
-  __device__ void copy_lane_from(const KS& src) {
-    for (int f = 0; f < Y.nf; f++) {
-      const int sz = Y.f_sz[f];
-      for (int64_t e = 0; e < Y.f_cnt[f]; e++) {
-        const char* sp = src.b + Y.f_off[f] + (e * kLaneBlock + src.l) * sz;
-        char* dp = ks.b + Y.f_off[f] + (e * kLaneBlock + ks.l) * sz;
-        for (int k = 0; k < sz; k++) dp[k] = sp[k];
-      }
-    }
-  }
   // Canonical hash of the key's NFA state (pending / new lists in order, each
   // StateEvent by content -- timestamp, type, event chains by event record --
   // with object identity kept: a StateEvent or StreamEvent seen before hashes
   // as its first-visit index, so shared objects (count-state aliasing) and
   // equal copies differ).  Two lanes whose states hash equal continue equally.
-  __device__ uint16_t& cse(int i) { return ks.at<uint16_t>(Y.o_cse, i); }
-  __device__ uint16_t& cev(int i) { return ks.at<uint16_t>(Y.o_cev, i); }
+  // canonical ids carry the hash call's stamp in the high half (no clearing)
+  __device__ uint32_t& cse(int i) { return ks.at<uint32_t>(Y.o_cse, i); }
+  __device__ uint32_t& cev(int i) { return ks.at<uint32_t>(Y.o_cev, i); }
   __device__ uint64_t state_hash() {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t x) {
@@ -254,27 +243,33 @@ struct Lane {
       h *= 1099511628211ull;
       h ^= h >> 29;
     };
-    for (int i = 0; i <= Y.SC; i++) cse(i) = NIL;
-    for (int i = 0; i <= Y.EC; i++) cev(i) = NIL;
-    uint16_t nse = 0, nev = 0;
+    uint32_t stamp = (misc(MISC_HSTAMP) + 1) & 0xFFFFu;
+    if (stamp == 0) {   // wrapped: clear once
+      for (int i = 0; i <= Y.SC; i++) cse(i) = 0;
+      for (int i = 0; i <= Y.EC; i++) cev(i) = 0;
+      stamp = 1;
+    }
+    misc(MISC_HSTAMP) = stamp;
+    const uint32_t hi = stamp << 16;
+    uint32_t nse = 0, nev = 0;
     auto hse = [&](uint16_t s) {
       if (s > Y.SC) return;
-      if (cse(s) != NIL) {
-        mix(0xA0000ull + cse(s));
+      if ((cse(s) & 0xFFFF0000u) == hi) {
+        mix(0xA0000ull + (cse(s) & 0xFFFFu));
         return;
       }
-      cse(s) = nse++;
+      cse(s) = hi | nse++;
       mix(0xB0000ull);
       mix((uint64_t)sts(s));
       mix(stype(s));
       for (int st = 0; st < Y.nstates; st++) {
         mix(0xC0000ull + st);
         for (uint16_t e = sev(s, st); e != NIL && e < Y.EC; e = enext(e)) {
-          if (cev(e) != NIL) {
-            mix(0xD0000ull + cev(e));
+          if ((cev(e) & 0xFFFF0000u) == hi) {
+            mix(0xD0000ull + (cev(e) & 0xFFFFu));
             break;
           }
-          cev(e) = nev++;
+          cev(e) = hi | nev++;
           const uint16_t r = erec(e);
           if (r >= Y.RC) continue;
           mix((uint64_t)rts(r));
@@ -284,14 +279,24 @@ struct Lane {
       }
     };
     for (int p = 0; p < P.npre; p++) {
-      mix(fl(p) & (FL_INIT | FL_STARTED | FL_SSRESET | FL_INACTIVE));
+      mix(fl(p));
+      mix((uint64_t)lst(p));
       const int a = pn(p), b = nn(p);
       mix(0xE0000ull + a);
       for (int i = 0; i < a; i++) hse(pend(p, i));
       mix(0xF0000ull + b);
       for (int i = 0; i < b; i++) hse(nw(p, i));
     }
+    const int rn = misc(MISC_RETN);
+    mix(0x100000ull + rn);
+    for (int i = 0; i < rn; i++) hse(retl(i));
+    for (int sc = 0; sc < P.nsched; sc++) {
+      const int n = sqn(sc);
+      mix(0x110000ull + n);
+      for (int i = 0; i < n; i++) mix((uint64_t)sq(sc, i));
+    }
     mix(evret);
+    mix(misc(MISC_SEEDED) != 0);
     return h;
   }
 
@@ -1163,7 +1168,7 @@ struct Lane {
   }
   __device__ uint64_t new_tag() { return ((uint64_t)slot << 24) | (uint64_t)(tagc++ & 0xFFFFFF); }
   __device__ void emit(uint16_t s, uint64_t tag) {
-    if (last_seq < own_from) return;   // warm-up event of a window lane
+    if (quiet) return;   // warm-up event of a window lane
     unsigned long long idx = atomicAdd(&A.ctl->rows, 1ull);
     if ((int64_t)idx >= A.R) {
       ovf |= OV_ROWS;
@@ -1195,7 +1200,8 @@ struct Lane {
     fill_free(Y.o_se_free, Y.sew, Y.SC);
     fill_free(Y.o_ev_free, Y.evw, Y.EC);
     fill_free(Y.o_rec_free, Y.recw, Y.RC);
-    for (int i = 0; i < MISC_N; i++) misc(i) = 0;
+    for (int i = 0; i < MISC_N; i++)
+      if (i != MISC_HSTAMP) misc(i) = 0;   // the hash stamp outlives reseeding (stale canonical ids)
     misc(MISC_FREE_SE) = (uint32_t)Y.SC;
     misc(MISC_FREE_EV) = (uint32_t)Y.EC;
     misc(MISC_FREE_REC) = (uint32_t)Y.RC;
@@ -1236,10 +1242,9 @@ struct Lane {
     int r = alloc_bit(Y.o_rec_free, Y.recw, Y.RC, OV_REC, MISC_FREE_REC, MISC_HINT_REC);
     rts(r) = ts;
     uint32_t nm = 0;
-    const ColSet& cs = row < 0 ? A.prefix : A.batch;   // rows < 0: the previous push's tail
-    const int64_t cr = row < 0 ? row + A.n_pre : row;
+    const ColSet& cs = A.batch;
     for (int c = 0; c < cs.ncols; c++) {
-      Val v = col_load(cs, cr, c);
+      Val v = col_load(cs, row, c);
       rval(r, c) = v.b;
       if (v.null) nm |= 1u << c;
     }
@@ -1250,7 +1255,7 @@ struct Lane {
   __device__ void process_event(int64_t row) {
     maybe_gc();
     const int si = A.stream;
-    const int64_t ts = row < 0 ? A.prefix.ts[row + A.n_pre] : A.batch.ts[row];
+    const int64_t ts = A.batch.ts[row];
     const uint16_t rec = make_rec(row, ts);
     stabilize(si, ts);
     const int np = P.nsp[si];
@@ -1405,35 +1410,55 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   L.t_prim = L.t_sec = L.t_ter = 0;
   L.cdone = -1;
   L.last_seq = a.seq0;
-  L.own_from = INT64_MIN;
+  L.quiet = false;
   if (a.chunk_len > 0) {
-    // Window lane.  Lane 0 continues the exact carried state (slot 0, the
-    // previous push's end state); lane c > 0 starts fresh `warm` events before
-    // its chunk (output suppressed) and is valid when its state after the
-    // warm-up equals lane c-1's state at its end (hash_w[c] == hash_e[c-1],
-    // checked by k_win_check; on any mismatch the host reruns the push on one
-    // lane from slot 0).
+    // Window lane.  Lanes c < c_exact start at row 0 from a copy of the carried
+    // state (slot 0, copied by k_lane_copy) and replay the one-lane run
+    // exactly; lane c >= c_exact starts fresh `warm` events before its chunk
+    // (output suppressed) and is valid when its state before its first owned
+    // event equals lane c-1's state after its last (hash_w[c] == hash_e[c-1],
+    // k_win_check; on a mismatch the host reruns the push with longer warm-ups).
+    // Calls' timers fire and single-receiver runs flush before the row that
+    // follows them, so they belong to the lane that owns that row.
     const int64_t ob = lane_id * a.chunk_len;
     const int64_t oe = ob + a.chunk_len < a.n_keyed ? ob + a.chunk_len : a.n_keyed;
+    const bool exact = lane_id < a.c_exact;
     L.key = 0;
-    L.cdone = a.ncalls - 1;   // no timers in this mode
-    if (lane_id == 0) {
-      KS carry;
-      carry.b = a.state;
-      carry.l = 0;
-      L.copy_lane_from(carry);
+    int64_t wb;
+    uint32_t cur_run;
+    if (exact) {
       if (L.misc(MISC_SEEDED) == 0) L.seed(a.start_time);
       L.evret = L.misc(MISC_EVRET);
+      wb = 0;
+      cur_run = 0xFFFFFFFFu;
     } else {
       L.evret = 0;
       L.seed(a.start_time);
-      int64_t wb = ob - a.warm;
-      if (wb < -a.n_pre) wb = -a.n_pre;
-      L.own_from = a.seq0 + ob;
-      for (int64_t row = wb; row < ob && !L.ovf; row++) L.process_event(row);
-      a.hash_w[lane_id] = L.state_hash();
+      wb = ob - a.warm;
+      const int c0 = a.call_of[wb];
+      L.cdone = (wb > 0 && a.call_of[wb - 1] == c0) ? c0 : c0 - 1;
+      cur_run = a.run_id[wb];
     }
-    for (int64_t row = ob; row < oe && !L.ovf; row++) L.process_event(row);
+    for (int64_t row = wb; row < oe && !L.ovf; row++) {
+      if (row == ob) {
+        L.quiet = false;
+        if (!exact) a.hash_w[lane_id] = L.state_hash();
+      } else if (row == wb) {
+        L.quiet = true;
+      }
+      const uint32_t run = a.run_id[row];
+      if (run != cur_run) {
+        L.flush_run();
+        cur_run = run;
+      }
+      L.fire_upto(a.call_of[row]);
+      L.process_event(row);
+    }
+    L.quiet = false;
+    if (oe == a.n_keyed) {   // the push's last lane closes it like the one-lane run
+      if (!L.ovf) L.flush_run();
+      if (!L.ovf) L.fire_upto(a.ncalls - 1);
+    }
     L.misc(MISC_EVRET) = L.evret;
     a.hash_e[lane_id] = L.state_hash();
     if (L.ovf) atomicOr(&a.ctl->overflow, L.ovf);
@@ -1484,23 +1509,35 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   if (live) atomicAdd(&a.ctl->live, live);
 }
 
-// window lanes: lane c > 0 is valid iff its warm-up state equals lane c-1's end state
-__global__ void k_win_check(const uint64_t* hw, const uint64_t* he, int64_t nl, unsigned int* bad) {
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; c < nl; c += (int64_t)gridDim.x * blockDim.x)
+// window lanes: lane c >= c_exact is valid iff its warm-up state equals lane c-1's end state
+__global__ void k_win_check(const uint64_t* hw, const uint64_t* he, int64_t c0, int64_t nl, unsigned int* bad) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + (c0 > 1 ? c0 : 1); c < nl;
+       c += (int64_t)gridDim.x * blockDim.x)
     if (hw[c] != he[c - 1]) atomicAdd(bad, 1u);
 }
 
-// the last lane's end state becomes the carried state (slot 0)
-__global__ void k_win_carry(const NfaProg* __restrict__ gprog, const NfaLayout* __restrict__ glay,
-                            const NfaRunArgs* __restrict__ ap, int64_t src_slot) {
-  const NfaRunArgs& a = *ap;
-  Lane L(*gprog, *glay, a, a.es);
-  L.ks.b = a.state;
-  L.ks.l = 0;
-  KS src;
-  src.b = a.state + (src_slot / kLaneBlock) * glay->blk;
-  src.l = (int)(src_slot % kLaneBlock);
-  L.copy_lane_from(src);
+// one key's state (every field of slot src) into slots [dst0, dst0 + ndst):
+// blockIdx.y = field, x over (element, destination); consecutive threads write
+// consecutive lanes of one element
+__global__ void k_lane_copy(const NfaLayout* __restrict__ glay, char* __restrict__ state, int64_t src,
+                            int64_t dst0, int64_t ndst) {
+  const NfaLayout& Y = *glay;
+  const int f = blockIdx.y;
+  const int sz = Y.f_sz[f];
+  const int64_t total = Y.f_cnt[f] * ndst;
+  const char* sb = state + (src / kLaneBlock) * Y.blk + Y.f_off[f];
+  const int sl = (int)(src % kLaneBlock);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i / ndst, d = dst0 + i % ndst;
+    const char* sp = sb + (e * kLaneBlock + sl) * sz;
+    char* dp = state + (d / kLaneBlock) * Y.blk + Y.f_off[f] + (e * kLaneBlock + d % kLaneBlock) * sz;
+    switch (sz) {
+      case 8: *reinterpret_cast<uint64_t*>(dp) = *reinterpret_cast<const uint64_t*>(sp); break;
+      case 4: *reinterpret_cast<uint32_t*>(dp) = *reinterpret_cast<const uint32_t*>(sp); break;
+      case 2: *reinterpret_cast<uint16_t*>(dp) = *reinterpret_cast<const uint16_t*>(sp); break;
+      default: *dp = *sp;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- batch preparation
@@ -1987,11 +2024,11 @@ struct NfaEngine : Engine {
   // carry to the next push (prefix) instead of key blocks.
   bool windowed = false;
   int64_t win_warm = 0;
-  int win_stream = 0;
-  DevBuf pre_ts[2], pre_col[2][kMaxCols], pre_nul[2][kMaxCols], d_hash;
-  int64_t win_fallbacks = 0;   // pushes rerun on one lane (a lane's warm-up state disagreed)
-  int pre_cur = 0;
-  int64_t n_pre = 0;
+  int64_t win_span = 0;      // sequences: events a partial can span (0: unbounded)
+  int64_t win_horizon = 0;   // patterns: longest within / for time (0: none)
+  DevBuf d_hash;
+  int64_t win_fallbacks = 0;   // window passes rerun with longer warm-ups
+  const bool win_debug = getenv("SHD_NFA_DEBUG") != nullptr;
   bool partitioned = false;
   int key_expr[kNStream], key_col[kNStream], key_type[kNStream];
   // key blocks
@@ -2029,7 +2066,6 @@ struct NfaEngine : Engine {
     counters = shd_counters{};
     nslots = 0;
     epoch = 0;
-    n_pre = 0;
     if (state.p && slot_cap > 0) SHD_HIP(hipMemset(state.p, 0, (size_t)(slot_cap / kLaneBlock) * lay.blk));
     if (ht_state.p && ht_cap > 0) SHD_HIP(hipMemset(ht_state.p, 0, (size_t)ht_cap * 4));
     SHD_HIP(hipDeviceSynchronize());
@@ -2037,17 +2073,10 @@ struct NfaEngine : Engine {
 
   // key blocks (all per-key NFA state) + key directory, byte for byte
   void save_state(SnapW& w) override {
-    if (windowed) {   // carried state (slot 0's block) + the carried tail events
-      const auto& types = plan.stream_types[win_stream];
+    if (windowed) {   // the carried state: slot 0's block (+ the learned warm-up)
       w.put<int64_t>(win_warm);
       w.put<int64_t>(slot_cap > 0 ? 1 : 0);
       if (slot_cap > 0) w.dev(state.p, (size_t)lay.blk);
-      w.put<int64_t>(n_pre);
-      w.dev(pre_ts[pre_cur].p, (size_t)n_pre * 8);
-      for (size_t c = 0; c < types.size(); c++) {
-        w.dev(pre_col[pre_cur][c].p, (size_t)n_pre * type_size(types[c]));
-        w.dev(pre_nul[pre_cur][c].p, (size_t)n_pre);
-      }
       return;
     }
     w.put<int64_t>(slot_cap);
@@ -2062,24 +2091,14 @@ struct NfaEngine : Engine {
   }
   void load_state(SnapR& r) override {
     if (windowed) {
-      const auto& types = plan.stream_types[win_stream];
       const int64_t ww = r.get<int64_t>();
-      if (ww < 1 || ww > (1 << 16)) throw Error(SHD_E_ARG, "snapshot of a different plan");
+      if (ww < 0 || ww > ((int64_t)1 << 40)) throw Error(SHD_E_ARG, "snapshot of a different plan");
       if (r.get<int64_t>() != 0) {
         ensure_slots(kLaneBlock);
         r.dev_into(state.p, (size_t)lay.blk);
+        nslots = 1;
       }
       win_warm = ww;
-      const int64_t np = r.get<int64_t>();
-      if (np < 0 || np > win_warm) throw Error(SHD_E_ARG, "snapshot of a different plan");
-      reserve_prefix(0, std::max<int64_t>(np, 1));
-      r.dev_into(pre_ts[0].p, (size_t)np * 8);
-      for (size_t c = 0; c < types.size(); c++) {
-        r.dev_into(pre_col[0][c].p, (size_t)np * type_size(types[c]));
-        r.dev_into(pre_nul[0][c].p, (size_t)np);
-      }
-      pre_cur = 0;
-      n_pre = np;
       return;
     }
     const int64_t sc = r.get<int64_t>(), ns = r.get<int64_t>(), hc = r.get<int64_t>();
@@ -2294,52 +2313,35 @@ struct NfaEngine : Engine {
     return nseg;
   }
 
-  void reserve_prefix(int k, int64_t n) {
-    const auto& types = plan.stream_types[win_stream];
-    pre_ts[k].reserve(n * 8);
-    for (size_t c = 0; c < types.size(); c++) {
-      pre_col[k][c].reserve(n * type_size(types[c]));
-      pre_nul[k][c].reserve(n);
-    }
+  // copy slot src's state into slots [dst0, dst0 + ndst)
+  void lane_copy(int64_t src, int64_t dst0, int64_t ndst) {
+    if (ndst <= 0) return;
+    int64_t mx = 1;
+    for (int f = 0; f < lay.nf; f++) mx = std::max<int64_t>(mx, lay.f_cnt[f]);
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, ceil_div(mx * ndst, kBlock));
+    hipLaunchKernelGGL(k_lane_copy, dim3(gx, (unsigned)lay.nf), dim3(kBlock), 0, stream, dev_args(lay), state.as<char>(),
+                       src, dst0, ndst);
+    SHD_CHECK_LAUNCH();
   }
 
-  ColSet prefix_cs() {
-    const auto& types = plan.stream_types[win_stream];
-    ColSet cs{};
-    cs.ncols = (int)types.size();
-    cs.ts = pre_ts[pre_cur].as<int64_t>();
-    cs.n = n_pre;
-    for (size_t c = 0; c < types.size(); c++) {
-      cs.col[c] = pre_col[pre_cur][c].p;
-      cs.nul[c] = pre_nul[pre_cur][c].as<uint8_t>();
-      cs.type[c] = types[c];
-    }
-    return cs;
-  }
-
-  // the last `warm` events of (prefix ++ batch) become the next prefix
-  void roll_prefix(const Staged& b) {
-    const auto& types = plan.stream_types[win_stream];
-    const int64_t keep = std::min<int64_t>(win_warm, n_pre + b.n);
-    const int64_t from_b = std::min<int64_t>(keep, b.n), from_p = keep - from_b;
-    const int nx = pre_cur ^ 1;
-    reserve_prefix(nx, std::max<int64_t>(win_warm, 1));
-    hipStream_t s = stream;
-    auto cp = [&](void* dst, const void* src, size_t bytes) {
-      if (bytes) SHD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
-    };
-    cp(pre_ts[nx].p, pre_ts[pre_cur].as<int64_t>() + (n_pre - from_p), from_p * 8);
-    cp(pre_ts[nx].as<int64_t>() + from_p, b.cs.ts + (b.n - from_b), from_b * 8);
-    for (size_t c = 0; c < types.size(); c++) {
-      const int64_t sz = type_size(types[c]);
-      cp(pre_col[nx][c].p, pre_col[pre_cur][c].as<char>() + (n_pre - from_p) * sz, from_p * sz);
-      cp(pre_col[nx][c].as<char>() + from_p * sz, (const char*)b.cs.col[c] + (b.n - from_b) * sz, from_b * sz);
-      cp(pre_nul[nx][c].p, pre_nul[pre_cur][c].as<uint8_t>() + (n_pre - from_p), from_p);
-      if (b.cs.nul[c]) cp(pre_nul[nx][c].as<uint8_t>() + from_p, b.cs.nul[c] + (b.n - from_b), from_b);
-      else if (from_b) SHD_HIP(hipMemsetAsync(pre_nul[nx][c].as<uint8_t>() + from_p, 0, from_b, s));
-    }
-    pre_cur = nx;
-    n_pre = keep;
+  // Warm-up length for window lanes: a sequence partial lives at most `span`
+  // events; a pattern partial bounded by `within` / `for` time H lives about
+  // H / (mean event spacing) events of this push (verification catches the rest)
+  int64_t win_warm_hint(const Staged& b) {
+    if (win_span > 0) return 2 * win_span + 2;
+    if (win_horizon <= 0 || b.n < 2) return 64;
+    int64_t t2[2];
+    SHD_HIP(hipMemcpyAsync(&t2[0], b.cs.ts, 8, hipMemcpyDeviceToHost, stream));
+    SHD_HIP(hipMemcpyAsync(&t2[1], b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, stream));
+    SHD_HIP(hipStreamSynchronize(stream));
+    const double dt = (double)(t2[1] - t2[0]) / (double)(b.n - 1);
+    if (!(dt > 0)) return 64;
+    // timers fire at call boundaries: a partial outlives its time by up to a call
+    int64_t call_max = 0;
+    for (size_t c = 0; c + 1 < b.call_offsets.size(); c++)
+      call_max = std::max<int64_t>(call_max, b.call_offsets[c + 1] - b.call_offsets[c]);
+    if (prog.nsched == 0) call_max = 0;
+    return (int64_t)std::min<double>(1e9, 1.25 * ((double)win_horizon / dt + (double)call_max) + 64);
   }
 
   // One push (b != nullptr) or one time change (b == nullptr, time t).
@@ -2395,21 +2397,9 @@ struct NfaEngine : Engine {
     bool win_one = false;   // window push rerun on one lane
 
     if (win) {
-      // lanes of ~64 events, enough lanes to fill the chip
-      int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(1024, n / 16384));
-      if (const char* e = getenv("SHD_NFA_CHUNK")) chunk = std::max(1, atoi(e));
-      const int64_t nl = ceil_div(n, chunk);
-      ensure_slots(nl + 1);
-      d_hash.reserve(2 * nl * 8);
-      ra.hash_w = d_hash.as<uint64_t>();
-      ra.hash_e = d_hash.as<uint64_t>() + nl;
-      ra.chunk_len = chunk;
-      ra.warm = win_warm;
-      ra.n_pre = n_pre;
-      if (n_pre > 0) ra.prefix = prefix_cs();
+      ensure_slots(1);
+      nslots = 1;
       ra.lanes_over_slots = 0;
-      ra.nlanes = nl;
-      ra.nseg = nl;
       if (n > 0) {
         hipLaunchKernelGGL(k_call_run, dim3(grid_for(n)), dim3(kBlock), 0, s, (const int32_t*)d_call_of.as<int32_t>(),
                            n, d_run.as<uint32_t>());
@@ -2459,39 +2449,66 @@ struct NfaEngine : Engine {
     ra.st_nul = st_nul.as<uint8_t>();
     ra.ctl = d_ctl.as<NfaCtl>();
     NfaCtl hc{};
-    if (ra.nlanes > 0) {
-      SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
-      const NfaProg* dp = dev_args(prog);
-      const NfaLayout* dl = dev_args(lay);
-      const NfaRunArgs* dra = dev_args(ra);
-      hipLaunchKernelGGL(k_nfa_run, dim3((unsigned)ceil_div(ra.nlanes, kLaneBlock)), dim3(kLaneBlock), 0, s, dp, dl,
-                         dra);
-      SHD_CHECK_LAUNCH();
-      if (win && ra.nlanes > 1)
-        hipLaunchKernelGGL(k_win_check, dim3(grid_for(ra.nlanes)), dim3(kBlock), 0, s,
-                           (const uint64_t*)ra.hash_w, (const uint64_t*)ra.hash_e, ra.nlanes, &d_ctl.as<NfaCtl>()->count);
-      hc = read_ctl();
-      if (win && !hc.overflow) {
-        if (hc.count == 0) {
-          // every lane verified: the last lane's end state is the carried state
-          hipLaunchKernelGGL(k_win_carry, dim3(1), dim3(1), 0, s, dp, dl, dra, ra.nlanes);
-          SHD_CHECK_LAUNCH();
-        } else {
-          // a lane's warm-up did not reach its predecessor's state: rerun the
-          // push on one lane from the carried state (exact), longer warm-ups next
-          win_fallbacks++;
-          win_warm = std::min<int64_t>(win_warm * 2, 1 << 16);
-          SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
-          ra.chunk_len = 0;
-          ra.lanes_over_slots = 0;
-          ra.nlanes = 1;
-          ra.nseg = 1;
+    const NfaProg* dp = dev_args(prog);
+    const NfaLayout* dl = dev_args(lay);
+    if (win) {
+      // window lanes; a failed verification reruns the push with doubled
+      // warm-ups, down to the one-lane run once a warm-up spans most of it
+      int64_t warm = std::max<int64_t>(win_warm, win_warm_hint(*b));
+      for (;;) {
+        if (4 * warm >= n) {
           win_one = true;
-          hipLaunchKernelGGL(k_nfa_run, dim3(1), dim3(kLaneBlock), 0, s, dp, dl, dev_args(ra));
-          SHD_CHECK_LAUNCH();
-          hc = read_ctl();
+          break;
         }
+        // lanes of >= 32 events, enough of them to fill the chip, and a
+        // warm-up of at most 4 chunks
+        int64_t chunk = std::max<int64_t>({32, std::min<int64_t>(1024, n / 16384), ceil_div(warm, 4)});
+        if (const char* e = getenv("SHD_NFA_CHUNK")) chunk = std::max(1, atoi(e));
+        const int64_t nl = ceil_div(n, chunk);
+        const int64_t c0 = std::min<int64_t>(nl, warm / chunk + 1);   // lanes with ob <= warm
+        ensure_slots(nl + 1);   // may move the key blocks
+        ra.state = state.as<char>();
+        d_hash.reserve(2 * nl * 8);
+        ra.hash_w = d_hash.as<uint64_t>();
+        ra.hash_e = d_hash.as<uint64_t>() + nl;
+        ra.chunk_len = chunk;
+        ra.warm = warm;
+        ra.c_exact = c0;
+        ra.nlanes = nl;
+        ra.nseg = nl;
+        lane_copy(0, 1, c0);
+        SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
+        hipLaunchKernelGGL(k_nfa_run, dim3((unsigned)ceil_div(nl, kLaneBlock)), dim3(kLaneBlock), 0, s, dp, dl,
+                           dev_args(ra));
+        SHD_CHECK_LAUNCH();
+        if (nl > c0)
+          hipLaunchKernelGGL(k_win_check, dim3(grid_for(nl)), dim3(kBlock), 0, s, (const uint64_t*)ra.hash_w,
+                             (const uint64_t*)ra.hash_e, c0, nl, &d_ctl.as<NfaCtl>()->count);
+        hc = read_ctl();
+        if (win_debug)
+          std::fprintf(stderr, "[shd nfa window] n=%lld warm=%lld chunk=%lld lanes=%lld exact=%lld bad=%u ovf=0x%x\n",
+                       (long long)n, (long long)warm, (long long)chunk, (long long)nl, (long long)c0, hc.count,
+                       hc.overflow);
+        if (hc.overflow || hc.count == 0) {
+          if (!hc.overflow) lane_copy(nl, 0, 1);   // the last lane's end state is carried
+          win_warm = warm;
+          break;
+        }
+        win_fallbacks++;
+        warm *= 2;
       }
+      if (win_one) {
+        ra.chunk_len = 0;
+        ra.nlanes = 1;
+        ra.nseg = 1;
+      }
+    }
+    if (ra.nlanes > 0 && (!win || win_one)) {
+      SHD_HIP(hipMemsetAsync(d_ctl.p, 0, sizeof(NfaCtl), s));
+      hipLaunchKernelGGL(k_nfa_run, dim3((unsigned)ceil_div(ra.nlanes, kLaneBlock)), dim3(kLaneBlock), 0, s, dp, dl,
+                         dev_args(ra));
+      SHD_CHECK_LAUNCH();
+      hc = read_ctl();
     }
     mark("nfa");
     if (hc.overflow || (int64_t)hc.rows > R) {
@@ -2505,7 +2522,6 @@ struct NfaEngine : Engine {
     }
     const int64_t m = (int64_t)hc.rows;
     if (m > 0) order_rows(m, partitioned || (win && !win_one), timers, n);   // window lanes: merge by event order
-    if (win) roll_prefix(*b);
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -2524,7 +2540,7 @@ struct NfaEngine : Engine {
     counters.matches += m;
     counters.partials += (int64_t)hc.partials;
     counters.partial_scans += (int64_t)hc.scans;
-    counters.carry = windowed ? n_pre : (int64_t)hc.live;
+    counters.carry = (int64_t)hc.live;
     counters.kernel_ns = (int64_t)(ms * 1e6);
   }
 
@@ -2744,8 +2760,9 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
       }
   }
 
-  // window lanes: unpartitioned sequence, every-started, one stream, multi
-  // receiver (per (event, state) callbacks), no absent states, bounded span
+  // window lanes: unpartitioned, every-started, and partials bounded -- a
+  // sequence (a partial survives an event only by advancing on it) or a
+  // pattern with `within` / `for` times; the span / horizon sizes the warm-up
   {
     std::function<int64_t(const PNode&)> span = [&](const PNode& n) -> int64_t {
       switch (n.kind) {
@@ -2760,31 +2777,34 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
       }
       return -1;
     };
-    int used = 0, ws = -1;
-    for (size_t st = 0; st < streamPres.size(); st++)
-      if (!streamPres[st].empty()) {
-        used++;
-        ws = (int)st;
-      }
     bool every_start = false;
     for (int i = 0; i < npre; i++)
       if (g.pres[i].isStart && g.posts[g.pres[i].thisPost].nextEvery >= 0) every_start = true;
-    const int64_t sp = span(p.root);
+    // (an absent operand of `and` / `or` keeps partials past its time: not bounded)
+    int64_t horizon = std::max<int64_t>(P.within, 0);
+    bool absent_logical = false;
+    for (int i = 0; i < npre; i++) {
+      if (P.pre[i].waiting > 0) horizon = std::max<int64_t>(horizon, P.pre[i].waiting);
+      if (P.pre[i].kind == PK_ABSENT_LOGICAL) absent_logical = true;
+    }
+    if (absent_logical && !(p.state_type == 1)) horizon = 0;
+    const bool seq = p.state_type == 1;
     const char* wenv = getenv("SHD_NFA_WINDOW");
-    if (!e->partitioned && p.state_type == 1 && g.n_sched == 0 && sp > 0 && sp <= 256 && used == 1 &&
-        streamPres[ws].size() > 1 && every_start && !(wenv && wenv[0] == '0') && list_hint == 0) {
+    if (!e->partitioned && every_start && (seq || horizon > 0) && !(wenv && wenv[0] == '0') && list_hint == 0) {
       e->windowed = true;
-      e->win_stream = ws;
-      e->win_warm = 2 * sp + 2;
+      const int64_t sp = span(p.root);
+      e->win_span = seq && sp > 0 ? sp : 0;
+      e->win_horizon = seq ? 0 : horizon;
     }
   }
 
   // per-key capacities: one key (unpartitioned) gets deep lists, many keys get lean blocks
   NfaLayout& Y = e->lay;
-  const bool many = e->partitioned || e->windowed;
+  const bool many = e->partitioned;
   // list_hint (a pattern query handing its open partials over): the one key of
-  // an unpartitioned plan must hold about that many partials at once
-  int L0 = many ? 32 : 2048, S0 = many ? 128 : 8192;
+  // an unpartitioned plan must hold about that many partials at once; window
+  // lanes (one key state per lane, thousands of lanes) sit in between
+  int L0 = many ? 32 : (e->windowed ? 256 : 2048), S0 = many ? 128 : (e->windowed ? 1024 : 8192);
   if (!many && list_hint > 0) {
     while (L0 < 2 * list_hint && L0 < 32768) L0 *= 2;
     S0 = std::max(S0, std::min(2 * L0, 32768));
@@ -2846,8 +2866,8 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.o_wk = field(Y.WK + 1, 4);
   Y.o_key = field(1, 8);
   Y.o_misc = field(MISC_N, 4);
-  Y.o_cse = field(Y.SC + 1, 2);
-  Y.o_cev = field(Y.EC + 1, 2);
+  Y.o_cse = field(Y.SC + 1, 4);
+  Y.o_cev = field(Y.EC + 1, 4);
   Y.blk = off;
   return e;
 }

@@ -142,6 +142,11 @@ WINDOW_SEQS = {
     "seq13": wl.S4_APPS["seq"].replace("<2:5>", "<1:3>"),
     "seq14": wl.S4_APPS["seq"].replace("<2:5>", "<1:4>").replace("price<e2[last].price", "price<e1.price"),
     "bare": wl.S4_APPS["bare"],
+    # unbounded count (`+`): the warm-up is learned (verification doubles it)
+    "seqplus": wl.S4_APPS["seqplus"],
+    # patterns bounded by an absent `for` time: timers fire inside the lanes
+    "not": wl.S4_APPS["not"],
+    "not100": wl.S4_APPS["not"].replace("price>98", "price>95").replace("for 1 sec", "for 100 milliseconds"),
 }
 
 
@@ -149,11 +154,13 @@ WINDOW_SEQS = {
 @pytest.mark.parametrize("chunk", ["auto", "1", "5", "64"])
 @pytest.mark.parametrize("parts", [1, 4])
 def test_sequence_window_lanes(hip_available, monkeypatch, name, chunk, parts):
-    """Unpartitioned bounded-span every-sequences run as window lanes (one
-    lane per chunk of events, each replaying the events before its chunk from a
-    fresh state; the push's tail carries to the next push): rows identical to
-    the oracle and to the one-lane NFA, for lanes of one event and micro-batch
-    cuts inside partials.  `bare` (no every) stays on one lane."""
+    """Unpartitioned every-started sequences and time-bounded patterns run as
+    window lanes (one lane per chunk of events; the first lanes continue the
+    carried state exactly, the others replay a warm-up from a fresh state and
+    are verified against their predecessor's end state; a failed check reruns
+    the push with longer warm-ups): rows identical to the oracle and to the
+    one-lane NFA, for lanes of one event and micro-batch cuts inside partials.
+    `bare` (no every) stays on one lane."""
     if chunk != "auto":
         monkeypatch.setenv("SHD_NFA_CHUNK", chunk)
     qp, _ = compile_single_query(WINDOW_SEQS[name])
@@ -166,5 +173,7 @@ def test_sequence_window_lanes(hip_available, monkeypatch, name, chunk, parts):
     monkeypatch.setenv("SHD_NFA_WINDOW", "0")
     one, _, _ = run_device(qp, batches)
     assert_same_rows(dev, one)
-    if name in ("seq13", "seq14"):
+    if name in ("seq13", "seq14", "seqplus"):
         assert len(ora[2]) > 1000
+    if name in ("not", "not100"):
+        assert len(ora[2]) > 20
