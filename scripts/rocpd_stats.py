@@ -22,7 +22,9 @@ def stats(db):
 
 
 if __name__ == "__main__":
-    db = sys.argv[1] if len(sys.argv) > 1 else glob.glob("gpurun_out/**/*.db", recursive=True)[0]
+    db = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    if not db.endswith(".db"):   # a directory: its (first) database
+        db = sorted(glob.glob(db + "/**/*.db", recursive=True))[0]
     print("kernel,calls,total_us,avg_us,percent")
     for name, n, t, a, pc in stats(db):
         print('"%s",%d,%.3f,%.3f,%.3f' % (name, n, t, a, pc))

@@ -98,7 +98,8 @@ struct NfaLayout {
   int64_t o_rec_ts, o_rec_val, o_rec_nul, o_rec_free, o_rec_mark;
   int64_t o_ret, o_tmp, o_wk, o_key, o_misc;
   int64_t o_cse, o_cev;              // canonical ids (window-lane state hashes)
-  int64_t blk;
+  int64_t blk;   // bytes of one block of W key states
+  int W;         // key states interleaved per block: 64 (lock-step keys) or 1 (one key contiguous)
   // field table (one key's state = these fields, lane-interleaved): lane copies
   static constexpr int kMaxFields = 40;
   int nf;
@@ -106,7 +107,20 @@ struct NfaLayout {
   int64_t f_off[kMaxFields], f_cnt[kMaxFields];
 };
 
+// SHD_NFA_PROF builds: per-phase shader-clock totals over all lanes (ctl->prof)
+#ifdef SHD_NFA_PROF
+#define NFA_PROF_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define NFA_PROF_ADD(k, v) prof[k] += __builtin_amdgcn_s_memtime() - v
+#define NFA_PROF_ADDL(o, k, v) o.prof[k] += __builtin_amdgcn_s_memtime() - v
+#else
+#define NFA_PROF_ADDL(o, k, v)
+#define NFA_PROF_T0(v)
+#define NFA_PROF_ADD(k, v)
+#endif
+constexpr int kProfN = 8;
+
 struct NfaCtl {
+  unsigned long long prof[kProfN];
   unsigned long long rows;
   unsigned long long partials;
   unsigned long long scans;
@@ -160,9 +174,10 @@ struct NfaRunArgs {
 struct KS {
   char* b;
   int l;
+  int w;   // interleave width of the block (NfaLayout::W)
   template <class T>
   __device__ __forceinline__ T& at(int64_t off, int64_t e) const {
-    return *reinterpret_cast<T*>(b + off + (e * kLaneBlock + l) * (int64_t)sizeof(T));
+    return *reinterpret_cast<T*>(b + off + (e * w + l) * (int64_t)sizeof(T));
   }
 };
 
@@ -199,6 +214,9 @@ struct Lane {
   uint64_t t_prim, t_sec, t_ter;
   int64_t last_seq;
   bool quiet;   // window lanes: warm-up events (no output)
+#ifdef SHD_NFA_PROF
+  uint64_t prof[kProfN] = {};
+#endif
   int cdone;
 
   __device__ Lane(const NfaProg& p, const NfaLayout& y, const NfaRunArgs& a, DExprSet e)
@@ -1169,6 +1187,7 @@ struct Lane {
   __device__ uint64_t new_tag() { return ((uint64_t)slot << 24) | (uint64_t)(tagc++ & 0xFFFFFF); }
   __device__ void emit(uint16_t s, uint64_t tag) {
     if (quiet) return;   // warm-up event of a window lane
+    NFA_PROF_T0(t4);
     unsigned long long idx = atomicAdd(&A.ctl->rows, 1ull);
     if ((int64_t)idx >= A.R) {
       ovf |= OV_ROWS;
@@ -1186,6 +1205,7 @@ struct Lane {
     A.st_p[idx] = t_prim;
     A.st_s[idx] = t_sec;
     A.st_t[idx] = t_ter;
+    NFA_PROF_ADD(4, t4);
   }
 
   // ---------------------------------------------------------------- key lifecycle
@@ -1253,11 +1273,18 @@ struct Lane {
   }
 
   __device__ void process_event(int64_t row) {
+    NFA_PROF_T0(t0);
     maybe_gc();
+    NFA_PROF_ADD(0, t0);
+    NFA_PROF_T0(t1);
     const int si = A.stream;
     const int64_t ts = A.batch.ts[row];
     const uint16_t rec = make_rec(row, ts);
+    NFA_PROF_ADD(1, t1);
+    NFA_PROF_T0(t2);
     stabilize(si, ts);
+    NFA_PROF_ADD(2, t2);
+    NFA_PROF_T0(t3);
     const int np = P.nsp[si];
     last_seq = A.seq0 + row;
     if (np > 1) {
@@ -1287,6 +1314,8 @@ struct Lane {
       for (int i = 0; i < nret; i++) push_ret(tmpl(i));
       misc(MISC_TMPN) = 0;
     }
+    NFA_PROF_ADD(3, t3);
+    NFA_PROF_ADD(7, t0);
   }
 
   __device__ void flush_run() {
@@ -1401,8 +1430,9 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
   }
   Lane L(sprog, slay, a, es);
   L.slot = slot;
-  L.ks.b = a.state + (slot / kLaneBlock) * slay.blk;
-  L.ks.l = (int)(slot % kLaneBlock);
+  L.ks.b = a.state + (slot / slay.W) * slay.blk;
+  L.ks.l = (int)(slot % slay.W);
+  L.ks.w = slay.W;
   L.ovf = 0;
   L.partials = 0;
   L.scans = 0;
@@ -1442,16 +1472,20 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     for (int64_t row = wb; row < oe && !L.ovf; row++) {
       if (row == ob) {
         L.quiet = false;
+        NFA_PROF_T0(th);
         if (!exact) a.hash_w[lane_id] = L.state_hash();
+        NFA_PROF_ADDL(L, 5, th);
       } else if (row == wb) {
         L.quiet = true;
       }
+      NFA_PROF_T0(tf);
       const uint32_t run = a.run_id[row];
       if (run != cur_run) {
         L.flush_run();
         cur_run = run;
       }
       L.fire_upto(a.call_of[row]);
+      NFA_PROF_ADDL(L, 6, tf);
       L.process_event(row);
     }
     L.quiet = false;
@@ -1461,6 +1495,9 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     }
     L.misc(MISC_EVRET) = L.evret;
     a.hash_e[lane_id] = L.state_hash();
+#ifdef SHD_NFA_PROF
+    for (int k = 0; k < kProfN; k++) atomicAdd(&a.ctl->prof[k], (unsigned long long)L.prof[k]);
+#endif
     if (L.ovf) atomicOr(&a.ctl->overflow, L.ovf);
     if (L.partials) atomicAdd(&a.ctl->partials, L.partials);
     if (L.scans) atomicAdd(&a.ctl->scans, L.scans);
@@ -1525,12 +1562,13 @@ __global__ void k_lane_copy(const NfaLayout* __restrict__ glay, char* __restrict
   const int f = blockIdx.y;
   const int sz = Y.f_sz[f];
   const int64_t total = Y.f_cnt[f] * ndst;
-  const char* sb = state + (src / kLaneBlock) * Y.blk + Y.f_off[f];
-  const int sl = (int)(src % kLaneBlock);
+  const int W = Y.W;
+  const char* sb = state + (src / W) * Y.blk + Y.f_off[f];
+  const int sl = (int)(src % W);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = i / ndst, d = dst0 + i % ndst;
-    const char* sp = sb + (e * kLaneBlock + sl) * sz;
-    char* dp = state + (d / kLaneBlock) * Y.blk + Y.f_off[f] + (e * kLaneBlock + d % kLaneBlock) * sz;
+    const char* sp = sb + (e * W + sl) * sz;
+    char* dp = state + (d / W) * Y.blk + Y.f_off[f] + (e * W + d % W) * sz;
     switch (sz) {
       case 8: *reinterpret_cast<uint64_t*>(dp) = *reinterpret_cast<const uint64_t*>(sp); break;
       case 4: *reinterpret_cast<uint32_t*>(dp) = *reinterpret_cast<const uint32_t*>(sp); break;
@@ -1689,11 +1727,10 @@ __global__ void k_slot_lookup(const uint64_t* seg_key, int64_t nseg, uint32_t* h
 }
 
 // rebuild the directory from the key blocks (after growth)
-__global__ void k_slot_rebuild(const char* state, int64_t blk, int64_t o_key, int64_t nslots, uint32_t* ht_state,
-                               uint64_t* ht_key, uint32_t* ht_slot, uint64_t mask, uint32_t epoch) {
+__global__ void k_slot_rebuild(const char* state, int64_t blk, int W, int64_t o_key, int64_t nslots,
+                               uint32_t* ht_state, uint64_t* ht_key, uint32_t* ht_slot, uint64_t mask, uint32_t epoch) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k =
-        *reinterpret_cast<const uint64_t*>(state + (s / kLaneBlock) * blk + o_key + (s % kLaneBlock) * 8);
+    const uint64_t k = *reinterpret_cast<const uint64_t*>(state + (s / W) * blk + o_key + (s % W) * 8);
     uint64_t h = mix64(k) & mask;
     for (uint64_t probe = 0; probe <= mask; probe++) {
       if (atomicCAS(&ht_state[h], 0u, epoch) == 0) {
@@ -1706,12 +1743,12 @@ __global__ void k_slot_rebuild(const char* state, int64_t blk, int64_t o_key, in
   }
 }
 
-__global__ void k_store_keys(char* state, int64_t blk, int64_t o_key, const uint64_t* seg_key,
+__global__ void k_store_keys(char* state, int64_t blk, int W, int64_t o_key, const uint64_t* seg_key,
                              const uint32_t* seg_slot, int64_t nseg) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += (int64_t)gridDim.x * blockDim.x) {
     uint32_t s = seg_slot[g];
     if (s == 0xFFFFFFFFu) continue;
-    *reinterpret_cast<uint64_t*>(state + (s / kLaneBlock) * blk + o_key + (s % kLaneBlock) * 8) = seg_key[g];
+    *reinterpret_cast<uint64_t*>(state + (s / W) * blk + o_key + (s % W) * 8) = seg_key[g];
   }
 }
 
@@ -2066,7 +2103,7 @@ struct NfaEngine : Engine {
     counters = shd_counters{};
     nslots = 0;
     epoch = 0;
-    if (state.p && slot_cap > 0) SHD_HIP(hipMemset(state.p, 0, (size_t)(slot_cap / kLaneBlock) * lay.blk));
+    if (state.p && slot_cap > 0) SHD_HIP(hipMemset(state.p, 0, (size_t)(slot_cap / lay.W) * lay.blk));
     if (ht_state.p && ht_cap > 0) SHD_HIP(hipMemset(ht_state.p, 0, (size_t)ht_cap * 4));
     SHD_HIP(hipDeviceSynchronize());
   }
@@ -2084,7 +2121,7 @@ struct NfaEngine : Engine {
     w.put<int64_t>(ht_cap);
     w.put<uint32_t>(epoch);
     w.put<int64_t>((int64_t)lay.blk);
-    w.dev(state.p, (size_t)(slot_cap / kLaneBlock) * lay.blk);
+    w.dev(state.p, (size_t)(slot_cap / lay.W) * lay.blk);
     w.dev(ht_state.p, (size_t)ht_cap * 4);
     w.dev(ht_key.p, (size_t)ht_cap * 8);
     w.dev(ht_slot.p, (size_t)ht_cap * 4);
@@ -2105,7 +2142,7 @@ struct NfaEngine : Engine {
     const uint32_t ep = r.get<uint32_t>();
     if (r.get<int64_t>() != (int64_t)lay.blk || sc < 0 || ns < 0 || ns > sc || hc < 0 || sc % kLaneBlock)
       throw Error(SHD_E_ARG, "snapshot of a different plan");
-    const size_t sb = (size_t)(sc / kLaneBlock) * lay.blk;
+    const size_t sb = (size_t)(sc / lay.W) * lay.blk;
     state.reserve(std::max<size_t>(sb, 1));
     r.dev_into(state.p, sb);
     ht_state.reserve(std::max<int64_t>(hc, 1) * 4);
@@ -2156,10 +2193,10 @@ struct NfaEngine : Engine {
     int64_t nc = std::max<int64_t>(need, slot_cap * 2);
     nc = (nc + kLaneBlock - 1) / kLaneBlock * kLaneBlock;
     DevBuf nb;
-    nb.reserve((size_t)(nc / kLaneBlock) * lay.blk);
-    size_t old = (size_t)(slot_cap / kLaneBlock) * lay.blk;
+    nb.reserve((size_t)(nc / lay.W) * lay.blk);
+    size_t old = (size_t)(slot_cap / lay.W) * lay.blk;
     if (old) SHD_HIP(hipMemcpyAsync(nb.p, state.p, old, hipMemcpyDeviceToDevice, stream));
-    SHD_HIP(hipMemsetAsync((char*)nb.p + old, 0, (size_t)(nc / kLaneBlock) * lay.blk - old, stream));
+    SHD_HIP(hipMemsetAsync((char*)nb.p + old, 0, (size_t)(nc / lay.W) * lay.blk - old, stream));
     SHD_HIP(hipStreamSynchronize(stream));
     std::swap(state.p, nb.p);
     std::swap(state.cap, nb.cap);
@@ -2178,7 +2215,7 @@ struct NfaEngine : Engine {
     if (nslots > 0) {
       epoch++;
       hipLaunchKernelGGL(k_slot_rebuild, dim3(grid_for(nslots)), dim3(kBlock), 0, stream, (const char*)state.p,
-                         lay.blk, lay.o_key, nslots, ht_state.as<uint32_t>(), ht_key.as<uint64_t>(),
+                         lay.blk, lay.W, lay.o_key, nslots, ht_state.as<uint32_t>(), ht_key.as<uint64_t>(),
                          ht_slot.as<uint32_t>(), (uint64_t)(ht_cap - 1), epoch);
       SHD_CHECK_LAUNCH();
     }
@@ -2304,7 +2341,7 @@ struct NfaEngine : Engine {
                        (uint64_t)(ht_cap - 1), epoch, &d_ctl.as<NfaCtl>()->count, d_seg_slot.as<uint32_t>(),
                        timers ? d_slot_seg.as<int32_t>() : nullptr);
     SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_store_keys, dim3(grid_for(nseg)), dim3(kBlock), 0, s, state.as<char>(), lay.blk, lay.o_key,
+    hipLaunchKernelGGL(k_store_keys, dim3(grid_for(nseg)), dim3(kBlock), 0, s, state.as<char>(), lay.blk, lay.W, lay.o_key,
                        (const uint64_t*)d_seg_key.as<uint64_t>(), (const uint32_t*)d_seg_slot.as<uint32_t>(), nseg);
     SHD_CHECK_LAUNCH();
     hc = read_ctl();
@@ -2485,10 +2522,19 @@ struct NfaEngine : Engine {
           hipLaunchKernelGGL(k_win_check, dim3(grid_for(nl)), dim3(kBlock), 0, s, (const uint64_t*)ra.hash_w,
                              (const uint64_t*)ra.hash_e, c0, nl, &d_ctl.as<NfaCtl>()->count);
         hc = read_ctl();
-        if (win_debug)
+        if (win_debug) {
           std::fprintf(stderr, "[shd nfa window] n=%lld warm=%lld chunk=%lld lanes=%lld exact=%lld bad=%u ovf=0x%x\n",
                        (long long)n, (long long)warm, (long long)chunk, (long long)nl, (long long)c0, hc.count,
                        hc.overflow);
+#ifdef SHD_NFA_PROF
+          std::fprintf(stderr, "[shd nfa prof] per lane-event clocks: gc %.0f rec %.0f stabilize %.0f process %.0f "
+                       "emit %.0f hash/lane %.0f fire %.0f event %.0f\n",
+                       hc.prof[0] / (double)(n + nl * warm), hc.prof[1] / (double)(n + nl * warm),
+                       hc.prof[2] / (double)(n + nl * warm), hc.prof[3] / (double)(n + nl * warm),
+                       hc.prof[4] / (double)(n + nl * warm), hc.prof[5] / (double)nl,
+                       hc.prof[6] / (double)(n + nl * warm), hc.prof[7] / (double)(n + nl * warm));
+#endif
+        }
         if (hc.overflow || hc.count == 0) {
           if (!hc.overflow) lane_copy(nl, 0, 1);   // the last lane's end state is carried
           win_warm = warm;
@@ -2802,9 +2848,13 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   NfaLayout& Y = e->lay;
   const bool many = e->partitioned;
   // list_hint (a pattern query handing its open partials over): the one key of
-  // an unpartitioned plan must hold about that many partials at once; window
-  // lanes (one key state per lane, thousands of lanes) sit in between
-  int L0 = many ? 32 : (e->windowed ? 256 : 2048), S0 = many ? 128 : (e->windowed ? 1024 : 8192);
+  // an unpartitioned plan must hold about that many partials at once (window
+  // lanes too: each holds the one key's whole state; sequence lanes less)
+  int L0 = many ? 32 : 2048, S0 = many ? 128 : 8192;
+  if (e->windowed && e->win_horizon == 0) {   // sequence lanes: partials die unless they advance
+    L0 = 128;
+    S0 = 512;
+  }
   if (!many && list_hint > 0) {
     while (L0 < 2 * list_hint && L0 < 32768) L0 *= 2;
     S0 = std::max(S0, std::min(2 * L0, 32768));
@@ -2828,11 +2878,17 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.sew = (Y.SC + 1 + 63) / 64;
   Y.evw = (Y.EC + 1 + 63) / 64;
   Y.recw = (Y.RC + 1 + 63) / 64;
+  // window lanes diverge (each walks its own chunk): one lane's state contiguous
+  // so its accesses share cache lines; per-key lanes of a partitioned plan
+  // interleave 64 keys per block
+  Y.W = e->windowed ? 1 : kLaneBlock;
+  if (const char* w = getenv("SHD_NFA_INTERLEAVE")) Y.W = w[0] == '0' ? 1 : kLaneBlock;
+  const int64_t falign = Y.W == 1 ? 16 : 256;
   int64_t off = 0;
   Y.nf = 0;
   auto field = [&](int64_t count, int sz) {
     int64_t o = off;
-    off += (count * kLaneBlock * sz + 255) & ~int64_t(255);
+    off += (count * Y.W * sz + falign - 1) & ~(falign - 1);
     Y.f_off[Y.nf] = o;
     Y.f_cnt[Y.nf] = count;
     Y.f_sz[Y.nf] = sz;
