@@ -200,9 +200,11 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
 // hashed: digits are taken from key_bucket_mix(key) instead of the key, so
 // bits < 32 groups equal keys into 2^bits buckets (stable: input order inside
 // a bucket) while the array still carries the raw keys.
+// shift0: the passes start at digit bit shift0 (the lower digits were sorted
+// already, e.g. by a fused prepare + first pass).
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
-                            bool hashed = false, uint32_t kbase = 0);
+                            bool hashed = false, uint32_t kbase = 0, int shift0 = 0);
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt);
 // Digit totals (256 per pass, u32) of the last radix pass run with `scratch`

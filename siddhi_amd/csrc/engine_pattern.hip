@@ -327,11 +327,14 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   prep_block_reduce<kBlock>(acc, blk, blockIdx.x);
 }
 
-// Fused prepare + one stable hashed bucket pass (the bucketed walk's layout):
-// k_bkt_hist counts the 256 buckets of every tile from the key column alone
-// (plain 32-bit attribute keys), k_bkt_scatter prepares the rows in registers
-// (prep_row) and writes (key, flags|row, ts32) straight to their bucket
-// positions -- the prepared rows never make a round trip through HBM.
+// Fused prepare + one stable radix pass: k_bkt_hist counts the 256 digits of
+// every tile from the key column alone (plain 32-bit attribute keys),
+// k_bkt_scatter prepares the rows in registers (prep_row) and writes (key,
+// flags|row, ts32) straight to their digit positions -- the prepared rows never
+// make a round trip through HBM.  H: hashed buckets (key_bucket_mix, the
+// bucketed walk's layout); else the key's low byte (the first LSD pass of the
+// sort path's key sort, whose later passes run on digits of key - kbase with
+// kbase a multiple of 256).
 constexpr int kBktRounds = 16;   // rows per lane of a scatter tile (4096 rows / tile)
 
 __device__ __forceinline__ uint32_t bkt_key32(const PrepArgs& a, int64_t r) {
@@ -343,6 +346,7 @@ __device__ __forceinline__ uint32_t bkt_key32(const PrepArgs& a, int64_t r) {
   return gld((const uint32_t*)x.batch.col[a.key_col], br);
 }
 
+template <bool H>
 __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restrict__ ap, int64_t n_ext,
                                                        uint32_t* __restrict__ hist, int nb) {
   const PrepArgs& a = *ap;
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restric
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kBktRounds; r++)
-    if (wb + r * 64 + lane < n_ext) atomicAdd(&h[w][key_bucket_mix(k[r]) & 255u], 1u);
+    if (wb + r * 64 + lane < n_ext) atomicAdd(&h[w][rs_hdigit<H>(k[r], 0, 0u)], 1u);
   __syncthreads();
   if (tid < 256) {
     uint32_t c = 0;
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restric
   }
 }
 
-template <bool FAST>
+template <bool FAST, bool H>
 __global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __restrict__ ap, int64_t n_ext,
                                                           const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ offs,
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __rest
     v[r] = (f << kRowBits) | (uint32_t)li;
     x[r] = (uint32_t)t32;
   }
-  rs_scatter_tile<uint32_t, kBktRounds, true, true>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
+  rs_scatter_tile<uint32_t, kBktRounds, true, H>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
   prep_block_reduce<kRsBlock>(acc, blk, tile);
 }
 
@@ -2031,16 +2035,16 @@ struct PatternEngine : Engine {
       uint32_t* hist = d_sort.as<uint32_t>();
       uint32_t* offs = hist + (int64_t)nbt * 256;
       uint32_t* tot = offs + (int64_t)nbt * 256;
-      hipLaunchKernelGGL(k_bkt_hist, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
+      hipLaunchKernelGGL(k_bkt_hist<true>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
       SHD_CHECK_LAUNCH();
       radix_digit_scan(hist, nbt, offs, tot, s);
       if (fast1)
-        hipLaunchKernelGGL(k_bkt_scatter<true>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+        hipLaunchKernelGGL((k_bkt_scatter<true, true>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
                            (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
                            d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
                            d_blk.as<PrepAgg>());
       else
-        hipLaunchKernelGGL(k_bkt_scatter<false>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+        hipLaunchKernelGGL((k_bkt_scatter<false, true>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
                            (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
                            d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
                            d_blk.as<PrepAgg>());
@@ -2211,17 +2215,56 @@ struct PatternEngine : Engine {
     d_blk.reserve((size_t)3 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!keyed || pa.key_col >= 0);
-    if (fast1)
-      hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                         d_blk.as<PrepAgg>());
-    else
-      hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                         d_blk.as<PrepAgg>());
-    SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
-    SHD_CHECK_LAUNCH();
+    // partitioned plans with a plain 32-bit key column: prepare fused into the
+    // key sort's first LSD pass (the key's low byte) -- the prepared rows go
+    // straight to their first-pass positions instead of a round trip through HBM
+    // (SHD_HASH_BITS asks for hashed buckets: the unfused sort)
+    // Measured on MI355X (P3, 50 M-event pushes): 2.8 ms for the fused pass
+    // against 0.9 + 0.7 ms unfused (the fused scatter's per-row prepare
+    // serialises its loads), so it is opt-in (SHD_SORT_FUSED=1) until its
+    // loads are batched.
+    const bool fused1 = partitioned && !key64 && pa.key_col >= 0 && getenv("SHD_SORT_FUSED") &&
+                        !getenv("SHD_HASH_BITS");
+    if (fused1) {
+      const int nbt = (int)ceil_div(n_ext, rs_tile(kBktRounds));
+      if ((size_t)nbt * std::max(sizeof(PrepAgg), sizeof(ScanOut)) > d_blk.cap)
+        d_blk.reserve((size_t)std::max<int64_t>(3 * nblk, nbt) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
+      d_k32_alt.reserve(n_ext * 4);
+      d_pv_alt.reserve(n_ext * 4);
+      d_ts_alt.reserve(n_ext * 4);
+      d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
+      uint32_t* hist = d_sort.as<uint32_t>();
+      uint32_t* offs = hist + (int64_t)nbt * 256;
+      uint32_t* tot = offs + (int64_t)nbt * 256;
+      hipLaunchKernelGGL(k_bkt_hist<false>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
+      SHD_CHECK_LAUNCH();
+      radix_digit_scan(hist, nbt, offs, tot, s);
+      if (fast1)
+        hipLaunchKernelGGL((k_bkt_scatter<true, false>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
+                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                           d_blk.as<PrepAgg>());
+      else
+        hipLaunchKernelGGL((k_bkt_scatter<false, false>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
+                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
+                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                           d_blk.as<PrepAgg>());
+      SHD_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
+      SHD_CHECK_LAUNCH();
+    } else {
+      if (fast1)
+        hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                           d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                           d_blk.as<PrepAgg>());
+      else
+        hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                           d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                           d_blk.as<PrepAgg>());
+      SHD_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
+      SHD_CHECK_LAUNCH();
+    }
     SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     PrepAgg pg;
@@ -2254,7 +2297,14 @@ struct PatternEngine : Engine {
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
       uint32_t kbase = 0;
-      if (bits <= 32 && !type_key64(key_type[slot])) {
+      if (fused1) {
+        // the first pass sorted by the key's low byte: digits of key - kbase
+        // with kbase a multiple of 256 continue it
+        kbase = (uint32_t)(kmin & ~(uint64_t)255);
+        int rb = 0;
+        while (rb < 64 && ((kmax - kbase) >> rb)) rb++;
+        bits = std::max(rb, 8);
+      } else if (bits <= 32 && !type_key64(key_type[slot])) {
         int rb = 0;
         while (rb < 64 && ((kmax - kmin) >> rb)) rb++;
         if (rb < bits) {
@@ -2262,22 +2312,33 @@ struct PatternEngine : Engine {
           kbase = (uint32_t)kmin;
         }
       }
-      if (bits <= 32) {
-        const int hb = hashed_bucket_bits(pg, n_ext, bits, prune);
-        if (hb > 0) {
-          bits = hb;
-          hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
+      bool in_alt = false;
+      if (fused1) {
+        d_k32.reserve(n_ext * 4);
+        bool back = false;
+        radix_sort_triples_u32(d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                               d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), n_ext, bits, d_sort, s,
+                               back, false, kbase, 8);
+        in_alt = !back;   // the first pass wrote the alt arrays
+        skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
+      } else {
+        if (bits <= 32) {
+          const int hb = hashed_bucket_bits(pg, n_ext, bits, prune);
+          if (hb > 0) {
+            bits = hb;
+            hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
+          }
+        }
+        d_pv_alt.reserve(n_ext * 4);
+        d_ts_alt.reserve(n_ext * 4);
+        if (key64 && bits <= 32) {
+          hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
+                             d_k32.as<uint32_t>(), n_ext);
+          SHD_CHECK_LAUNCH();
         }
       }
-      d_pv_alt.reserve(n_ext * 4);
-      d_ts_alt.reserve(n_ext * 4);
-      bool in_alt = false;
-      if (key64 && bits <= 32) {
-        hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
-                           d_k32.as<uint32_t>(), n_ext);
-        SHD_CHECK_LAUNCH();
-      }
-      if (bits <= 32) {
+      if (fused1) {
+      } else if (bits <= 32) {
         d_k32_alt.reserve(n_ext * 4);
         radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
                                d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,

@@ -248,7 +248,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const K* __restrict__ k
 
 template <class K, int R, bool P2, bool H = false>
 static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, uint32_t* vals_alt, uint32_t* w_alt,
-                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt, K kb = 0) {
+                           int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt, K kb = 0,
+                           int shift0 = 0) {
   in_alt = false;
   if (n <= 1 || bits <= 0) return;
   // k_rs_hist reads full tiles of 32-bit keys with 16-byte loads
@@ -265,7 +266,7 @@ static void radix_sort_run(K* keys, uint32_t* vals, uint32_t* w, K* keys_alt, ui
   const int xcd = getenv("SHD_RS_NOXCD") ? 0 : 1;   // A/B switch for the tile order
   K* ki = keys; uint32_t* vi = vals; uint32_t* wi = w;
   K* ko = keys_alt; uint32_t* vo = vals_alt; uint32_t* wo = w_alt;
-  for (int shift = 0; shift < bits; shift += 8) {
+  for (int shift = shift0; shift < bits; shift += 8) {
     hipLaunchKernelGGL((k_rs_hist<K, R, H>), dim3(nb), dim3(kRsBlock), 0, s, (const K*)ki, n, shift, hist, nb, xcd, kb);
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_rs_digit_scan, dim3(256), dim3(kRsBlock), 0, s, (const uint32_t*)hist, nb, offs, dtot);
@@ -305,13 +306,13 @@ void radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, ui
 
 void radix_sort_triples_u32(uint32_t* keys, uint32_t* vals, uint32_t* w, uint32_t* keys_alt, uint32_t* vals_alt,
                             uint32_t* w_alt, int64_t n, int bits, DevBuf& scratch, hipStream_t s, bool& in_alt,
-                            bool hashed, uint32_t kbase) {
+                            bool hashed, uint32_t kbase, int shift0) {
   if (hashed)
     radix_sort_run<uint32_t, kRsRounds, true, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s,
-                                                    in_alt);
+                                                    in_alt, 0u, shift0);
   else
     radix_sort_run<uint32_t, kRsRounds, true>(keys, vals, w, keys_alt, vals_alt, w_alt, n, bits, scratch, s, in_alt,
-                                              kbase);
+                                              kbase, shift0);
 }
 
 void radix_sort_triples_u64(uint64_t* keys, uint32_t* vals, uint32_t* w, uint64_t* keys_alt, uint32_t* vals_alt,
