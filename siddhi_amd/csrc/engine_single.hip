@@ -1129,14 +1129,21 @@ __device__ __forceinline__ int64_t gallop_first(int64_t p, Pred pred) {
 }
 
 // phase 4: window aggregates at the last add of every (group, call) run ->
-// the emission inputs of k_emit (first / last_of / resv / resn / resc); the
-// group tables get the window state after the push at every segment end
+// one packed emission record at the run's first item (k_emit<true> reads it
+// there: last item, null mask, one 8-byte value per aggregator with avg
+// already divided), so a run costs one contiguous scattered write; the group
+// tables get the window state after the push at every segment end
+struct RunRecHdr {
+  uint32_t last;   // item of the run's last add (the emitted event)
+  uint32_t nul;    // bit j: aggregator j is null
+};
+__host__ __device__ constexpr int64_t run_rec_words(int nagg) { return 1 + nagg; }
+
 template <int NC>
 __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__ ap, const uint32_t* sk,
                                                      const uint32_t* sp, const uint32_t* se, const int32_t* scall,
                                                      const DD* S, const int32_t* NN, const uint8_t* iargn,
-                                                     uint64_t* resv, uint8_t* resn, int64_t* resc, uint8_t* first,
-                                                     uint32_t* last_of) {
+                                                     uint64_t* rec, uint8_t* first) {
   const SegArgs& a = *ap;
   const int64_t total = a.total;
   for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total; p = total) {
@@ -1173,12 +1180,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__
     window(x, k, kin);
     const int64_t rs = gallop_first(p, [&](int64_t q) { return sk[q] == g && scall[q] == call; });
     const uint32_t xf = sp[rs];
-    first[xf] = 1;
-    last_of[xf] = x;
+    uint64_t vals[kMaxAggs];
+    uint32_t nul = 0;
     for (int j = 0; j < a.nagg; j++) {
       const int c = a.chan[j];
       uint64_t ob = 0;
-      uint8_t on = 0;
+      bool on = false;
       if (a.kind[j] == SHD_AGG_COUNT) {
         ob = (uint64_t)(p - k + 1);
       } else {
@@ -1187,16 +1194,21 @@ __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__
         if (a.kind[j] == SHD_AGG_SUM) {
           // a null operand leaves the sum (null once nothing is left; float sums: null)
           const bool xn = iargn[j * a.cap + x] != 0;
-          on = (uint8_t)(xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0));
+          on = xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0);
+          ob = on ? 0ull : p_f64(v);
         } else {
-          on = (uint8_t)(nnw == 0);   // avg: value / count at emission
-          resc[j * a.cap + x] = nnw;
+          // avg = value / count (AvgAttributeAggregatorExecutor: value / count as double)
+          on = nnw == 0;
+          ob = on ? 0ull : p_f64(__ddiv_rn(v, (double)nnw));
         }
-        ob = on ? 0ull : p_f64(v);
       }
-      resv[j * a.cap + x] = ob;
-      resn[j * a.cap + x] = on;
+      vals[j] = ob;
+      nul |= on ? 1u << j : 0u;
     }
+    uint64_t* r = rec + (int64_t)xf * run_rec_words(a.nagg);
+    r[0] = (uint64_t)x | ((uint64_t)nul << 32);
+    for (int j = 0; j < a.nagg; j++) r[1 + j] = vals[j];
+    first[xf] = 1;
   }
 }
 
@@ -1219,6 +1231,8 @@ struct EmitArgs {
   int64_t seq0;
 };
 
+// REC: the run's values come from its packed record (segmented-scan mode)
+template <bool REC>
 __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap, int64_t nnew, const uint32_t* fcnt, const uint32_t* foff,
                                                  const uint32_t* last_of, const int32_t* ievrow, const int32_t* call_of,
                                                  const uint64_t* resv, const uint8_t* resn, const int64_t* resc,
@@ -1231,16 +1245,27 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
   for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < nnew; t0 = nnew) {
     if (!fcnt[t0]) continue;
     int64_t tf = a.C + t0;
-    int64_t tl = last_of[tf];
-    int64_t ev = ievrow[tl];
+    int64_t tl;
     uint64_t av[kMaxAggs];
     uint8_t an[kMaxAggs];
-    for (int g = 0; g < a.nagg; g++) {
-      av[g] = resv[g * a.cap + tl];
-      an[g] = resn[g * a.cap + tl];
-      // avg = value / count (AvgAttributeAggregatorExecutor: value / count as double)
-      if (a.kind[g] == SHD_AGG_AVG && !an[g]) av[g] = p_f64(__ddiv_rn(v_f64(av[g]), (double)resc[g * a.cap + tl]));
+    if (REC) {
+      const uint64_t* r = resv + tf * run_rec_words(a.nagg);
+      const uint64_t h = r[0];
+      tl = (int64_t)(uint32_t)h;
+      for (int g = 0; g < a.nagg; g++) {
+        av[g] = r[1 + g];
+        an[g] = (uint8_t)((h >> (32 + g)) & 1u);
+      }
+    } else {
+      tl = last_of[tf];
+      for (int g = 0; g < a.nagg; g++) {
+        av[g] = resv[g * a.cap + tl];
+        an[g] = resn[g * a.cap + tl];
+        // avg = value / count (AvgAttributeAggregatorExecutor: value / count as double)
+        if (a.kind[g] == SHD_AGG_AVG && !an[g]) av[g] = p_f64(__ddiv_rn(v_f64(av[g]), (double)resc[g * a.cap + tl]));
+      }
     }
+    int64_t ev = ievrow[tl];
     RowCtx cx{&cs, ev, av, an};
     int64_t row = a.row0 + foff[t0];
     for (int c = 0; c < a.nout; c++) {
@@ -1290,7 +1315,7 @@ struct SingleEngine : Engine {
   int nch = 0;                       // distinct aggregated expressions (channels)
   int ch_agg[kMaxChan] = {}, ch_type[kMaxChan] = {};
   int chan_of[kMaxAggs] = {};
-  DevBuf sval, snn, se, scall, tagg, segS, segNN;
+  DevBuf sval, snn, se, scall, tagg, segS, segNN, rec;
   // group state (dense by key)
   DevBuf g_dsum, g_lsum, g_cnt;
   int64_t g_nkeys = 0;
@@ -1597,12 +1622,20 @@ struct SingleEngine : Engine {
     ea.row0 = out.count;
     ea.chunk0 = chunk_seq;
     ea.seq0 = seq;
-    hipLaunchKernelGGL(k_emit, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m,
-                       (const uint32_t*)fcnt.as<uint32_t>(), (const uint32_t*)foff.as<uint32_t>(),
-                       (const uint32_t*)last_of.as<uint32_t>(), (const int32_t*)ievrow.as<int32_t>(),
-                       (const int32_t*)d_call_of.as<int32_t>(), (const uint64_t*)resv.as<uint64_t>(),
-                       (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
-                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
+    if (seg_mode)
+      hipLaunchKernelGGL(k_emit<true>, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m,
+                         (const uint32_t*)fcnt.as<uint32_t>(), (const uint32_t*)foff.as<uint32_t>(),
+                         (const uint32_t*)last_of.as<uint32_t>(), (const int32_t*)ievrow.as<int32_t>(),
+                         (const int32_t*)d_call_of.as<int32_t>(), (const uint64_t*)rec.as<uint64_t>(),
+                         (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
+                         out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
+    else
+      hipLaunchKernelGGL(k_emit<false>, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ea), m,
+                         (const uint32_t*)fcnt.as<uint32_t>(), (const uint32_t*)foff.as<uint32_t>(),
+                         (const uint32_t*)last_of.as<uint32_t>(), (const int32_t*)ievrow.as<int32_t>(),
+                         (const int32_t*)d_call_of.as<int32_t>(), (const uint64_t*)resv.as<uint64_t>(),
+                         (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
+                         out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
     SHD_CHECK_LAUNCH();
     out.count += nrows;
     counters.matches += nrows;
@@ -1639,11 +1672,11 @@ struct SingleEngine : Engine {
                        (const SegAcc<NC>*)tagg.as<SegAcc<NC>>(), segS.as<DD>(), segNN.as<int32_t>());
     SHD_CHECK_LAUNCH();
     mark("seg_scan");
+    rec.reserve((size_t)cap * run_rec_words(nagg) * 8);
     hipLaunchKernelGGL(k_seg_emit<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sk, sp,
                        (const uint32_t*)se.as<uint32_t>(), (const int32_t*)scall.as<int32_t>(),
                        (const DD*)segS.as<DD>(), (const int32_t*)segNN.as<int32_t>(),
-                       (const uint8_t*)iargn[cur].as<uint8_t>(), resv.as<uint64_t>(), resn.as<uint8_t>(),
-                       resc.as<int64_t>(), first.as<uint8_t>(), last_of.as<uint32_t>());
+                       (const uint8_t*)iargn[cur].as<uint8_t>(), rec.as<uint64_t>(), first.as<uint8_t>());
     SHD_CHECK_LAUNCH();
     mark("seg_window");
   }
@@ -1783,11 +1816,13 @@ struct SingleEngine : Engine {
       throw Error(SHD_E_UNSUPPORTED, "group-by key outside the dense device range");
     ensure_groups((int64_t)kmax + 1);
     const int64_t nops = m + X;
-    resv.reserve(std::max(nagg, 1) * cap * 8);
-    resc.reserve(std::max(nagg, 1) * cap * 8);
-    resn.reserve(std::max(nagg, 1) * cap);
+    if (!seg_mode) {   // (segmented-scan mode: packed run records instead)
+      resv.reserve(std::max(nagg, 1) * cap * 8);
+      resc.reserve(std::max(nagg, 1) * cap * 8);
+      resn.reserve(std::max(nagg, 1) * cap);
+      last_of.reserve(cap * 4);
+    }
     first.reserve(cap);
-    last_of.reserve(cap * 4);
     if (total > 0) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
     if (seg_mode && total > 0) {
       agg_segscan(total, kmax, cap);
