@@ -21,7 +21,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 python3 scripts/pmc_summary.py --trace gpurun_out/${R}_trace/k_kernel_trace.csv \
     --fetch gpurun_out/${R}_pmc_FETCH_SIZE/k_counter_collection.csv \
-    --write gpurun_out/${R}_pmc_WRITE_SIZE/k_counter_collection.csv --events $EV \
+    --write gpurun_out/${R}_pmc_WRITE_SIZE/k_counter_collection.csv --events $EV --pushes ${PUSHES:-8} \
     --out gpurun_out/${R}_pmc_${CFG}.json > /dev/null || exit 1
 cp gpurun_out/${R}_pmc_${CFG}.json profiles/
 timeout -k 10 600 python3 -u bench.py --config $CFG > gpurun_out/${R}_bench_${CFG}.json 2> gpurun_out/${R}_bench_${CFG}.err
