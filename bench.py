@@ -322,114 +322,135 @@ def main():
     else:
         qp = plan_query(qa, item, StringDictionary())
 
-    # P3 shards by partition key with no data-path collective (each rank owns a
-    # key slice and receives its events); --input roundrobin adds the RCCL
-    # all-to-all re-route of events that arrive at the wrong rank
-    mode = args.input if args.input != "auto" else "prepartitioned"
+    # Config 3: at N > 1 the headline is one global stream over
+    # 10 M keys held round-robin by the ranks and re-routed to the key owners
+    # with an RCCL all-to-all per micro-batch; the prepartitioned measurement
+    # (events arrive at their owner, keys_per_gpu each, no data-path
+    # collective) runs alongside.  N = 1 is prepartitioned (nothing to route).
+    mode = args.input if args.input != "auto" else ("roundrobin" if world > 1 else "prepartitioned")
     if mode == "roundrobin" and not pattern:
         mode = "prepartitioned"   # window configs are unpartitioned: replicas
-    # inputs resident in HBM before the timed region
-    if mode == "prepartitioned":
-        # rank r owns key slice r and its own events (no data-path collective)
-        kb = args.key_base if args.key_base >= 0 else rank * keys
-        sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=kb, dev=dev)
-        seqs = None
-    else:
-        # one global stream over world*keys keys, held round-robin; re-routed per micro-batch
-        sym, price, vol, ts, seqs = gen_roundrobin_columns(torch, n, keys * world, delta, rank, world, dev)
-    torch.cuda.synchronize()
-    from siddhi_amd import exchange as ex
-    he.context(local)
-    dq = he.DeviceQuery(qp.ir, device=local)
-    batch = min(args.batch, n)
-    cuts = list(range(0, n, batch)) + [n]
-    offs_all = wl.call_offsets(n)
 
-    routed_total = [0]
-
-    def run_step(collect=None, cuts=cuts):
-        dq.reset()
-        tot = {}
-        for a, b in zip(cuts[:-1], cuts[1:]):
-            if seqs is None:
-                # InputHandler calls of 1024 events inside the micro-batch
-                lo = np.searchsorted(offs_all, a)
-                hi = np.searchsorted(offs_all, b)
-                co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
-                cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
-                dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE,
-                            co.astype(np.int64), True)
-            else:
-                # RCCL all-to-all: every event to its key's owner, arrival order restored by seq
-                (rs, rp, rv, rt), rseq, _ = ex.route([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b],
-                                                     seqs[a:b], world)
-                m = rs.numel()
-                routed_total[0] += m
-                if m == 0:
-                    continue
-                co = ex.call_offsets_from_seq(rseq, 1024).numpy()   # (host copy: orders torch's stream)
-                torch.cuda.current_stream().synchronize()   # routed columns complete before the engine's stream reads them
-                dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
-                            he.SHD_MEM_DEVICE, co.astype(np.int64), True)
-            dq.discard()
-            if collect is not None:
-                for k, v in dq.stage_times().items():
-                    tot[k] = tot.get(k, 0) + v
-        if collect is not None:
-            collect.append(tot)
-        return dq.counters()
-
-    for sb in [int(x) for x in args.sweep_batches.split(",") if x]:
-        # micro-batch size sweep (diagnostic): same data, same query
-        sc = list(range(0, n, sb)) + [n]
-        run_step(cuts=sc)
-        torch.cuda.synchronize()
-        sr = []
-        t0 = time.perf_counter()
-        for _ in range(max(args.steps, 1)):
-            run_step(sr, cuts=sc)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / max(args.steps, 1)
-        st = {k: round(sum(r.get(k, 0) for r in sr) / len(sr) / 1e6, 3) for k in sr[0]} if sr else {}
-        if rank == 0:
-            print(json.dumps({"sweep_batch": sb, "ms_per_step": round(dt * 1e3, 3),
-                              "events_per_s": round(n * world / dt, 1), "stage_ms_per_step": st}),
-                  file=sys.stderr, flush=True)
-
-    # SURVEY.md §8d algorithmic bytes need the reference's pending-scan counts
-    # (P-bar: (partial, event) pairs its pending lists visit).  The sort path's
-    # walks count exactly those; the bucketed walk skips expiry visits beyond its
-    # `within` lookahead, so the counts come from one untimed step on the sort path.
-    calib = None
-    if pattern:
-        prev = os.environ.get("SHD_NO_BUCKET")
-        os.environ["SHD_NO_BUCKET"] = "1"
-        calib = run_step()
-        if prev is None:
-            del os.environ["SHD_NO_BUCKET"]
+    def measure(mode):
+        kb = None
+        # inputs resident in HBM before the timed region
+        if mode == "prepartitioned":
+            # rank r owns key slice r and its own events (no data-path collective)
+            kb = args.key_base if args.key_base >= 0 else rank * keys
+            sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=kb, dev=dev)
+            seqs = None
         else:
-            os.environ["SHD_NO_BUCKET"] = prev
-    for _ in range(args.warmup):
-        run_step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    stage_runs = []
-    t0 = time.perf_counter()
-    counters = None
-    for _ in range(args.steps):
-        counters = run_step(stage_runs)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed / args.steps * 1e3
-    total_events = n * world * args.steps
-    value = total_events / elapsed
+            # one global stream over `keys` keys in all, held round-robin; re-routed per micro-batch
+            sym, price, vol, ts, seqs = gen_roundrobin_columns(torch, n, keys, delta, rank, world, dev)
+        torch.cuda.synchronize()
+        from siddhi_amd import exchange as ex
+        he.context(local)
+        dq = he.DeviceQuery(qp.ir, device=local)
+        batch = min(args.batch, n)
+        cuts = list(range(0, n, batch)) + [n]
+        offs_all = wl.call_offsets(n)
+
+        routed_total = [0]
+
+        def run_step(collect=None, cuts=cuts):
+            dq.reset()
+            tot = {}
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                if seqs is None:
+                    # InputHandler calls of 1024 events inside the micro-batch
+                    lo = np.searchsorted(offs_all, a)
+                    hi = np.searchsorted(offs_all, b)
+                    co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
+                    cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
+                    dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE,
+                                co.astype(np.int64), True)
+                else:
+                    # RCCL all-to-all: every event to its key's owner, arrival order restored by seq
+                    (rs, rp, rv, rt), rseq, _ = ex.route([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b],
+                                                         seqs[a:b], world)
+                    m = rs.numel()
+                    routed_total[0] += m
+                    if m == 0:
+                        continue
+                    co = ex.call_offsets_from_seq(rseq, 1024).numpy()   # (host copy: orders torch's stream)
+                    torch.cuda.current_stream().synchronize()   # routed columns complete before the engine's stream reads them
+                    dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
+                                he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+                dq.discard()
+                if collect is not None:
+                    for k, v in dq.stage_times().items():
+                        tot[k] = tot.get(k, 0) + v
+            if collect is not None:
+                collect.append(tot)
+            return dq.counters()
+
+        for sb in [int(x) for x in args.sweep_batches.split(",") if x]:
+            # micro-batch size sweep (diagnostic): same data, same query
+            sc = list(range(0, n, sb)) + [n]
+            run_step(cuts=sc)
+            torch.cuda.synchronize()
+            sr = []
+            t0 = time.perf_counter()
+            for _ in range(max(args.steps, 1)):
+                run_step(sr, cuts=sc)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / max(args.steps, 1)
+            st = {k: round(sum(r.get(k, 0) for r in sr) / len(sr) / 1e6, 3) for k in sr[0]} if sr else {}
+            if rank == 0:
+                print(json.dumps({"sweep_batch": sb, "ms_per_step": round(dt * 1e3, 3),
+                                  "events_per_s": round(n * world / dt, 1), "stage_ms_per_step": st}),
+                      file=sys.stderr, flush=True)
+
+        # SURVEY.md §8d algorithmic bytes need the reference's pending-scan counts
+        # (P-bar: (partial, event) pairs its pending lists visit).  The sort path's
+        # walks count exactly those; the bucketed walk skips expiry visits beyond its
+        # `within` lookahead, so the counts come from one untimed step on the sort path.
+        calib = None
+        if pattern:
+            prev = os.environ.get("SHD_NO_BUCKET")
+            os.environ["SHD_NO_BUCKET"] = "1"
+            calib = run_step()
+            if prev is None:
+                del os.environ["SHD_NO_BUCKET"]
+            else:
+                os.environ["SHD_NO_BUCKET"] = prev
+        for _ in range(args.warmup):
+            run_step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        stage_runs = []
+        t0 = time.perf_counter()
+        counters = None
+        for _ in range(args.steps):
+            counters = run_step(stage_runs)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        ms_per_step = elapsed / args.steps * 1e3
+        total_events = n * world * args.steps
+        value = total_events / elapsed
+        return dict(sym=sym, price=price, vol=vol, ts=ts, seqs=seqs, kb=kb, dq=dq, calib=calib, counters=counters,
+                    stage_runs=stage_runs, elapsed=elapsed, ms_per_step=ms_per_step, value=value, batch=batch,
+                    offs_all=offs_all, total_events=total_events)
+
+    M = measure(mode)
+    sym, price, vol, ts, seqs, kb, dq, calib = (M[k] for k in ("sym", "price", "vol", "ts", "seqs", "kb", "dq", "calib"))
+    counters, stage_runs, elapsed, ms_per_step, value = (M[k] for k in ("counters", "stage_runs", "elapsed",
+                                                                        "ms_per_step", "value"))
+    batch, offs_all, total_events = M["batch"], M["offs_all"], M["total_events"]
+    alongside = None
+    if world > 1 and mode == "roundrobin" and args.input == "auto":
+        A = measure("prepartitioned")
+        A["dq"].close()
+        alongside = {"input": "prepartitioned", "keys_per_gpu": keys, "value": round(A["value"], 1),
+                     "ms_per_step": round(A["ms_per_step"], 3), "matches": A["counters"]["matches"] * world}
+        del A
 
     # per-stage device times (HIP events on the query's stream), averaged per step
     stages = {}
@@ -489,7 +510,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
-            "config": {"workload": args.config, "events_per_gpu": n, "keys_per_gpu": keys, "delta_ms": delta,
+            "config": {"workload": args.config, "events_per_gpu": n,
+                       ("keys_total" if mode == "roundrobin" else "keys_per_gpu"): keys, "delta_ms": delta,
                        "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world,
                        "input": mode + (" (RCCL all-to-all re-route)" if mode == "roundrobin" else "")},
             "matches_per_s": round(matches_per_s, 1),
@@ -500,6 +522,8 @@ def main():
             "cpu_baseline": cpu,
             "parity_prefix": prefix,
         }
+        if alongside:
+            line["alongside"] = alongside
         print(json.dumps(line))
     dq.close()
     if dist:

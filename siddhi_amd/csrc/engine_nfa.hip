@@ -2878,10 +2878,10 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.sew = (Y.SC + 1 + 63) / 64;
   Y.evw = (Y.EC + 1 + 63) / 64;
   Y.recw = (Y.RC + 1 + 63) / 64;
-  // window lanes diverge (each walks its own chunk): one lane's state contiguous
-  // so its accesses share cache lines; per-key lanes of a partitioned plan
-  // interleave 64 keys per block
-  Y.W = e->windowed ? 1 : kLaneBlock;
+  // 64 key states interleaved per block; SHD_NFA_INTERLEAVE=0 keeps one key
+  // state contiguous (measured slower on window lanes too: S4-seq 158 vs 182 M
+  // events/s, S4P-seqplus 190 vs 199 M)
+  Y.W = kLaneBlock;
   if (const char* w = getenv("SHD_NFA_INTERLEAVE")) Y.W = w[0] == '0' ? 1 : kLaneBlock;
   const int64_t falign = Y.W == 1 ? 16 : 256;
   int64_t off = 0;
