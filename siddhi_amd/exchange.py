@@ -79,11 +79,12 @@ def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world:
     """
     dtypes = [c.dtype for c in cols]
     if world == 1:
-        order = torch.argsort(seq, stable=True)
+        order = _seq_order(seq)
         return [c[order] for c in cols], seq[order], {"sent": 0, "received": 0}
     owner = owner_of(key, world)
-    order = torch.argsort(owner, stable=True)
-    send = pack(list(cols) + [seq])[order]
+    # stable bucket order by owner: one 8-bit radix pass (world <= 256)
+    _, order = torch.sort(owner.to(torch.uint8), stable=True)
+    send = pack([c[order] for c in cols] + [seq[order]])
     counts = torch.bincount(owner, minlength=world).to(torch.int64)
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
@@ -93,14 +94,27 @@ def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world:
     recv = torch.empty(int(sum(out_splits)), dtype=torch.int64, device=send.device)
     dist.all_to_all_single(recv, send.reshape(-1), out_splits, in_splits, group=group)
     recv = recv.view(-1, k)
-    rseq = recv[:, k - 1].contiguous()
-    o = torch.argsort(rseq, stable=True)
-    recv = recv[o]
-    out = unpack(recv[:, :k - 1], dtypes)
+    # every sender's rows arrive in seq order; restore the global order
+    o = _seq_order(recv[:, k - 1])
+    out = [c[o] for c in unpack(recv[:, :k - 1], dtypes)]
+    rseq = recv[:, k - 1][o]
     rank = dist.get_rank(group)
     stats = {"sent": int(counts.sum().item() - counts[rank].item()),
              "received": int(recv_counts.sum().item() - recv_counts[rank].item())}
-    return out, recv[:, k - 1].contiguous(), stats
+    return out, rseq, stats
+
+
+def _seq_order(seq: torch.Tensor) -> torch.Tensor:
+    """Stable ascending order of sequence numbers; sorted on 32-bit offsets from
+    the minimum when the micro-batch's span fits (half the radix passes)."""
+    if seq.numel() == 0:
+        return torch.zeros(0, dtype=torch.int64, device=seq.device)
+    lo = seq.min()
+    if int(seq.max() - lo) < 2 ** 31:
+        _, o = torch.sort((seq - lo).to(torch.int32), stable=True)
+    else:
+        _, o = torch.sort(seq, stable=True)
+    return o
 
 
 def merge_outputs(parts):
