@@ -69,14 +69,27 @@ def unpack(m: torch.Tensor, dtypes: List[torch.dtype]) -> List[torch.Tensor]:
 
 
 def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int,
-          group: Optional[dist.ProcessGroup] = None) -> Tuple[List[torch.Tensor], torch.Tensor, Dict[str, int]]:
+          group: Optional[dist.ProcessGroup] = None, nulls: Optional[List[Optional[torch.Tensor]]] = None):
     """All-to-all re-route of one micro-batch by key owner.
 
-    cols: the event columns (1-D, equal length, any of int32/int64/float64);
-    key:  the partition key of every event (integer ids);
-    seq:  global arrival sequence numbers (int64).
-    Returns (received columns, received seq, stats), in increasing seq order.
+    cols:  the event columns (1-D, equal length, any of int32/int64/float64);
+    key:   the partition key of every event (integer ids);
+    seq:   global arrival sequence numbers (int64);
+    nulls: optional per-column null masks (bool/uint8, None = no nulls); they
+           travel as one extra packed bit-mask column.
+    Returns (received columns, received seq, stats), in increasing seq order,
+    plus the received null masks (uint8, one per column) when `nulls` is given.
     """
+    if nulls is not None:
+        if len(nulls) != len(cols) or len(cols) > 62:
+            raise ValueError("one null mask (or None) per column, at most 62 columns")
+        bits = torch.zeros(seq.numel(), dtype=torch.int64, device=seq.device)
+        for j, m in enumerate(nulls):
+            if m is not None:
+                bits |= m.to(torch.int64) << j
+        rc, rseq, stats = route(list(cols) + [bits], key, seq, world, group)
+        rb = rc.pop()
+        return rc, rseq, stats, [((rb >> j) & 1).to(torch.uint8) for j in range(len(cols))]
     dtypes = [c.dtype for c in cols]
     if world == 1:
         order = _seq_order(seq)

@@ -35,9 +35,13 @@ def _rank_main(rank, world, path, outdir):
     for a, b in ((0, half), (half, len(idx))):
         rc, rseq, stats = ex.route([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world)
         parts.append((rc, rseq))
+    # null masks travel with their events (price null on every 7th, volume on every 5th global event)
+    nul = [None, torch.from_numpy(idx % 7 == 0), torch.from_numpy(idx % 5 == 0), None]
+    _, nseq, _, rn = ex.route(cols, cols[0], seq, world, nulls=nul)
     np.savez(os.path.join(outdir, "r%d.npz" % rank),
              **{"c%d_%d" % (i, j): parts[i][0][j].numpy() for i in range(2) for j in range(4)},
-             seq0=parts[0][1].numpy(), seq1=parts[1][1].numpy())
+             seq0=parts[0][1].numpy(), seq1=parts[1][1].numpy(), nseq=nseq.numpy(),
+             **{"n%d" % j: rn[j].numpy() for j in range(4)})
     dist.destroy_process_group()
 
 
@@ -62,6 +66,15 @@ def test_route_delivers_own_keys_in_arrival_order(routed):
         price = np.concatenate([z["c0_1"], z["c1_1"]])
         ts = np.concatenate([z["c0_3"], z["c1_3"]])
         assert np.array_equal(sym, s[seq]) and np.array_equal(price, p[seq]) and np.array_equal(ts, t[seq])
+
+
+def test_route_carries_null_masks(routed):
+    for r, z in enumerate(routed):
+        seq = z["nseq"]
+        assert np.all(np.diff(seq) > 0)
+        assert not z["n0"].any() and not z["n3"].any()
+        assert np.array_equal(z["n1"].astype(bool), seq % 7 == 0)
+        assert np.array_equal(z["n2"].astype(bool), seq % 5 == 0)
 
 
 def test_call_offsets_follow_global_calls():
