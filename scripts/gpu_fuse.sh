@@ -1,0 +1,13 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for v in off 4 8 16; do
+  unset SHD_SORT_FUSED SHD_FUSE_ROUNDS
+  [ $v != off ] && export SHD_SORT_FUSED=1 SHD_FUSE_ROUNDS=$v
+  timeout -k 10 200 python -u bench.py --config P3 --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/fuse_$v.json 2>/dev/null || exit 1
+  echo "$v $(python3 -c "import json; d=json.load(open('gpurun_out/fuse_$v.json')); print(round(d['value']/1e9,2), 'G ev/s', d['stage_ms_per_step'], d['counters']['matches'])")"
+done
+SHD_SORT_FUSED=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py > gpurun_out/pytest_fuse.log 2>&1
+echo "pytest fused rc=$?"; tail -2 gpurun_out/pytest_fuse.log

@@ -346,7 +346,7 @@ __device__ __forceinline__ uint32_t bkt_key32(const PrepArgs& a, int64_t r) {
   return gld((const uint32_t*)x.batch.col[a.key_col], br);
 }
 
-template <bool H>
+template <bool H, int R = kBktRounds>
 __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restrict__ ap, int64_t n_ext,
                                                        uint32_t* __restrict__ hist, int nb) {
   const PrepArgs& a = *ap;
@@ -354,16 +354,16 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restric
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
   const int tile = rs_tile_of(blockIdx.x, nb);
-  const int64_t wb = (int64_t)tile * rs_tile(kBktRounds) + (int64_t)w * 64 * kBktRounds;
-  uint32_t k[kBktRounds];
+  const int64_t wb = (int64_t)tile * rs_tile(R) + (int64_t)w * 64 * R;
+  uint32_t k[R];
 #pragma unroll
-  for (int r = 0; r < kBktRounds; r++) {
+  for (int r = 0; r < R; r++) {
     const int64_t idx = wb + r * 64 + lane;
     k[r] = bkt_key32(a, idx < n_ext ? idx : n_ext - 1);
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kBktRounds; r++)
+  for (int r = 0; r < R; r++)
     if (wb + r * 64 + lane < n_ext) atomicAdd(&h[w][rs_hdigit<H>(k[r], 0, 0u)], 1u);
   __syncthreads();
   if (tid < 256) {
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restric
   }
 }
 
-template <bool FAST, bool H>
+template <bool FAST, bool H, int R = kBktRounds>
 __global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __restrict__ ap, int64_t n_ext,
                                                           const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ offs,
@@ -385,16 +385,16 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __rest
   const DExprSet es = a.es;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = rs_tile_of(blockIdx.x, nb);
-  const int64_t t0 = (int64_t)tile * rs_tile(kBktRounds);
-  const int64_t wb = t0 + (int64_t)w * 64 * kBktRounds;
+  const int64_t t0 = (int64_t)tile * rs_tile(R);
+  const int64_t wb = t0 + (int64_t)w * 64 * R;
   const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
   const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
   const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
   const int64_t tbase = a.x.batch.ts[0];
   PrepAcc acc;
-  uint32_t k[kBktRounds], v[kBktRounds], x[kBktRounds];
+  uint32_t k[R], v[R], x[R];
 #pragma unroll
-  for (int r = 0; r < kBktRounds; r++) {
+  for (int r = 0; r < R; r++) {
     const int64_t idx = wb + r * 64 + lane;
     const bool ok = idx < n_ext;
     const int64_t li = ok ? idx : n_ext - 1;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __rest
     v[r] = (f << kRowBits) | (uint32_t)li;
     x[r] = (uint32_t)t32;
   }
-  rs_scatter_tile<uint32_t, kBktRounds, true, H>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
+  rs_scatter_tile<uint32_t, R, true, H>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
   prep_block_reduce<kRsBlock>(acc, blk, tile);
 }
 
@@ -2226,7 +2226,9 @@ struct PatternEngine : Engine {
     const bool fused1 = partitioned && !key64 && pa.key_col >= 0 && getenv("SHD_SORT_FUSED") &&
                         !getenv("SHD_HASH_BITS");
     if (fused1) {
-      const int nbt = (int)ceil_div(n_ext, rs_tile(kBktRounds));
+      const int fr = getenv("SHD_FUSE_ROUNDS") ? atoi(getenv("SHD_FUSE_ROUNDS")) : 8;
+      const int R1 = fr == 4 ? 4 : (fr == 16 ? 16 : 8);
+      const int nbt = (int)ceil_div(n_ext, rs_tile(R1));
       if ((size_t)nbt * std::max(sizeof(PrepAgg), sizeof(ScanOut)) > d_blk.cap)
         d_blk.reserve((size_t)std::max<int64_t>(3 * nblk, nbt) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
       d_k32_alt.reserve(n_ext * 4);
@@ -2236,20 +2238,27 @@ struct PatternEngine : Engine {
       uint32_t* hist = d_sort.as<uint32_t>();
       uint32_t* offs = hist + (int64_t)nbt * 256;
       uint32_t* tot = offs + (int64_t)nbt * 256;
-      hipLaunchKernelGGL(k_bkt_hist<false>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
-      SHD_CHECK_LAUNCH();
-      radix_digit_scan(hist, nbt, offs, tot, s);
-      if (fast1)
-        hipLaunchKernelGGL((k_bkt_scatter<true, false>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
-                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
-                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                           d_blk.as<PrepAgg>());
-      else
-        hipLaunchKernelGGL((k_bkt_scatter<false, false>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
-                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
-                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                           d_blk.as<PrepAgg>());
-      SHD_CHECK_LAUNCH();
+#define SHD_FUSED1(RR)                                                                                              \
+  do {                                                                                                              \
+    hipLaunchKernelGGL((k_bkt_hist<false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);      \
+    SHD_CHECK_LAUNCH();                                                                                             \
+    radix_digit_scan(hist, nbt, offs, tot, s);                                                                      \
+    if (fast1)                                                                                                      \
+      hipLaunchKernelGGL((k_bkt_scatter<true, false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,       \
+                         (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,                    \
+                         d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),                 \
+                         d_blk.as<PrepAgg>());                                                                      \
+    else                                                                                                            \
+      hipLaunchKernelGGL((k_bkt_scatter<false, false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,      \
+                         (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,                    \
+                         d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),                 \
+                         d_blk.as<PrepAgg>());                                                                      \
+    SHD_CHECK_LAUNCH();                                                                                             \
+  } while (0)
+      if (R1 == 4) SHD_FUSED1(4);
+      else if (R1 == 16) SHD_FUSED1(16);
+      else SHD_FUSED1(8);
+#undef SHD_FUSED1
       hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
       SHD_CHECK_LAUNCH();
     } else {
