@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=50_000_000, help="micro-batch size (events)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads of the per-key parallel CPU baseline (partitioned configs; 0=skip)")
     ap.add_argument("--key-base", type=int, default=-1,
                     help="first key id of this rank's slice (default rank * keys; diagnostics)")
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
@@ -150,6 +152,56 @@ def cpu_baseline(cfg_name, app, keys, delta, sample):
              "sample": "first %d events of the %s stream (%d keys, delta %g ms), C++ restatement of the "
                        "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)},
             concat_rows(parts), qp)
+
+
+def cpu_baseline_parallel(cfg_name, app, keys, delta, sample, threads):
+    """SURVEY.md §8d's per-key CPU variant: the oracle on `threads` host threads,
+    thread t owning the partition keys with key % threads == t (a partitioned
+    query's keys are independent: PartitionStreamReceiver), each fed its keys'
+    events of every InputHandler call in arrival order.  ctypes releases the GIL
+    inside orc_push, so the threads run in parallel."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_engine import OracleQueryEngine
+    from parity import compile_single_query
+    from siddhi_amd import workloads as wl
+    qp, _ = compile_single_query(app)
+    s, p, v, t = wl.stock_stream(sample, keys, delta, seed_offset=0)
+    offs = wl.call_offsets(sample)
+    shard = s.astype(np.int64) % threads
+    work = []
+    for w in range(threads):
+        idx = np.nonzero(shard == w)[0]
+        vals = np.ascontiguousarray(np.stack([s[idx].astype(np.uint64), p[idx].view(np.uint64),
+                                              v[idx].view(np.uint64)], axis=1))
+        nul = np.zeros_like(vals, dtype=np.uint8)
+        tt = np.ascontiguousarray(t[idx])
+        cuts = np.searchsorted(idx, offs)   # this shard's slice of every call
+        work.append((vals, nul, tt, cuts))
+    engines = [OracleQueryEngine(qp, None) for _ in range(threads)]
+
+    def run(w):
+        vals, nul, tt, cuts = work[w]
+        eng = engines[w]
+        lib = eng.lib
+        for c in range(len(cuts) - 1):
+            a, b = int(cuts[c]), int(cuts[c + 1])
+            if b > a:
+                lib.orc_push(eng.h, 0, b - a, tt[a:].ctypes.data, vals[a:].ctypes.data, nul[a:].ctypes.data, 1)
+                lib.orc_clear_rows(eng.h)
+
+    ths = [threading.Thread(target=run, args=(w,)) for w in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    for e in engines:
+        e.close()
+    return {"value": sample / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": "first %d events of the %s stream, keys sharded over %d host threads (key %% %d), one oracle "
+                      "engine per thread (oracle/oracle.cpp)" % (sample, cfg_name, threads, threads)}
 
 
 def parity_prefix(torch, he, qp, cols, ts, offs_all, prefix, ora_rows):
@@ -489,12 +541,15 @@ def main():
     matches_per_s = counters["matches"] * world * args.steps / elapsed
 
     cpu = None
+    cpu_mt = None
     prefix = None
     if rank == 0 and world == 1 and args.cpu_sample != 0:
         sample = args.cpu_sample if args.cpu_sample > 0 else (2_000_000 if pattern else 1_000_000)
         cpu, ora_rows, _ = cpu_baseline(args.config, app, keys, delta, min(sample, n))
         if pattern and mode == "prepartitioned" and kb == 0:
             prefix = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, min(sample, n), ora_rows)
+        if pattern and isinstance(item, qc.Partition) and args.cpu_threads > 0:
+            cpu_mt = cpu_baseline_parallel(args.config, app, keys, delta, min(4 * sample, n), args.cpu_threads)
 
     if rank == 0:
         line = {
@@ -520,6 +575,7 @@ def main():
             "stage_ms_per_step": {k: round(v / 1e6, 3) for k, v in stages.items()},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "cpu_baseline_parallel": cpu_mt,
             "parity_prefix": prefix,
         }
         if alongside:
