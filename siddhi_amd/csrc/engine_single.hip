@@ -1110,6 +1110,102 @@ __global__ __launch_bounds__(kBlock) void k_seg_apply(int64_t total, const uint3
   }
 }
 
+// LDS-staged variants of phases 1 and 3 (NC <= 2): the tile's keys, operand
+// bits and values are loaded coalesced into LDS, every thread folds its
+// kSegPer consecutive positions from there, and phase 3 stages S / NN in LDS
+// for coalesced stores -- the per-thread strided global accesses of the plain
+// kernels touch kSegPer times more cache lines per wave instruction.
+template <int NC>
+struct SegTileLds {
+  uint32_t k[kSegTile + 1];   // k[0]: the key before the tile
+  uint8_t m[kSegTile];
+  double v[NC][kSegTile];     // operands, then S.hi
+  double lo[NC][kSegTile];    // S.lo (phase 3)
+  int32_t nn[NC][kSegTile];   // NN (phase 3)
+};
+
+template <int NC>
+__device__ __forceinline__ int seg_stage_tile(SegTileLds<NC>& L, int64_t t0, int64_t total, const uint32_t* sk,
+                                              const double* sval, const uint8_t* snn) {
+  const int nt = (int)(total - t0 < kSegTile ? total - t0 : kSegTile);
+  for (int i = threadIdx.x; i < nt; i += kBlock) {
+    L.k[i + 1] = sk[t0 + i];
+    L.m[i] = snn[t0 + i];
+#pragma unroll
+    for (int c = 0; c < NC; c++) L.v[c][i] = sval[c * total + t0 + i];
+  }
+  if (threadIdx.x == 0) L.k[0] = t0 > 0 ? sk[t0 - 1] : 0xFFFFFFFFu;
+  __syncthreads();
+  return nt;
+}
+
+template <int NC>
+__device__ __forceinline__ SegAcc<NC> seg_lds_range(const SegTileLds<NC>& L, int64_t t0, int nt) {
+  SegAcc<NC> acc = seg_identity<NC>();
+  const int i0 = threadIdx.x * kSegPer;
+#pragma unroll
+  for (int i = 0; i < kSegPer; i++) {
+    const int li = i0 + i;
+    if (li >= nt) break;
+    const uint32_t k = L.k[li + 1];
+    if (t0 + li == 0 || k != L.k[li]) acc = seg_identity<NC>(), acc.flag = 1;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      acc.s[c] = dd_add(acc.s[c], DD{L.v[c][li], 0.0});
+      acc.nn[c] += (L.m[li] >> c) & 1;
+    }
+  }
+  return acc;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_tiles_lds(int64_t total, const uint32_t* sk, const double* sval,
+                                                          const uint8_t* snn, SegAcc<NC>* tagg) {
+  __shared__ SegAcc<NC> wagg[kBlock / 64];
+  __shared__ SegTileLds<NC> L;
+  const int64_t t0 = (int64_t)blockIdx.x * kSegTile;
+  const int nt = seg_stage_tile<NC>(L, t0, total, sk, sval, snn);
+  const SegAcc<NC> mine = seg_lds_range<NC>(L, t0, nt);
+  SegAcc<NC> tot;
+  seg_block_exclusive<NC>(mine, seg_identity<NC>(), wagg, &tot);
+  if (threadIdx.x == 0) tagg[blockIdx.x] = tot;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_apply_lds(int64_t total, const uint32_t* sk, const double* sval,
+                                                          const uint8_t* snn, const SegAcc<NC>* tcarry, DD* S,
+                                                          int32_t* NN) {
+  __shared__ SegAcc<NC> wagg[kBlock / 64];
+  __shared__ SegTileLds<NC> L;
+  const int64_t t0 = (int64_t)blockIdx.x * kSegTile;
+  const int nt = seg_stage_tile<NC>(L, t0, total, sk, sval, snn);
+  const SegAcc<NC> mine = seg_lds_range<NC>(L, t0, nt);
+  SegAcc<NC> run = seg_block_exclusive<NC>(mine, tcarry[blockIdx.x], wagg, nullptr);
+  const int i0 = threadIdx.x * kSegPer;
+#pragma unroll
+  for (int i = 0; i < kSegPer; i++) {
+    const int li = i0 + i;
+    if (li >= nt) break;
+    if (t0 + li == 0 || L.k[li + 1] != L.k[li]) run = seg_identity<NC>(), run.flag = 1;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      run.s[c] = dd_add(run.s[c], DD{L.v[c][li], 0.0});
+      run.nn[c] += (L.m[li] >> c) & 1;
+      L.v[c][li] = run.s[c].hi;   // each position is read before it is overwritten, by its own thread
+      L.lo[c][li] = run.s[c].lo;
+      L.nn[c][li] = run.nn[c];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nt; i += kBlock) {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      S[c * total + t0 + i] = DD{L.v[c][i], L.lo[c][i]};
+      NN[c * total + t0 + i] = L.nn[c][i];
+    }
+  }
+}
+
 // smallest q in [0, p] with pred(q), where pred holds on a suffix ending at p
 template <class Pred>
 __device__ __forceinline__ int64_t gallop_first(int64_t p, Pred pred) {
@@ -1662,14 +1758,25 @@ struct SingleEngine : Engine {
     tagg.reserve(nt * sizeof(SegAcc<NC>));
     segS.reserve((size_t)NC * total * sizeof(DD));
     segNN.reserve((size_t)NC * total * 4);
-    hipLaunchKernelGGL(k_seg_tiles<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
-                       (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(), tagg.as<SegAcc<NC>>());
+    const bool lds = NC <= 2 && !getenv("SHD_SEG_NOLDS");
+    if (lds)
+      hipLaunchKernelGGL(k_seg_tiles_lds<(NC <= 2 ? NC : 1)>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                         (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(),
+                         (SegAcc<(NC <= 2 ? NC : 1)>*)tagg.as<char>());
+    else
+      hipLaunchKernelGGL(k_seg_tiles<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                         (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(), tagg.as<SegAcc<NC>>());
     SHD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_seg_tilescan<NC>, dim3(1), dim3(kBlock), 0, s, tagg.as<SegAcc<NC>>(), nt);
     SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_seg_apply<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
-                       (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(),
-                       (const SegAcc<NC>*)tagg.as<SegAcc<NC>>(), segS.as<DD>(), segNN.as<int32_t>());
+    if (lds)
+      hipLaunchKernelGGL(k_seg_apply_lds<(NC <= 2 ? NC : 1)>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                         (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(),
+                         (const SegAcc<(NC <= 2 ? NC : 1)>*)tagg.as<char>(), segS.as<DD>(), segNN.as<int32_t>());
+    else
+      hipLaunchKernelGGL(k_seg_apply<NC>, dim3((unsigned)nt), dim3(kBlock), 0, s, total, sk,
+                         (const double*)sval.as<double>(), (const uint8_t*)snn.as<uint8_t>(),
+                         (const SegAcc<NC>*)tagg.as<SegAcc<NC>>(), segS.as<DD>(), segNN.as<int32_t>());
     SHD_CHECK_LAUNCH();
     mark("seg_scan");
     rec.reserve((size_t)cap * run_rec_words(nagg) * 8);
