@@ -1007,6 +1007,64 @@ __global__ __launch_bounds__(kBlock) void k_seg_gather(const SegArgs* __restrict
   }
 }
 
+// Packed item records (NC <= 2): everything the sorted copies need of item x
+// in one 8*NC + 8 byte record written in item order (coalesced), so the
+// gather by sorted position reads one record per item instead of 2 + 2*NC
+// scattered words.  w = (call + 1) | nn << 30 (calls of a push < 2^30).
+template <int NC>
+struct SegItem {
+  double v[NC];
+  uint32_t e;
+  uint32_t w;
+};
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_pack(const SegArgs* __restrict__ ap, const uint64_t* iargv,
+                                                     const uint8_t* iargn, const uint32_t* e, const int32_t* icall,
+                                                     SegItem<NC>* items) {
+  const SegArgs& a = *ap;
+  const int64_t total = a.total;
+  for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total; x = total) {
+    SegItem<NC> it;
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const int g = a.ch_agg[c];
+      const uint64_t b = iargv[g * a.cap + x];
+      const bool nul = iargn[g * a.cap + x] != 0;
+      double v;
+      switch (a.ch_type[c]) {   // Number.doubleValue() of the operand
+        case SHD_T_INT: v = (double)v_i32(b); break;
+        case SHD_T_LONG: v = (double)(int64_t)b; break;
+        case SHD_T_FLOAT: v = (double)v_f32(b); break;
+        default: v = v_f64(b);
+      }
+      it.v[c] = nul ? 0.0 : v;
+      m |= nul ? 0u : (1u << c);
+    }
+    const int32_t call = x >= a.C ? icall[x] : -1;
+    it.e = e[x];
+    it.w = ((uint32_t)(call + 1) & 0x3FFFFFFFu) | (m << 30);
+    items[x] = it;
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(kBlock) void k_seg_gather_packed(const SegArgs* __restrict__ ap, const uint32_t* sp,
+                                                              const SegItem<NC>* items, double* sval, uint8_t* snn,
+                                                              uint32_t* se, int32_t* scall) {
+  const SegArgs& a = *ap;
+  const int64_t total = a.total;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total; p = total) {
+    const SegItem<NC> it = items[sp[p]];
+#pragma unroll
+    for (int c = 0; c < NC; c++) sval[c * total + p] = it.v[c];
+    snn[p] = (uint8_t)(it.w >> 30);
+    se[p] = it.e;
+    scall[p] = (int32_t)(it.w & 0x3FFFFFFFu) - 1;
+  }
+}
+
 // this thread's kSegPer consecutive positions as one segmented range
 template <int NC>
 __device__ __forceinline__ SegAcc<NC> seg_thread_range(int64_t p0, int64_t total, const uint32_t* sk,
@@ -1411,7 +1469,7 @@ struct SingleEngine : Engine {
   int nch = 0;                       // distinct aggregated expressions (channels)
   int ch_agg[kMaxChan] = {}, ch_type[kMaxChan] = {};
   int chan_of[kMaxAggs] = {};
-  DevBuf sval, snn, se, scall, tagg, segS, segNN, rec;
+  DevBuf sval, snn, se, scall, tagg, segS, segNN, rec, seg_items;
   // group state (dense by key)
   DevBuf g_dsum, g_lsum, g_cnt;
   int64_t g_nkeys = 0;
@@ -1748,10 +1806,24 @@ struct SingleEngine : Engine {
     snn.reserve(total);
     se.reserve(total * 4);
     scall.reserve(total * 4);
-    hipLaunchKernelGGL(k_seg_gather<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sp,
-                       (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(),
-                       (const uint32_t*)e_exp.as<uint32_t>(), (const int32_t*)icall.as<int32_t>(), sval.as<double>(),
-                       snn.as<uint8_t>(), se.as<uint32_t>(), scall.as<int32_t>());
+    if (NC <= 2 && !getenv("SHD_SEG_UNPACKED")) {
+      constexpr int N2 = NC <= 2 ? NC : 1;
+      // packed in item order (coalesced), then one record read per sorted position
+      seg_items.reserve((size_t)total * sizeof(SegItem<N2>));
+      hipLaunchKernelGGL(k_seg_pack<N2>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa,
+                         (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(),
+                         (const uint32_t*)e_exp.as<uint32_t>(), (const int32_t*)icall.as<int32_t>(),
+                         (SegItem<N2>*)seg_items.as<char>());
+      SHD_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_seg_gather_packed<N2>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sp,
+                         (const SegItem<N2>*)seg_items.as<char>(), sval.as<double>(), snn.as<uint8_t>(),
+                         se.as<uint32_t>(), scall.as<int32_t>());
+    } else {
+      hipLaunchKernelGGL(k_seg_gather<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sp,
+                         (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(),
+                         (const uint32_t*)e_exp.as<uint32_t>(), (const int32_t*)icall.as<int32_t>(), sval.as<double>(),
+                         snn.as<uint8_t>(), se.as<uint32_t>(), scall.as<int32_t>());
+    }
     SHD_CHECK_LAUNCH();
     mark("seg_gather");
     const int64_t nt = ceil_div(total, kSegTile);
