@@ -1296,7 +1296,7 @@ __host__ __device__ constexpr int64_t run_rec_words(int nagg) { return 1 + nagg;
 template <int NC>
 __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__ ap, const uint32_t* sk,
                                                      const uint32_t* sp, const uint32_t* se, const int32_t* scall,
-                                                     const DD* S, const int32_t* NN, const uint8_t* iargn,
+                                                     const DD* S, const int32_t* NN, const uint8_t* snn,
                                                      uint64_t* rec, uint8_t* first) {
   const SegArgs& a = *ap;
   const int64_t total = a.total;
@@ -1346,8 +1346,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__
         int32_t nnw = 0;
         const double v = chan_val(c, kin, nnw);
         if (a.kind[j] == SHD_AGG_SUM) {
-          // a null operand leaves the sum (null once nothing is left; float sums: null)
-          const bool xn = iargn[j * a.cap + x] != 0;
+          // a null operand leaves the sum (null once nothing is left; float sums: null);
+          // the operand's null bit travels with the sorted position (channel c)
+          const bool xn = ((snn[p] >> c) & 1u) == 0;
           on = xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0);
           ob = on ? 0ull : p_f64(v);
         } else {
@@ -1855,7 +1856,7 @@ struct SingleEngine : Engine {
     hipLaunchKernelGGL(k_seg_emit<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, d_sa, sk, sp,
                        (const uint32_t*)se.as<uint32_t>(), (const int32_t*)scall.as<int32_t>(),
                        (const DD*)segS.as<DD>(), (const int32_t*)segNN.as<int32_t>(),
-                       (const uint8_t*)iargn[cur].as<uint8_t>(), rec.as<uint64_t>(), first.as<uint8_t>());
+                       (const uint8_t*)snn.as<uint8_t>(), rec.as<uint64_t>(), first.as<uint8_t>());
     SHD_CHECK_LAUNCH();
     mark("seg_window");
   }
