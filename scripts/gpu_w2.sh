@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-w2}
 timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-    tests/test_gpu_segscan.py tests/test_gpu_parity.py -k "window or segscan or W2 or agg or group" > gpurun_out/pytest_$TAG.log 2>&1
+    tests/test_gpu_segscan.py tests/test_gpu_kat.py tests/test_multi_query.py tests/test_gpu_parity.py -k "window or segscan or W2 or agg or group or kat or multi" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 for c in W2-length W2-time; do

@@ -1376,6 +1376,10 @@ struct EmitArgs {
   ColSet cs;
   DExprSet es;
   DExpr outs[kMaxCols];
+  // single-instruction outputs decoded on the host: 1 = attribute load (arg =
+  // attribute), 2 = aggregator (arg = index), 0 = the interpreter
+  int32_t okind[kMaxCols];
+  int32_t oarg[kMaxCols];
   int nout;
   int nagg;
   int kind[kMaxAggs];
@@ -1424,7 +1428,15 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
     RowCtx cx{&cs, ev, av, an};
     int64_t row = a.row0 + foff[t0];
     for (int c = 0; c < a.nout; c++) {
-      Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
+      Val v;
+      if (a.okind[c] == 1) {
+        v = col_load(cs, ev, a.oarg[c]);
+      } else if (a.okind[c] == 2) {
+        v.b = av[a.oarg[c]];
+        v.null = an[a.oarg[c]];
+      } else {
+        v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
+      }
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
@@ -1769,7 +1781,19 @@ struct SingleEngine : Engine {
     ea.cs = b.cs;
     ea.es = dset();
     ea.nout = (int)outs.size();
-    for (size_t c = 0; c < outs.size(); c++) ea.outs[c] = dexpr(outs[c]);
+    for (size_t c = 0; c < outs.size(); c++) {
+      ea.outs[c] = dexpr(outs[c]);
+      const auto& code = plan.exprs[outs[c]];
+      ea.okind[c] = 0;
+      if (code.size() == 1 && code[0].op == SHD_OP_LOAD) {
+        ea.okind[c] = 1;
+        ea.oarg[c] = code[0].c & 0xFFFF;
+      } else if (code.size() == 1 && code[0].op == SHD_OP_AGG && code[0].a >= 0 && code[0].a < nagg) {
+        ea.okind[c] = 2;
+        ea.oarg[c] = code[0].a;
+      }
+      if (getenv("SHD_NO_FAST_OUT")) ea.okind[c] = 0;
+    }
     ea.nagg = nagg;
     for (int g = 0; g < nagg; g++) ea.kind[g] = plan.aggs[g].kind;
     ea.cap = cap;
