@@ -193,6 +193,7 @@ struct ItemArgs {
   int nagg;
   DExpr agg_arg[kMaxAggs];
   int has_arg[kMaxAggs];
+  int arg_col[kMaxAggs];   // >= 0: the argument is a plain attribute load (no interpreter)
   int ngroup;
   DExpr group;
   int group_col;
@@ -227,7 +228,9 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
       Val v;
       v.b = 0;
       v.null = 1;
-      if (a.has_arg[g]) v = eval_expr(es.ins + a.agg_arg[g].off, a.agg_arg[g].len, es.consts, cx);
+      if (a.has_arg[g])
+        v = a.arg_col[g] >= 0 ? col_load(cs, i, a.arg_col[g])
+                              : eval_expr(es.ins + a.agg_arg[g].off, a.agg_arg[g].len, es.consts, cx);
       iargv[g * cap + t] = v.b;
       iargn[g * cap + t] = (uint8_t)v.null;
     }
@@ -1965,7 +1968,11 @@ struct SingleEngine : Engine {
     ia.nagg = nagg;
     for (int g = 0; g < nagg; g++) {
       ia.has_arg[g] = plan.aggs[g].expr >= 0;
-      if (ia.has_arg[g]) ia.agg_arg[g] = dexpr(plan.aggs[g].expr);
+      ia.arg_col[g] = -1;
+      if (ia.has_arg[g]) {
+        ia.agg_arg[g] = dexpr(plan.aggs[g].expr);
+        if (!getenv("SHD_NO_FAST_OUT")) ia.arg_col[g] = plain_load_attr(plan, plan.aggs[g].expr);
+      }
     }
     ia.ngroup = group_expr >= 0;
     if (ia.ngroup) {
