@@ -81,6 +81,7 @@ struct Plan {
   struct Agg { int kind, expr, type; };
   std::vector<Agg> aggs;
   std::vector<int> group_by;
+  int64_t null_str_id = -1;   // dictionary id of "null" (string group keys)
   int having = -1;
   std::vector<std::pair<int, int>> outputs;  // (type, expr)
 };
@@ -203,6 +204,8 @@ Plan decode(const int32_t* w, int64_t n) {
     int e = r.next();
     p.outputs.push_back({t, e});
   }
+  // optional trailing section: dictionary id of the string "null" (group keys)
+  if (r.i + 2 <= r.n) p.null_str_id = r.next64();
   return p;
 }
 
@@ -1797,17 +1800,48 @@ struct Engine {
 
   std::vector<Val> agg_vals;
 
+  // GroupByKeyGenerator.constructEventKey (C/query/selector/GroupByKeyGenerator.java:63-73):
+  // the key is the concatenation of String.valueOf of every group-by value, so
+  // two values build one key exactly when their texts agree: a null string and
+  // the string "null" both print "null"; every NaN prints "NaN"; 0.0 and -0.0
+  // differ.  Canonical (value, null) pairs with those identifications (a value
+  // containing the ":-:" delimiter is not identified across attributes).
+  std::vector<std::pair<uint64_t, uint8_t>> group_key(const EvalCtx& cx) {
+    std::vector<std::pair<uint64_t, uint8_t>> gk;
+    for (int g : p.group_by) {
+      Val v = eval(p, g, cx);
+      const int t = expr_type(p, g);
+      if (v.null && t == SHD_T_STRING && p.null_str_id >= 0) {
+        gk.push_back({(uint64_t)p.null_str_id, 0});
+        continue;
+      }
+      if (v.null) {
+        gk.push_back({0, 1});
+        continue;
+      }
+      uint64_t b = v.b;
+      if (t == SHD_T_FLOAT) {
+        const float f = as_f32(b);
+        b = f != f ? 0x7fc00000ull : (uint64_t)(uint32_t)b;
+      } else if (t == SHD_T_DOUBLE) {
+        double d;
+        memcpy(&d, &b, 8);
+        if (d != d) b = 0x7ff8000000000000ull;
+      } else if (t == SHD_T_INT || t == SHD_T_BOOL) {
+        b = (uint64_t)(uint32_t)b;
+      }
+      gk.push_back({b, 0});
+    }
+    return gk;
+  }
+
   // AttributeAggregatorExecutor.execute for each aggregator (plan order)
   void run_aggs(KeySingle* ks, Ev* e) {
     agg_vals.assign(p.aggs.size(), Val{});
     if (p.aggs.empty()) return;
-    std::vector<std::pair<uint64_t, uint8_t>> gk;
     EvalCtx cx;
     cx.ev = e;
-    for (int g : p.group_by) {
-      Val v = eval(p, g, cx);
-      gk.push_back({v.null ? 0 : v.b, (uint8_t)v.null});
-    }
+    std::vector<std::pair<uint64_t, uint8_t>> gk = group_key(cx);
     GroupAgg& ga = ks->groups[gk];
     if (ga.a.size() != p.aggs.size()) ga.a.resize(p.aggs.size());
     for (size_t i = 0; i < p.aggs.size(); i++) {
@@ -1990,11 +2024,7 @@ struct Engine {
       bool on = (e->type == CURRENT && p.current_on) || (e->type == EXPIRED && p.expired_on);
       if (!on) continue;
       if (group) {
-        std::vector<std::pair<uint64_t, uint8_t>> gk;
-        for (int g : p.group_by) {
-          Val v = eval(p, g, cx);
-          gk.push_back({v.null ? 0 : v.b, (uint8_t)v.null});
-        }
+        std::vector<std::pair<uint64_t, uint8_t>> gk = group_key(cx);
         auto it = gmap.find(gk);
         if (it == gmap.end()) { gorder.push_back(gk); gmap[gk] = r; }
         else it->second = r;

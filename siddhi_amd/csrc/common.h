@@ -130,6 +130,7 @@ struct Plan {
   struct Agg { int kind, expr, type; };
   std::vector<Agg> aggs;
   std::vector<int> group_by;
+  int64_t null_str_id = -1;   // dictionary id of "null" (string group keys, GroupByKeyGenerator)
   int having = -1;
   std::vector<std::pair<int, int>> outputs;  // (type, expr)
 };

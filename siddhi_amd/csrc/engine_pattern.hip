@@ -1195,11 +1195,30 @@ __global__ __launch_bounds__(kBwThreads) void k_bkt_walk(const BktArgs* __restri
     const int64_t p1 = p0 + A.ch < be ? p0 + A.ch : be;
     const int64_t pl = p1 + A.la < be ? p1 + A.la : be;
     const int nown = (int)(p1 - p0), nreg = (int)(pl - p0);
-    __syncthreads();   // the previous chunk's LDS readers are done
-    for (int i = tid; i < nreg; i += kBwThreads) {
-      lkey[i] = skey[p0 + i];
-      lts[i] = sts[p0 + i];
-      lpv[i] = spv[p0 + i];
+    {
+      // every load of the staged region issued before the first LDS store (one
+      // memory round trip per chunk, not one per 512 positions)
+      constexpr int kPer = kBwEntries / kBwThreads;
+      uint32_t rk[kPer], rp[kPer];
+      int32_t rt[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kBwThreads;
+        const int64_t q = p0 + (i < nreg ? i : 0);
+        rk[j] = skey[q];
+        rt[j] = sts[q];
+        rp[j] = spv[q];
+      }
+      __syncthreads();   // the previous chunk's LDS readers are done
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kBwThreads;
+        if (i < nreg) {
+          lkey[i] = rk[j];
+          lts[i] = rt[j];
+          lpv[i] = rp[j];
+        }
+      }
     }
     for (int i = tid; i <= kBwSub; i += kBwThreads) cnt[i] = 0;
     __syncthreads();

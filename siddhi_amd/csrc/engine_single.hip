@@ -33,6 +33,7 @@ namespace {
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kAddBit = 0x80000000u;
 constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
+constexpr int kMaxGroupAttrs = 4;
 
 struct RowCtx {
   const ColSet* cs;
@@ -56,6 +57,40 @@ struct RowCtx {
 __device__ __forceinline__ uint64_t canon_key(Val v, int type) {
   if (type == SHD_T_FLOAT) return p_f64((double)v_f32(v.b));
   return v.b;
+}
+
+// One group-by value as a canonical word: two values share a word exactly
+// when String.valueOf prints them alike (the reference's group key is that
+// text, C/query/selector/GroupByKeyGenerator.java:63-73): a null string is the
+// string "null" (its dictionary id), every NaN is one NaN, 0.0 and -0.0 stay
+// apart; other nulls set isnull (word 0).
+__device__ __forceinline__ uint64_t group_word(Val v, int type, int64_t null_str_id, bool& isnull) {
+  isnull = false;
+  if (v.null) {
+    if (type == SHD_T_STRING && null_str_id >= 0) return (uint64_t)null_str_id;
+    isnull = true;
+    return 0;
+  }
+  switch (type) {
+    case SHD_T_FLOAT: {
+      const float f = v_f32(v.b);
+      return f != f ? 0x7fc00000ull : (uint64_t)(uint32_t)v.b;
+    }
+    case SHD_T_DOUBLE: {
+      const double d = __longlong_as_double((long long)v.b);
+      return d != d ? 0x7ff8000000000000ull : v.b;
+    }
+    case SHD_T_INT:
+    case SHD_T_BOOL:
+    case SHD_T_STRING: return (uint64_t)(uint32_t)v.b;
+    default: return v.b;
+  }
+}
+
+__host__ __device__ __forceinline__ uint64_t gdict_mix(uint64_t z) {   // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
 }
 
 // ---------------------------------------------------------------- calls / time
@@ -194,10 +229,17 @@ struct ItemArgs {
   DExpr agg_arg[kMaxAggs];
   int has_arg[kMaxAggs];
   int arg_col[kMaxAggs];   // >= 0: the argument is a plain attribute load (no interpreter)
-  int ngroup;
-  DExpr group;
-  int group_col;
-  int group_type;
+  int ngroup;                 // group-by attributes (0..kMaxGroupAttrs)
+  DExpr group[kMaxGroupAttrs];
+  int group_col[kMaxGroupAttrs];
+  int group_type[kMaxGroupAttrs];
+  int dense;                  // 1: the one key value is the dense group id (string ids, bool)
+  int64_t null_str_id;        // group id of a null string key (the string "null")
+  // dictionary mode: per new item, the canonical key words, null mask and hash
+  uint64_t* gkw;              // [ngroup][n_new]
+  uint8_t* gkn;
+  uint64_t* gh;
+  int64_t gstride;            // words per group attribute in gkw (>= new items)
   int64_t C;
 };
 
@@ -217,10 +259,28 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
     RowCtx cx{&cs, i, nullptr, nullptr};
     uint64_t k = 0;
     if (a.ngroup) {
-      Val kv = a.group_col >= 0 ? col_load(cs, i, a.group_col)
-                                : eval_expr(es.ins + a.group.off, a.group.len, es.consts, cx);
-      if (kv.null) atomicOr(null_key_flag, 1u);
-      k = kv.null ? 0 : canon_key(kv, a.group_type);
+      // GroupByKeyGenerator.constructEventKey: String.valueOf of every value
+      // joined -- canonical words with the same identifications (group_word)
+      uint64_t h = 0x9E3779B97F4A7C15ull;
+      uint8_t nm = 0;
+      for (int g = 0; g < a.ngroup; g++) {
+        Val kv = a.group_col[g] >= 0 ? col_load(cs, i, a.group_col[g])
+                                     : eval_expr(es.ins + a.group[g].off, a.group[g].len, es.consts, cx);
+        bool isnull = false;
+        const uint64_t w = group_word(kv, a.group_type[g], a.null_str_id, isnull);
+        if (a.dense) {
+          k = isnull ? 2u : w;   // bool null: its own group (the text "null")
+        } else {
+          a.gkw[(int64_t)g * a.gstride + off[i]] = w;
+          nm |= (uint8_t)((isnull ? 1u : 0u) << g);
+          h = gdict_mix(h ^ gdict_mix(w + 0x632BE59BD9B4E019ull * (uint64_t)(g + 1)));
+        }
+      }
+      if (!a.dense) {
+        h = gdict_mix(h ^ ((uint64_t)nm << 56));
+        a.gkn[off[i]] = nm;
+        a.gh[off[i]] = h;
+      }
     }
     ikey[t] = k;
     its[t] = cs.ts[i];
@@ -237,6 +297,130 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
     ievrow[t] = (int32_t)i;
     icall[t] = call_of[i];
     inow[t] = call_now[call_of[i]];
+  }
+}
+
+// ---------------------------------------------------------------- group dictionary
+// Group keys that are not dense ids (numeric / multi-attribute / nullable
+// non-string keys) map to dense group ids through an open-addressing table on
+// the device: tag (hash with bit 63 set, 0 = empty; its low bits are the home slot), id, the key words and null mask.
+// Lookups are read-only; a push with unseen keys inserts them in a second
+// phase (misses compacted, sorted by hash, one leader per distinct key, CAS
+// insertion of distinct keys -- no thread ever waits on another), then looks
+// the missed items up again.
+constexpr uint64_t kTagBit = 1ull << 63;
+struct GDict {
+  unsigned long long* tag;
+  uint32_t* id;
+  uint64_t* kw;     // [nk][cap]
+  uint8_t* kn;
+  uint64_t cap;     // power of two
+  int nk;
+};
+
+__device__ __forceinline__ bool gdict_find(const GDict& d, uint64_t h, const uint64_t* key, int64_t kstride,
+                                           int64_t ki, uint8_t nul, uint32_t& id) {
+  const unsigned long long tg = (unsigned long long)(h | kTagBit);
+  uint64_t slot = h & (d.cap - 1);
+  for (uint64_t probe = 0; probe < d.cap; probe++) {
+    const unsigned long long t = d.tag[slot];
+    if (t == 0ull) return false;
+    if (t == tg && d.kn[slot] == nul) {
+      bool eq = true;
+      for (int g = 0; g < d.nk; g++) eq = eq && d.kw[(uint64_t)g * d.cap + slot] == key[(int64_t)g * kstride + ki];
+      if (eq) {
+        id = d.id[slot];
+        return true;
+      }
+    }
+    slot = (slot + 1) & (d.cap - 1);
+  }
+  return false;
+}
+
+// Group id of new item i (or a miss flag): ikey[C + i].
+__global__ __launch_bounds__(kBlock) void k_gdict_lookup(GDict d, int64_t n, const uint64_t* gh, const uint64_t* gkw,
+                                                         const uint8_t* gkn, int64_t gstride, int64_t C,
+                                                         uint64_t* ikey, uint32_t* miss) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
+    uint32_t id;
+    const bool hit = gdict_find(d, gh[i], gkw, gstride, i, gkn[i], id);
+    if (hit) ikey[C + i] = id;
+    miss[i] = hit ? 0u : 1u;
+  }
+}
+
+// Second look-up over the compacted misses (all present after the insert).
+__global__ __launch_bounds__(kBlock) void k_gdict_relookup(GDict d, int64_t nm, const uint32_t* midx, const uint64_t* gh,
+                                                           const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
+                                                           int64_t C, uint64_t* ikey) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nm; j = nm) {
+    const int64_t i = midx[j];
+    uint32_t id = 0xFFFFFFFFu;
+    gdict_find(d, gh[i], gkw, gstride, i, gkn[i], id);
+    ikey[C + i] = id;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gdict_compact(const uint32_t* miss, const uint32_t* moff, int64_t n,
+                                                          const uint64_t* gh, uint32_t* midx, uint64_t* mh) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
+    if (!miss[i]) continue;
+    midx[moff[i]] = (uint32_t)i;
+    mh[moff[i]] = gh[i];
+  }
+}
+
+// Leaders among the hash-sorted misses: the first of each distinct key (an
+// equal-hash run is searched back for an equal key; such runs hold one key
+// unless 64-bit hashes collide).
+__global__ __launch_bounds__(kBlock) void k_gdict_leaders(int64_t nm, const uint64_t* sh, const uint32_t* sidx,
+                                                          const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
+                                                          int nk, uint32_t* lead) {
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nm; p = nm) {
+    const int64_t i = sidx[p];
+    bool leader = true;
+    for (int64_t q = p - 1; q >= 0 && sh[q] == sh[p]; q--) {
+      const int64_t j = sidx[q];
+      bool eq = gkn[j] == gkn[i];
+      for (int g = 0; g < nk && eq; g++) eq = gkw[(int64_t)g * gstride + j] == gkw[(int64_t)g * gstride + i];
+      if (eq) {
+        leader = false;
+        break;
+      }
+    }
+    lead[p] = leader ? 1u : 0u;
+  }
+}
+
+// CAS insertion of distinct keys (the leaders): ids base + leader rank.
+__global__ __launch_bounds__(kBlock) void k_gdict_insert(GDict d, int64_t nm, const uint64_t* sh, const uint32_t* sidx,
+                                                         const uint32_t* lead, const uint32_t* lrank,
+                                                         const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
+                                                         uint32_t base) {
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nm; p = nm) {
+    if (!lead[p]) continue;
+    const int64_t i = sidx[p];
+    const uint64_t h = sh[p];
+    const unsigned long long tg = (unsigned long long)(h | kTagBit);
+    uint64_t slot = h & (d.cap - 1);
+    while (atomicCAS(&d.tag[slot], 0ull, tg) != 0ull) slot = (slot + 1) & (d.cap - 1);
+    d.id[slot] = base + lrank[p];
+    d.kn[slot] = gkn[i];
+    for (int g = 0; g < d.nk; g++) d.kw[(uint64_t)g * d.cap + slot] = gkw[(int64_t)g * gstride + i];
+  }
+}
+
+// Table growth: re-insert every entry of `o` into the empty table `d`.
+__global__ __launch_bounds__(kBlock) void k_gdict_rehash(GDict o, GDict d) {
+  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < o.cap; s = o.cap) {
+    const unsigned long long tg = o.tag[s];
+    if (tg == 0ull) continue;
+    uint64_t slot = (uint64_t)tg & (d.cap - 1);
+    while (atomicCAS(&d.tag[slot], 0ull, tg) != 0ull) slot = (slot + 1) & (d.cap - 1);
+    d.id[slot] = o.id[s];
+    d.kn[slot] = o.kn[s];
+    for (int g = 0; g < d.nk; g++) d.kw[(uint64_t)g * d.cap + slot] = o.kw[(uint64_t)g * o.cap + s];
   }
 }
 
@@ -1465,7 +1649,16 @@ struct SingleEngine : Engine {
   int64_t wparam = 0;
   bool partitioned = false;
   int key_expr = -1, key_col = -1, key_type = 0;
-  int group_expr = -1, group_col = -1, group_type = 0;
+  // group by: up to kMaxGroupAttrs attributes; dense ids (one string / bool
+  // attribute) or the device group dictionary (GDict) for every other key
+  int ngk = 0;
+  int gk_expr[kMaxGroupAttrs] = {}, gk_col[kMaxGroupAttrs] = {}, gk_type[kMaxGroupAttrs] = {};
+  bool gdense = false;
+  DevBuf gd_tag, gd_id, gd_kw, gd_kn;
+  uint64_t gd_cap = 0;
+  int64_t gd_count = 0;
+  DevBuf g_kw, g_kn, g_h, g_miss, g_moff, g_midx, g_mh, g_midx_alt, g_mh_alt, g_lead, g_lrank, g_ctr;
+  PinnedBuf h_ctr;
   std::vector<int> outs;
   std::vector<int> types;
   int nagg = 0;
@@ -1511,6 +1704,93 @@ struct SingleEngine : Engine {
       SHD_HIP(hipMemsetAsync(g_lsum.p, 0, g_lsum.cap, stream));
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
+    gd_count = 0;
+    if (gd_cap) SHD_HIP(hipMemsetAsync(gd_tag.p, 0, gd_cap * 8, stream));
+  }
+
+  GDict gdict() {
+    return GDict{gd_tag.as<unsigned long long>(), gd_id.as<uint32_t>(), gd_kw.as<uint64_t>(), gd_kn.as<uint8_t>(), gd_cap,
+                 ngk};
+  }
+
+  // Table with room for `need` entries at load <= 1/2 (rehash on growth).
+  void gdict_reserve(int64_t need) {
+    uint64_t cap = gd_cap ? gd_cap : 1024;
+    while ((int64_t)(cap / 2) < need) cap *= 2;
+    if (cap == gd_cap) return;
+    DevBuf t, i, k, n;
+    t.reserve(cap * 8);
+    i.reserve(cap * 4);
+    k.reserve((size_t)std::max(ngk, 1) * cap * 8);
+    n.reserve(cap);
+    SHD_HIP(hipMemsetAsync(t.p, 0, cap * 8, stream));
+    GDict nd{t.as<unsigned long long>(), i.as<uint32_t>(), k.as<uint64_t>(), n.as<uint8_t>(), cap, ngk};
+    if (gd_cap && gd_count) {
+      hipLaunchKernelGGL(k_gdict_rehash, dim3(grid_cover((int64_t)gd_cap)), dim3(kBlock), 0, stream, gdict(), nd);
+      SHD_CHECK_LAUNCH();
+    }
+    SHD_HIP(hipStreamSynchronize(stream));
+    std::swap(gd_tag.p, t.p); std::swap(gd_tag.cap, t.cap);
+    std::swap(gd_id.p, i.p); std::swap(gd_id.cap, i.cap);
+    std::swap(gd_kw.p, k.p); std::swap(gd_kw.cap, k.cap);
+    std::swap(gd_kn.p, n.p); std::swap(gd_kn.cap, n.cap);
+    gd_cap = cap;
+  }
+
+  // Dense group ids of the m new items [C, C + m) (dictionary mode): look up,
+  // insert the keys never seen before, look the misses up again.
+  void gdict_assign(int64_t m, int64_t gstride) {
+    if (m <= 0) return;
+    hipStream_t s = stream;
+    gdict_reserve(1);
+    g_miss.reserve(m * 4);
+    g_moff.reserve(m * 4);
+    g_ctr.reserve(64);
+    h_ctr.reserve(64);
+    hipLaunchKernelGGL(k_gdict_lookup, dim3(grid_cover(m)), dim3(kBlock), 0, s, gdict(), m,
+                       (const uint64_t*)g_h.as<uint64_t>(), (const uint64_t*)g_kw.as<uint64_t>(),
+                       (const uint8_t*)g_kn.as<uint8_t>(), gstride, C, ikey[cur].as<uint64_t>(), g_miss.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    scan_exclusive_u32(g_miss.as<uint32_t>(), g_moff.as<uint32_t>(), m, g_ctr.as<uint32_t>(), d_scan, s);
+    SHD_HIP(hipMemcpyAsync(h_ctr.p, g_ctr.p, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t nm = h_ctr.as<uint32_t>()[0];
+    if (nm == 0) return;
+    g_midx.reserve(nm * 4);
+    g_mh.reserve(nm * 8);
+    g_midx_alt.reserve(nm * 4);
+    g_mh_alt.reserve(nm * 8);
+    hipLaunchKernelGGL(k_gdict_compact, dim3(grid_cover(m)), dim3(kBlock), 0, s, (const uint32_t*)g_miss.as<uint32_t>(),
+                       (const uint32_t*)g_moff.as<uint32_t>(), m, (const uint64_t*)g_h.as<uint64_t>(),
+                       g_midx.as<uint32_t>(), g_mh.as<uint64_t>());
+    SHD_CHECK_LAUNCH();
+    bool in_alt = false;
+    radix_sort_pairs_u64(g_mh.as<uint64_t>(), g_midx.as<uint32_t>(), g_mh_alt.as<uint64_t>(), g_midx_alt.as<uint32_t>(),
+                         nm, 64, d_sort, s, in_alt);
+    const uint64_t* sh = in_alt ? g_mh_alt.as<uint64_t>() : g_mh.as<uint64_t>();
+    const uint32_t* sidx = in_alt ? g_midx_alt.as<uint32_t>() : g_midx.as<uint32_t>();
+    g_lead.reserve(nm * 4);
+    g_lrank.reserve(nm * 4);
+    hipLaunchKernelGGL(k_gdict_leaders, dim3(grid_cover(nm)), dim3(kBlock), 0, s, nm, sh, sidx,
+                       (const uint64_t*)g_kw.as<uint64_t>(), (const uint8_t*)g_kn.as<uint8_t>(), gstride, ngk,
+                       g_lead.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    scan_exclusive_u32(g_lead.as<uint32_t>(), g_lrank.as<uint32_t>(), nm, g_ctr.as<uint32_t>() + 1, d_scan, s);
+    SHD_HIP(hipMemcpyAsync(h_ctr.as<uint32_t>() + 1, g_ctr.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t nu = h_ctr.as<uint32_t>()[1];
+    if (gd_count + nu >= (int64_t)0xFFFFFFF0ll) throw Error(SHD_E_CAPACITY, "more than 2^32 group-by keys");
+    gdict_reserve(gd_count + nu);
+    hipLaunchKernelGGL(k_gdict_insert, dim3(grid_cover(nm)), dim3(kBlock), 0, s, gdict(), nm, sh, sidx,
+                       (const uint32_t*)g_lead.as<uint32_t>(), (const uint32_t*)g_lrank.as<uint32_t>(),
+                       (const uint64_t*)g_kw.as<uint64_t>(), (const uint8_t*)g_kn.as<uint8_t>(), gstride,
+                       (uint32_t)gd_count);
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_gdict_relookup, dim3(grid_cover(nm)), dim3(kBlock), 0, s, gdict(), nm, sidx,
+                       (const uint64_t*)g_h.as<uint64_t>(), (const uint64_t*)g_kw.as<uint64_t>(),
+                       (const uint8_t*)g_kn.as<uint8_t>(), gstride, C, ikey[cur].as<uint64_t>());
+    SHD_CHECK_LAUNCH();
+    gd_count += nu;
   }
 
   // window contents (items [0, C) of slot `cur`) + dense per-group aggregates
@@ -1531,6 +1811,15 @@ struct SingleEngine : Engine {
       w.dev(g_dsum.p, gb);
       w.dev(g_lsum.p, gb);
       w.dev(g_cnt.p, gb);
+    }
+    // group dictionary (dictionary-mode group keys)
+    w.put<uint64_t>(gd_cap);
+    w.put<int64_t>(gd_count);
+    if (gd_cap) {
+      w.dev(gd_tag.p, gd_cap * 8);
+      w.dev(gd_id.p, gd_cap * 4);
+      w.dev(gd_kw.p, (size_t)std::max(ngk, 1) * gd_cap * 8);
+      w.dev(gd_kn.p, gd_cap);
     }
   }
   void load_state(SnapR& r) override {
@@ -1562,6 +1851,23 @@ struct SingleEngine : Engine {
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
     if (nk > 0 || !g_nkeys) g_nkeys = nk;
+    const uint64_t dcap = r.get<uint64_t>();
+    const int64_t dcount = r.get<int64_t>();
+    if (dcap & (dcap - 1)) throw Error(SHD_E_ARG, "snapshot of a different plan");
+    gd_count = 0;
+    if (gd_cap) SHD_HIP(hipMemsetAsync(gd_tag.p, 0, gd_cap * 8, stream));
+    if (dcap) {
+      gd_tag.reserve(dcap * 8);
+      gd_id.reserve(dcap * 4);
+      gd_kw.reserve((size_t)std::max(ngk, 1) * dcap * 8);
+      gd_kn.reserve(dcap);
+      r.dev_into(gd_tag.p, dcap * 8);
+      r.dev_into(gd_id.p, dcap * 4);
+      r.dev_into(gd_kw.p, (size_t)std::max(ngk, 1) * dcap * 8);
+      r.dev_into(gd_kn.p, dcap);
+      gd_cap = dcap;
+      gd_count = dcount;
+    }
     counters.carry = C;
   }
 
@@ -1974,11 +2280,22 @@ struct SingleEngine : Engine {
         if (!getenv("SHD_NO_FAST_OUT")) ia.arg_col[g] = plain_load_attr(plan, plan.aggs[g].expr);
       }
     }
-    ia.ngroup = group_expr >= 0;
-    if (ia.ngroup) {
-      ia.group = dexpr(group_expr);
-      ia.group_col = group_col;
-      ia.group_type = group_type;
+    ia.ngroup = ngk;
+    for (int g = 0; g < ngk; g++) {
+      ia.group[g] = dexpr(gk_expr[g]);
+      ia.group_col[g] = gk_col[g];
+      ia.group_type[g] = gk_type[g];
+    }
+    ia.dense = gdense;
+    ia.null_str_id = plan.null_str_id;
+    if (ngk && !gdense) {
+      g_kw.reserve((size_t)ngk * std::max<int64_t>(m, 1) * 8);
+      g_kn.reserve(std::max<int64_t>(m, 1));
+      g_h.reserve(std::max<int64_t>(m, 1) * 8);
+      ia.gkw = g_kw.as<uint64_t>();
+      ia.gkn = g_kn.as<uint8_t>();
+      ia.gh = g_h.as<uint64_t>();
+      ia.gstride = std::max<int64_t>(m, 1);
     }
     ia.C = C;
     hipLaunchKernelGGL(k_make_items, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ia), n,
@@ -1988,6 +2305,7 @@ struct SingleEngine : Engine {
                        iargn[cur].as<uint8_t>(), ievrow.as<int32_t>(), icall.as<int32_t>(), inow.as<int64_t>(), cap,
                        (uint32_t*)(d_tot.as<uint64_t>() + 5));
     SHD_CHECK_LAUNCH();
+    if (ngk && !gdense) gdict_assign(m, std::max<int64_t>(m, 1));
     mark("window_items");
     // expiry positions
     e_exp.reserve(std::max<int64_t>(total, 1) * 4);
@@ -2020,11 +2338,10 @@ struct SingleEngine : Engine {
     reduce_max_u64(ikey[cur].as<uint64_t>(), total, d_kmax, s);
     SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 48, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    if (h_tot.as<uint32_t>()[10]) throw Error(SHD_E_UNSUPPORTED, "null group-by key on the device path");
     const int64_t X = (int64_t)h_tot.as<uint64_t>()[1];
     const uint64_t kmax = h_tot.as<uint64_t>()[2];
-    if ((int64_t)kmax >= kMaxDenseKey)
-      throw Error(SHD_E_UNSUPPORTED, "group-by key outside the dense device range");
+    if ((int64_t)kmax >= kMaxDenseKey)   // dense string ids: more than 2^26 distinct strings
+      throw Error(SHD_E_CAPACITY, "more than 2^26 group-by keys in the dense group tables");
     ensure_groups((int64_t)kmax + 1);
     const int64_t nops = m + X;
     if (!seg_mode) {   // (segmented-scan mode: packed run records instead)
@@ -2209,13 +2526,17 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
     e->key_col = plain_load_attr(p, e->key_expr);
     e->key_type = expr_result_type(p, e->key_expr, {});
   }
-  if (p.group_by.size() > 1) { why = "multi-attribute group by"; return nullptr; }
-  if (!p.group_by.empty()) {
-    e->group_expr = p.group_by[0];
-    e->group_col = plain_load_attr(p, e->group_expr);
-    e->group_type = expr_result_type(p, e->group_expr, {});
-    if (e->group_type == SHD_T_FLOAT || e->group_type == SHD_T_DOUBLE) { why = "floating group key"; return nullptr; }
+  if (p.group_by.size() > (size_t)kMaxGroupAttrs) { why = "more than 4 group-by attributes"; return nullptr; }
+  e->ngk = (int)p.group_by.size();
+  for (int g = 0; g < e->ngk; g++) {
+    e->gk_expr[g] = p.group_by[g];
+    e->gk_col[g] = plain_load_attr(p, e->gk_expr[g]);
+    e->gk_type[g] = expr_result_type(p, e->gk_expr[g], {});
   }
+  // dense ids: one string attribute (dictionary ids; null = the id of "null")
+  // or one bool attribute (0, 1, null = 2); the group dictionary otherwise
+  e->gdense = e->ngk == 1 && ((e->gk_type[0] == SHD_T_STRING && p.null_str_id >= 0) || e->gk_type[0] == SHD_T_BOOL);
+  if (getenv("SHD_GROUP_DICT")) e->gdense = false;   // tests: dictionary path for every key
   return e;
 }
 

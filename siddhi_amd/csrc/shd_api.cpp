@@ -155,6 +155,8 @@ Plan decode_plan(const int32_t* w, int64_t n) {
     int e = r.next();
     p.outputs.push_back({t, e});
   }
+  // optional trailing section: dictionary id of the string "null" (group keys)
+  if (r.i + 2 <= r.n) p.null_str_id = r.next64();
   // validation: expression ids, stack depth, constants
   auto check_expr = [&](int e) {
     if (e < 0 || e >= (int)p.exprs.size()) throw Error(SHD_E_INVALID_PLAN, "bad expression id");

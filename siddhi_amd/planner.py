@@ -117,6 +117,11 @@ class Plan:
     group_by: List[int] = field(default_factory=list)
     having: int = -1
     outputs: List[Tuple[str, int, int]] = field(default_factory=list)     # (name, type, expr)
+    # dictionary id of the string "null": a null string group-by value builds
+    # the same group key as the string "null" (GroupByKeyGenerator appends
+    # String.valueOf(null), C/query/selector/GroupByKeyGenerator.java:63-73);
+    # -1 when no group-by attribute is a string.  Optional trailing IR words.
+    null_str_id: int = -1
     target: str = ""
     # descriptive (host/runtime only)
     states: List[Meta] = field(default_factory=list)
@@ -160,6 +165,7 @@ class Plan:
         w.append(len(self.outputs))
         for _, t, e in self.outputs:
             w.extend([t, e])
+        w.extend(_split64(self.null_str_id))
         return w
 
     def to_bytes(self) -> bytes:
@@ -489,8 +495,10 @@ def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta],
         names.append(oa.name)
         types.append(t)
     for g in sel.group_by:
-        eid, _ = ec.compile(g, cs, 0)
+        eid, gt = ec.compile(g, cs, 0)
         plan.group_by.append(eid)
+        if gt == T_STRING:
+            plan.null_str_id = ec.dict.id("null")
     if sel.having is not None:
         raise UnsupportedPlanException("having is outside the round-1 hot path")
     return names, types
@@ -525,8 +533,6 @@ def _plan_state(app, q, dictionary, partition, extra_streams) -> QueryPlan:
                 eid, _ = ec.compile(f, state_id, IDX_CURRENT, want_bool=True)
                 fids.append(eid)
             wait = el.waiting_ms if el.waiting_ms is not None else -1
-            if el.absent and el.waiting_ms is None:
-                raise UnsupportedPlanException("absent state without 'for' time")
             return [NODE_STREAM, state_id, sidx, int(el.absent), *_split64(wait), len(fids), *fids]
         if isinstance(el, qc.NextSE):
             a = walk(el.a)
