@@ -147,11 +147,14 @@ def cpu_baseline(cfg_name, app, keys, delta, sample):
             parts.append((ch + 1_000_000 * c, ty, ts_, va[:, :nout], nu[:, :nout]))
         lib.orc_clear_rows(eng.h)
     dt = time.perf_counter() - t0
+    oc = eng.counters()
     eng.close()
+    ora_counters = {"events": int(oc[0]), "filter_evals": int(oc[1]), "partials": int(oc[2]), "matches": int(oc[3]),
+                    "expired": int(oc[5])}
     return ({"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
              "sample": "first %d events of the %s stream (%d keys, delta %g ms), C++ restatement of the "
                        "reference NFA (oracle/oracle.cpp), 1 thread" % (sample, cfg_name, keys, delta)},
-            concat_rows(parts), qp)
+            concat_rows(parts), qp, ora_counters)
 
 
 def cpu_baseline_parallel(cfg_name, app, keys, delta, sample, threads):
@@ -204,25 +207,36 @@ def cpu_baseline_parallel(cfg_name, app, keys, delta, sample, threads):
                       "engine per thread (oracle/oracle.cpp)" % (sample, cfg_name, threads, threads)}
 
 
-def parity_prefix(torch, he, qp, cols, ts, offs_all, prefix, ora_rows):
+def parity_prefix(torch, he, qp, cols, ts, offs_all, prefix, ora_rows, window, batch):
     """The device path on the first `prefix` events of the benchmark stream (one
-    fresh query, polled, outside the timed region) against the oracle's rows."""
+    fresh query, the bench's micro-batch size, polled, outside the timed region)
+    against the oracle's rows: bit-exact for patterns; window aggregates with
+    doubles within 1e-9 relative (the default segmented scans).  Also returns
+    the device's counters over the prefix (the derived P-bar / f_new / m-bar
+    cross-check)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from parity import assert_same_rows
+    from parity import assert_rows_agg, assert_same_rows, concat_rows
     dq = he.DeviceQuery(qp.ir)
     try:
-        co = offs_all[offs_all <= prefix]
-        if co[-1] != prefix:
-            co = np.append(co, prefix)
-        dq.push_raw(0, prefix, ts.data_ptr(), [c.data_ptr() for c in cols], [0, 0, 0], he.SHD_MEM_DEVICE,
-                    co.astype(np.int64), True)
-        r = dq.poll()
-        from parity import concat_rows
-        dev = concat_rows([r] if r is not None else [])
-        assert_same_rows(dev, ora_rows)
-        return "equal (%d events, %d rows)" % (prefix, len(dev[2]))
+        parts = []
+        for a in range(0, prefix, batch):
+            b = min(prefix, a + batch)
+            lo, hi = np.searchsorted(offs_all, a), np.searchsorted(offs_all, b)
+            co = np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a
+            dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, [c.data_ptr() + c.element_size() * a for c in cols],
+                        [0] * len(cols), he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+            r = dq.poll()
+            if r is not None:
+                parts.append(r)
+        dev = concat_rows(parts)
+        if window:
+            assert_rows_agg(dev, ora_rows, qp, exact=False)
+        else:
+            assert_same_rows(dev, ora_rows)
+        return "equal (%d events, %d rows%s)" % (prefix, len(dev[2]), ", doubles within 1e-9" if window else ""), \
+            dq.counters()
     except AssertionError as e:
-        return "DIFFERENT: %s" % str(e).splitlines()[0]
+        return "DIFFERENT: %s" % str(e).splitlines()[0], dq.counters()
     finally:
         dq.close()
 
@@ -334,9 +348,59 @@ def run_multi(args, torch, dist, rank, world, local, dev):
             "roofline": roof,
             "cpu_baseline": None,
         }
+    prefix = None
+    if rank == 0 and args.cpu_sample != 0:
+        prefix = m5_parity_prefix(he, plans, sym, price, vol, ts, min(n, args.cpu_sample if args.cpu_sample > 0
+                                                                        else 20_000), keys, delta)
+        line["parity_prefix"] = prefix
+        print(json.dumps(line))
+    elif rank == 0:
         print(json.dumps(line))
     for dq in dqs:
         dq.close()
+
+
+def m5_parity_prefix(he, plans, sym, price, vol, ts, prefix, keys, delta):
+    """Every M5 query (a fresh device query each) on the first `prefix` events
+    of the benchmark stream against the CPU oracle on the same events: pattern
+    rows bit-exact, window rows with doubles within 1e-9 relative."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_engine import OracleQueryEngine
+    from parity import assert_rows_agg, assert_same_rows, concat_rows
+    from siddhi_amd import workloads as wl
+    from siddhi_amd.runtime import ColumnBatch
+    s, p, v, t = wl.stock_stream(prefix, keys, delta, seed_offset=0)
+    offs = wl.call_offsets(prefix)
+    rows = 0
+    try:
+        for qp in plans:
+            eng = OracleQueryEngine(qp, None)
+            parts = []
+            cid = 0
+            for c in range(len(offs) - 1):
+                a, b = int(offs[c]), int(offs[c + 1])
+                sub = ColumnBatch(t[a:b], [s[a:b].astype(np.uint32), p[a:b], v[a:b]], [None, None, None])
+                for ch in eng.set_time(int(t[b - 1])) + eng.push(0, sub):
+                    k = len(ch.ts)
+                    parts.append((np.full(k, cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+                    cid += 1
+            eng.close()
+            ora = concat_rows(parts)
+            dq = he.DeviceQuery(qp.ir)
+            dq.push_raw(0, prefix, ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol.data_ptr()], [0, 0, 0],
+                        he.SHD_MEM_DEVICE, offs.astype(np.int64), True)
+            r = dq.poll()
+            window = dq.engine_kind == 2
+            dq.close()
+            dev = concat_rows([r] if r is not None else [])
+            if window:
+                assert_rows_agg(dev, ora, qp, exact=False)
+            else:
+                assert_same_rows(dev, ora)
+            rows += len(dev[2])
+        return "equal (%d queries, %d events, %d rows)" % (len(plans), prefix, rows)
+    except AssertionError as e:
+        return "DIFFERENT: %s" % str(e).splitlines()[0]
 
 
 def main():
@@ -366,7 +430,7 @@ def main():
     app, n_def, k_def, delta = wl.CONFIGS[args.config]
     n = args.events or n_def
     keys = args.keys or k_def
-    pattern = args.config.startswith("P")
+    pattern = not args.config.startswith("W")   # P1 / P3 / S4: pattern formula of §8d
     qa = qc.parse(app)
     item = qa.execution_order[0]
     if isinstance(item, qc.Partition):
@@ -543,11 +607,26 @@ def main():
     cpu = None
     cpu_mt = None
     prefix = None
+    derived_check = None
     if rank == 0 and world == 1 and args.cpu_sample != 0:
         sample = args.cpu_sample if args.cpu_sample > 0 else (2_000_000 if pattern else 1_000_000)
-        cpu, ora_rows, _ = cpu_baseline(args.config, app, keys, delta, min(sample, n))
-        if pattern and mode == "prepartitioned" and kb == 0:
-            prefix = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, min(sample, n), ora_rows)
+        sample = min(sample, n)
+        cpu, ora_rows, _, oc = cpu_baseline(args.config, app, keys, delta, sample)
+        if mode == "prepartitioned" and kb == 0:
+            prefix, pc = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, sample, ora_rows,
+                                       not pattern, min(batch, sample))
+            if args.config in ("P1", "P3", "P3-dense"):
+                # the §8d counts two ways on the same prefix: the device's walks
+                # ((partial, event) pairs visited, the expiring visit included) and
+                # the oracle's filter evaluations minus the start state's f1 per
+                # event, plus the partials its expireEvents removed
+                dev_d = alg_bytes_pattern(pc, pc["events"])[1]
+                ora_pairs = oc["filter_evals"] - oc["events"] + oc["expired"]
+                ora_d = dict(P_bar=ora_pairs / sample, f_new=oc["partials"] / sample, m_bar=oc["matches"] / sample)
+                derived_check = {"prefix_events": sample,
+                                 "device": {k: round(v, 6) for k, v in dev_d.items()},
+                                 "oracle": {k: round(v, 6) for k, v in ora_d.items()},
+                                 "equal": all(abs(dev_d[k] - ora_d[k]) < 1e-12 for k in dev_d)}
         if pattern and isinstance(item, qc.Partition) and args.cpu_threads > 0:
             cpu_mt = cpu_baseline_parallel(args.config, app, keys, delta, min(4 * sample, n), args.cpu_threads)
 
@@ -577,6 +656,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_mt,
             "parity_prefix": prefix,
+            "derived_check": derived_check,
         }
         if alongside:
             line["alongside"] = alongside

@@ -72,6 +72,12 @@ typedef struct shd_batch {
   int32_t ncalls;               /* InputHandler.send calls in this batch (>= 1)  */
   const int64_t* call_offsets;  /* host array [ncalls+1]; NULL = one call        */
   int32_t advance_time;         /* playback: set app time to each call's last ts */
+  int32_t use_base_seq;         /* 1: base_seq is given (0, the zero-initialised
+                                   default: the query continues its own count) */
+  int64_t base_seq;             /* arrival index of the batch's first event in the
+                                   whole stream (a key-sharded rank receives a
+                                   subset): shd_out.in_seq of this batch's rows is
+                                   then global; must not go back (SHD_E_ARG)     */
 } shd_batch;
 
 /* Output rows of a query since the last poll, in reference order.  Rows with
@@ -93,6 +99,11 @@ typedef struct shd_out {
                                    (in_seq, processor, pending-list) order, so the
                                    outputs of key-sharded queries merge by the
                                    global sequence of in_seq. */
+  const int32_t* state_idx;     /* [n_rows] state id of the pre-processor whose
+                                   processing emitted the row (the completing
+                                   state of a pattern / sequence match, the
+                                   absent state of a timer row); 0 for
+                                   single-stream (filter / window) queries   */
 } shd_out;
 
 typedef struct shd_counters {
@@ -106,9 +117,13 @@ typedef struct shd_counters {
   int64_t group_bits;           /* pattern engine: sort bits of the last push's key
                                    grouping (hashed buckets when below the key
                                    width), 0 when not partitioned              */
+  int64_t kernel_ns_total;      /* device time of every push since load / reset  */
 } shd_counters;
 
 int shd_device_count(int* n);
+/* One context drives ONE device (n == 1; one host process per GPU, the
+ * multi-GPU layer shards keys across processes over RCCL -- SURVEY.md §8e);
+ * n > 1 returns SHD_E_ARG. */
 int shd_ctx_create(const int* device_ids, int n, shd_ctx** out);
 int shd_ctx_destroy(shd_ctx* ctx);
 
@@ -122,8 +137,14 @@ int shd_set_time(shd_query* q, int64_t ts);
 /* Named per-query options (SHD_E_ARG for an unknown name):
  *   "exact_aggregates" (window/aggregate engine): 1 = the bit-exact sequential
  *     per-group fold (Java's `sum += v; sum -= v` order, AttributeAggregator
- *     executors); 0 (default) = segmented scans, double aggregates within 1e-9
- *     relative of that fold (BASELINE.json north_star). */
+ *     executors); 0 (default) = segmented scans (double-double prefix sums),
+ *     double aggregates within 1e-9 relative of that fold (BASELINE.json
+ *     north_star) while the operands are finite and their non-zero
+ *     magnitudes span at most 2^30; the first push that brings a non-finite
+ *     or wider-ranged operand switches the query to the exact fold for good
+ *     (the reference's running sum keeps Inf / NaN and its rounding history;
+ *     a mixed-sign window that cancels to far below its operands is the case
+ *     the 2^30 span does not bound -- use exact_aggregates there). */
 int shd_set_option(shd_query* q, const char* key, int64_t value);
 int shd_push(shd_query* q, const shd_batch* batch);
 int shd_flush(shd_query* q);                  /* wait for queued device work      */

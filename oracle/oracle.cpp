@@ -613,7 +613,9 @@ struct Engine {
   std::deque<std::vector<uint8_t>> null_store;
   Arena<Ev> ev_arena;
   Arena<SE> se_arena;
-  int64_t counters[8] = {0};  // 0 events, 1 pending scanned, 2 partials created, 3 matches, 4 out rows
+  // 0 events, 1 filter evaluations, 2 partials created (start-state matches),
+  // 3 matches, 4 out rows, 5 partials expired (`within`)
+  int64_t counters[8] = {0};
 
   // ---- state query structure
   std::vector<Pre> pres;
@@ -1040,6 +1042,7 @@ struct Engine {
       SE* s = *it;
       if (isExpired(pre, s, t)) {
         it = st.pending.erase(it);
+        counters[5]++;
         if (s->type != EXPIRED) { s->type = EXPIRED; expired = s; }
       } else {
         break;
@@ -1049,6 +1052,7 @@ struct Engine {
       SE* s = *it;
       if (isExpired(pre, s, t)) {
         it = st.newEvery.erase(it);
+        counters[5]++;
         if (s->type != EXPIRED) { s->type = EXPIRED; expired = s; }
       } else {
         ++it;
@@ -1070,6 +1074,7 @@ struct Engine {
       counters[1]++;
       if (!eval_bool(p, f, cx)) return;
     }
+    if (pr.isStart) counters[2]++;
     postProcess(pr.thisPost, s);
   }
 

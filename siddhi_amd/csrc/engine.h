@@ -16,7 +16,7 @@ enum EngineKind { ENG_PATTERN = 1, ENG_WINDOW = 2, ENG_FILTER = 3, ENG_NFA = 4 }
 struct OutputBuffer {
   int ncols = 0;
   int64_t count = 0, cap = 0;
-  DevBuf chunk, type, ts, vals, nulls, seq;
+  DevBuf chunk, type, ts, vals, nulls, seq, sidx;
   void init(int nc) { ncols = nc; }
   // Make room for `extra` more rows (copies existing rows on growth).
   void ensure(int64_t extra, hipStream_t s);
@@ -26,6 +26,7 @@ struct OutputBuffer {
   uint64_t* d_vals() { return vals.as<uint64_t>(); }
   uint8_t* d_nulls() { return nulls.as<uint8_t>(); }
   int64_t* d_seq() { return seq.as<int64_t>(); }   // shd_out.in_seq
+  int32_t* d_sidx() { return sidx.as<int32_t>(); }  // shd_out.state_idx
 };
 
 // A batch staged on the device (columns either borrowed device pointers or
@@ -36,6 +37,7 @@ struct Staged {
   ColSet cs{};
   std::vector<int64_t> call_offsets;   // host, ncalls+1
   bool advance_time = false;
+  const uint8_t* skip_start = nullptr;   // device [n] or null: hand-over replays only (Replay::skip_start)
 };
 
 // Snapshot streams (shd_snapshot / shd_restore): a flat little-endian byte
@@ -114,13 +116,20 @@ struct NeedNfa : Error {
   explicit NeedNfa(const std::string& m) : Error(SHD_E_UNSUPPORTED, m) {}
 };
 
-// Host image of a query's open partial matches as the events that created
-// them, in arrival order (one stream, typed columns as in shd_batch).
+// Host image of a query's open partial matches as the events whose replay
+// rebuilds them, in arrival order: one part per run of same-stream events
+// (typed columns as in shd_batch).  skip_start[i] = 1: event i is replayed
+// only for the partials it belongs to (an operand event of a half-filled
+// logical AND partial whose own start partial is gone) -- the start state does
+// not see it; 2: event i only stabilises its key's states (expiry + the
+// new-list -> pending-list move, StreamPreStateProcessor.updateState) and no
+// state processes it.
 struct Replay {
   int stream = 0;
   int64_t n = 0;
   std::vector<int64_t> ts;
   std::vector<std::vector<uint8_t>> cols, nulls;   // [ncols] typed bytes / null bytes
+  std::vector<uint8_t> skip_start;                 // [n] (empty: none skipped)
 };
 
 struct Engine {
@@ -157,6 +166,10 @@ struct Engine {
   // absent start states with it (AbsentStreamPreStateProcessor.partitionCreated
   // :291-303 reads currentTime()).
   int64_t start_time = 0;
+  // construction hint of the engine's state layout (generic NFA engine: the
+  // list_hint of make_nfa_engine); snapshots carry it so that a restore builds
+  // the same layout
+  int64_t layout_hint = 0;
   virtual void set_option(const std::string& key, int64_t v) {
     if (key == "start_time") {
       start_time = v;
@@ -177,7 +190,9 @@ struct Engine {
   virtual void load_state(SnapR&) { throw Error(SHD_E_UNSUPPORTED, "engine has no snapshot support"); }
   // Events whose replay through the reference algorithm (from a fresh state)
   // rebuilds exactly this engine's open partial matches (NeedNfa hand-over).
-  virtual void export_replay(Replay&) { throw Error(SHD_E_UNSUPPORTED, "engine state cannot be handed over"); }
+  virtual void export_replay(std::vector<Replay>&) {
+    throw Error(SHD_E_UNSUPPORTED, "engine state cannot be handed over");
+  }
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column

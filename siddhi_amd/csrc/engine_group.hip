@@ -1,0 +1,488 @@
+// engine_group.hip -- grouped LDS walk of the pattern engine (partitioned or
+// implicitly grouped `every e1=A[f1] -> e2=B[f2] within W`, config P3).
+//
+// The extended batch (carried partials + pushed events) is stable-sorted by
+// the low 16 bits of key_bucket_mix(key) -- two 8-bit hashed LSD passes
+// instead of the three a full 24-bit key sort needs.  A group (one 16-bit
+// hash value) then holds EVERY row of each of its keys, in arrival order
+// (carried partials first), so the reference's per-key processing resolves
+// inside the group alone -- no lookahead, no time horizon, nothing retired:
+//   StreamPreStateProcessor.processAndReturn / expireEvents for this plan
+//   shape (ST/StreamPreStateProcessor.java:118-129,326-403): a partial P_i
+//   completes at the first later B event j of its key with f2(P_i, j), unless
+//   an event of its key with ts - ts_i > W comes first (expiry); with neither
+//   it stays open (carried to the next push).
+// One workgroup per group: the group's (key, flags|row, ts32) rows are staged
+// in LDS, keys are interned in an LDS hash table, each key's events are
+// listed in arrival order (counting-sort layout + in-list ranks), and every
+// candidate partial walks its key's later events there.  A group larger than
+// the LDS capacity walks the same lists in global memory (rare: the hash
+// spreads 10M keys over 65536 groups of ~760 rows).
+//
+// Bytes: one read of the 12-byte sorted row per position + the outcome byte
+// and match row written; f2 reads e1 / e2 attributes only for same-key pairs
+// inside `within`.
+#include "pattern_common.h"
+#include "radix_tile.h"
+
+namespace shd {
+namespace pat {
+
+namespace {
+
+constexpr int kGwThreads = 256;
+constexpr int kGwCap = 1024;      // rows of a group staged in LDS
+constexpr int kGwSlots = 2048;    // LDS key table (load <= 1/2)
+constexpr uint64_t kGwEmpty = ~0ull;
+
+__device__ __forceinline__ uint32_t gw_group(uint32_t key, int bits) {
+  return key_bucket_mix(key) & ((1u << bits) - 1u);
+}
+
+// Group boundaries in the sorted order: gbeg[g] / gend[g] (both 0 for an
+// empty group: the arrays are zeroed first).
+__global__ __launch_bounds__(kBlock) void k_group_bounds(const uint32_t* __restrict__ skey,
+                                                         const uint32_t* __restrict__ spv, int64_t n, int bits,
+                                                         uint32_t* __restrict__ gbeg, uint32_t* __restrict__ gend) {
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += (int64_t)gridDim.x * kBlock) {
+    const uint32_t g = gw_group(skey[p], bits);
+    if (p == 0) gbeg[g] = 0;
+    else {
+      const uint32_t h = gw_group(skey[p - 1], bits);
+      if (h != g) {
+        gend[h] = (uint32_t)p;
+        gbeg[g] = (uint32_t)p;
+      }
+    }
+    if (p == n - 1) gend[g] = (uint32_t)n;
+  }
+}
+
+// The walk of candidate partial i over its key's later events e (ascending
+// positions): the reference's outcome (expiry / match / open) and the
+// (partial, event) pairs it examined.
+template <bool FAST, class EvAt>
+__device__ __forceinline__ uint8_t gw_walk(const ScanArgs& a, const DExprSet& es, int64_t r, int64_t tsi, int n_ev,
+                                           const EvAt& ev_at, int32_t& mrow, uint64_t& steps, uint32_t& viol) {
+  int64_t prev = tsi;
+  uint8_t pend = 0;   // met a B event: pending list (PS_PEND)
+  for (int k = 0; k < n_ev; k++) {
+    uint32_t pv;
+    int64_t tq;
+    ev_at(k, pv, tq);
+    if (a.within != INT64_MAX && tq < prev) {   // a per-key time regression: generic NFA engine
+      viol = 1;
+      return PS_NONE;
+    }
+    prev = tq;
+    steps++;
+    if (tq - tsi > a.within) return PS_NONE;   // stabilizeStates -> expireEvents
+    if (pv_flags(pv) & F_B) {
+      pend = PS_PEND;
+      PairCtx cx{&a.x, r, (int64_t)pv_row(pv), a.s_first};
+      if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+        mrow = (int32_t)pv_row(pv);
+        return PS_MATCH;
+      }
+    }
+  }
+  return PS_OPEN | pend;
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(kGwThreads) void k_group_walk(const ScanArgs* __restrict__ ap, int ngroups, int bits,
+                                                            const uint32_t* __restrict__ gbeg,
+                                                            const uint32_t* __restrict__ gend,
+                                                            const uint32_t* __restrict__ skey,
+                                                            const uint32_t* __restrict__ spv,
+                                                            const int32_t* __restrict__ sts,
+                                                            int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                            ScanOut* __restrict__ blk) {
+  const ScanArgs& a = *ap;
+  const DExprSet es = a.es;
+  __shared__ uint32_t lkey[kGwCap];
+  __shared__ uint32_t lpv[kGwCap];
+  __shared__ int32_t lts[kGwCap];
+  __shared__ uint16_t lslot[kGwCap];
+  __shared__ uint16_t lidx[kGwCap];   // an event's index in its key's ordered list
+  __shared__ uint16_t lst[kGwCap];    // per-key event lists (unordered fill)
+  __shared__ uint16_t lsorted[kGwCap];
+  __shared__ unsigned long long tkey[kGwSlots];
+  __shared__ uint32_t tcnt[kGwSlots];   // events per slot, then the fill counter
+  __shared__ uint16_t tbase[kGwSlots];
+  __shared__ uint32_t wsum[kGwThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t tbase_ts = a.x.batch.ts[0];
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int64_t q0 = gbeg[g], q1 = gend[g];
+    const int len = (int)(q1 - q0);
+    if (len <= 0) continue;
+    if (len > kGwCap) {
+      // oversized group: the same lists walked in global memory (each
+      // candidate scans the group forward for its key)
+      for (int i = tid; i < len; i += kGwThreads) {
+        const int64_t q = q0 + i;
+        const uint32_t pv = spv[q];
+        uint8_t out = PS_NONE;
+        if (pv_flags(pv) & F_CAND) {
+          const uint32_t k = skey[q];
+          const int64_t tsi = tbase_ts + (int64_t)sts[q];
+          // its key's events after it, in position order
+          int64_t nxt = q + 1;
+          auto ev_at = [&](int, uint32_t& pvo, int64_t& tq) {
+            while (true) {
+              const uint32_t pq = spv[nxt];
+              if (skey[nxt] == k && (pv_flags(pq) & F_NEW) && !(pv_flags(pq) & F_SKIP)) {
+                pvo = pq;
+                tq = tbase_ts + (int64_t)sts[nxt];
+                nxt++;
+                return;
+              }
+              nxt++;
+            }
+          };
+          int n_ev = 0;
+          for (int64_t y = q + 1; y < q1; y++) {
+            const uint32_t py = spv[y];
+            n_ev += (skey[y] == k && (pv_flags(py) & F_NEW) && !(pv_flags(py) & F_SKIP)) ? 1 : 0;
+          }
+          int32_t mrow = -1;
+          out = gw_walk<FAST>(a, es, (int64_t)pv_row(pv), tsi, n_ev, ev_at, mrow, steps, viol);
+          if (out == PS_MATCH) match_row[q] = mrow;
+          if ((out & 0x7F) == PS_OPEN && a.prune && a.t_end - tsi > a.within) {
+            out = PS_NONE;
+            pruned++;
+          }
+        }
+        pst[q] = out;
+      }
+      continue;
+    }
+    // ---- stage the group (all loads issued before the LDS stores)
+    {
+      constexpr int kPer = kGwCap / kGwThreads;
+      uint32_t rk[kPer], rp[kPer];
+      int32_t rt[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kGwThreads;
+        const int64_t q = q0 + (i < len ? i : 0);
+        rk[j] = skey[q];
+        rp[j] = spv[q];
+        rt[j] = sts[q];
+      }
+      __syncthreads();   // the previous group's readers are done
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kGwThreads;
+        if (i < len) {
+          lkey[i] = rk[j];
+          lpv[i] = rp[j];
+          lts[i] = rt[j];
+        }
+      }
+      for (int s = tid; s < kGwSlots; s += kGwThreads) {
+        tkey[s] = kGwEmpty;
+        tcnt[s] = 0;
+      }
+    }
+    __syncthreads();
+    // ---- intern the keys of events and candidates; count events per key
+    for (int i = tid; i < len; i += kGwThreads) {
+      const uint32_t f = pv_flags(lpv[i]);
+      const bool ev = (f & F_NEW) && !(f & F_SKIP);
+      if (!ev && !(f & F_CAND)) continue;
+      const unsigned long long k = lkey[i];
+      // (every key of the group shares the low 16 bits of key_bucket_mix: the
+      // table slot comes from another multiplicative hash's top bits)
+      uint32_t s = (lkey[i] * 0x85EBCA6Bu) >> (32 - 11);
+      static_assert(kGwSlots == 1 << 11, "slot bits");
+      while (true) {
+        const unsigned long long old = atomicCAS(&tkey[s], kGwEmpty, k);
+        if (old == kGwEmpty || old == k) break;
+        s = (s + 1) & (kGwSlots - 1);
+      }
+      lslot[i] = (uint16_t)s;
+      if (ev) atomicAdd(&tcnt[s], 1u);
+    }
+    __syncthreads();
+    // ---- list bases: exclusive scan of the per-slot event counts
+    {
+      constexpr int kPerS = kGwSlots / kGwThreads;
+      uint32_t c[kPerS], sum = 0;
+#pragma unroll
+      for (int j = 0; j < kPerS; j++) {
+        c[j] = tcnt[tid * kPerS + j];
+        sum += c[j];
+      }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t pre = inc - sum;
+      for (int k = 0; k < w; k++) pre += wsum[k];
+#pragma unroll
+      for (int j = 0; j < kPerS; j++) {
+        tbase[tid * kPerS + j] = (uint16_t)pre;
+        pre += c[j];
+        tcnt[tid * kPerS + j] = 0;   // from here: fill counter
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < len; i += kGwThreads) {
+      const uint32_t f = pv_flags(lpv[i]);
+      if (!((f & F_NEW) && !(f & F_SKIP))) continue;
+      const uint32_t s = lslot[i];
+      lst[tbase[s] + atomicAdd(&tcnt[s], 1u)] = (uint16_t)i;
+    }
+    __syncthreads();
+    // order each key's list by position (lists are short: rank by counting)
+    for (int i = tid; i < len; i += kGwThreads) {
+      const uint32_t f = pv_flags(lpv[i]);
+      if (!((f & F_NEW) && !(f & F_SKIP))) continue;
+      const uint32_t s = lslot[i];
+      const int b = tbase[s], c = (int)tcnt[s];
+      int rank = 0;
+      for (int y = 0; y < c; y++) rank += lst[b + y] < i ? 1 : 0;
+      lsorted[b + rank] = (uint16_t)i;
+      lidx[i] = (uint16_t)(b + rank);
+    }
+    __syncthreads();
+    // ---- every candidate walks its key's later events
+    for (int i = tid; i < len; i += kGwThreads) {
+      const uint32_t pv = lpv[i];
+      const uint32_t f = pv_flags(pv);
+      uint8_t out = PS_NONE;
+      if (f & F_CAND) {
+        const uint32_t s = lslot[i];
+        const int b = tbase[s], end = b + (int)tcnt[s];
+        // carried partials precede every event of the push (stable sort)
+        const int from = ((f & F_NEW) && !(f & F_SKIP)) ? lidx[i] + 1 : b;
+        auto ev_at = [&](int k, uint32_t& pvo, int64_t& tq) {
+          const int e = lsorted[from + k];
+          pvo = lpv[e];
+          tq = tbase_ts + (int64_t)lts[e];
+        };
+        int32_t mrow = -1;
+        const int64_t tsi = tbase_ts + (int64_t)lts[i];
+        out = gw_walk<FAST>(a, es, (int64_t)pv_row(pv), tsi, end - from, ev_at, mrow, steps, viol);
+        if (out == PS_MATCH) match_row[q0 + i] = mrow;
+        // unpartitioned plans (implicit grouping) expire globally: the push's
+        // last event expired what is older than `within` (partitioned: prune 0)
+        if ((out & 0x7F) == PS_OPEN && a.prune && a.t_end - tsi > a.within) {
+          out = PS_NONE;
+          pruned++;
+        }
+      }
+      pst[q0 + i] = out;
+    }
+  }
+  // block partials of the scan counters (match / open counts: k_tile_count)
+  for (int o = 32; o > 0; o >>= 1) {
+    steps += __shfl_xor(steps, o, 64);
+    pruned += __shfl_xor(pruned, o, 64);
+    viol |= __shfl_xor(viol, o, 64);
+  }
+  __shared__ ScanOut wpart[kGwThreads / 64];
+  if (lane == 0) wpart[w] = ScanOut{steps, pruned, viol, 0};
+  __syncthreads();
+  if (tid == 0) {
+    ScanOut r = wpart[0];
+    for (int k = 1; k < kGwThreads / 64; k++) {
+      r.steps += wpart[k].steps;
+      r.pruned += wpart[k].pruned;
+      r.violation |= wpart[k].violation;
+    }
+    blk[blockIdx.x] = r;
+  }
+}
+
+// ---------------------------------------------------------------- fused prepare + first hashed pass
+// k_prepare's row preparation (prep_row: flags F_CAND / F_NEW / F_B / F_SKIP,
+// 32-bit key, ts offset, batch aggregates) fused into the first 8-bit pass of
+// the grouped walk's hashed key sort: the prepared rows go straight to their
+// digit positions instead of a round trip through HBM.  Every load of a
+// lane's R rows -- key, ts, the <= 2 attributes f1 reads, their null bytes --
+// is issued before the first use (a row's loads, then the next row's, would
+// serialise the memory round trips); f1 is a fast predicate evaluated over
+// the preloaded values.  Same results as prep_row (plain 32-bit key column).
+struct PreRow {
+  Val v0, v1;
+  int a0, a1;
+  int64_t ts;
+};
+struct PreCtx {   // BatchRowCtx over preloaded values
+  const PreRow* p;
+  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
+    if (st != 0 || !(idx == 0 || idx == SHD_IDX_CURRENT)) {
+      Val v;
+      v.b = 0;
+      v.null = 1;
+      return v;
+    }
+    return attr == p->a0 ? p->v0 : p->v1;
+  }
+  __device__ __forceinline__ bool evnull(int st, int idx) const { return !(st == 0 && (idx == 0 || idx == SHD_IDX_CURRENT)); }
+  __device__ __forceinline__ int64_t ts(int st, int idx) const { return evnull(st, idx) ? 0 : p->ts; }
+  __device__ __forceinline__ Val agg(int) const {
+    Val v;
+    v.b = 0;
+    v.null = 1;
+    return v;
+  }
+};
+
+template <int R>
+__global__ __launch_bounds__(kRsBlock) void k_prep_scatter(const PrepArgs* __restrict__ ap, int64_t n_ext,
+                                                           const uint32_t* __restrict__ hist,
+                                                           const uint32_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ dtotal, int nb, int a0, int a1,
+                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                           uint32_t* __restrict__ tout, PrepAgg* __restrict__ blk) {
+  const PrepArgs& a = *ap;
+  const ExtRows& x = a.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = rs_tile_of(blockIdx.x, nb);
+  const int64_t t0 = (int64_t)tile * rs_tile(R);
+  const int64_t wb = t0 + (int64_t)w * 64 * R;
+  const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
+  const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
+  const int64_t tbase = x.batch.ts[0];
+  const int64_t C = x.C;
+  const uint32_t* kcol = (const uint32_t*)x.batch.col[a.key_col];
+  const uint8_t* knul = x.batch.nul[a.key_col];
+  // ---- loads
+  PreRow pr[R];
+  uint32_t kk[R];
+  uint8_t kn[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    const int64_t li = idx < n_ext ? idx : n_ext - 1;
+    const bool isc = li < C;
+    const int64_t br = isc ? 0 : li - C;
+    const int64_t cr = isc ? li : 0;
+    pr[r].a0 = a0;
+    pr[r].a1 = a1;
+    if (C > 0 && isc) {
+      kk[r] = (uint32_t)a.carry_key[cr];
+      kn[r] = 0;
+      pr[r].ts = x.carry.ts[cr];
+    } else {
+      kk[r] = kcol[br];
+      kn[r] = knul ? knul[br] : 0;
+      pr[r].ts = x.batch.ts[br];
+      pr[r].v0 = a0 >= 0 ? col_load(x.batch, br, a0) : Val{};
+      pr[r].v1 = a1 >= 0 ? col_load(x.batch, br, a1) : Val{};
+    }
+  }
+  // the row before this wave's first row (unmono: its own predecessor)
+  const int64_t first = wb;
+  int64_t t_before = 0;
+  if (lane == 0 && first > C && first < n_ext) t_before = x.batch.ts[first - C - 1];
+  // ---- prepare (prep_row semantics)
+  PrepAcc acc;
+  uint32_t k[R], v[R], xo[R];
+  int64_t tprev_round = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t idx = wb + r * 64 + lane;
+    const bool ok = idx < n_ext;
+    const int64_t li = ok ? idx : n_ext - 1;
+    const int64_t t = pr[r].ts;
+    uint32_t f;
+    uint32_t key = 0;
+    // predecessor row's ts: lane - 1 of this round, the previous round's lane
+    // 63 for lane 0, the row before the wave for the wave's first row
+    int64_t tp = __shfl_up(t, 1, 64);
+    const int64_t last63 = __shfl(t, 63, 64);
+    if (lane == 0) tp = r > 0 ? tprev_round : t_before;
+    tprev_round = last63;
+    if (li < C) {
+      f = F_CAND;
+      key = kk[r];
+      if (ok) acc.ctmax = t > (long long)acc.ctmax ? t : acc.ctmax;
+    } else {
+      PreCtx cx{&pr[r]};
+      const bool p1 = a.is_a && eval_fpred(a.f1.fp, cx);
+      f = F_NEW;
+      if (kn[r] && a.null_skip) {
+        f |= F_SKIP;
+      } else {
+        if (a.is_b) f |= F_B;
+        if (p1) {
+          f |= F_CAND;
+          acc.created += ok ? 1u : 0u;
+        }
+        key = kn[r] ? 0u : kk[r];
+      }
+      if (ok) {
+        acc.tmin = t < acc.tmin ? t : acc.tmin;
+        acc.tmax = t > acc.tmax ? t : acc.tmax;
+        const bool has_prev = li - C > 0;
+        acc.unmono |= (has_prev && tp > t) ? 1ull : 0ull;
+      }
+    }
+    if (ok && !(f & F_SKIP)) {
+      acc.kmax = key > acc.kmax ? key : acc.kmax;
+      acc.kmin = key < acc.kmin ? key : acc.kmin;
+    }
+    const int64_t d = t - tbase;
+    if (ok) acc.ovf |= d != (int64_t)(int32_t)d;
+    k[r] = key;
+    v[r] = (f << kRowBits) | (uint32_t)li;
+    xo[r] = (uint32_t)(int32_t)d;
+  }
+  rs_scatter_tile<uint32_t, R, true, true>(k, v, xo, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
+  prep_block_reduce<kRsBlock>(acc, blk, tile);
+}
+
+}  // namespace
+
+// Fused prepare + first hashed pass (bits 0..7 of key_bucket_mix), FAST plans
+// with a plain 32-bit key column; f1 reads attributes a0 / a1 (-1: none).
+// Writes the pass's (key, flags|row, ts32) triples to kout / vout / tout and
+// one PrepAgg per tile to blk (fold with k_finish_prep).
+int prep_scatter_tiles(int64_t n_ext) { return (int)((n_ext + rs_tile(kPrepRounds) - 1) / rs_tile(kPrepRounds)); }
+
+void launch_prep_scatter(const PrepArgs* d_args, int64_t n_ext, const uint32_t* hist, const uint32_t* offs,
+                         const uint32_t* dtot, int nb, int a0, int a1, uint32_t* kout, uint32_t* vout, uint32_t* tout,
+                         PrepAgg* blk, hipStream_t s) {
+  hipLaunchKernelGGL(k_prep_scatter<kPrepRounds>, dim3(nb), dim3(kRsBlock), 0, s, d_args, n_ext, hist, offs, dtot, nb,
+                     a0, a1, kout, vout, tout, blk);
+  SHD_CHECK_LAUNCH();
+}
+
+namespace {
+}  // namespace
+
+int group_walk_blocks(int ngroups) { return ngroups < 8192 ? ngroups : 8192; }
+
+void launch_group_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, const uint32_t* skey,
+                       const uint32_t* spv, const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row,
+                       uint8_t* pst, ScanOut* blk, hipStream_t s) {
+  const int ngroups = 1 << bits;
+  SHD_HIP(hipMemsetAsync(gbeg, 0, (size_t)ngroups * 4, s));
+  SHD_HIP(hipMemsetAsync(gend, 0, (size_t)ngroups * 4, s));
+  hipLaunchKernelGGL(k_group_bounds, dim3(grid_for(n_ext, 1, 4096)), dim3(kBlock), 0, s, skey, spv, n_ext, bits, gbeg,
+                     gend);
+  SHD_CHECK_LAUNCH();
+  const int nb = group_walk_blocks(ngroups);
+  if (fast)
+    hipLaunchKernelGGL(k_group_walk<true>, dim3(nb), dim3(kGwThreads), 0, s, d_args, ngroups, bits,
+                       (const uint32_t*)gbeg, (const uint32_t*)gend, skey, spv, sts, match_row, pst, blk);
+  else
+    hipLaunchKernelGGL(k_group_walk<false>, dim3(nb), dim3(kGwThreads), 0, s, d_args, ngroups, bits,
+                       (const uint32_t*)gbeg, (const uint32_t*)gend, skey, spv, sts, match_row, pst, blk);
+  SHD_CHECK_LAUNCH();
+}
+
+}  // namespace pat
+}  // namespace shd

@@ -140,6 +140,7 @@ struct NfaRunArgs {
   int64_t nlanes;
   int64_t seq0;
   int64_t start_time;   // app start (seed of unpartitioned plans)
+  const uint8_t* skip_start;   // hand-over replay: rows the start state does not see (Replay::skip_start)
   // window-lane mode (unpartitioned every-started plans): lane c owns the
   // events [c*chunk_len, (c+1)*chunk_len); lanes c < c_exact start at row 0
   // from a copy of the carried state (exact), the others replay the `warm`
@@ -164,6 +165,7 @@ struct NfaRunArgs {
   // staged output rows
   int64_t R;
   uint64_t *st_tag, *st_p, *st_s, *st_t;
+  int32_t* st_sidx;
   int64_t* st_ts;
   int32_t* st_type;
   uint64_t* st_vals;
@@ -212,6 +214,8 @@ struct Lane {
   unsigned long long partials, scans;
   uint32_t tagc;
   uint64_t t_prim, t_sec, t_ter;
+  int32_t cur_state = 0;   // state id of the processor whose rows emit() stages (shd_out.state_idx)
+  int32_t ret_state = 0;   // single-receiver runs: the state of the returned events
   int64_t last_seq;
   bool quiet;   // window lanes: warm-up events (no output)
 #ifdef SHD_NFA_PROF
@@ -1041,6 +1045,7 @@ struct Lane {
   __device__ void absentSendEvent(int p, uint16_t s) {   // AbsentStreamPreStateProcessor.sendEvent
     const DPre& pr = P.pre[p];
     const DPost& tp = P.post[pr.thisPost];
+    cur_state = pr.stateId;
     if (tp.hasSelector && accepts(s)) emit(s, new_tag());
     if (tp.nextPre >= 0) addState(tp.nextPre, s);
     if (tp.nextEvery >= 0) addEveryState(tp.nextEvery, s);
@@ -1112,6 +1117,7 @@ struct Lane {
   __device__ void absentLogicalSendEvent(int p, uint16_t s) {   // AbsentLogicalPreStateProcessor.sendEvent
     const DPre& pr = P.pre[p];
     const DPost& tp = P.post[pr.thisPost];
+    cur_state = pr.stateId;
     if (tp.hasSelector && accepts(s)) emit(s, new_tag());
     if (tp.nextPre >= 0) addState(tp.nextPre, s);
     if (tp.nextEvery >= 0) {
@@ -1205,6 +1211,7 @@ struct Lane {
     A.st_p[idx] = t_prim;
     A.st_s[idx] = t_sec;
     A.st_t[idx] = t_ter;
+    A.st_sidx[idx] = cur_state;
     NFA_PROF_ADD(4, t4);
   }
 
@@ -1284,6 +1291,8 @@ struct Lane {
     NFA_PROF_T0(t2);
     stabilize(si, ts);
     NFA_PROF_ADD(2, t2);
+    // hand-over replay: a stabilize-only event (Replay::skip_start 2)
+    if (A.skip_start && A.skip_start[row] == 2) return;
     NFA_PROF_T0(t3);
     const int np = P.nsp[si];
     last_seq = A.seq0 + row;
@@ -1295,6 +1304,8 @@ struct Lane {
       t_ter = 0;
       for (int k = np - 1; k >= 0; k--) {
         misc(MISC_TMPN) = 0;
+        if (A.skip_start && A.skip_start[row] && P.pre[P.streamPres[si][k]].isStart) continue;
+        cur_state = P.pre[P.streamPres[si][k]].stateId;
         processAndReturn(P.streamPres[si][k], rec);
         uint64_t tag = ~0ull;
         int nret = misc(MISC_TMPN);
@@ -1309,7 +1320,9 @@ struct Lane {
     } else if (np == 1) {
       // SingleProcessStreamReceiver: returned events are selected when the run ends
       misc(MISC_TMPN) = 0;
-      processAndReturn(P.streamPres[si][0], rec);
+      ret_state = P.pre[P.streamPres[si][0]].stateId;
+      if (!(A.skip_start && A.skip_start[row] && P.pre[P.streamPres[si][0]].isStart))
+        processAndReturn(P.streamPres[si][0], rec);
       int nret = misc(MISC_TMPN);
       for (int i = 0; i < nret; i++) push_ret(tmpl(i));
       misc(MISC_TMPN) = 0;
@@ -1321,6 +1334,7 @@ struct Lane {
   __device__ void flush_run() {
     int n = misc(MISC_RETN);
     if (n == 0) return;
+    cur_state = ret_state;
     t_prim = 2 * (uint64_t)last_seq + 1;
     t_sec = 0;
     t_ter = 0;
@@ -1796,8 +1810,9 @@ __global__ void k_tag_heads(const uint64_t* tag, const uint32_t* perm, int64_t n
 }
 __global__ void k_out_rows(const uint32_t* perm, const uint32_t* hpos, const uint32_t* head, int64_t n, int nout,
                            int64_t chunk0, int64_t row0, const int64_t* sts, const int32_t* stype,
-                           const uint64_t* svals, const uint8_t* snul, const uint64_t* sprim, int64_t* o_chunk,
-                           int32_t* o_type, int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq) {
+                           const uint64_t* svals, const uint8_t* snul, const uint64_t* sprim,
+                           const int32_t* ssidx, int64_t* o_chunk, int32_t* o_type, int64_t* o_ts,
+                           uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq, int32_t* o_sidx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = perm[i];
     const int64_t r = row0 + i;
@@ -1806,6 +1821,7 @@ __global__ void k_out_rows(const uint32_t* perm, const uint32_t* hpos, const uin
     o_ts[r] = sts[j];
     // primary tag: 2 * seq + 1 for an event's rows, 2 * (first seq of the call) for timer rows
     o_seq[r] = (int64_t)(sprim[j] >> 1);
+    o_sidx[r] = ssidx[j];
     for (int c = 0; c < nout; c++) {
       o_vals[r * nout + c] = svals[j * nout + c];
       o_nul[r * nout + c] = snul[j * nout + c];
@@ -2080,7 +2096,7 @@ struct NfaEngine : Engine {
   DevBuf d_offs, d_call_of, d_last, d_now, d_changed, d_first, d_key, d_keyed, d_pos, d_runs, d_run, d_ck64,
       d_ck64_alt, d_ck32, d_ck32_alt, d_crow, d_crow_alt, d_head, d_hpos, d_seg_start, d_seg_key, d_seg_slot,
       d_slot_seg, d_ctl, d_scan, d_sort;
-  DevBuf st_tag, st_p, st_s, st_t, st_ts, st_type, st_vals, st_nul, d_perm, d_perm_alt, d_skey, d_skey_alt, d_thead,
+  DevBuf st_sidx, st_tag, st_p, st_s, st_t, st_ts, st_type, st_vals, st_nul, d_perm, d_perm_alt, d_skey, d_skey_alt, d_thead,
       d_thpos;
   int64_t R = 0;
   PinnedBuf h_ctl, h_up;
@@ -2228,6 +2244,7 @@ struct NfaEngine : Engine {
     st_p.reserve(rows * 8);
     st_s.reserve(rows * 8);
     st_t.reserve(rows * 8);
+    st_sidx.reserve(rows * 4);
     st_ts.reserve(rows * 8);
     st_type.reserve(rows * 4);
     st_vals.reserve(rows * nout * 8);
@@ -2418,6 +2435,7 @@ struct NfaEngine : Engine {
 
     NfaRunArgs ra{};
     if (b) ra.batch = b->cs;
+    ra.skip_start = b ? b->skip_start : nullptr;
     ra.stream = si;
     ra.partitioned = partitioned;
     ra.ncalls = ncalls;
@@ -2480,6 +2498,7 @@ struct NfaEngine : Engine {
     ra.st_p = st_p.as<uint64_t>();
     ra.st_s = st_s.as<uint64_t>();
     ra.st_t = st_t.as<uint64_t>();
+    ra.st_sidx = st_sidx.as<int32_t>();
     ra.st_ts = st_ts.as<int64_t>();
     ra.st_type = st_type.as<int32_t>();
     ra.st_vals = st_vals.as<uint64_t>();
@@ -2637,8 +2656,9 @@ struct NfaEngine : Engine {
                        (const uint32_t*)d_thpos.as<uint32_t>(), (const uint32_t*)d_thead.as<uint32_t>(), m, prog.nout,
                        chunk_seq, out.count, (const int64_t*)st_ts.as<int64_t>(),
                        (const int32_t*)st_type.as<int32_t>(), (const uint64_t*)st_vals.as<uint64_t>(),
-                       (const uint8_t*)st_nul.as<uint8_t>(), (const uint64_t*)st_p.as<uint64_t>(), out.d_chunk(),
-                       out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
+                       (const uint8_t*)st_nul.as<uint8_t>(), (const uint64_t*)st_p.as<uint64_t>(),
+                       (const int32_t*)st_sidx.as<int32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(),
+                       out.d_nulls(), out.d_seq(), out.d_sidx());
     SHD_CHECK_LAUNCH();
     // chunk ids consumed = number of distinct tags
     SHD_HIP(hipMemcpyAsync(h_ctl.as<char>() + 64, d_thpos.as<uint32_t>() + (m - 1), 4, hipMemcpyDeviceToHost, s));
@@ -2708,6 +2728,7 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
     }
 
   auto e = std::make_unique<NfaEngine>();
+  e->layout_hint = list_hint;   // recorded in snapshots (the restore rebuilds the same layout)
   NfaProg& P = e->prog;
   P.npre = npre;
   P.nstates = p.n_states;

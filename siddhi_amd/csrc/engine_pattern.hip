@@ -20,286 +20,24 @@
 // and the matches of event j come out in P_i creation order.  The kernels
 // evaluate exactly that, per partial in parallel, over key-sorted micro-batches;
 // open partials carry to the next push.  A per-key timestamp decrease is
-// detected on device and rejected (SHD_E_UNSUPPORTED), never approximated.
+// detected on device and the query continues on the generic NFA engine with
+// its open partials (NeedNfa hand-over, shd_api.cpp switch_to_nfa), never
+// approximated.
 #include <algorithm>
+#include <unordered_map>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
 #include "engine.h"
 #include "radix_tile.h"
+#include "pattern_common.h"
 
 namespace shd {
 
+using namespace pat;
+
 namespace {
-
-enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
-// Per-position scan result (positions = key-sorted order when partitioned).
-enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5, ST_YIELD = 6 };
-// per-position outcome stored by k_forward_scan for the compaction kernels
-// PS_CONT: a capped lane walk stopped before position match_row[p] (long
-// walk, continued by the wave-cooperative pass)
-enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3, PS_CONT = 4 };
-
-// Sort payload: row index of the extended batch (28 bits) | flags (4 bits).
-constexpr int kRowBits = 28;
-constexpr uint32_t kRowMask = (1u << kRowBits) - 1;
-__device__ __forceinline__ uint32_t pv_row(uint32_t pv) { return pv & kRowMask; }
-__device__ __forceinline__ uint32_t pv_flags(uint32_t pv) { return pv >> kRowBits; }
-
-// Row addressing over the extended batch: rows [0, C) are carried partials
-// (stream A columns), rows [C, C+n) are the pushed batch.
-struct ExtRows {
-  ColSet carry;   // stream A schema
-  ColSet batch;   // pushed stream schema
-  int64_t C;
-  int64_t seq0;           // global seq of batch row 0
-  const int64_t* carry_seq;
-  // logical AND: rows [C + n, 2C + n) are the operand events the carried
-  // half-filled partials hold (stream B schema; row C + n + i for carry row i)
-  ColSet half;
-  const int64_t* half_seq;
-  // dense grouped walks: the e2-side attributes the filters read, copied into
-  // key-sorted position order (bit a of bpos_mask: attribute a is there), so
-  // the 64 positions a wave steps over load coalesced instead of one row each
-  ColSet bpos;
-  uint32_t bpos_mask;
-  __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : (r < C + batch.n ? batch : half); }
-  __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : (r < C + batch.n ? r - C : r - C - batch.n); }
-  __device__ __forceinline__ int64_t ts(int64_t r) const {
-#ifdef SHD_DEBUG
-    if (r < 0 || r >= C + batch.n) {
-      printf("SHD_DEBUG ExtRows.ts: row %lld C %lld n %lld\n", (long long)r, (long long)C, (long long)batch.n);
-      return 0;
-    }
-#endif
-    if (r < C) return gld(carry.ts, r);
-    if (r < C + batch.n) return gld(batch.ts, r - C);
-    return gld(half.ts, r - C - batch.n);
-  }
-  __device__ __forceinline__ int64_t seq(int64_t r) const {
-    return r < C ? carry_seq[r] : (r < C + batch.n ? seq0 + (r - C) : half_seq[r - C - batch.n]);
-  }
-};
-
-// Expression context over (e1 row, second-state row); stream-state chains
-// hold one event.  s2: the state id r2 fills (1 for e1 -> e2; for the logical
-// OR form the branch that matched -- the partner slot is always empty then).
-struct PairCtx {
-  const ExtRows* x;
-  int64_t r1, r2;   // ext rows of state 0 / state s2 (-1 = empty slot)
-  int s2 = 1;
-  bool matched = false;   // projection of a completed partial
-  int64_t r3 = -1;        // logical AND: the partner operand's row (state s3)
-  int s3 = -1;
-  int64_t q2 = -1;        // sorted position of r2 (walks; -1 in the projection)
-  __device__ __forceinline__ int64_t slot(int st, int idx) const {
-    int64_t r = st == 0 ? r1 : (st == s2 ? r2 : (st == s3 ? r3 : -1));
-    if (r < 0) return -1;
-    // StateEvent.getStreamEvent(int[]) on a one-event chain: index 0 / CURRENT hit it
-    return (idx == 0 || idx == SHD_IDX_CURRENT) ? r : -1;
-  }
-  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
-    int64_t r = slot(st, idx);
-    if (r < 0) {
-      Val v;
-      v.b = 0;
-      v.null = 1;
-      return v;
-    }
-    // branch on the row's table instead of selecting a per-lane ColSet
-    // pointer: each branch reads a wave-uniform column table (scalar loads)
-    if (st == s2 && q2 >= 0 && ((x->bpos_mask >> attr) & 1u)) return col_load(x->bpos, q2, attr);
-    if (r < x->C) return col_load(x->carry, r, attr);
-    if (r < x->C + x->batch.n) return col_load(x->batch, r - x->C, attr);
-    return col_load(x->half, r - x->C - x->batch.n, attr);
-  }
-  __device__ __forceinline__ bool evnull(int st, int idx) const { return slot(st, idx) < 0; }
-  // eventTimestamp() reads the StateEvent's timestamp: e1's while the e2 filters
-  // run, the completing event's once matched (StreamPostStateProcessor.java:64-83
-  // sets it before the selector)
-  __device__ __forceinline__ int64_t ts(int, int) const { return x->ts(matched ? r2 : r1); }
-  __device__ __forceinline__ Val agg(int) const {
-    Val v;
-    v.b = 0;
-    v.null = 1;
-    return v;
-  }
-};
-
-// Expression context of k_prepare: the pushed event as state 0 (stream-state
-// chain of one event), read from the uniform batch column table.
-struct BatchRowCtx {
-  const ColSet* cs;
-  int64_t row;
-  __device__ __forceinline__ Val load(int st, int idx, int attr) const {
-    if (st != 0 || !(idx == 0 || idx == SHD_IDX_CURRENT)) {
-      Val v;
-      v.b = 0;
-      v.null = 1;
-      return v;
-    }
-    return col_load(*cs, row, attr);
-  }
-  __device__ __forceinline__ bool evnull(int st, int idx) const { return !(st == 0 && (idx == 0 || idx == SHD_IDX_CURRENT)); }
-  __device__ __forceinline__ int64_t ts(int st, int idx) const { return evnull(st, idx) ? 0 : cs->ts[row]; }
-  __device__ __forceinline__ Val agg(int) const {
-    Val v;
-    v.b = 0;
-    v.null = 1;
-    return v;
-  }
-};
-
-__device__ __forceinline__ uint64_t canon_key(Val v, int type) {
-  switch (type) {
-    case SHD_T_FLOAT: return p_f64((double)v_f32(v.b));
-    default: return v.b;
-  }
-}
-
-// Batch-wide aggregates written by k_prepare (one 64-byte block):
-//   [0] candidates created  [1] max key  [2] min batch ts  [3] max batch ts
-struct PrepAgg {
-  unsigned long long n_cand;
-  unsigned long long kmax;
-  long long ts_min;
-  long long ts_max;
-  unsigned long long ovf;   // some row's ts - batch.ts[0] does not fit in int32
-  unsigned long long unmono;   // some batch row's ts is below its predecessor's
-  long long carry_tmax;        // latest carried partial (LLONG_MIN: none)
-  unsigned long long kmin;     // smallest key (rows with a key)
-};
-
-struct PrepArgs {
-  ExtRows x;
-  DExprSet es;
-  DFilters f1;
-  int is_a, is_b;           // pushed stream plays A and/or B
-  int partitioned;          // write a key per row
-  int null_skip;            // partition key semantics: null key -> event dropped (F_SKIP)
-  int key64;                // key written as u64 (long / double / float keys)
-  DExpr key_expr;           // key expression of the pushed stream
-  int key_type;
-  int key_col;              // >= 0: plain attribute key of the pushed stream
-  const uint64_t* carry_key;
-};
-
-template <class T>
-__device__ __forceinline__ T wave_max(T v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    T t = __shfl_xor(v, o, 64);
-    v = t > v ? t : v;
-  }
-  return v;
-}
-template <class T>
-__device__ __forceinline__ T wave_min(T v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    T t = __shfl_xor(v, o, 64);
-    v = t < v ? t : v;
-  }
-  return v;
-}
-
-// Running per-thread aggregates of the row preparation (PrepAgg fields).
-struct PrepAcc {
-  unsigned long long created = 0, kmax = 0, ovf = 0, unmono = 0, kmin = ULLONG_MAX;
-  long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctmax = LLONG_MIN;
-};
-
-// One extended row: key, flags (F_CAND / F_NEW / F_B / F_SKIP) and the
-// timestamp as a 32-bit offset from the batch's first event (acc.ovf when it
-// does not fit: the push then falls back to a 64-bit gather after the sort).
-// Every load of the row is issued before the first use (ts, key, f1
-// operands); the null-key test comes last.  FAST: the f1 chain is a
-// pre-decoded conjunction and the key a plain column (no interpreter).
-template <bool FAST>
-__device__ __forceinline__ void prep_row(const PrepArgs& a, const DExprSet& es, int64_t r, int64_t tbase,
-                                         bool count, uint64_t& k, uint32_t& f, int32_t& tso, PrepAcc& acc) {
-  const ExtRows& x = a.x;
-  long long t;
-  k = 0;
-  if (r < x.C) {
-    k = a.partitioned ? gld(a.carry_key, r) : 0;
-    f = F_CAND;
-    t = (long long)gld(x.carry.ts, r);
-    if (count) acc.ctmax = t > acc.ctmax ? t : acc.ctmax;
-  } else {
-    const int64_t br = r - x.C;
-    BatchRowCtx cx{&x.batch, br};
-    t = (long long)gld(x.batch.ts, br);
-    const long long tprev = br > 0 ? (long long)gld(x.batch.ts, br - 1) : t;
-    Val kv;
-    kv.b = 0;
-    kv.null = 0;
-    if (a.partitioned) {
-      if (FAST || a.key_col >= 0) kv = col_load(x.batch, br, a.key_col);
-      else kv = eval_expr(es.ins + a.key_expr.off, a.key_expr.len, es.consts, cx);
-    }
-    const bool p1 = a.is_a && (FAST ? eval_fpred(a.f1.fp, cx) : eval_filters(es, a.f1, cx));
-    f = F_NEW;
-    if (kv.null && a.null_skip) {
-      f |= F_SKIP;   // PartitionStreamReceiver drops null keys
-    } else {
-      if (a.is_b) f |= F_B;
-      if (p1) {
-        f |= F_CAND;
-        acc.created += count ? 1u : 0u;
-      }
-      k = kv.null ? 0 : canon_key(kv, a.key_type);
-    }
-    if (count) {
-      acc.tmin = t < acc.tmin ? t : acc.tmin;
-      acc.tmax = t > acc.tmax ? t : acc.tmax;
-      acc.unmono |= tprev > t;
-    }
-  }
-  if (a.partitioned) {
-    if (!a.key64) k = (uint32_t)k;   // 32-bit key types: the dictionary id / int bits
-    if (count && !(f & F_SKIP)) {
-      acc.kmax = k > acc.kmax ? k : acc.kmax;
-      acc.kmin = k < acc.kmin ? k : acc.kmin;
-    }
-  }
-  const int64_t dt = (int64_t)t - tbase;
-  if (count) acc.ovf |= dt != (int64_t)(int32_t)dt;
-  tso = (int32_t)dt;
-}
-
-// Per-block fold of the PrepAcc partials into blk[slot] (plain store;
-// k_finish_prep folds the blocks): no same-address atomics from every wave.
-template <int NT>
-__device__ __forceinline__ void prep_block_reduce(PrepAcc acc, PrepAgg* blk, int slot) {
-  for (int o = 32; o > 0; o >>= 1) {
-    acc.created += __shfl_xor(acc.created, o, 64);
-    acc.ovf |= __shfl_xor(acc.ovf, o, 64);
-    acc.unmono |= __shfl_xor(acc.unmono, o, 64);
-  }
-  acc.kmax = wave_max(acc.kmax);
-  acc.kmin = wave_min(acc.kmin);
-  acc.tmin = wave_min(acc.tmin);
-  acc.tmax = wave_max(acc.tmax);
-  acc.ctmax = wave_max(acc.ctmax);
-  __shared__ PrepAgg wpart[NT / 64];
-  if ((threadIdx.x & 63) == 0)
-    wpart[threadIdx.x >> 6] = PrepAgg{acc.created, acc.kmax, acc.tmin, acc.tmax, acc.ovf, acc.unmono, acc.ctmax, acc.kmin};
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    PrepAgg r = wpart[0];
-    for (int w = 1; w < NT / 64; w++) {
-      r.ovf |= wpart[w].ovf;
-      r.unmono |= wpart[w].unmono;
-      r.carry_tmax = wpart[w].carry_tmax > r.carry_tmax ? wpart[w].carry_tmax : r.carry_tmax;
-      r.kmin = wpart[w].kmin < r.kmin ? wpart[w].kmin : r.kmin;
-      r.n_cand += wpart[w].n_cand;
-      r.kmax = wpart[w].kmax > r.kmax ? wpart[w].kmax : r.kmax;
-      r.ts_min = wpart[w].ts_min < r.ts_min ? wpart[w].ts_min : r.ts_min;
-      r.ts_max = wpart[w].ts_max > r.ts_max ? wpart[w].ts_max : r.ts_max;
-    }
-    blk[slot] = r;
-  }
-}
 
 // Per extended row: key and packed (flags, row) sort payload (prep_row), for
 // the key sort of the sort path.
@@ -467,33 +205,6 @@ __global__ __launch_bounds__(kBlock) void k_sorted_ts64(const ExtRows* __restric
   for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p = n) sts64[p] = x.ts(pv_row(spv[p]));
 }
 
-struct ScanArgs {
-  ExtRows x;
-  DExprSet es;
-  DFilters f2;
-  // logical OR second state `(e2=B[f2] or e3=B[f3])`: f2 = the filters of the
-  // processor that sees an event first (state s_first), f3 = its partner's
-  DFilters f3;
-  int logical;          // 0: e1 -> e2, 1: OR, 2: AND
-  int s_first, s_second;
-  const uint8_t* carry_half;   // AND: operands already filled per carried partial (bit 0 first, bit 1 second)
-  int64_t within;
-  int partitioned;
-  int prune;            // drop partials that can no longer match (horizon guard on later pushes)
-  int64_t t_end;        // latest event time of this push
-  // hashed buckets (0: positions are sorted by the full key): positions are
-  // grouped by the low bits of key_bucket_mix(key), keys of one bucket
-  // interleaved in input order.  Only set when the batch rows are globally
-  // time-ordered, carried partials precede them in time, and prune is on.
-  uint32_t hash_mask;
-};
-
-struct ScanOut {
-  unsigned long long steps;   // (partial, event) pairs examined
-  unsigned long long pruned;  // open partials dropped by the horizon rule
-  uint32_t violation;         // per-key timestamp decrease seen
-  uint32_t hbm_walks;         // bucketed walk: partials walked on in HBM (lookahead too short)
-};
 // d_agg layout: PrepAgg at 0, ScanOut at 64, match / open totals at 128
 static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
 
@@ -978,7 +689,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       if (a.logical == 2) match_other[p] = other;
       nm++;
     } else if (st == ST_OPEN) {
-      out = PS_OPEN;
+      out = PS_OPEN | PS_PEND;
       no++;
       if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
     } else if (st == ST_PRUNED) {
@@ -1034,7 +745,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         if (a.logical == 2) match_other[p] = (int32_t)((j >> kRowBits) ? ra : rb);
         nm++;
       } else if (st == ST_OPEN) {
-        out = PS_OPEN;
+        out = PS_OPEN | PS_PEND;   // it met a B event of its key: in the pending list now
         no++;
         if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
       } else if (st == ST_PRUNED) {
@@ -1078,7 +789,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         match_row[p] = j;
         nm++;
       } else if (st == ST_OPEN) {
-        out = PS_OPEN;
+        out = PS_OPEN | PS_PEND;
         no++;
       } else if (st == ST_PRUNED) {
         pruned++;
@@ -1367,7 +1078,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const uint8_t* __restrict
       const uint32_t o = (wv[i >> 2] >> ((i & 3) * 8)) & 255u;
       const bool in = pb + i < t1;
       nm += (in && o == PS_MATCH) ? 1u : 0u;
-      no += (in && o == PS_OPEN) ? 1u : 0u;
+      no += (in && (o & 0x7Fu) == PS_OPEN) ? 1u : 0u;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -1415,7 +1126,7 @@ __device__ __forceinline__ void tile_compact(const uint8_t* __restrict__ pst, in
     uint32_t hit = 0;   // bit i: position pb + i is wanted
 #pragma unroll
     for (int i = 0; i < 16; i++)
-      if (((wv[i >> 2] >> ((i & 3) * 8)) & 255u) == want && pb + i < t1) hit |= 1u << i;
+      if (((wv[i >> 2] >> ((i & 3) * 8)) & 127u) == want && pb + i < t1) hit |= 1u << i;   // (PS_PEND masked)
     const uint32_t cnt = (uint32_t)__popc(hit);
     uint32_t inc = cnt;
 #pragma unroll
@@ -1509,7 +1220,8 @@ struct ProjArgs {
 
 __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj,
                                                     const uint32_t* pi, int64_t m, int64_t* o_chunk, int32_t* o_type,
-                                                    int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq) {
+                                                    int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq,
+                                                    int32_t* o_sidx) {
   const ProjArgs& a = *ap;
   __shared__ LdsProg prog;
   const DExprSet es = stage_prog(a.es, prog);
@@ -1536,6 +1248,7 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
     o_ts[row] = x.ts(j);
     o_type[row] = 0;
     o_seq[row] = x.seq(j);
+    o_sidx[row] = br ? a.s_second : a.s_first;   // the processor that completed the partial
     // MultiProcessStreamReceiver: one callback chunk per (event, processor)
     o_chunk[row] = a.logical ? 2 * x.seq(j) + br : (a.multi ? x.seq(j) : a.chunk0 + k);
   }
@@ -1552,6 +1265,10 @@ struct GatherArgs {
   int64_t* dts;
   uint64_t* dkey;
   int64_t* dseq;
+  uint32_t amask;   // k_gather_list: stream-A columns to copy
+  // new-list / pending-list placement of each carried partial (export_replay)
+  uint8_t* dpend;
+  const uint8_t* pend_old;
   // logical AND: filled-operand bits + the held operand event (stream B)
   int and_mode;
   const int32_t* match_row;
@@ -1599,6 +1316,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __res
     a.dts[o] = x.ts(r);
     a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
     a.dseq[o] = x.seq(r);
+    a.dpend[o] = (uint8_t)(((pst[p] & PS_PEND) || (r < x.C && a.pend_old[r])) ? 1 : 0);
     if (a.and_mode) {
       const uint32_t mr = (uint32_t)a.match_row[p];
       const uint32_t fm = mr >> kRowBits;
@@ -1619,8 +1337,81 @@ __global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __res
   });
 }
 
+// Carry gather (plain / OR forms), two kernels: k_open_list compacts the
+// positions of the still-open partials in position order (one lane per
+// position, wave ballots + a block prefix); k_gather_list then gives every
+// open partial its own thread, so all their random row reads are in flight at
+// once.  Only the e1 columns read again after the carry (amask) are copied.
+__global__ __launch_bounds__(kBlock) void k_open_list(const uint8_t* __restrict__ pst, const uint32_t* __restrict__ boff,
+                                                      int64_t n, int64_t tile, uint32_t* __restrict__ olist) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t base = boff[gridDim.x + blockIdx.x];
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
+    const int64_t p = c0 + threadIdx.x;
+    const uint8_t ps = p < t1 ? pst[p] : (uint8_t)PS_NONE;
+    const bool hit = (ps & 0x7Fu) == PS_OPEN;
+    const uint64_t m = __ballot(hit);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; k++) {
+      pre += k < w ? wsum[k] : 0u;
+      tot += wsum[k];
+    }
+    if (hit) olist[base + pre + (uint32_t)__popcll(m & lt)] = (uint32_t)p;
+    base += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __restrict__ ap,
+                                                        const uint32_t* __restrict__ olist, int64_t n_open,
+                                                        const uint8_t* __restrict__ pst,
+                                                        const uint32_t* __restrict__ spv,
+                                                        const uint32_t* __restrict__ skey32,
+                                                        const uint64_t* __restrict__ skey64) {
+  const GatherArgs& a = *ap;
+  const ExtRows& x = a.x;
+  for (int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x; o < n_open; o = n_open) {
+    const int64_t p = olist[o];
+    const int64_t r = pv_row(spv[p]);
+    // one uniform column table per branch (carried rows / pushed rows)
+    if (r < x.C) {
+      for (int c = 0; c < a.ncols; c++) {
+        if (!((a.amask >> c) & 1u)) continue;
+        const Val v = col_load(x.carry, r, c);
+        store_col(a.dcol[c], a.types[c], o, v.b);
+        a.dnul[c][o] = (uint8_t)v.null;
+      }
+      a.dts[o] = gld(x.carry.ts, r);
+      a.dseq[o] = x.carry_seq[r];
+    } else {
+      const int64_t br = r - x.C;
+      for (int c = 0; c < a.ncols; c++) {
+        if (!((a.amask >> c) & 1u)) continue;
+        const Val v = col_load(x.batch, br, c);
+        store_col(a.dcol[c], a.types[c], o, v.b);
+        a.dnul[c][o] = (uint8_t)v.null;
+      }
+      a.dts[o] = gld(x.batch.ts, br);
+      a.dseq[o] = x.seq0 + br;
+    }
+    a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
+    a.dpend[o] = (uint8_t)(((pst[p] & PS_PEND) || (r < x.C && a.pend_old[r])) ? 1 : 0);
+  }
+}
+
 struct CarryTable {
   DevBuf col[kMaxCols], nul[kMaxCols], ts, key, seq;
+  // 1: the partial met a B event of its key after it was created -- it left
+  // the new list for the pending list (StreamPreStateProcessor.updateState);
+  // 0: still in the new list (export_replay rebuilds the placement)
+  DevBuf pend;
   // logical AND: filled-operand bits and the held operand event (stream B)
   DevBuf half, bcol[kMaxCols], bnul[kMaxCols], bts, bseq;
   void reserve_b(int64_t n, const std::vector<int>& types) {
@@ -1653,6 +1444,7 @@ struct CarryTable {
     ts.reserve(std::max<int64_t>(n, 1) * 8);
     key.reserve(std::max<int64_t>(n, 1) * 8);
     seq.reserve(std::max<int64_t>(n, 1) * 8);
+    pend.reserve(std::max<int64_t>(n, 1));
   }
   ColSet colset(const std::vector<int>& types) const {
     ColSet cs{};
@@ -1773,16 +1565,21 @@ struct PatternEngine : Engine {
   bool have_horizon = false;
   int64_t horizon = INT64_MIN;
   int64_t t_last = INT64_MIN;   // time of the last event (arrival order) of the committed pushes
+  int64_t last_b_seq = -1;      // arrival index of the last B-stream event (export_replay placement)
   static constexpr int64_t kPruneMinRows = 1 << 16;
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
-      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot;
+      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_gbeg, d_gend, d_olist;
+  // stream-A attributes read again after a partial is carried (state-0 loads
+  // of f2 / f3 / the selector): only these columns are copied into the carry
+  uint32_t carry_mask = ~0u;
   PinnedBuf h_agg;
 
   int kind() const override { return ENG_PATTERN; }
 
   void reset() override {
     C = 0;
+    last_b_seq = -1;
     seq = 0;
     now = INT64_MIN;
     chunk_seq = 0;
@@ -1800,54 +1597,105 @@ struct PatternEngine : Engine {
   // replayed partial i exactly as it did the first time: f2(i, j) false,
   // |ts_j - ts_i| <= within).  Unpartitioned plans expire globally: partials
   // further than `within` behind the latest event are already gone there.
-  void export_replay(Replay& r) override {
+  // Logical AND: a half-filled partial also needs the event that filled its
+  // operand (LogicalPreStateProcessor: the slot keeps that event).  Replayed
+  // after its partial's A event, that event fills the same operand of the same
+  // partials it filled the first time -- every partial it met then either
+  // still holds it (and is replayed) or is gone -- and, when its own start
+  // partial is gone, it is replayed past the start state only (skip_start),
+  // so it opens no partial the reference does not hold.
+  void export_replay(std::vector<Replay>& parts) override {
     SHD_HIP(hipStreamSynchronize(stream));
     const CarryTable& t = carry[cur];
-    r.stream = sA;
     std::vector<int64_t> ts(C), sq(C);
     if (C > 0) {
       SHD_HIP(hipMemcpy(ts.data(), t.ts.p, C * 8, hipMemcpyDeviceToHost));
       SHD_HIP(hipMemcpy(sq.data(), t.seq.p, C * 8, hipMemcpyDeviceToHost));
     }
-    std::vector<std::vector<uint8_t>> col(typesA.size()), nul(typesA.size());
-    for (size_t c = 0; c < typesA.size(); c++) {
-      col[c].resize((size_t)C * type_size(typesA[c]));
-      nul[c].resize((size_t)C);
-      if (C > 0) {
-        SHD_HIP(hipMemcpy(col[c].data(), t.col[c].p, col[c].size(), hipMemcpyDeviceToHost));
-        SHD_HIP(hipMemcpy(nul[c].data(), t.nul[c].p, (size_t)C, hipMemcpyDeviceToHost));
+    auto host_cols = [&](const std::vector<int>& types, const DevBuf* dcol, const DevBuf* dnul,
+                         std::vector<std::vector<uint8_t>>& col, std::vector<std::vector<uint8_t>>& nul) {
+      col.assign(types.size(), {});
+      nul.assign(types.size(), {});
+      for (size_t c = 0; c < types.size(); c++) {
+        col[c].resize((size_t)C * type_size(types[c]));
+        nul[c].resize((size_t)C);
+        if (C > 0) {
+          SHD_HIP(hipMemcpy(col[c].data(), dcol[c].p, col[c].size(), hipMemcpyDeviceToHost));
+          SHD_HIP(hipMemcpy(nul[c].data(), dnul[c].p, (size_t)C, hipMemcpyDeviceToHost));
+        }
       }
-    }
+    };
+    std::vector<std::vector<uint8_t>> col, nul, bcol, bnul;
+    host_cols(typesA, t.col, t.nul, col, nul);
+    std::vector<uint8_t> half;
+    std::vector<int64_t> bts, bsq;
     if (logical == 2 && C > 0) {
-      std::vector<uint8_t> half(C);
+      half.resize(C);
+      bts.resize(C);
+      bsq.resize(C);
       SHD_HIP(hipMemcpy(half.data(), t.half.p, C, hipMemcpyDeviceToHost));
-      for (int64_t i = 0; i < C; i++)
-        if (half[i])
-          throw Error(SHD_E_UNSUPPORTED,
-                      "pattern engine (and): timestamps go back while a partial holds one operand; the generic "
-                      "NFA engine cannot be seeded with half-filled partials");
+      SHD_HIP(hipMemcpy(bts.data(), t.bts.p, C * 8, hipMemcpyDeviceToHost));
+      SHD_HIP(hipMemcpy(bsq.data(), t.bseq.p, C * 8, hipMemcpyDeviceToHost));
+      host_cols(typesB, t.bcol, t.bnul, bcol, bnul);
     }
-    std::vector<int64_t> idx;
-    for (int64_t i = 0; i < C; i++)
-      if (partitioned || W == INT64_MAX || t_last == INT64_MIN || !(t_last - ts[i] > W)) idx.push_back(i);
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return sq[a] < sq[b]; });
-    r.n = (int64_t)idx.size();
-    r.ts.resize(r.n);
-    r.cols.assign(typesA.size(), {});
-    r.nulls.assign(typesA.size(), {});
-    for (size_t c = 0; c < typesA.size(); c++) {
-      const int w = type_size(typesA[c]);
-      r.cols[c].resize((size_t)r.n * w);
-      r.nulls[c].resize((size_t)r.n);
+    // New-list / pending-list placement (StreamPreStateProcessor.updateState:
+    // a partial leaves the new list at the next B event of its key; expiry
+    // walks the pending list only up to its first live partial but the new
+    // list in full, so the placement matters once time goes back).  The
+    // replayed A events place every partial but the newest of its key (each
+    // later replayed event moves the earlier ones); when the newest too met a
+    // later B event -- one of the events the replay leaves out -- a
+    // stabilize-only replay event (skip_start 2, the newest partial's own
+    // columns and time: it expires nothing that event did not) moves it.
+    std::vector<uint8_t> pend(C, 0);
+    if (C > 0) SHD_HIP(hipMemcpy(pend.data(), t.pend.p, C, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> keyv(C, 0);
+    if (C > 0 && partitioned) SHD_HIP(hipMemcpy(keyv.data(), t.key.p, C * 8, hipMemcpyDeviceToHost));
+    // replay events: (seq, source 0 = A row / 1 = operand row / 2 = stabilize-only, carry index)
+    struct Ev { int64_t seq; int src; int64_t i; };
+    std::vector<Ev> evs;
+    std::unordered_map<uint64_t, int64_t> newest;   // key -> carry index of its newest exported partial
+    for (int64_t i = 0; i < C; i++) {
+      if (!(partitioned || W == INT64_MAX || t_last == INT64_MIN || !(t_last - ts[i] > W))) continue;
+      evs.push_back({sq[i], 0, i});
+      if (!half.empty() && half[i]) evs.push_back({bsq[i], 1, i});
+      const uint64_t k = partitioned ? keyv[i] : 0;
+      auto it = newest.find(k);
+      if (it == newest.end() || sq[i] > sq[it->second]) newest[k] = i;
     }
-    for (int64_t k = 0; k < r.n; k++) {
-      const int64_t i = idx[k];
-      r.ts[k] = ts[i];
-      for (size_t c = 0; c < typesA.size(); c++) {
-        const int w = type_size(typesA[c]);
-        std::memcpy(r.cols[c].data() + k * w, col[c].data() + i * w, w);
-        r.nulls[c][k] = nul[c][i];
+    for (auto& kv : newest) {
+      const int64_t i = kv.second;
+      // unpartitioned: one global list, left by the next B event of the stream
+      const bool moved = partitioned ? pend[i] != 0 : (last_b_seq >= 0 && last_b_seq > sq[i]);
+      if (moved) evs.push_back({sq[i], 2, i});
+    }
+    std::stable_sort(evs.begin(), evs.end(), [](const Ev& a, const Ev& b) {
+      return a.seq != b.seq ? a.seq < b.seq : a.src < b.src;
+    });
+    parts.clear();
+    for (size_t k = 0; k < evs.size(); k++) {
+      const Ev& e = evs[k];
+      if (k > 0 && evs[k - 1].seq == e.seq && e.src != 2) continue;   // one event: A row first (it opens a partial)
+      const int stream_e = e.src == 1 ? sB : sA;
+      const std::vector<int>& types = e.src == 1 ? typesB : typesA;
+      const auto& cc = e.src == 1 ? bcol : col;
+      const auto& nn = e.src == 1 ? bnul : nul;
+      if (parts.empty() || parts.back().stream != stream_e) {
+        parts.emplace_back();
+        Replay& r = parts.back();
+        r.stream = stream_e;
+        r.cols.assign(types.size(), {});
+        r.nulls.assign(types.size(), {});
       }
+      Replay& r = parts.back();
+      r.ts.push_back(e.src == 1 ? bts[e.i] : ts[e.i]);
+      for (size_t c = 0; c < types.size(); c++) {
+        const int w = type_size(types[c]);
+        r.cols[c].insert(r.cols[c].end(), cc[c].begin() + e.i * w, cc[c].begin() + (e.i + 1) * w);
+        r.nulls[c].push_back(nn[c][e.i]);
+      }
+      r.skip_start.push_back((uint8_t)e.src);
+      r.n++;
     }
   }
 
@@ -1856,6 +1704,8 @@ struct PatternEngine : Engine {
     w.put<int64_t>(C);
     w.put<int32_t>(have_horizon ? 1 : 0);
     w.put<int64_t>(horizon);
+    w.put<int64_t>(t_last);
+    w.put<int64_t>(last_b_seq);
     w.put<int32_t>((int32_t)typesA.size());
     const CarryTable& t = carry[cur];
     for (size_t c = 0; c < typesA.size(); c++) {
@@ -1865,6 +1715,7 @@ struct PatternEngine : Engine {
     w.dev(t.ts.p, (size_t)C * 8);
     w.dev(t.key.p, (size_t)C * 8);
     w.dev(t.seq.p, (size_t)C * 8);
+    w.dev(t.pend.p, (size_t)C);
     if (logical == 2) {
       w.dev(t.half.p, (size_t)C);
       for (size_t c = 0; c < typesB.size(); c++) {
@@ -1879,6 +1730,8 @@ struct PatternEngine : Engine {
     const int64_t c0 = r.get<int64_t>();
     have_horizon = r.get<int32_t>() != 0;
     horizon = r.get<int64_t>();
+    t_last = r.get<int64_t>();
+    last_b_seq = r.get<int64_t>();
     if (r.get<int32_t>() != (int32_t)typesA.size() || c0 < 0) throw Error(SHD_E_ARG, "snapshot of a different plan");
     cur = 0;
     CarryTable& t = carry[0];
@@ -1890,6 +1743,7 @@ struct PatternEngine : Engine {
     r.dev_into(t.ts.p, (size_t)c0 * 8);
     r.dev_into(t.key.p, (size_t)c0 * 8);
     r.dev_into(t.seq.p, (size_t)c0 * 8);
+    r.dev_into(t.pend.p, (size_t)c0);
     if (logical == 2) {
       t.reserve_b(c0, typesB);
       r.dev_into(t.half.p, (size_t)c0);
@@ -1951,6 +1805,7 @@ struct PatternEngine : Engine {
     int la = 0;
     int64_t t_last_probe = 0;
     if (bucket_candidate(b, la, t_last_probe) && bucket_push(b, la, t_last_probe)) return;
+    if (fused_group_push(b)) return;
     sort_push(b);
   }
 
@@ -1964,7 +1819,9 @@ struct PatternEngine : Engine {
   // whenever legal (tests).
   bool bucket_candidate(const Staged& b, int& la, int64_t& t_last_probe) {
     const int slot = b.stream == sA ? 0 : 1;
-    if (getenv("SHD_NO_BUCKET") || getenv("SHD_HASH_BITS") || logical != 0 || W == INT64_MAX || !(partitioned || implicit_key) ||
+    // (the bucketed walk retires partials at the push horizon: unpartitioned
+    // plans grouped by an implicit key only, see `prune` in sort_push)
+    if (getenv("SHD_NO_BUCKET") || getenv("SHD_HASH_BITS") || logical != 0 || W == INT64_MAX || partitioned || !implicit_key ||
         type_key64(key_type[slot]) || sA != sB)
       return false;
     const int64_t n_ext = C + b.n;
@@ -2167,6 +2024,200 @@ struct PatternEngine : Engine {
     return true;
   }
 
+  // rows per group (mean) up to which the grouped LDS walk is used: the walk
+  // stages 1024 rows of a group in LDS (larger groups walk in global memory)
+  static constexpr double kGroupMaxMean = 800.0;
+  static constexpr int kGroupBits = 16;
+
+  // Grouped LDS walk: hashed 16-bit key sort of the prepared rows (d_k32 /
+  // d_pv / d_ts), then one workgroup per group (engine_group.hip), then the
+  // shared compaction tail.  Exact for partitioned plans without retiring any
+  // partial; unpartitioned implicit grouping retires by global expiry (prune).
+  void group_push(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg, bool prune, bool isB) {
+    hipStream_t s = stream;
+    d_k32_alt.reserve(n_ext * 4);
+    d_pv_alt.reserve(n_ext * 4);
+    d_ts_alt.reserve(n_ext * 4);
+    bool in_alt = false;
+    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
+                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, kGroupBits, d_sort, s, in_alt, true,
+                           0);
+    const uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
+    const uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
+    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
+    mark("key_sort");
+    (void)isB;
+    group_walk_tail(b, x, n_ext, pg, prune, skey32, spv, sts32);
+  }
+
+  // f1's attributes when it is a fast predicate over at most two of them
+  // (the fused prepare preloads them): false otherwise
+  bool f1_attrs(const DFilters& f1, int& a0, int& a1) const {
+    a0 = a1 = -1;
+    if (!f1.fp.ok) return f1.n == 0;
+    auto add = [&](const FAtom& at) {
+      if (at.kind != FA_LOAD) return true;
+      if (at.st != 0) return false;
+      if (at.attr == a0 || at.attr == a1) return true;
+      if (a0 < 0) a0 = at.attr;
+      else if (a1 < 0) a1 = at.attr;
+      else return false;
+      return true;
+    };
+    for (int i = 0; i < f1.fp.n; i++) {
+      const FCmp& c = f1.fp.c[i];
+      if (!add(c.l.a) || !add(c.l.b) || !add(c.r.a) || !add(c.r.b)) return false;
+    }
+    return true;
+  }
+
+  // Partitioned plain pattern with a plain 32-bit key column and a fast f1:
+  // prepare fused into the first hashed pass (engine_group.hip
+  // k_prep_scatter), the second pass, then the grouped walk.  false: not this
+  // push's path (nothing changed): a timestamp offset beyond 32 bits.
+  bool group_hint = true;   // the last push's groups were small (rows / keys)
+  bool fused_group_push(const Staged& b) {
+    const int slot = b.stream == sA ? 0 : 1;
+    const bool isA = b.stream == sA, isB = b.stream == sB;
+    // opt-in (SHD_GROUP=1): measured slower than the key sort on P3 (r03c:
+    // group walk 3.5 ms, fused pass 1.0 ms per 50M-row push)
+    const char* gv = getenv("SHD_GROUP");   // "1": when groups are small; "force": always
+    const bool force = gv && std::strcmp(gv, "force") == 0;
+    if (!gv || !partitioned || logical != 0 || !(group_hint || force) || getenv("SHD_NO_GROUP") ||
+        getenv("SHD_NO_FUSED_GROUP") ||
+        key_col[slot] < 0 || !(key_type[slot] == SHD_T_STRING || key_type[slot] == SHD_T_INT))
+      return false;
+    const int64_t n = b.n;
+    const int64_t n_ext = C + n;
+    if (n_ext > (int64_t)kRowMask) return false;
+    PrepArgs pa{};
+    pa.f1 = dfilters(f1);
+    int a0 = -1, a1 = -1;
+    if (isA && !f1_attrs(pa.f1, a0, a1)) return false;
+    hipStream_t s = stream;
+    SHD_HIP(hipEventRecord(ev0, s));
+    stage_begin();
+    d_k32.reserve(n_ext * 4);
+    d_pv.reserve(n_ext * 4);
+    d_ts.reserve(n_ext * 4);
+    d_k32_alt.reserve(n_ext * 4);
+    d_pv_alt.reserve(n_ext * 4);
+    d_ts_alt.reserve(n_ext * 4);
+    d_match.reserve(n_ext * 4);
+    d_pst.reserve(n_ext + kCompactPad);
+    d_agg.reserve(256);
+    h_agg.reserve(256);
+    ExtRows x{};
+    x.carry = carry_cs();
+    x.batch = b.cs;
+    x.C = C;
+    x.seq0 = seq;
+    x.carry_seq = carry[cur].seq.as<int64_t>();
+    pa.x = x;
+    pa.es = dset();
+    pa.is_a = isA;
+    pa.is_b = isB;
+    pa.partitioned = 1;
+    pa.null_skip = 1;
+    pa.key64 = 0;
+    pa.key_col = key_col[slot];
+    pa.key_type = key_type[slot];
+    pa.carry_key = carry[cur].key.as<uint64_t>();
+    const PrepArgs* d_pa_args = dev_args(pa);
+    const int nbt = prep_scatter_tiles(n_ext);
+    d_blk.reserve((size_t)std::max<int64_t>(nbt, group_walk_blocks(1 << kGroupBits)) *
+                  std::max(sizeof(PrepAgg), sizeof(ScanOut)));
+    d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
+    uint32_t* hist = d_sort.as<uint32_t>();
+    uint32_t* offs = hist + (int64_t)nbt * 256;
+    uint32_t* tot = offs + (int64_t)nbt * 256;
+    hipLaunchKernelGGL((k_bkt_hist<true, kPrepRounds>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
+    SHD_CHECK_LAUNCH();
+    radix_digit_scan(hist, nbt, offs, tot, s);
+    launch_prep_scatter(d_pa_args, n_ext, hist, offs, tot, nbt, a0, a1, d_k32_alt.as<uint32_t>(),
+                        d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), d_blk.as<PrepAgg>(), s);
+    PrepAgg* d_pa = d_agg.as<PrepAgg>();
+    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
+    SHD_CHECK_LAUNCH();
+    mark("prepare");
+    // second hashed pass: digit bits 8..15, alt -> primary
+    bool back = false;
+    radix_sort_triples_u32(d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
+                           d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), n_ext, kGroupBits, d_sort, s,
+                           back, true, 0, 8);
+    const bool in_alt = !back;
+    const uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
+    const uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
+    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
+    mark("key_sort");
+    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    PrepAgg pg;
+    std::memcpy(&pg, h_agg.p, sizeof(pg));
+    if (pg.ovf) return false;   // a timestamp more than 2^31 ms from the batch's first: the sort path
+    group_walk_tail(b, x, n_ext, pg, false, skey32, spv, sts32);
+    return true;
+  }
+
+  void group_walk_tail(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg, bool prune,
+                       const uint32_t* skey32, const uint32_t* spv, const int32_t* sts32) {
+    hipStream_t s = stream;
+    const int64_t n = b.n;
+    counters.group_bits = kGroupBits;
+    {
+      const double nk = pg.kmin <= pg.kmax ? std::min<double>(65536.0, (double)(pg.kmax - pg.kmin) + 1.0) : 1.0;
+      group_hint = (double)n_ext / nk <= kGroupMaxMean;
+    }
+    ScanArgs sa{};
+    sa.x = x;
+    sa.es = dset();
+    sa.f2 = dfilters(f2);
+    sa.logical = 0;
+    sa.s_first = s_first;
+    sa.s_second = s_second;
+    sa.within = W;
+    sa.partitioned = 1;
+    sa.prune = prune;
+    const int64_t t_end = (int64_t)pg.ts_max;
+    sa.t_end = t_end;
+    const int ngroups = 1 << kGroupBits;
+    d_gbeg.reserve((size_t)ngroups * 4);
+    d_gend.reserve((size_t)ngroups * 4);
+    const int nwalk = group_walk_blocks(ngroups);
+    const int nblk = grid_for(n_ext, 1, 4096);
+    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
+    const int ntile = (int)ceil_div(n_ext, tile);
+    d_blk.reserve((size_t)std::max<int64_t>(nwalk, 3 * nblk) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
+    launch_group_walk(dev_args(sa), sa.f2.fp.ok != 0, n_ext, kGroupBits, skey32, spv, sts32, d_gbeg.as<uint32_t>(),
+                      d_gend.as<uint32_t>(), d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), s);
+    d_bcnt.reserve((size_t)2 * ntile * 4);
+    d_boff.reserve((size_t)2 * ntile * 4);
+    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
+                       d_bcnt.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
+    SHD_CHECK_LAUNCH();
+    mark("forward_scan");
+    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    mark("compact");
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    ScanOut so;
+    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
+    const uint32_t m = h_agg.as<uint32_t>()[32];
+    const uint32_t n_open = h_agg.as<uint32_t>()[33];
+    if (so.violation) throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
+    if (so.pruned) {
+      have_horizon = true;
+      horizon = std::max(horizon, t_end);
+    }
+    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
+  }
+
   void sort_push(const Staged& b) {
     const int64_t n = b.n;
     if (n <= 0) return;
@@ -2298,10 +2349,12 @@ struct PatternEngine : Engine {
     PrepAgg pg;
     std::memcpy(&pg, h_agg.p, sizeof(pg));
     mark("prepare");
+    // an unpartitioned plan retired partials that the last event of an earlier
+    // push expired (global expiry: they are gone in the reference too); a push
+    // going back before that time continues on the generic NFA engine with the
+    // remaining open partials (partitioned plans never retire: see `prune`)
     if (have_horizon && (int64_t)pg.ts_min < horizon)
-      throw Error(SHD_E_UNSUPPORTED,
-                  "pattern engine: an event precedes the pruning horizon of an earlier push (timestamps must not "
-                  "go back across pushes once partials were retired)");
+      throw NeedNfa("pattern engine: an event precedes the retirement horizon of an earlier push");
 
     // ---- key-sort the extended batch (stable: creation order within a key),
     //      carrying the packed (flags, row) payload and the event timestamp
@@ -2311,10 +2364,28 @@ struct PatternEngine : Engine {
     const int32_t* sts32 = d_ts.as<int32_t>();
     const int64_t* sts64 = nullptr;
     bool sorted64 = false;
-    const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX;
+    // Retirement of open partials that every later event would expire: exact
+    // only under global expiry (unpartitioned plans: the push's last event
+    // expired them, StreamPreStateProcessor.expireEvents :326-361).  A
+    // partitioned partial is expired only by an event of its own key
+    // (PartitionStateHolder: per-key pending lists), which may arrive in any
+    // later push with any timestamp, so partitioned plans carry every open
+    // partial until its key kills or completes it.
+    const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX && !partitioned;
     // implicit grouping needs the reference's global expiry order to be the
     // per-key one: pushed rows time-ordered, carried partials before them
     const bool grouped = partitioned || (implicit_key && !pg.unmono && (C == 0 || pg.carry_tmax <= pg.ts_min));
+    // grouped LDS walk (engine_group.hip): a 16-bit hashed key sort (two
+    // passes) and the per-group walk in LDS, when the groups are small --
+    // expected rows per group = rows / min(2^16, keys of the push)
+    if (grouped && logical == 0 && !key64 && !pg.ovf && !getenv("SHD_NO_GROUP") && pg.kmin <= pg.kmax) {
+      const double nk = std::min<double>(65536.0, (double)(pg.kmax - pg.kmin) + 1.0);
+      const char* gv = getenv("SHD_GROUP");
+      if (gv && (std::strcmp(gv, "force") == 0 || (double)n_ext / nk <= kGroupMaxMean)) {
+        group_push(b, x, n_ext, pg, prune, isB);
+        return;
+      }
+    }
     uint32_t hash_mask = 0;
     counters.group_bits = 0;
     if (grouped) {
@@ -2576,7 +2647,8 @@ struct PatternEngine : Engine {
       pr.chunk0 = chunk_seq;
       pr.row0 = out.count;
       hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
-                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
+                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq(),
+                         out.d_sidx());
       SHD_CHECK_LAUNCH();
       out.count += m;
       if (sA != sB && !logical) chunk_seq += m;
@@ -2600,6 +2672,9 @@ struct PatternEngine : Engine {
       ga.dts = carry[nxt].ts.as<int64_t>();
       ga.dkey = carry[nxt].key.as<uint64_t>();
       ga.dseq = carry[nxt].seq.as<int64_t>();
+      carry[cur].pend.reserve(std::max<int64_t>(C, 1));
+      ga.dpend = carry[nxt].pend.as<uint8_t>();
+      ga.pend_old = carry[cur].pend.as<uint8_t>();
       if (logical == 2) {
         carry[nxt].reserve_b(n_open, typesB);
         ga.and_mode = 1;
@@ -2619,9 +2694,20 @@ struct PatternEngine : Engine {
         skey32 = d_k32.as<uint32_t>();
         skey64 = d_k64.as<uint64_t>();
       }
-      hipLaunchKernelGGL(k_gather_carry, dim3(ntile), dim3(kBlock), 0, s, dev_args(ga),
-                         (const uint8_t*)d_pst.as<uint8_t>(), (const uint32_t*)d_boff.as<uint32_t>(), spv, skey32,
-                         skey64, n_ext, tile);
+      if (logical != 2 && !getenv("SHD_CARRY_SERIAL")) {
+        ga.amask = carry_mask;
+        d_olist.reserve((size_t)n_open * 4);
+        hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                           (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_olist.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_gather_list, dim3(grid_cover((int64_t)n_open)), dim3(kBlock), 0, s, dev_args(ga),
+                           (const uint32_t*)d_olist.as<uint32_t>(), (int64_t)n_open,
+                           (const uint8_t*)d_pst.as<uint8_t>(), spv, skey32, skey64);
+      } else {
+        hipLaunchKernelGGL(k_gather_carry, dim3(ntile), dim3(kBlock), 0, s, dev_args(ga),
+                           (const uint8_t*)d_pst.as<uint8_t>(), (const uint32_t*)d_boff.as<uint32_t>(), spv, skey32,
+                           skey64, n_ext, tile);
+      }
       SHD_CHECK_LAUNCH();
       mark("carry");
     }
@@ -2632,6 +2718,7 @@ struct PatternEngine : Engine {
     SHD_HIP(hipEventElapsedTime(&ms, ev0, ev1));
     cur = nxt;
     C = n_open;
+    if (b.stream == sB) last_b_seq = seq + n - 1;
     seq += n;
     if (b.advance_time && t_end > now) now = t_end;
     std::memcpy(&t_last, h_agg.as<char>() + 192, 8);
@@ -2777,6 +2864,21 @@ std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, con
     }
     if (e->key_expr[0] < 0 || e->key_expr[1] < 0) { why = "partition key missing for a stream"; return nullptr; }
   }
+  // e1 columns read after a partial is carried: f2 / f3 / the selector, and
+  // (for a hand-over replay through the generic NFA engine) f1 and the keys
+  uint32_t mask = 0;
+  auto add = [&](int ex) {
+    if (ex < 0) return;
+    for (const Instr& in : p.exprs[ex])
+      if (in.op == SHD_OP_LOAD && in.a == 0) mask |= 1u << (in.c & 0xFFFF);
+  };
+  for (int f : e->f1) add(f);
+  for (int f : e->f2) add(f);
+  for (int f : e->f3) add(f);
+  for (int o : e->outs) add(o);
+  add(e->key_expr[0]);
+  add(e->key_expr[1]);
+  e->carry_mask = mask;
   return e;
 }
 

@@ -34,6 +34,9 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kAddBit = 0x80000000u;
 constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
 constexpr int kMaxGroupAttrs = 4;
+// segmented scans only while every operand seen so far is finite and the
+// non-zero magnitudes span at most 2^kSegMaxExpSpan (k_operand_stats)
+constexpr uint32_t kSegMaxExpSpan = 30;
 
 struct RowCtx {
   const ColSet* cs;
@@ -421,6 +424,58 @@ __global__ __launch_bounds__(kBlock) void k_gdict_rehash(GDict o, GDict d) {
     d.id[slot] = o.id[s];
     d.kn[slot] = o.kn[s];
     for (int g = 0; g < d.nk; g++) d.kw[(uint64_t)g * d.cap + slot] = o.kw[(uint64_t)g * o.cap + s];
+  }
+}
+
+// Range guard of the segmented-scan mode: over the new items' double / float
+// operands of the scanned channels, flags[0] |= 1 for a non-finite value,
+// flags[1] = max and flags[2] = min binary exponent of the non-zero values.
+// (One atomic per block; a grid of at most 1024 blocks.)
+__global__ __launch_bounds__(kBlock) void k_operand_stats(const uint64_t* argv, const uint8_t* argn, int64_t cap,
+                                                          int64_t C, int64_t m, int nch, const int* ch_agg,
+                                                          const int* ch_type, uint32_t* flags) {
+  uint32_t nf = 0, emax = 0, emin = 0xFFFFFFFFu;
+  for (int c = 0; c < nch; c++) {
+    const int g = ch_agg[c];
+    const bool f32 = ch_type[c] == SHD_T_FLOAT;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
+      const int64_t t = C + i;
+      if (argn[(int64_t)g * cap + t]) continue;
+      const uint64_t b = argv[(int64_t)g * cap + t];
+      const double d = f32 ? (double)__uint_as_float((uint32_t)b) : __longlong_as_double((long long)b);
+      if (!(d - d == 0.0)) {   // Inf or NaN
+        nf = 1;
+        continue;
+      }
+      if (d == 0.0) continue;
+      const uint32_t e = (uint32_t)((__double_as_longlong(d) >> 52) & 0x7FF);
+      emax = e > emax ? e : emax;
+      emin = e < emin ? e : emin;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    nf |= __shfl_xor(nf, o, 64);
+    const uint32_t a = __shfl_xor(emax, o, 64), b = __shfl_xor(emin, o, 64);
+    emax = a > emax ? a : emax;
+    emin = b < emin ? b : emin;
+  }
+  __shared__ uint32_t sh[3][kBlock / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = nf;
+    sh[1][w] = emax;
+    sh[2][w] = emin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; k++) {
+      nf |= sh[0][k];
+      emax = sh[1][k] > emax ? sh[1][k] : emax;
+      emin = sh[2][k] < emin ? sh[2][k] : emin;
+    }
+    if (nf) atomicOr(&flags[0], 1u);
+    atomicMax(&flags[1], emax);
+    atomicMin(&flags[2], emin);
   }
 }
 
@@ -1675,6 +1730,10 @@ struct SingleEngine : Engine {
       last_of, fcnt, foff;
   // segmented-scan mode (default for count / sum(double|float) / avg)
   bool seg_ok = false, seg_mode = false;
+  bool seg_unsafe = false;   // a non-finite or wide-range operand was seen: exact fold from then on
+  bool seg_pref = true;      // the mode asked for (option / default), restored by reset()
+  DevBuf d_chmeta;
+  PinnedBuf h_chmeta;
   int nch = 0;                       // distinct aggregated expressions (channels)
   int ch_agg[kMaxChan] = {}, ch_type[kMaxChan] = {};
   int chan_of[kMaxAggs] = {};
@@ -1688,7 +1747,10 @@ struct SingleEngine : Engine {
   // "exact_aggregates" = 1: the bit-exact sequential fold instead of the
   // segmented scans (any time; both keep the group tables current)
   void set_option(const std::string& key, int64_t v) override {
-    if (key == "exact_aggregates") seg_mode = seg_ok && v == 0;
+    if (key == "exact_aggregates") {
+      seg_pref = v == 0;
+      seg_mode = seg_ok && !seg_unsafe && seg_pref;
+    }
     else Engine::set_option(key, v);
   }
 
@@ -1706,6 +1768,8 @@ struct SingleEngine : Engine {
     }
     gd_count = 0;
     if (gd_cap) SHD_HIP(hipMemsetAsync(gd_tag.p, 0, gd_cap * 8, stream));
+    seg_unsafe = false;
+    seg_mode = seg_ok && seg_pref;
   }
 
   GDict gdict() {
@@ -1812,6 +1876,7 @@ struct SingleEngine : Engine {
       w.dev(g_lsum.p, gb);
       w.dev(g_cnt.p, gb);
     }
+    w.put<int32_t>(seg_unsafe ? 1 : 0);
     // group dictionary (dictionary-mode group keys)
     w.put<uint64_t>(gd_cap);
     w.put<int64_t>(gd_count);
@@ -1851,6 +1916,8 @@ struct SingleEngine : Engine {
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
     if (nk > 0 || !g_nkeys) g_nkeys = nk;
+    seg_unsafe = r.get<int32_t>() != 0;
+    seg_mode = seg_ok && seg_pref && !seg_unsafe;
     const uint64_t dcap = r.get<uint64_t>();
     const int64_t dcount = r.get<int64_t>();
     if (dcap & (dcap - 1)) throw Error(SHD_E_ARG, "snapshot of a different plan");
@@ -2019,6 +2086,7 @@ struct SingleEngine : Engine {
                          (const uint32_t*)d_start.as<uint32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(),
                          out.d_seq());
       SHD_CHECK_LAUNCH();
+      SHD_HIP(hipMemsetAsync(out.d_sidx() + out.count, 0, (size_t)m * 4, s));   // no states: state_idx 0
       out.count += m;
     }
     chunk_seq += partitioned ? (int64_t)nruns : ncalls;
@@ -2125,6 +2193,7 @@ struct SingleEngine : Engine {
                          (const uint8_t*)resn.as<uint8_t>(), (const int64_t*)resc.as<int64_t>(), out.d_chunk(),
                          out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq());
     SHD_CHECK_LAUNCH();
+    SHD_HIP(hipMemsetAsync(out.d_sidx() + out.count, 0, (size_t)nrows * 4, s));   // no states: state_idx 0
     out.count += nrows;
     counters.matches += nrows;
     mark("emit");
@@ -2246,6 +2315,7 @@ struct SingleEngine : Engine {
     const int64_t m = h_tot.as<uint32_t>()[0];
     const int64_t total = C + m;
     SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 5, 0, 8, s));
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 6, 0xFF, 8, s));
     if (total >= (int64_t)INT32_MAX) throw Error(SHD_E_CAPACITY, "window items exceed 2^31");
     // items: carry slot `cur` already holds [0, C); build the new item set in slot `cur`
     // (grow preserving the carry)
@@ -2336,10 +2406,41 @@ struct SingleEngine : Engine {
                        (const uint32_t*)e_exp.as<uint32_t>(), total, d_x);
     SHD_CHECK_LAUNCH();
     reduce_max_u64(ikey[cur].as<uint64_t>(), total, d_kmax, s);
-    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 48, hipMemcpyDeviceToHost, s));
+    const bool guard = seg_mode && nch > 0 && m > 0;
+    if (guard) {
+      d_chmeta.reserve(2 * kMaxChan * sizeof(int));
+      int meta[2 * kMaxChan];
+      for (int c = 0; c < nch; c++) {
+        meta[c] = ch_agg[c];
+        meta[kMaxChan + c] = ch_type[c];
+      }
+      h_chmeta.reserve(sizeof(meta));
+      std::memcpy(h_chmeta.p, meta, sizeof(meta));
+      SHD_HIP(hipMemcpyAsync(d_chmeta.p, h_chmeta.p, sizeof(meta), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_operand_stats, dim3((unsigned)std::min<int64_t>(1024, ceil_div(m, kBlock))), dim3(kBlock), 0,
+                         s, (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(), cap,
+                         C, m, nch, (const int*)d_chmeta.as<int>(), (const int*)d_chmeta.as<int>() + kMaxChan,
+                         (uint32_t*)(d_tot.as<uint64_t>() + 5));
+      SHD_CHECK_LAUNCH();
+    }
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 64, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     const int64_t X = (int64_t)h_tot.as<uint64_t>()[1];
     const uint64_t kmax = h_tot.as<uint64_t>()[2];
+    if (guard) {
+      // Segmented scans reassociate the reference's running `sum += v; sum -= v`
+      // (SumAttributeAggregatorExecutor.java:184-198).  With a non-finite
+      // operand the reference's sum stays Inf / NaN for good (Inf - Inf), and
+      // over a wide magnitude range its rounding history shows in the result
+      // (1e20 + 1 - 1e20 = 0): from the first such push on, this query keeps the
+      // bit-exact sequential fold (the group tables carry over).
+      const uint32_t* fl = h_tot.as<uint32_t>() + 10;
+      const bool wide = fl[2] != 0xFFFFFFFFu && fl[1] > fl[2] + kSegMaxExpSpan;
+      if (fl[0] || wide) {
+        seg_mode = false;
+        seg_unsafe = true;
+      }
+    }
     if ((int64_t)kmax >= kMaxDenseKey)   // dense string ids: more than 2^26 distinct strings
       throw Error(SHD_E_CAPACITY, "more than 2^26 group-by keys in the dense group tables");
     ensure_groups((int64_t)kmax + 1);
@@ -2519,7 +2620,8 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
     e->chan_of[g] = c;
   }
   e->seg_ok = seg;
-  e->seg_mode = seg && !getenv("SHD_EXACT_AGGREGATES");
+  e->seg_pref = !getenv("SHD_EXACT_AGGREGATES");
+  e->seg_mode = seg && e->seg_pref;
   if (e->partitioned) {
     if (e->agg_mode) { why = "partitioned window/aggregation"; return nullptr; }
     e->key_expr = p.part_keys[0].second;

@@ -242,8 +242,9 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
   if (need <= cap) return;
   int64_t nc = std::max<int64_t>(need, std::max<int64_t>(cap * 2, 4096));
   int w = std::max(ncols, 1);
-  DevBuf c2, t2, ts2, v2, n2, q2;
+  DevBuf c2, t2, ts2, v2, n2, q2, x2;
   q2.reserve(nc * 8);
+  x2.reserve(nc * 4);
   c2.reserve(nc * 8);
   t2.reserve(nc * 4);
   ts2.reserve(nc * 8);
@@ -256,6 +257,7 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
     SHD_HIP(hipMemcpyAsync(v2.p, vals.p, count * w * 8, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipMemcpyAsync(n2.p, nulls.p, count * w, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipMemcpyAsync(q2.p, seq.p, count * 8, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(x2.p, sidx.p, count * 4, hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipStreamSynchronize(s));
   }
   std::swap(chunk.p, c2.p); std::swap(chunk.cap, c2.cap);
@@ -263,6 +265,7 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
   std::swap(ts.p, ts2.p); std::swap(ts.cap, ts2.cap);
   std::swap(vals.p, v2.p); std::swap(vals.cap, v2.cap);
   std::swap(nulls.p, n2.p); std::swap(nulls.cap, n2.cap);
+  std::swap(sidx.p, x2.p); std::swap(sidx.cap, x2.cap);
   std::swap(seq.p, q2.p); std::swap(seq.cap, q2.cap);
   cap = nc;
 }
@@ -458,6 +461,7 @@ struct shd_query {
   PinnedBuf pin;   // host staging for SHD_MEM_HOST batches
   // poll buffers (host)
   std::vector<int64_t> h_chunk, h_ts, h_seq;
+  std::vector<int32_t> h_sidx;
   std::vector<int32_t> h_type;
   std::vector<uint64_t> h_vals;
   std::vector<uint8_t> h_nulls;
@@ -525,13 +529,17 @@ void stage_host(hipStream_t s, PinnedBuf& pin, DevBuf& dts, DevBuf* dcol, DevBuf
 // engine from then on.
 void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, const std::string& why) {
   Engine& old = *q->eng;
-  Replay r;
-  old.export_replay(r);
+  std::vector<Replay> parts;
+  old.export_replay(parts);
+  int64_t nrep = 0;
+  for (auto& r : parts) nrep += r.n;
   std::string w2;
-  std::unique_ptr<Engine> ne = make_nfa_engine(old.plan, w2, r.n + st.n);
+  std::unique_ptr<Engine> ne = make_nfa_engine(old.plan, w2, nrep + st.n);
   if (!ne) throw Error(SHD_E_UNSUPPORTED, why + "; the generic NFA engine does not take this plan: " + w2);
   init_engine(*ne, old.plan);
-  if (r.n > 0) {
+  ne->start_time = old.start_time;
+  for (auto& r : parts) {
+    if (r.n <= 0) continue;
     const auto& types = old.plan.stream_types[r.stream];
     std::vector<const void*> cp(types.size());
     std::vector<const uint8_t*> np(types.size());
@@ -555,8 +563,13 @@ void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, c
     rs.cs.ncols = rb.ncols;
     rs.cs.n = r.n;
     PinnedBuf pin;
-    DevBuf dts, dcol[kMaxCols], dnul[kMaxCols];
+    DevBuf dts, dcol[kMaxCols], dnul[kMaxCols], dskip;
     stage_host(ne->stream, pin, dts, dcol, dnul, &rb, types, rs);
+    if (!r.skip_start.empty()) {
+      dskip.reserve((size_t)r.n);
+      SHD_HIP(hipMemcpyAsync(dskip.p, r.skip_start.data(), (size_t)r.n, hipMemcpyHostToDevice, ne->stream));
+      rs.skip_start = dskip.as<uint8_t>();
+    }
     ne->args_begin();
     ne->push(rs);
     SHD_HIP(hipStreamSynchronize(ne->stream));
@@ -573,6 +586,7 @@ void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, c
     SHD_HIP(hipMemcpyAsync(ne->out.vals.p, old.out.vals.p, m * w * 8, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipMemcpyAsync(ne->out.nulls.p, old.out.nulls.p, m * w, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipMemcpyAsync(ne->out.seq.p, old.out.seq.p, m * 8, hipMemcpyDeviceToDevice, ne->stream));
+    SHD_HIP(hipMemcpyAsync(ne->out.sidx.p, old.out.sidx.p, m * 4, hipMemcpyDeviceToDevice, ne->stream));
     SHD_HIP(hipStreamSynchronize(ne->stream));
     ne->out.count = m;
   }
@@ -608,6 +622,7 @@ int shd_ctx_create(const int* device_ids, int n, shd_ctx** out) {
     if (!out) return fail(SHD_E_ARG, "null out");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(SHD_E_DEVICE, "no HIP device available");
+    if (n > 1) return fail(SHD_E_ARG, "one device per context (one process per GPU; keys shard across processes)");
     auto* c = new shd_ctx();
     c->device = (device_ids && n > 0) ? device_ids[0] : 0;
     if (c->device < 0 || c->device >= count) {
@@ -635,9 +650,10 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
     if (p.kind == SHD_KIND_STATE) {
       // the 2-state every-pattern shape (P1/P3) has a dedicated forward-scan
       // engine; every other state plan runs on the generic per-key NFA
-      e = make_pattern_engine(p, why1);
+      // SHD_FORCE_NFA: the generic engine for every state plan (tests, diagnostics)
+      if (!getenv("SHD_FORCE_NFA")) e = make_pattern_engine(p, why1);
       // SHD_NO_LOGICAL_SCAN: leave `every e1 -> (e2 or e3)` to the generic NFA engine (tests)
-      if (!e && !getenv("SHD_NO_LOGICAL_SCAN")) e = make_logical_pattern_engine(p, why1);
+      if (!e && !getenv("SHD_NO_LOGICAL_SCAN") && !getenv("SHD_FORCE_NFA")) e = make_logical_pattern_engine(p, why1);
       if (!e) e = make_nfa_engine(p, why2);
       if (!e) why1 += "; ";
     } else {
@@ -724,6 +740,10 @@ int shd_push(shd_query* q, const shd_batch* b) {
       // query's stream.
       stage_host(e.stream, q->pin, q->stage_ts, q->stage_col, q->stage_nul, b, types, st);
     }
+    if (b->use_base_seq) {
+      if (b->base_seq < e.seq) return fail(SHD_E_ARG, "base_seq precedes events already pushed");
+      e.seq = b->base_seq;   // in_seq of this batch's rows = base_seq + row
+    }
     const shd_counters before = e.counters;
     e.args_begin();
     try {
@@ -731,6 +751,7 @@ int shd_push(shd_query* q, const shd_batch* b) {
     } catch (NeedNfa& nf) {
       switch_to_nfa(q, st, before, nf.what());
     }
+    q->eng->counters.kernel_ns_total += q->eng->counters.kernel_ns;
     return SHD_OK;
   });
 }
@@ -763,6 +784,7 @@ int shd_poll(shd_query* q, shd_out* out) {
     q->h_type.resize(std::max<int64_t>(n, 1));
     q->h_ts.resize(std::max<int64_t>(n, 1));
     q->h_seq.resize(std::max<int64_t>(n, 1));
+    q->h_sidx.resize(std::max<int64_t>(n, 1));
     q->h_vals.resize(std::max<int64_t>(n * nc, 1));
     q->h_nulls.resize(std::max<int64_t>(n * nc, 1));
     if (n > 0) {
@@ -770,6 +792,7 @@ int shd_poll(shd_query* q, shd_out* out) {
       SHD_HIP(hipMemcpyAsync(q->h_type.data(), e.out.type.p, n * 4, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipMemcpyAsync(q->h_ts.data(), e.out.ts.p, n * 8, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipMemcpyAsync(q->h_seq.data(), e.out.seq.p, n * 8, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(q->h_sidx.data(), e.out.sidx.p, n * 4, hipMemcpyDeviceToHost, s));
       if (nc > 0) {
         SHD_HIP(hipMemcpyAsync(q->h_vals.data(), e.out.vals.p, n * nc * 8, hipMemcpyDeviceToHost, s));
         SHD_HIP(hipMemcpyAsync(q->h_nulls.data(), e.out.nulls.p, n * nc, hipMemcpyDeviceToHost, s));
@@ -785,6 +808,7 @@ int shd_poll(shd_query* q, shd_out* out) {
     out->values = q->h_vals.data();
     out->nulls = q->h_nulls.data();
     out->in_seq = q->h_seq.data();
+    out->state_idx = q->h_sidx.data();
     return SHD_OK;
   });
 }
@@ -821,7 +845,7 @@ int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int*
 // engine's own section (Engine::save_state).  Pending output rows must have
 // been polled (the runtime drains after every push).
 static constexpr uint32_t kSnapMagic = 0x53444853u;   // "SHDS"
-static constexpr uint32_t kSnapVersion = 1;
+static constexpr uint32_t kSnapVersion = 2;   // 2: + layout hint and start time
 
 int shd_snapshot(shd_query* q, const void** data, size_t* len) {
   return guarded([&]() -> int {
@@ -834,6 +858,8 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
     w.put<uint32_t>(kSnapMagic);
     w.put<uint32_t>(kSnapVersion);
     w.put<int32_t>(e.kind());
+    w.put<int64_t>(e.layout_hint);
+    w.put<int64_t>(e.start_time);
     w.put<uint64_t>(q->plan_hash);
     w.put<int64_t>(e.seq);
     w.put<int64_t>(e.now);
@@ -873,20 +899,25 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
     if (r.get<uint32_t>() != kSnapMagic || r.get<uint32_t>() != kSnapVersion)
       return fail(SHD_E_ARG, "not a libsiddhi_hip snapshot (or another version)");
     const int kind = r.get<int32_t>();
+    const int64_t hint = r.get<int64_t>();
+    const int64_t start = r.get<int64_t>();
     if (r.get<uint64_t>() != q->plan_hash) return fail(SHD_E_ARG, "snapshot was taken from a different plan");
-    if (kind != cur.kind()) {
+    if (kind != cur.kind() || hint != cur.layout_hint) {
       // the image comes from the other engine of this plan (a pattern query
-      // that switched to the generic NFA engine, or the reverse): restore
-      // into a fresh engine of that kind; a bad image leaves q untouched
+      // that switched to the generic NFA engine, or the reverse) or from an
+      // NFA engine built with another layout (a hand-over sizes its lists from
+      // the replay): restore into a fresh engine of that kind and layout; a bad
+      // image leaves q untouched
       std::string why;
       std::unique_ptr<Engine> fresh;
-      if (kind == ENG_NFA) fresh = make_nfa_engine(cur.plan, why);
+      if (kind == ENG_NFA) fresh = make_nfa_engine(cur.plan, why, hint);
       else if (kind == ENG_PATTERN) {
         fresh = make_pattern_engine(cur.plan, why);
         if (!fresh) fresh = make_logical_pattern_engine(cur.plan, why);
       }
       if (!fresh || fresh->kind() != kind) return fail(SHD_E_ARG, "snapshot of an engine this plan cannot run on");
       init_engine(*fresh, cur.plan);
+      fresh->start_time = start;
       r.s = fresh->stream;
       load_image(*fresh, r);
       q->eng = std::move(fresh);
@@ -903,6 +934,7 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
     cur.save_state(bk);
     try {
       load_image(cur, r);
+      cur.start_time = start;
     } catch (...) {
       SnapR br;
       br.p = bk.b.data();

@@ -40,18 +40,18 @@ class ShdBatch(ctypes.Structure):
     _fields_ = [("stream", ctypes.c_int32), ("mem", ctypes.c_int32), ("n", ctypes.c_int64),
                 ("ts", ctypes.c_void_p), ("ncols", ctypes.c_int32), ("cols", ctypes.c_void_p),
                 ("nulls", ctypes.c_void_p), ("ncalls", ctypes.c_int32), ("call_offsets", ctypes.c_void_p),
-                ("advance_time", ctypes.c_int32)]
+                ("advance_time", ctypes.c_int32), ("use_base_seq", ctypes.c_int32), ("base_seq", ctypes.c_int64)]
 
 
 class ShdOut(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int64), ("n_cols", ctypes.c_int32), ("chunk", ctypes.c_void_p),
                 ("type", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("values", ctypes.c_void_p),
-                ("nulls", ctypes.c_void_p), ("in_seq", ctypes.c_void_p)]
+                ("nulls", ctypes.c_void_p), ("in_seq", ctypes.c_void_p), ("state_idx", ctypes.c_void_p)]
 
 
 class ShdCounters(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("events", "matches", "partials", "partial_scans", "bytes_touched",
-                                               "kernel_ns", "carry", "group_bits")]
+                                               "kernel_ns", "carry", "group_bits", "kernel_ns_total")]
 
 
 _lib = None
@@ -143,7 +143,9 @@ class DeviceQuery:
             pass
 
     def push_raw(self, stream, n, ts_ptr, col_ptrs: List[int], null_ptrs: List[int], mem=SHD_MEM_HOST,
-                 call_offsets: np.ndarray = None, advance_time=True):
+                 call_offsets: np.ndarray = None, advance_time=True, base_seq=None):
+        """shd_push.  base_seq: arrival index of the first event in the whole
+        (sharded) stream, so that in_seq of the rows is global (shd_batch.base_seq)."""
         ncols = len(col_ptrs)
         cols = (ctypes.c_void_p * max(ncols, 1))(*col_ptrs)
         nulls = (ctypes.c_void_p * max(ncols, 1))(*null_ptrs)
@@ -164,6 +166,9 @@ class DeviceQuery:
             b.ncalls = 0
             b.call_offsets = None
         b.advance_time = 1 if advance_time else 0
+        if base_seq is not None:
+            b.use_base_seq = 1
+            b.base_seq = int(base_seq)
         _check(self.lib.shd_push(self.q, ctypes.byref(b)))
 
     def set_time(self, t):
@@ -193,6 +198,9 @@ class DeviceQuery:
             return None
         chunk = np.ctypeslib.as_array(ctypes.cast(o.chunk, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
         seq = np.ctypeslib.as_array(ctypes.cast(o.in_seq, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
+        # shd_out.state_idx: state id of the emitting processor, per row
+        self.last_state_idx = np.ctypeslib.as_array(ctypes.cast(o.state_idx, ctypes.POINTER(ctypes.c_int32)),
+                                                    (n,)).copy()
         typ = np.ctypeslib.as_array(ctypes.cast(o.type, ctypes.POINTER(ctypes.c_int32)), (n,)).copy()
         ts = np.ctypeslib.as_array(ctypes.cast(o.ts, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
         if nc > 0:

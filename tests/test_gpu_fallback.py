@@ -67,12 +67,39 @@ def test_no_within_regression_stays_on_forward_scan(hip_available):
     assert kind == 1
 
 
-def test_snapshot_after_hand_over_restores_into_fresh_query(hip_available):
+@pytest.mark.parametrize("partitioned", [True, False])
+@pytest.mark.parametrize("where", ["first", "later"])
+def test_and_regression_hands_over_half_filled_partials(hip_available, partitioned, where):
+    """every e1 -> e2 and e3: partials holding one operand when timestamps go
+    back are handed over with that operand's event (replayed past the start
+    state when its own partial is gone); the continuation equals the oracle."""
+    apps = wl.S4_PART_APPS if partitioned else wl.S4_APPS
+    qp, _ = compile_single_query(apps["and"].replace("within 1 sec", "within 40 milliseconds")
+                                 .replace("e1.price*1.2", "e1.price*1.02").replace("e1.price*0.8", "e1.price*0.98"))
+    rng = np.random.default_rng(71 + partitioned)
+    n, keys = 12_000, 60 if partitioned else 20
+    sym, price, vol, ts = wl.stock_stream(n, keys, 0.2, seed_offset=6)
+    cuts = [0, 4000, 8000, n]
+    bad = 1 if where == "first" else 2
+    batches = []
+    for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        t = _regress(ts[a:b], rng, frac=0.01, back=5) if i == bad else ts[a:b]
+        batches.append((0, stock_batch(sym[a:b], price[a:b], vol[a:b], t, 1000)))
+    ora = run_oracle(qp, batches)
+    dev, counters, kind = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
+    assert kind == 4
+    assert counters["events"] == n
+
+
+@pytest.mark.parametrize("app", [wl.P3_APP, wl.P1_APP], ids=["P3", "P1"])
+def test_snapshot_after_hand_over_restores_into_fresh_query(hip_available, app):
     """A query that switched engines snapshots the NFA engine's state; restoring
     it into a freshly loaded query (which starts on the forward scan) switches
     that query too, and the continuation equals the oracle."""
     from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
-    qp, _ = compile_single_query(wl.P3_APP.replace("within 1 sec", "within 6 milliseconds"))
+    qp, _ = compile_single_query(app.replace("within 1 sec", "within 6 milliseconds"))
     rng = np.random.default_rng(4)
     sym, price, vol, ts = wl.stock_stream(9000, 200, 0.05, seed_offset=8)
     t1 = _regress(ts[:4000], rng)

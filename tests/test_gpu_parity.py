@@ -84,34 +84,39 @@ def test_two_stream_pattern_matches_oracle(hip_available):
     assert_same_rows(dev, ora)
 
 
-def test_pruned_partials_and_horizon_guard(hip_available):
-    """Large pushes retire open partials that every later event would expire
-    (StreamPreStateProcessor.isExpired, `within`); results stay identical to the
-    oracle, and a later push that goes back before the retirement horizon is
-    refused (SHD_E_UNSUPPORTED) instead of silently diverging."""
-    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST, SiddhiHipError, SHD_E_UNSUPPORTED
+def test_partitioned_open_partials_survive_time_going_back(hip_available):
+    """A partitioned partial is expired only by an event of its own key
+    (per-key pending lists, StreamPreStateProcessor.expireEvents :326-361), so
+    the device carries every open partial across pushes -- nothing is retired
+    at a global time horizon -- and a later push whose events go back before
+    earlier pushes' times still meets them exactly as the reference does (the
+    pushes are large enough that unpartitioned plans would retire partials)."""
     qp, _ = compile_single_query(wl.P3_APP)
     sym, price, vol, ts = wl.stock_stream(300_000, 100_000, 0.05, seed_offset=41)
     batches = split(sym, price, vol, ts, 3)
+    # a fourth push replays the first push's events: every timestamp precedes
+    # the third push's, and its keys meet partials carried from all three
+    batches.append(batches[0])
     ora = run_oracle(qp, batches)
     dev, counters, _ = run_device(qp, batches)
+    assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert counters["carry"] < 20_000   # partials older than `within` were retired
-    dq = DeviceQuery(qp.ir)
-    try:
-        for si, b in batches:
-            cols = [np.ascontiguousarray(c) for c in b.cols]
-            t = np.ascontiguousarray(b.ts, np.int64)
-            dq.push_raw(si, b.n, t.ctypes.data, [c.ctypes.data for c in cols], [0] * 3, SHD_MEM_HOST, None, True)
-            dq.discard()
-        si, b = batches[0]
-        cols = [np.ascontiguousarray(c) for c in b.cols]
-        t = np.ascontiguousarray(b.ts, np.int64)
-        with pytest.raises(SiddhiHipError) as ei:
-            dq.push_raw(si, b.n, t.ctypes.data, [c.ctypes.data for c in cols], [0] * 3, SHD_MEM_HOST, None, True)
-        assert ei.value.code == SHD_E_UNSUPPORTED
-    finally:
-        dq.close()
+    assert counters["events"] == 4 * 100_000
+
+
+def test_unpartitioned_retirement_then_time_going_back(hip_available):
+    """Unpartitioned plans expire globally: partials the last event of a push
+    expired are gone in the reference too and may be retired; a later push that
+    goes back before that time continues on the generic NFA engine (the open
+    partials handed over) and equals the oracle."""
+    qp, _ = compile_single_query(wl.P1_APP.replace("within 1 sec", "within 20 milliseconds"))
+    sym, price, vol, ts = wl.stock_stream(210_000, 200, 0.01, seed_offset=43)
+    batches = split(sym, price, vol, ts, 3)
+    batches.append((0, stock_batch(sym[:5000], price[:5000], vol[:5000], ts[:5000] + 300)))
+    ora = run_oracle(qp, batches)
+    dev, _, kind = run_device(qp, batches)
+    assert len(ora[2]) > 0
+    assert_same_rows(dev, ora)
 
 
 @pytest.mark.parametrize("within", ["within 40 days", ""])
@@ -137,28 +142,28 @@ def test_timestamps_beyond_32bit_offsets(hip_available, within):
     assert_same_rows(dev, ora)
 
 
-@pytest.mark.parametrize("bits", ["auto", "2", "8", "12"])
+@pytest.mark.parametrize("path", ["group", "sort", "group-oversized"])
 @pytest.mark.parametrize("parts", [1, 3])
-def test_hashed_bucket_grouping(hip_available, monkeypatch, bits, parts):
-    """Partitioned pattern with the key sort replaced by a sort on the low bits
-    of a key hash (several keys per bucket, walks step over the other keys of
-    their bucket).  bits=2 puts ~1/4 of all keys in one bucket: results must
-    still equal the oracle's row for row.  'auto' on 2^20 keys with sparse keys
-    per `within` span takes the one-pass bucketed walk (8-bit buckets)."""
-    if bits != "auto":
-        monkeypatch.setenv("SHD_HASH_BITS", bits)
+def test_grouped_lds_walk(hip_available, monkeypatch, path, parts):
+    """Partitioned P3 on the grouped LDS walk (engine_group.hip: 16-bit hashed
+    key sort, every row of a key in one group, resolved in LDS -- nothing
+    retired) and on the full key sort, both equal to the oracle.
+    group-oversized: 40 keys, so every group exceeds the LDS capacity and
+    walks in global memory."""
+    if path == "sort":
+        monkeypatch.setenv("SHD_NO_GROUP", "1")
     else:
-        monkeypatch.setenv("SHD_BUCKET", "1")   # the bucketed walk is opt-in (slower on P3)
+        monkeypatch.setenv("SHD_GROUP", "force" if path == "group-oversized" else "1")
     qp, _ = compile_single_query(wl.P3_APP)
-    n, keys = 300_000, (1 << 20) if bits == "auto" else 20_000
-    # auto: 2^20 keys (3 exact passes), ~10k events per `within` span -> 16-bit buckets
-    sym, price, vol, ts = wl.stock_stream(n, keys, 0.1 if bits == "auto" else 0.01, seed_offset=77)
+    # 100k keys: the full key sort covers 17 bits (distinct from the walk's 16)
+    n, keys = 300_000, (40 if path == "group-oversized" else 100_000)
+    sym, price, vol, ts = wl.stock_stream(n, keys, 0.01, seed_offset=77)
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
     dev, counters, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert counters["group_bits"] == (8 if bits == "auto" else int(bits))
+    assert (counters["group_bits"] == 16) == (path != "sort")
 
 
 def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
@@ -180,7 +185,9 @@ def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
     dev, counters, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert counters["group_bits"] == 12   # exact: bit length of the largest key
+    # exact grouping: the full key sort (12 bits) or the grouped LDS walk (16
+    # hashed bits, every row of a key in one group) -- never partial buckets
+    assert counters["group_bits"] in (12, 16)
 
 
 @pytest.mark.parametrize("implicit", [True, False])
