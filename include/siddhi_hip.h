@@ -118,6 +118,10 @@ typedef struct shd_counters {
                                    grouping (hashed buckets when below the key
                                    width), 0 when not partitioned              */
   int64_t kernel_ns_total;      /* device time of every push since load / reset  */
+  int64_t dormant;              /* pattern engine, partitioned: open partials that
+                                   only a push going back in time can still meet
+                                   (kept outside the carry until their key's next
+                                   event expires them)                          */
 } shd_counters;
 
 int shd_device_count(int* n);

@@ -228,6 +228,8 @@ struct Engine {
 
 std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& why);
+// `every e1=A[f1] -> not A[fx] for T` (engine_absent.hip)
+std::unique_ptr<Engine> make_absent_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why);
 // list_hint: expected partials per key at once (sizes the per-key lists of an

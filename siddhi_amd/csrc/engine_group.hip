@@ -415,6 +415,7 @@ __global__ __launch_bounds__(kRsBlock) void k_prep_scatter(const PrepArgs* __res
       f = F_NEW;
       if (kn[r] && a.null_skip) {
         f |= F_SKIP;
+        key = (uint32_t)li;   // no key: spread over the groups (passed over by every walk)
       } else {
         if (a.is_b) f |= F_B;
         if (p1) {
@@ -461,9 +462,286 @@ void launch_prep_scatter(const PrepArgs* d_args, int64_t n_ext, const uint32_t* 
 }
 
 namespace {
+
+// ---------------------------------------------------------------- sorted LDS walk
+// The exact per-key order inside a hashed group: the group's rows (arrival
+// order after the stable 16-bit hashed sort) are staged in LDS and binned by
+// 10 more bits of key_bucket_mix(key) (1024 bins; the mix is a bijection, so
+// rows of one key share a bin and a bin holds few keys): a counting pass with
+// LDS atomics places them, and each row's rank among its bin's rows by arrival
+// index restores arrival order inside the bin (stable).  Each candidate then
+// walks the later rows of its bin in LDS, passing over other keys' rows: the
+// forward scan's semantics (walk_partial: expiry at the first later event of
+// the key with ts - ts_i > within, else a B event passing f2 completes it,
+// else it stays open -- dormant when every later event would expire it) with
+// no global loads but f2's attribute reads.  The group's rows are written back
+// in bin order (per key: creation order, all the compaction tail needs) with
+// the outcome byte / match row, as the forward scan writes them.
+constexpr int kLwThreads = 256;
+constexpr int kLwCap = 2048;
+constexpr int kLwBins = 1024;
+constexpr int kLwPer = kLwCap / kLwThreads;
+
+__device__ __forceinline__ uint32_t lw_bin(uint32_t key) { return (key_bucket_mix(key) >> 16) & (kLwBins - 1); }
+
+template <bool FAST>
+__global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restrict__ ap, int ngroups,
+                                                          const uint32_t* __restrict__ gbeg,
+                                                          const uint32_t* __restrict__ gend, uint32_t* __restrict__ skey,
+                                                          uint32_t* __restrict__ spv, const int32_t* __restrict__ sts,
+                                                          int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                          ScanOut* __restrict__ blk) {
+  const ScanArgs& a = *ap;
+  const DExprSet es = a.es;
+  __shared__ uint32_t lk[kLwCap];
+  __shared__ uint32_t lpv[kLwCap];
+  __shared__ int32_t lts[kLwCap];
+  __shared__ uint16_t lbin[kLwCap];     // binned (unordered), then arrival-ordered inside each bin
+  __shared__ uint16_t lord[kLwCap];
+  __shared__ uint32_t cnt[kLwBins];
+  __shared__ uint32_t bstart[kLwBins + 1];
+  __shared__ uint32_t wsum[kLwThreads / 64];
+  __shared__ uint32_t rbase;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t tbase = a.x.batch.ts[0];
+  const int64_t W = a.within;
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0, over = 0;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int64_t q0 = gbeg[g], q1 = gend[g];
+    const int len = (int)(q1 - q0);
+    if (len <= 0) continue;
+    if (len > kLwCap) {   // the host redoes this push on the full key sort
+      over += tid == 0 ? 1u : 0u;
+      continue;
+    }
+    // ---- stage: every load issued before the first LDS store
+    uint32_t rk[kLwPer], rp[kLwPer];
+    int32_t rt[kLwPer];
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      const int64_t q = q0 + (i < len ? i : 0);
+      rk[j] = skey[q];
+      rp[j] = spv[q];
+      rt[j] = sts[q];
+    }
+    __syncthreads();   // the previous group's readers are done
+    for (int b = tid; b < kLwBins; b += kLwThreads) cnt[b] = 0;
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      if (i < len) {
+        lk[i] = rk[j];
+        lpv[i] = rp[j];
+        lts[i] = rt[j];
+      }
+    }
+    __syncthreads();
+    // ---- counting pass: a slot per row in its bin (LDS atomics: unordered)
+    uint32_t slot[kLwPer];
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      slot[j] = i < len ? atomicAdd(&cnt[lw_bin(rk[j])], 1u) : 0u;
+    }
+    __syncthreads();
+    // bin starts: exclusive scan of cnt (4 bins per thread)
+    {
+      constexpr int kB = kLwBins / kLwThreads;
+      uint32_t c[kB], sum = 0;
+#pragma unroll
+      for (int j = 0; j < kB; j++) {
+        c[j] = cnt[tid * kB + j];
+        sum += c[j];
+      }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t pre = inc - sum;
+      for (int k = 0; k < w; k++) pre += wsum[k];
+#pragma unroll
+      for (int j = 0; j < kB; j++) {
+        bstart[tid * kB + j] = pre;
+        pre += c[j];
+      }
+      if (tid == kLwThreads - 1) bstart[kLwBins] = pre;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      if (i < len) lbin[bstart[lw_bin(rk[j])] + slot[j]] = (uint16_t)i;
+    }
+    __syncthreads();
+    // arrival order inside a bin: rank by arrival index among the bin's rows
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      if (i < len) {
+        const uint32_t bn = lw_bin(rk[j]);
+        const int b0 = (int)bstart[bn], b1 = (int)bstart[bn + 1];
+        int rank = 0;
+        for (int y = b0; y < b1; y++) rank += lbin[y] < (uint16_t)i ? 1 : 0;
+        lord[b0 + rank] = (uint16_t)i;
+      }
+    }
+    __syncthreads();
+    // ---- walks: each candidate over the later rows of its bin
+    for (int p0 = 0; p0 < len; p0 += kLwThreads) {   // rounds: uniform trip count (dormant row reservation)
+      const int p = p0 + tid;
+      uint8_t out = PS_NONE;
+      int i = 0;
+      uint32_t k = 0;
+      if (p < len) {
+      i = lord[p];
+      const uint32_t pv = lpv[i];
+      const uint32_t f = pv_flags(pv);
+      k = lk[i];
+      if (f & F_CAND) {
+        const int pend_end = (int)bstart[lw_bin(k) + 1];
+        const int64_t tsi = tbase + (int64_t)lts[i];
+        int64_t prev = tsi;
+        uint8_t st = ST_OPEN;
+        uint8_t pend = 0;
+        int32_t mrow = -1;
+        for (int q = p + 1; q < pend_end; q++) {
+          const int jj = lord[q];
+          if (lk[jj] != k) continue;   // another key of the bin
+          const uint32_t pq = lpv[jj];
+          const uint32_t fq = pv_flags(pq);
+          if ((fq & F_SKIP) || !(fq & F_NEW)) continue;   // a dropped event / a carried partial: not an event
+          const int64_t tq = tbase + (int64_t)lts[jj];
+          if (W != INT64_MAX && tq < prev) {   // a per-key time regression: generic NFA engine
+            viol = 1;
+            break;
+          }
+          prev = tq;
+          steps++;
+          if (tq - tsi > W) {   // stabilizeStates -> expireEvents
+            st = ST_DEAD;
+            break;
+          }
+          if (fq & F_B) {
+            pend = PS_PEND;
+            PairCtx cx{&a.x, (int64_t)pv_row(pv), (int64_t)pv_row(pq), a.s_first};
+            if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+              st = ST_MATCH;
+              mrow = (int32_t)pv_row(pq);
+              break;
+            }
+          }
+        }
+        if (st == ST_MATCH) {
+          out = PS_MATCH;
+          match_row[q0 + p] = mrow;
+        } else if (st == ST_OPEN) {
+          if (a.prune && a.t_end - tsi > W) {
+            pruned++;
+            if (a.spill) out = PS_DORM | pend;
+          } else {
+            out = PS_OPEN | pend;
+          }
+        }
+      }
+      if (a.lp && (f & F_NEW) && !(f & F_SKIP)) a.lp[k - a.lp_base] = a.push_idx;
+      skey[q0 + p] = k;
+      spv[q0 + p] = pv;
+      pst[q0 + p] = out;
+      }
+      if (a.direct) {
+        // this round's open (carry) or dormant partials -> rows of `fresh`, in
+        // position order (per key: creation order), one reservation per round
+        const bool dm = (out & 0x7Fu) == a.direct_val;
+        const uint64_t bm = __ballot(dm);
+        if (lane == 0) wsum[w] = (uint32_t)__popcll(bm);
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int kk = 0; kk < kLwThreads / 64; kk++) {
+          pre += kk < w ? wsum[kk] : 0u;
+          tot += wsum[kk];
+        }
+        if (tid == 0 && tot) rbase = atomicAdd(a.fresh_n, tot);
+        __syncthreads();
+        if (dm) {
+          const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+          const int64_t o = (int64_t)rbase + pre + (uint32_t)__popcll(bm & lt);
+          if (o < a.fresh_cap) {
+            const SpillCols& d = a.fresh;
+            const int64_t r = (int64_t)pv_row(lpv[i]);
+            const ColSet& cs = a.x.cs(r);
+            const int64_t row = a.x.row(r);
+            for (int c = 0; c < d.ncols; c++) {
+              if (!((a.amask >> c) & 1u)) continue;
+              const Val v = col_load(cs, row, c);
+              switch (d.types[c]) {
+                case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)d.col[c])[o] = (uint32_t)v.b; break;
+                case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)d.col[c])[o] = v.b; break;
+                case SHD_T_BOOL: ((uint8_t*)d.col[c])[o] = (uint8_t)v.b; break;
+              }
+              d.nul[c][o] = (uint8_t)v.null;
+            }
+            d.ts[o] = tbase + (int64_t)lts[i];
+            d.key[o] = k;
+            d.seq[o] = a.x.seq(r);
+            d.pend[o] = (uint8_t)(((out & PS_PEND) || (r < a.x.C && a.carry_pend[r])) ? 1 : 0);
+            if (d.push) d.push[o] = a.push_idx;
+          }
+        }
+        __syncthreads();   // wsum / rbase reused by the next round
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    steps += __shfl_xor(steps, o, 64);
+    pruned += __shfl_xor(pruned, o, 64);
+    viol |= __shfl_xor(viol, o, 64);
+    over += __shfl_xor(over, o, 64);
+  }
+  __shared__ ScanOut wpart[kLwThreads / 64];
+  if (lane == 0) wpart[w] = ScanOut{steps, pruned, viol, over};
+  __syncthreads();
+  if (tid == 0) {
+    ScanOut r = wpart[0];
+    for (int k = 1; k < kLwThreads / 64; k++) {
+      r.steps += wpart[k].steps;
+      r.pruned += wpart[k].pruned;
+      r.violation |= wpart[k].violation;
+      r.hbm_walks += wpart[k].hbm_walks;
+    }
+    blk[blockIdx.x] = r;
+  }
+}
+
 }  // namespace
 
 int group_walk_blocks(int ngroups) { return ngroups < 8192 ? ngroups : 8192; }
+
+int lds_walk_cap() { return kLwCap; }
+
+void launch_lds_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, uint32_t* skey, uint32_t* spv,
+                     const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row, uint8_t* pst,
+                     ScanOut* blk, int nblk, hipStream_t s) {
+  const int ngroups = 1 << bits;
+  SHD_HIP(hipMemsetAsync(gbeg, 0, (size_t)ngroups * 4, s));
+  SHD_HIP(hipMemsetAsync(gend, 0, (size_t)ngroups * 4, s));
+  hipLaunchKernelGGL(k_group_bounds, dim3(grid_for(n_ext, 1, 4096)), dim3(kBlock), 0, s, skey, spv, n_ext, bits, gbeg,
+                     gend);
+  SHD_CHECK_LAUNCH();
+  if (fast)
+    hipLaunchKernelGGL(k_lds_walk<true>, dim3(nblk), dim3(kLwThreads), 0, s, d_args, ngroups, (const uint32_t*)gbeg,
+                       (const uint32_t*)gend, skey, spv, sts, match_row, pst, blk);
+  else
+    hipLaunchKernelGGL(k_lds_walk<false>, dim3(nblk), dim3(kLwThreads), 0, s, d_args, ngroups, (const uint32_t*)gbeg,
+                       (const uint32_t*)gend, skey, spv, sts, match_row, pst, blk);
+  SHD_CHECK_LAUNCH();
+}
 
 void launch_group_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, const uint32_t* skey,
                        const uint32_t* spv, const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row,

@@ -377,7 +377,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       q++;
     }
   }
-  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = a.spill ? ST_DORM : ST_PRUNED;
   return st;
 }
 
@@ -498,8 +498,14 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
         if (a.logical == 2) match_row[p] = and_open_code(a, pv_row(pvp));   // carried half state unchanged
       } else if (st == ST_PRUNED) {
         pruned++;   // every later event is at or after t_end: it would expire this partial
+      } else if (st == ST_DORM) {
+        out = PS_DORM;
+        pruned++;
       }
     }
+    // the push index under the key of every event (dormant partials of that
+    // key, from earlier pushes, are expired by it)
+    if (a.lp && (pv_flags(pvp) & F_NEW) && !(pv_flags(pvp) & F_SKIP)) a.lp[k - a.lp_base] = a.push_idx;
     pst[p] = out;
   };
   const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
@@ -678,7 +684,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     first = false;
     q0 += 64;
   }
-  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = a.spill ? ST_DORM : ST_PRUNED;
   if (lane == 0) {
     steps += wsteps;
     if (wviol) viol = 1;
@@ -693,6 +699,9 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       no++;
       if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
     } else if (st == ST_PRUNED) {
+      pruned++;
+    } else if (st == ST_DORM) {
+      out = PS_DORM | PS_PEND;
       pruned++;
     }
     pst[p] = out;
@@ -750,6 +759,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
       } else if (st == ST_PRUNED) {
         pruned++;
+      } else if (st == ST_DORM) {
+        out = PS_DORM | PS_PEND;
+        pruned++;
       }
       pst[p] = out;
   };
@@ -792,6 +804,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         out = PS_OPEN | PS_PEND;
         no++;
       } else if (st == ST_PRUNED) {
+        pruned++;
+      } else if (st == ST_DORM) {
+        out = PS_DORM | PS_PEND;
         pruned++;
       } else if (st == ST_YIELD) {
         out = PS_CONT;
@@ -1266,6 +1281,9 @@ struct GatherArgs {
   uint64_t* dkey;
   int64_t* dseq;
   uint32_t amask;   // k_gather_list: stream-A columns to copy
+  const uint32_t* obase;   // k_gather_list: first output row (device word; null: 0)
+  uint32_t* dpush;         // dormant rows: the push index they became dormant in
+  uint32_t push_idx;
   // new-list / pending-list placement of each carried partial (export_replay)
   uint8_t* dpend;
   const uint8_t* pend_old;
@@ -1343,7 +1361,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __res
 // open partial its own thread, so all their random row reads are in flight at
 // once.  Only the e1 columns read again after the carry (amask) are copied.
 __global__ __launch_bounds__(kBlock) void k_open_list(const uint8_t* __restrict__ pst, const uint32_t* __restrict__ boff,
-                                                      int64_t n, int64_t tile, uint32_t* __restrict__ olist) {
+                                                      int64_t n, int64_t tile, uint32_t* __restrict__ olist,
+                                                      uint32_t val) {
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n ? t0 + tile : n;
   __shared__ uint32_t wsum[kBlock / 64];
@@ -1353,7 +1372,7 @@ __global__ __launch_bounds__(kBlock) void k_open_list(const uint8_t* __restrict_
   for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
     const int64_t p = c0 + threadIdx.x;
     const uint8_t ps = p < t1 ? pst[p] : (uint8_t)PS_NONE;
-    const bool hit = (ps & 0x7Fu) == PS_OPEN;
+    const bool hit = (ps & 0x7Fu) == val;
     const uint64_t m = __ballot(hit);
     if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
     __syncthreads();
@@ -1377,8 +1396,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __rest
                                                         const uint64_t* __restrict__ skey64) {
   const GatherArgs& a = *ap;
   const ExtRows& x = a.x;
-  for (int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x; o < n_open; o = n_open) {
-    const int64_t p = olist[o];
+  const int64_t obase = a.obase ? (int64_t)*a.obase : 0;
+  for (int64_t oi = (int64_t)blockIdx.x * kBlock + threadIdx.x; oi < n_open; oi = n_open) {
+    const int64_t p = olist[oi];
+    const int64_t o = obase + oi;
     const int64_t r = pv_row(spv[p]);
     // one uniform column table per branch (carried rows / pushed rows)
     if (r < x.C) {
@@ -1403,6 +1424,106 @@ __global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __rest
     }
     a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
     a.dpend[o] = (uint8_t)(((pst[p] & PS_PEND) || (r < x.C && a.pend_old[r])) ? 1 : 0);
+    if (a.dpush) a.dpush[o] = a.push_idx;
+  }
+}
+
+// Per-tile count of one outcome value (the low 7 bits of pst): the compaction
+// tiles of k_open_list for dormant partials.
+__global__ __launch_bounds__(kBlock) void k_tile_count_val(const uint8_t* __restrict__ pst, int64_t n, int64_t tile,
+                                                           uint32_t val, uint32_t* __restrict__ bcnt) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  uint32_t c = 0;
+  for (int64_t pb = t0 + (int64_t)threadIdx.x * 16; pb < t1; pb += kBlock * 16) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
+    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++) c += (pb + i < t1 && ((wv[i >> 2] >> ((i & 3) * 8)) & 127u) == val) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ uint32_t ws[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < kBlock / 64; k++) t += ws[k];
+    bcnt[blockIdx.x] = t;
+  }
+}
+
+// ---------------------------------------------------------------- dormant partials
+// A dormant partial (PS_DORM) of key K, made dormant at push p, is alive while
+// no event of K came in a later push (lp[K - base] <= p): every such event is
+// at or after the time that made it dormant, more than `within` after the
+// partial, so it expired it (StreamPreStateProcessor.expireEvents :326-361,
+// per key: PartitionStateHolder).  Only a push going back in time can still
+// meet an alive one -- the NFA hand-over replays them.
+__device__ __forceinline__ bool spill_alive(const SpillCols& s, int64_t i, const uint32_t* lp, uint64_t lp_base,
+                                            uint64_t lp_n) {
+  const uint64_t k = s.key[i] - lp_base;
+  return k >= lp_n || lp[k] <= s.push[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_spill_count(SpillCols s, int64_t n, int64_t tile, const uint32_t* lp,
+                                                        uint64_t lp_base, uint64_t lp_n, uint32_t* __restrict__ bcnt) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  uint32_t c = 0;
+  for (int64_t i = t0 + threadIdx.x; i < t1; i += kBlock) c += spill_alive(s, i, lp, lp_base, lp_n) ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ uint32_t ws[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < kBlock / 64; k++) t += ws[k];
+    bcnt[blockIdx.x] = t;
+  }
+}
+
+// Alive rows of src -> dst (order kept: per key in creation order).
+__global__ __launch_bounds__(kBlock) void k_spill_move(SpillCols src, SpillCols dst, int64_t n, int64_t tile,
+                                                       const uint32_t* lp, uint64_t lp_base, uint64_t lp_n,
+                                                       const uint32_t* __restrict__ boff) {
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t base = boff[blockIdx.x];
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
+    const int64_t i = c0 + threadIdx.x;
+    const bool hit = i < t1 && spill_alive(src, i, lp, lp_base, lp_n);
+    const uint64_t m = __ballot(hit);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; k++) {
+      pre += k < w ? wsum[k] : 0u;
+      tot += wsum[k];
+    }
+    if (hit) {
+      const int64_t o = base + pre + (uint32_t)__popcll(m & lt);
+      for (int c = 0; c < src.ncols; c++) {
+        switch (src.types[c]) {
+          case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT:
+            ((uint32_t*)dst.col[c])[o] = ((const uint32_t*)src.col[c])[i];
+            break;
+          case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)dst.col[c])[o] = ((const uint64_t*)src.col[c])[i]; break;
+          case SHD_T_BOOL: ((uint8_t*)dst.col[c])[o] = ((const uint8_t*)src.col[c])[i]; break;
+        }
+        dst.nul[c][o] = src.nul[c][i];
+      }
+      dst.ts[o] = src.ts[i];
+      dst.key[o] = src.key[i];
+      dst.seq[o] = src.seq[i];
+      dst.pend[o] = src.pend[i];
+      dst.push[o] = src.push[i];
+    }
+    base += tot;
+    __syncthreads();
   }
 }
 
@@ -1412,6 +1533,7 @@ struct CarryTable {
   // the new list for the pending list (StreamPreStateProcessor.updateState);
   // 0: still in the new list (export_replay rebuilds the placement)
   DevBuf pend;
+  DevBuf push;   // dormant table: the push index a row became dormant in
   // logical AND: filled-operand bits and the held operand event (stream B)
   DevBuf half, bcol[kMaxCols], bnul[kMaxCols], bts, bseq;
   void reserve_b(int64_t n, const std::vector<int>& types) {
@@ -1567,6 +1689,98 @@ struct PatternEngine : Engine {
   int64_t t_last = INT64_MIN;   // time of the last event (arrival order) of the committed pushes
   int64_t last_b_seq = -1;      // arrival index of the last B-stream event (export_replay placement)
   static constexpr int64_t kPruneMinRows = 1 << 16;
+  // Dormant partials (partitioned plain / OR plans, PS_DORM): open partials
+  // that every event from the push's latest time on would expire wait here,
+  // outside the next pushes' sort, until their key's next event expires them
+  // (lp: the last push index per key) -- or a push going back in time hands
+  // them to the NFA engine (unspill + export_replay).  Rows are per key in
+  // creation order and older than any carried row of their key.
+  CarryTable spill[2];
+  int scur = 0;
+  int64_t S = 0;              // alive dormant partials (as of the last push)
+  bool spill_off = false;     // keys span too wide a range for the lp table: carry everything
+  DevBuf d_lp;                // push index of each key's last event, keys [lp_base, lp_base + lp_n)
+  uint64_t lp_base = 0, lp_n = 0;
+  uint32_t push_idx = 0;      // pushes that updated lp
+  static constexpr uint64_t kLpMax = 1ull << 27;
+  DevBuf d_scnt, d_soff, d_dlist;
+  CarryTable fresh;            // sorted LDS walk: this push's dormant partials, written by the walk
+  bool dorm_direct = false;    // this push: fresh holds them (finish copies instead of gathering)
+  bool open_direct = false;    // this push: the walk wrote the next carry table (finish skips the gather)
+  // this push (sort_push -> finish)
+  bool spill_now = false;
+  uint32_t n_dorm = 0, n_surv = 0;
+  int64_t stile = 0;
+  int nst = 0;
+
+  bool spill_plan() const {
+    return partitioned && logical != 2 && W != INT64_MAX && !type_key64(key_type[0]) && !type_key64(key_type[1]) &&
+           !getenv("SHD_NO_SPILL");
+  }
+  SpillCols spill_cols(CarryTable& t) const {
+    SpillCols c{};
+    c.ncols = (int)typesA.size();
+    for (size_t i = 0; i < typesA.size(); i++) {
+      c.types[i] = (int32_t)typesA[i];
+      c.col[i] = t.col[i].p;
+      c.nul[i] = t.nul[i].as<uint8_t>();
+    }
+    c.ts = t.ts.as<int64_t>();
+    c.key = t.key.as<uint64_t>();
+    c.seq = t.seq.as<int64_t>();
+    c.pend = t.pend.as<uint8_t>();
+    c.push = t.push.as<uint32_t>();
+    return c;
+  }
+  // the lp table covers keys [kmin, kmax] (grown, zero-filled, old entries kept)
+  bool lp_cover(uint64_t kmin, uint64_t kmax) {
+    if (lp_n && kmin >= lp_base && kmax < lp_base + lp_n) return true;
+    const uint64_t lo = lp_n ? std::min(lp_base, kmin) : kmin;
+    const uint64_t hi = lp_n ? std::max(lp_base + lp_n - 1, kmax) : kmax;
+    if (hi - lo + 1 > kLpMax) return false;
+    const uint64_t nn = std::min<uint64_t>(kLpMax, (hi - lo + 1) + (hi - lo + 1) / 8 + 1024);
+    DevBuf nb;
+    nb.reserve(nn * 4);
+    SHD_HIP(hipMemsetAsync(nb.p, 0, nn * 4, stream));
+    if (lp_n)
+      SHD_HIP(hipMemcpyAsync(nb.as<uint32_t>() + (lp_base - lo), d_lp.p, lp_n * 4, hipMemcpyDeviceToDevice, stream));
+    SHD_HIP(hipStreamSynchronize(stream));
+    std::swap(d_lp.p, nb.p);
+    std::swap(d_lp.cap, nb.cap);
+    lp_base = lo;
+    lp_n = nn;
+    return true;
+  }
+  // dormant rows back into the carry, in front of the carried rows (exact:
+  // carrying every open partial is the reference's own state)
+  void unspill() {
+    if (S <= 0) return;
+    const int nxt = cur ^ 1;
+    CarryTable& d = carry[nxt];
+    CarryTable& sp = spill[scur];
+    const CarryTable& c = carry[cur];
+    d.reserve(S + C, typesA);
+    hipStream_t s = stream;
+    auto cp = [&](DevBuf& dst, const DevBuf& a, const DevBuf& b, size_t w) {
+      SHD_HIP(hipMemcpyAsync(dst.p, a.p, (size_t)S * w, hipMemcpyDeviceToDevice, s));
+      if (C > 0) SHD_HIP(hipMemcpyAsync(dst.as<char>() + (size_t)S * w, b.p, (size_t)C * w, hipMemcpyDeviceToDevice, s));
+    };
+    for (size_t i = 0; i < typesA.size(); i++) {
+      if (!((carry_mask >> i) & 1u)) continue;
+      cp(d.col[i], sp.col[i], c.col[i], type_size(typesA[i]));
+      cp(d.nul[i], sp.nul[i], c.nul[i], 1);
+    }
+    cp(d.ts, sp.ts, c.ts, 8);
+    cp(d.key, sp.key, c.key, 8);
+    cp(d.seq, sp.seq, c.seq, 8);
+    cp(d.pend, sp.pend, c.pend, 1);
+    SHD_HIP(hipStreamSynchronize(s));
+    cur = nxt;
+    C += S;
+    S = 0;
+    counters.carry = C;
+    counters.dormant = 0;
+  }
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
       d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_gbeg, d_gend, d_olist;
@@ -1578,6 +1792,10 @@ struct PatternEngine : Engine {
   int kind() const override { return ENG_PATTERN; }
 
   void reset() override {
+    S = 0;
+    push_idx = 0;
+    lp_n = 0;
+    spill_off = false;
     C = 0;
     last_b_seq = -1;
     seq = 0;
@@ -1605,6 +1823,7 @@ struct PatternEngine : Engine {
   // partial is gone, it is replayed past the start state only (skip_start),
   // so it opens no partial the reference does not hold.
   void export_replay(std::vector<Replay>& parts) override {
+    unspill();
     SHD_HIP(hipStreamSynchronize(stream));
     const CarryTable& t = carry[cur];
     std::vector<int64_t> ts(C), sq(C);
@@ -1701,6 +1920,7 @@ struct PatternEngine : Engine {
 
   // open partials (carry table) + horizon guard
   void save_state(SnapW& w) override {
+    unspill();   // the snapshot holds every open partial as a carried one
     w.put<int64_t>(C);
     w.put<int32_t>(have_horizon ? 1 : 0);
     w.put<int64_t>(horizon);
@@ -1802,6 +2022,9 @@ struct PatternEngine : Engine {
 
   void push(const Staged& b) override {
     if (b.n <= 0) return;
+    spill_now = false;
+    dorm_direct = false;
+    open_direct = false;
     int la = 0;
     int64_t t_last_probe = 0;
     if (bucket_candidate(b, la, t_last_probe) && bucket_push(b, la, t_last_probe)) return;
@@ -2084,6 +2307,7 @@ struct PatternEngine : Engine {
     const char* gv = getenv("SHD_GROUP");   // "1": when groups are small; "force": always
     const bool force = gv && std::strcmp(gv, "force") == 0;
     if (!gv || !partitioned || logical != 0 || !(group_hint || force) || getenv("SHD_NO_GROUP") ||
+        (spill_plan() && !spill_off) ||
         getenv("SHD_NO_FUSED_GROUP") ||
         key_col[slot] < 0 || !(key_type[slot] == SHD_T_STRING || key_type[slot] == SHD_T_INT))
       return false;
@@ -2216,6 +2440,130 @@ struct PatternEngine : Engine {
       horizon = std::max(horizon, t_end);
     }
     finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
+  }
+
+  // Dormant partials of this push (per-tile counts + offsets at [2 ntile,
+  // 3 ntile), total at d_mo[2]) and the alive rows of the dormant table
+  // (offsets d_soff, total d_mo[3]): lp already holds this push's events.
+  void dormant_counts(int64_t n_ext, int64_t tile, int ntile, uint32_t* d_mo) {
+    hipStream_t s = stream;
+    hipLaunchKernelGGL(k_tile_count_val, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext,
+                       tile, (uint32_t)PS_DORM, d_bcnt.as<uint32_t>() + 2 * ntile);
+    SHD_CHECK_LAUNCH();
+    scan_exclusive_u32(d_bcnt.as<uint32_t>() + 2 * ntile, d_boff.as<uint32_t>() + 2 * ntile, ntile, d_mo + 2, d_scan, s);
+    if (S > 0) {
+      nst = grid_for(S, 1, 4096);
+      stile = ceil_div(ceil_div(S, nst), kBlock) * kBlock;
+      nst = (int)ceil_div(S, stile);
+      d_scnt.reserve((size_t)nst * 4);
+      d_soff.reserve((size_t)nst * 4);
+      hipLaunchKernelGGL(k_spill_count, dim3(nst), dim3(kBlock), 0, s, spill_cols(spill[scur]), S, stile,
+                         (const uint32_t*)d_lp.as<uint32_t>(), lp_base, lp_n, d_scnt.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      scan_exclusive_u32(d_scnt.as<uint32_t>(), d_soff.as<uint32_t>(), nst, d_mo + 3, d_scan, s);
+    } else {
+      SHD_HIP(hipMemsetAsync(d_mo + 3, 0, 4, s));
+    }
+  }
+
+  // Sorted LDS walk (engine_group.hip k_lds_walk): a stable 16-bit hashed key
+  // sort (two passes instead of the full key's three), then per group the
+  // exact key order and the walks in LDS -- no forward-scan / resume passes
+  // over HBM.  Partitioned plain patterns with 32-bit keys and time offsets,
+  // groups of at most lds_walk_cap() rows (expected rows per group = rows /
+  // min(2^16, key range)).  false: some group was larger (nothing committed;
+  // the caller redoes the push on the full key sort).
+  static constexpr int kLdsBits = 16;
+  bool lds_skip = false;
+  bool lds_candidate(const PrepAgg& pg, int64_t n_ext, bool key64) const {
+    if (lds_skip || !partitioned || logical != 0 || key64 || pg.ovf || pg.kmin > pg.kmax || getenv("SHD_NO_LDSWALK") ||
+        getenv("SHD_GROUP"))
+      return false;
+    const double nk = std::min<double>((double)(1 << kLdsBits), (double)(pg.kmax - pg.kmin) + 1.0);
+    return (double)n_ext / nk <= 0.75 * lds_walk_cap();
+  }
+  bool lds_push(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg) {
+    hipStream_t s = stream;
+    d_k32_alt.reserve(n_ext * 4);
+    d_pv_alt.reserve(n_ext * 4);
+    d_ts_alt.reserve(n_ext * 4);
+    bool in_alt = false;
+    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
+                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, kLdsBits, d_sort, s, in_alt, true,
+                           0);
+    uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
+    uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
+    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
+    mark("key_sort");
+    ScanArgs sa{};
+    sa.x = x;
+    sa.es = dset();
+    sa.f2 = dfilters(f2);
+    sa.logical = 0;
+    sa.s_first = s_first;
+    sa.s_second = s_second;
+    sa.within = W;
+    sa.partitioned = 1;
+    sa.prune = 0;   // partitioned: every open partial is carried (per-key expiry)
+    if (!getenv("SHD_CARRY_GATHER")) {
+      // the walk writes the open partials straight into the next carry table
+      // (every candidate, carried or opened by this push, may stay open)
+      const int64_t cap = C + (int64_t)pg.n_cand;
+      CarryTable& nt = carry[cur ^ 1];
+      nt.reserve(cap, typesA);
+      carry[cur].pend.reserve(std::max<int64_t>(C, 1));
+      sa.direct = 1;
+      sa.direct_val = PS_OPEN;
+      sa.fresh = spill_cols(nt);
+      sa.fresh.push = nullptr;
+      sa.amask = carry_mask;
+      sa.fresh_n = reinterpret_cast<unsigned int*>(d_agg.as<char>() + 144);
+      sa.fresh_cap = cap;
+      sa.carry_pend = carry[cur].pend.as<uint8_t>();
+      SHD_HIP(hipMemsetAsync(d_agg.as<char>() + 144, 0, 4, s));
+    }
+    const int64_t t_end = (int64_t)pg.ts_max;
+    sa.t_end = t_end;
+    const int ngroups = 1 << kLdsBits;
+    d_gbeg.reserve((size_t)ngroups * 4);
+    d_gend.reserve((size_t)ngroups * 4);
+    const int nwalk = std::min(ngroups, 8192);
+    const int nblk = grid_for(n_ext, 1, 4096);
+    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
+    const int ntile = (int)ceil_div(n_ext, tile);
+    d_blk.reserve((size_t)std::max<int64_t>(nwalk, 3 * nblk) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
+    d_bcnt.reserve((size_t)3 * ntile * 4);
+    d_boff.reserve((size_t)3 * ntile * 4);
+    launch_lds_walk(dev_args(sa), sa.f2.fp.ok != 0, n_ext, kLdsBits, skey32, spv, sts32, d_gbeg.as<uint32_t>(),
+                    d_gend.as<uint32_t>(), d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), nwalk, s);
+    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
+                       d_bcnt.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
+    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
+    SHD_CHECK_LAUNCH();
+    mark("forward_scan");
+    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
+    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    mark("compact");
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 84, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    ScanOut so;
+    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
+    const uint32_t m = h_agg.as<uint32_t>()[32];
+    const uint32_t n_open = h_agg.as<uint32_t>()[33];
+    open_direct = sa.direct && h_agg.as<uint32_t>()[36] == n_open;
+    if (so.hbm_walks) return false;   // a group beyond the LDS capacity
+    if (so.violation) throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
+    if (so.pruned) {
+      have_horizon = true;
+      horizon = std::max(horizon, t_end);
+    }
+    counters.group_bits = kLdsBits;
+    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
+    return true;
   }
 
   void sort_push(const Staged& b) {
@@ -2371,14 +2719,40 @@ struct PatternEngine : Engine {
     // (PartitionStateHolder: per-key pending lists), which may arrive in any
     // later push with any timestamp, so partitioned plans carry every open
     // partial until its key kills or completes it.
-    const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX && !partitioned;
+    // partitioned: the same partials become dormant (PS_DORM) instead -- on
+    // the full key sort path; the sorted LDS walk carries every open partial
+    // (a per-event push-index write would be a random store there)
+    const bool lds = lds_candidate(pg, n_ext, key64);
+    bool spill_p = false;
+    if (!lds && spill_plan() && !spill_off) {
+      if (pg.kmin <= pg.kmax && !lp_cover(pg.kmin, pg.kmax)) spill_off = true;
+      else spill_p = S > 0 || n_ext >= kPruneMinRows || getenv("SHD_SPILL") != nullptr;
+    }
+    if (!spill_p && S > 0) {   // the dormant rows go back into the carry: redo the push with them
+      unspill();
+      sort_push(b);
+      return;
+    }
+    const bool prune = (n_ext >= kPruneMinRows && W != INT64_MAX && !partitioned) || spill_p;
+    if (lds) {
+      if (lds_push(b, x, n_ext, pg)) return;
+      lds_skip = true;   // redo this push on the full key sort
+      try {
+        sort_push(b);
+      } catch (...) {
+        lds_skip = false;
+        throw;
+      }
+      lds_skip = false;
+      return;
+    }
     // implicit grouping needs the reference's global expiry order to be the
     // per-key one: pushed rows time-ordered, carried partials before them
     const bool grouped = partitioned || (implicit_key && !pg.unmono && (C == 0 || pg.carry_tmax <= pg.ts_min));
     // grouped LDS walk (engine_group.hip): a 16-bit hashed key sort (two
     // passes) and the per-group walk in LDS, when the groups are small --
     // expected rows per group = rows / min(2^16, keys of the push)
-    if (grouped && logical == 0 && !key64 && !pg.ovf && !getenv("SHD_NO_GROUP") && pg.kmin <= pg.kmax) {
+    if (grouped && logical == 0 && !key64 && !pg.ovf && !spill_p && !getenv("SHD_NO_GROUP") && pg.kmin <= pg.kmax) {
       const double nk = std::min<double>(65536.0, (double)(pg.kmax - pg.kmin) + 1.0);
       const char* gv = getenv("SHD_GROUP");
       if (gv && (std::strcmp(gv, "force") == 0 || (double)n_ext / nk <= kGroupMaxMean)) {
@@ -2422,7 +2796,7 @@ struct PatternEngine : Engine {
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         if (bits <= 32) {
-          const int hb = hashed_bucket_bits(pg, n_ext, bits, prune);
+          const int hb = hashed_bucket_bits(pg, n_ext, bits, prune && !partitioned);
           if (hb > 0) {
             bits = hb;
             hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
@@ -2479,14 +2853,20 @@ struct PatternEngine : Engine {
     sa.partitioned = grouped;
     sa.prune = prune;
     sa.hash_mask = hash_mask;
+    if (spill_p) {
+      sa.spill = 1;
+      sa.lp = d_lp.as<uint32_t>();
+      sa.lp_base = lp_base;
+      sa.push_idx = push_idx + 1;
+    }
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     const bool fast2 = sa.f2.fp.ok != 0 && (!logical || sa.f3.fp.ok != 0);
     // contiguous tiles of positions per block (compaction offsets per block)
     const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
     const int ntile = (int)ceil_div(n_ext, tile);
-    d_bcnt.reserve((size_t)2 * ntile * 4);
-    d_boff.reserve((size_t)2 * ntile * 4);
+    d_bcnt.reserve((size_t)3 * ntile * 4);
+    d_boff.reserve((size_t)3 * ntile * 4);
     const bool ts64 = sts64 != nullptr;
     // deferred walks are dense when a partial expects another event of its key
     // inside `within` (every event, ungrouped): E = events per `within` span / keys
@@ -2581,6 +2961,8 @@ struct PatternEngine : Engine {
     uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
     scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
     scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    spill_now = spill_p;
+    if (spill_p) dormant_counts(n_ext, tile, ntile, d_mo);
     mark("compact");
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     // time of the push's last event in arrival order (NeedNfa hand-over: global expiry of unpartitioned plans)
@@ -2590,6 +2972,8 @@ struct PatternEngine : Engine {
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];
     const uint32_t n_open = h_agg.as<uint32_t>()[33];
+    n_dorm = spill_p ? h_agg.as<uint32_t>()[34] : 0u;
+    n_surv = spill_p ? h_agg.as<uint32_t>()[35] : 0u;
     if (so.violation)   // the generic NFA engine takes over (shd_push replays the open partials)
       throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
     if (so.pruned) {
@@ -2658,7 +3042,7 @@ struct PatternEngine : Engine {
     // ---- carry the still-open partials
     int nxt = cur ^ 1;
     carry[nxt].reserve(n_open, typesA);
-    if (n_open > 0) {
+    if (n_open > 0 && !open_direct) {
       GatherArgs ga{};
       ga.x = x;
       ga.ncols = (int)typesA.size();
@@ -2698,7 +3082,8 @@ struct PatternEngine : Engine {
         ga.amask = carry_mask;
         d_olist.reserve((size_t)n_open * 4);
         hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
-                           (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_olist.as<uint32_t>());
+                           (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_olist.as<uint32_t>(),
+                           (uint32_t)PS_OPEN);
         SHD_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_gather_list, dim3(grid_cover((int64_t)n_open)), dim3(kBlock), 0, s, dev_args(ga),
                            (const uint32_t*)d_olist.as<uint32_t>(), (int64_t)n_open,
@@ -2711,6 +3096,69 @@ struct PatternEngine : Engine {
       SHD_CHECK_LAUNCH();
       mark("carry");
     }
+    // ---- dormant table: its alive rows, then this push's dormant partials
+    const int sn = scur ^ 1;
+    if (spill_now) {
+      CarryTable& dst = spill[sn];
+      const int64_t ns = (int64_t)n_surv + n_dorm;
+      dst.reserve(ns, typesA);
+      dst.push.reserve((size_t)std::max<int64_t>(ns, 1) * 4);
+      if (S > 0 && n_surv > 0) {
+        hipLaunchKernelGGL(k_spill_move, dim3(nst), dim3(kBlock), 0, s, spill_cols(spill[scur]), spill_cols(dst), S,
+                           stile, (const uint32_t*)d_lp.as<uint32_t>(), lp_base, lp_n,
+                           (const uint32_t*)d_soff.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+      }
+      if (n_dorm > 0 && dorm_direct) {
+        // the walk wrote them: append after the survivors
+        const int64_t o = n_surv;
+        auto cp = [&](DevBuf& d, const DevBuf& src, size_t w) {
+          SHD_HIP(hipMemcpyAsync(d.as<char>() + (size_t)o * w, src.p, (size_t)n_dorm * w, hipMemcpyDeviceToDevice, s));
+        };
+        for (size_t c = 0; c < typesA.size(); c++) {
+          if (!((carry_mask >> c) & 1u)) continue;
+          cp(dst.col[c], fresh.col[c], type_size(typesA[c]));
+          cp(dst.nul[c], fresh.nul[c], 1);
+        }
+        cp(dst.ts, fresh.ts, 8);
+        cp(dst.key, fresh.key, 8);
+        cp(dst.seq, fresh.seq, 8);
+        cp(dst.pend, fresh.pend, 1);
+        cp(dst.push, fresh.push, 4);
+      } else if (n_dorm > 0) {
+        GatherArgs gd{};
+        gd.x = x;
+        gd.ncols = (int)typesA.size();
+        gd.partitioned = 1;
+        gd.key64 = 0;
+        for (size_t c = 0; c < typesA.size(); c++) {
+          gd.types[c] = (int32_t)typesA[c];
+          gd.dcol[c] = dst.col[c].p;
+          gd.dnul[c] = dst.nul[c].as<uint8_t>();
+        }
+        gd.dts = dst.ts.as<int64_t>();
+        gd.dkey = dst.key.as<uint64_t>();
+        gd.dseq = dst.seq.as<int64_t>();
+        carry[cur].pend.reserve(std::max<int64_t>(C, 1));
+        gd.dpend = dst.pend.as<uint8_t>();
+        gd.pend_old = carry[cur].pend.as<uint8_t>();
+        gd.amask = carry_mask;
+        gd.obase = reinterpret_cast<const uint32_t*>(d_agg.as<char>() + 140);   // survivors come first
+        gd.dpush = dst.push.as<uint32_t>();
+        gd.push_idx = push_idx + 1;
+        d_dlist.reserve((size_t)n_dorm * 4);
+        // dormant offsets at [2 ntile, 3 ntile): k_open_list reads boff[ntile + tile]
+        hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                           (const uint32_t*)d_boff.as<uint32_t>() + ntile, n_ext, tile, d_dlist.as<uint32_t>(),
+                           (uint32_t)PS_DORM);
+        SHD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_gather_list, dim3(grid_cover((int64_t)n_dorm)), dim3(kBlock), 0, s, dev_args(gd),
+                           (const uint32_t*)d_dlist.as<uint32_t>(), (int64_t)n_dorm,
+                           (const uint8_t*)d_pst.as<uint8_t>(), spv, skey32, skey64);
+        SHD_CHECK_LAUNCH();
+      }
+      mark("dormant");
+    }
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -2718,6 +3166,11 @@ struct PatternEngine : Engine {
     SHD_HIP(hipEventElapsedTime(&ms, ev0, ev1));
     cur = nxt;
     C = n_open;
+    if (spill_now) {
+      scur = sn;
+      S = (int64_t)n_surv + n_dorm;
+      push_idx++;
+    }
     if (b.stream == sB) last_b_seq = seq + n - 1;
     seq += n;
     if (b.advance_time && t_end > now) now = t_end;
@@ -2726,6 +3179,7 @@ struct PatternEngine : Engine {
     counters.matches += m;
     counters.partial_scans += (int64_t)so.steps;
     counters.carry = C;
+    counters.dormant = S;
     counters.kernel_ns = (int64_t)(ms * 1e6);
       counters.partials += (int64_t)n_cand;
   }

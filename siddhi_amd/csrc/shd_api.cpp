@@ -654,6 +654,8 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
       if (!getenv("SHD_FORCE_NFA")) e = make_pattern_engine(p, why1);
       // SHD_NO_LOGICAL_SCAN: leave `every e1 -> (e2 or e3)` to the generic NFA engine (tests)
       if (!e && !getenv("SHD_NO_LOGICAL_SCAN") && !getenv("SHD_FORCE_NFA")) e = make_logical_pattern_engine(p, why1);
+      // SHD_NO_ABSENT_SCAN: leave `every e1 -> not X for t` to the generic NFA engine (tests)
+      if (!e && !getenv("SHD_NO_ABSENT_SCAN") && !getenv("SHD_FORCE_NFA")) e = make_absent_engine(p, why1);
       if (!e) e = make_nfa_engine(p, why2);
       if (!e) why1 += "; ";
     } else {
@@ -914,6 +916,7 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
       else if (kind == ENG_PATTERN) {
         fresh = make_pattern_engine(cur.plan, why);
         if (!fresh) fresh = make_logical_pattern_engine(cur.plan, why);
+        if (!fresh) fresh = make_absent_engine(cur.plan, why);
       }
       if (!fresh || fresh->kind() != kind) return fail(SHD_E_ARG, "snapshot of an engine this plan cannot run on");
       init_engine(*fresh, cur.plan);

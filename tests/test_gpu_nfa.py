@@ -17,7 +17,10 @@ pytestmark = pytest.mark.gpu
 ENGINE_PATTERN, ENGINE_NFA = 1, 4
 # `every e1 -> (e2 or|and e3)` runs on the forward-scan pattern engine
 # (tests/test_gpu_logical.py); every other S4 shape on the generic NFA engine
-EXPECT_ENGINE = {"or": ENGINE_PATTERN, "Por": ENGINE_PATTERN, "and": ENGINE_PATTERN, "Pand": ENGINE_PATTERN}
+# (tests/test_gpu_logical.py), and `every e1 -> not X for t` (unpartitioned) on
+# the absent forward-scan engine (tests/test_gpu_absent.py)
+EXPECT_ENGINE = {"or": ENGINE_PATTERN, "Por": ENGINE_PATTERN, "and": ENGINE_PATTERN, "Pand": ENGINE_PATTERN,
+                 "not": ENGINE_PATTERN}
 
 
 def split(sym, price, vol, ts, parts, call=1024):
@@ -163,6 +166,7 @@ def test_sequence_window_lanes(hip_available, monkeypatch, name, chunk, parts):
     `bare` (no every) stays on one lane."""
     if chunk != "auto":
         monkeypatch.setenv("SHD_NFA_CHUNK", chunk)
+    monkeypatch.setenv("SHD_NO_ABSENT_SCAN", "1")   # `not ... for`: the NFA's window lanes, not the absent scan
     qp, _ = compile_single_query(WINDOW_SEQS[name])
     sym, price, vol, ts = wl.stock_stream(20000, 50, 1.0, seed_offset=77)
     batches = split(sym, price, vol, ts, parts, call=700)
@@ -177,3 +181,8 @@ def test_sequence_window_lanes(hip_available, monkeypatch, name, chunk, parts):
         assert len(ora[2]) > 1000
     if name in ("not", "not100"):
         assert len(ora[2]) > 20
+        monkeypatch.delenv("SHD_NO_ABSENT_SCAN")
+        monkeypatch.delenv("SHD_NFA_WINDOW")
+        scan, _, skind = run_device(qp, batches)   # the absent forward-scan engine
+        assert skind == ENGINE_PATTERN
+        assert_same_rows(scan, ora)
