@@ -40,21 +40,33 @@ __device__ __forceinline__ uint32_t gw_group(uint32_t key, int bits) {
 }
 
 // Group boundaries in the sorted order: gbeg[g] / gend[g] (both 0 for an
-// empty group: the arrays are zeroed first).
+// empty group: the arrays are zeroed first).  Four positions per thread (one
+// 16-byte load; the previous position's key from the neighbouring lane).
 __global__ __launch_bounds__(kBlock) void k_group_bounds(const uint32_t* __restrict__ skey,
                                                          const uint32_t* __restrict__ spv, int64_t n, int bits,
                                                          uint32_t* __restrict__ gbeg, uint32_t* __restrict__ gend) {
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t g = gw_group(skey[p], bits);
-    if (p == 0) gbeg[g] = 0;
-    else {
-      const uint32_t h = gw_group(skey[p - 1], bits);
-      if (h != g) {
-        gend[h] = (uint32_t)p;
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t qd = (int64_t)blockIdx.x * kBlock + threadIdx.x; qd < nq; qd += (int64_t)gridDim.x * kBlock) {
+    const int64_t p0 = qd << 2;
+    uint32_t k[4];
+    if (p0 + 3 < n && ((reinterpret_cast<uintptr_t>(skey) & 15) == 0)) {
+      const uint4 v = *reinterpret_cast<const uint4*>(skey + p0);
+      k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+    } else {
+      for (int j = 0; j < 4; j++) k[j] = p0 + j < n ? skey[p0 + j] : 0u;
+    }
+    uint32_t prev = p0 > 0 ? gw_group(skey[p0 - 1], bits) : 0xFFFFFFFFu;
+    for (int j = 0; j < 4; j++) {
+      const int64_t p = p0 + j;
+      if (p >= n) break;
+      const uint32_t g = gw_group(k[j], bits);
+      if (g != prev) {
+        if (p > 0) gend[prev] = (uint32_t)p;
         gbeg[g] = (uint32_t)p;
       }
+      if (p == n - 1) gend[g] = (uint32_t)n;
+      prev = g;
     }
-    if (p == n - 1) gend[g] = (uint32_t)n;
   }
 }
 
@@ -501,30 +513,57 @@ __global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restr
   __shared__ uint32_t cnt[kLwBins];
   __shared__ uint32_t bstart[kLwBins + 1];
   __shared__ uint32_t wsum[kLwThreads / 64];
-  __shared__ uint32_t rbase;
+  __shared__ uint32_t rbase, mbase, lcnt_o, lcnt_m, over_l;
+  if (threadIdx.x == 0) {
+    lcnt_o = 0;
+    lcnt_m = 0;
+    over_l = 0;
+  }
+  __syncthreads();
+  __shared__ uint8_t lout[kLwCap];     // per position: the walk's outcome (direct mode)
+  __shared__ uint32_t lmrow[kLwCap];   // per position: the match row
+  __shared__ uint32_t lpre[kLwThreads];  // per 8-position chunk: (open | match << 16) before it
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t tbase = a.x.batch.ts[0];
   const int64_t W = a.within;
   uint64_t steps = 0, pruned = 0;
   uint32_t viol = 0, over = 0;
-  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const int64_t q0 = gbeg[g], q1 = gend[g];
-    const int len = (int)(q1 - q0);
-    if (len <= 0) continue;
-    if (len > kLwCap) {   // the host redoes this push on the full key sort
-      over += tid == 0 ? 1u : 0u;
-      continue;
+  // software pipeline over this block's groups: the next group's rows are
+  // loaded while this one is binned and walked in LDS
+  uint32_t nk[kLwPer], np[kLwPer];
+  int32_t nt[kLwPer];
+  int64_t nq0 = 0, nq1 = 0;
+  auto fetch = [&](int gg) {
+    nq0 = gbeg[gg];
+    nq1 = gend[gg];
+    const int nl = (int)(nq1 - nq0);
+    if (nl <= 0 || nl > kLwCap) return;
+#pragma unroll
+    for (int j = 0; j < kLwPer; j++) {
+      const int i = tid + j * kLwThreads;
+      const int64_t q = nq0 + (i < nl ? i : 0);
+      nk[j] = skey[q];
+      np[j] = spv[q];
+      nt[j] = sts[q];
     }
-    // ---- stage: every load issued before the first LDS store
+  };
+  if ((int)blockIdx.x < ngroups) fetch(blockIdx.x);
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int64_t q0 = nq0, q1 = nq1;
+    const int len = (int)(q1 - q0);
     uint32_t rk[kLwPer], rp[kLwPer];
     int32_t rt[kLwPer];
 #pragma unroll
     for (int j = 0; j < kLwPer; j++) {
-      const int i = tid + j * kLwThreads;
-      const int64_t q = q0 + (i < len ? i : 0);
-      rk[j] = skey[q];
-      rp[j] = spv[q];
-      rt[j] = sts[q];
+      rk[j] = nk[j];
+      rp[j] = np[j];
+      rt[j] = nt[j];
+    }
+    if (g + (int)gridDim.x < ngroups) fetch(g + gridDim.x);
+    if (len <= 0) continue;
+    if (len > kLwCap) {   // the host redoes this push on the full key sort
+      over += tid == 0 ? 1u : 0u;
+      continue;
     }
     __syncthreads();   // the previous group's readers are done
     for (int b = tid; b < kLwBins; b += kLwThreads) cnt[b] = 0;
@@ -592,17 +631,13 @@ __global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restr
       }
     }
     __syncthreads();
-    // ---- walks: each candidate over the later rows of its bin
-    for (int p0 = 0; p0 < len; p0 += kLwThreads) {   // rounds: uniform trip count (dormant row reservation)
-      const int p = p0 + tid;
-      uint8_t out = PS_NONE;
-      int i = 0;
-      uint32_t k = 0;
-      if (p < len) {
-      i = lord[p];
+    // ---- walks: each candidate over the later rows of its bin (outcomes in LDS)
+    for (int p = tid; p < len; p += kLwThreads) {
+      const int i = lord[p];
       const uint32_t pv = lpv[i];
       const uint32_t f = pv_flags(pv);
-      k = lk[i];
+      const uint32_t k = lk[i];
+      uint8_t out = PS_NONE;
       if (f & F_CAND) {
         const int pend_end = (int)bstart[lw_bin(k) + 1];
         const int64_t tsi = tbase + (int64_t)lts[i];
@@ -639,7 +674,8 @@ __global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restr
         }
         if (st == ST_MATCH) {
           out = PS_MATCH;
-          match_row[q0 + p] = mrow;
+          lmrow[p] = (uint32_t)mrow;
+          if (!a.mj) match_row[q0 + p] = mrow;
         } else if (st == ST_OPEN) {
           if (a.prune && a.t_end - tsi > W) {
             pruned++;
@@ -650,51 +686,96 @@ __global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restr
         }
       }
       if (a.lp && (f & F_NEW) && !(f & F_SKIP)) a.lp[k - a.lp_base] = a.push_idx;
-      skey[q0 + p] = k;
-      spv[q0 + p] = pv;
-      pst[q0 + p] = out;
-      }
       if (a.direct) {
-        // this round's open (carry) or dormant partials -> rows of `fresh`, in
-        // position order (per key: creation order), one reservation per round
-        const bool dm = (out & 0x7Fu) == a.direct_val;
-        const uint64_t bm = __ballot(dm);
-        if (lane == 0) wsum[w] = (uint32_t)__popcll(bm);
-        __syncthreads();
-        uint32_t pre = 0, tot = 0;
+        lout[p] = out;
+      } else {
+        skey[q0 + p] = k;
+        spv[q0 + p] = pv;
+        pst[q0 + p] = out;
+      }
+    }
+    if (a.direct) {
+      // ---- the group's matches and carried / dormant partials, in position
+      // order (per key: creation order), into this block's regions
+      __syncthreads();
+      constexpr int kPerT = kLwCap / kLwThreads;
+      const int c0 = tid * kPerT;
+      uint32_t no = 0, nm = 0;
 #pragma unroll
-        for (int kk = 0; kk < kLwThreads / 64; kk++) {
-          pre += kk < w ? wsum[kk] : 0u;
-          tot += wsum[kk];
+      for (int j = 0; j < kPerT; j++) {
+        const int p = c0 + j;
+        const uint8_t o = p < len ? lout[p] : (uint8_t)PS_NONE;
+        no += (o & 0x7Fu) == a.direct_val ? 1u : 0u;
+        nm += o == PS_MATCH ? 1u : 0u;
+      }
+      // block exclusive scan of (no, nm) packed in one word (each < 2^16)
+      const uint32_t v = no | (nm << 16);
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      uint32_t pre = inc - v, tot = 0;
+      for (int kk = 0; kk < kLwThreads / 64; kk++) {
+        pre += kk < w ? wsum[kk] : 0u;
+        tot += wsum[kk];
+      }
+      const uint32_t to = tot & 0xFFFFu, tm = tot >> 16;
+      const uint32_t base_o = lcnt_o, base_m = lcnt_m;
+      const bool fits = base_o + to <= a.region && base_m + tm <= a.region;
+      __syncthreads();   // every thread read lcnt_* / wsum
+      if (tid == 0) {
+        if (!fits) over_l = 1;
+        else {
+          lcnt_o = base_o + to;
+          lcnt_m = base_m + tm;
         }
-        if (tid == 0 && tot) rbase = atomicAdd(a.fresh_n, tot);
-        __syncthreads();
-        if (dm) {
-          const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-          const int64_t o = (int64_t)rbase + pre + (uint32_t)__popcll(bm & lt);
-          if (o < a.fresh_cap) {
-            const SpillCols& d = a.fresh;
+      }
+      if (tid < kLwThreads) lpre[tid] = pre;   // this thread's 8-position chunk: (open, match) before it
+      __syncthreads();
+      if (fits && !over_l) {
+        // strided: every thread takes few rows, so their random operand
+        // loads are in flight together (a contiguous chunk would serialise them)
+        const SpillCols& d = a.fresh;
+        for (int p = tid; p < len; p += kLwThreads) {
+          const uint8_t o = lout[p];
+          const bool isopen = (o & 0x7Fu) == a.direct_val;
+          if (o != PS_MATCH && !isopen) continue;
+          uint32_t r2 = lpre[p / kPerT];
+          for (int y = p & ~(kPerT - 1); y < p; y++) {
+            const uint8_t oy = lout[y];
+            r2 += ((oy & 0x7Fu) == a.direct_val ? 1u : 0u) | (oy == PS_MATCH ? 0x10000u : 0u);
+          }
+          if (o == PS_MATCH) {
+            const int64_t ob = (int64_t)blockIdx.x * a.region + base_m + (r2 >> 16);
+            a.mj[ob] = lmrow[p];
+            a.mi[ob] = pv_row(lpv[lord[p]]);
+          } else {
+            const int i = lord[p];
+            const int64_t ob = (int64_t)blockIdx.x * a.region + base_o + (r2 & 0xFFFFu);
             const int64_t r = (int64_t)pv_row(lpv[i]);
             const ColSet& cs = a.x.cs(r);
             const int64_t row = a.x.row(r);
             for (int c = 0; c < d.ncols; c++) {
               if (!((a.amask >> c) & 1u)) continue;
-              const Val v = col_load(cs, row, c);
+              const Val vv = col_load(cs, row, c);
               switch (d.types[c]) {
-                case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)d.col[c])[o] = (uint32_t)v.b; break;
-                case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)d.col[c])[o] = v.b; break;
-                case SHD_T_BOOL: ((uint8_t*)d.col[c])[o] = (uint8_t)v.b; break;
+                case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)d.col[c])[ob] = (uint32_t)vv.b; break;
+                case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)d.col[c])[ob] = vv.b; break;
+                case SHD_T_BOOL: ((uint8_t*)d.col[c])[ob] = (uint8_t)vv.b; break;
               }
-              d.nul[c][o] = (uint8_t)v.null;
+              d.nul[c][ob] = (uint8_t)vv.null;
             }
-            d.ts[o] = tbase + (int64_t)lts[i];
-            d.key[o] = k;
-            d.seq[o] = a.x.seq(r);
-            d.pend[o] = (uint8_t)(((out & PS_PEND) || (r < a.x.C && a.carry_pend[r])) ? 1 : 0);
-            if (d.push) d.push[o] = a.push_idx;
+            d.ts[ob] = tbase + (int64_t)lts[i];
+            d.key[ob] = lk[i];
+            d.seq[ob] = a.x.seq(r);
+            d.pend[ob] = (uint8_t)(((o & PS_PEND) || (r < a.x.C && a.carry_pend[r])) ? 1 : 0);
+            if (d.push) d.push[ob] = a.push_idx;
           }
         }
-        __syncthreads();   // wsum / rbase reused by the next round
       }
     }
   }
@@ -715,11 +796,66 @@ __global__ __launch_bounds__(kLwThreads) void k_lds_walk(const ScanArgs* __restr
       r.violation |= wpart[k].violation;
       r.hbm_walks += wpart[k].hbm_walks;
     }
+    if (over_l) r.hbm_walks += 1;   // a region overflowed: the host redoes the push
     blk[blockIdx.x] = r;
+    if (a.blk_open) {
+      a.blk_open[blockIdx.x] = lcnt_o;
+      a.blk_match[blockIdx.x] = lcnt_m;
+    }
+  }
+}
+
+// Block regions of the sorted LDS walk -> contiguous rows: block b's count_b
+// rows at [b * region, ...) move to [off_b, off_b + count_b) (one block per region).
+__global__ __launch_bounds__(kBlock) void k_region_rows(SpillCols src, SpillCols dst, uint32_t amask, int64_t region,
+                                                        const uint32_t* __restrict__ cnt,
+                                                        const uint32_t* __restrict__ off) {
+  const int b = blockIdx.x;
+  const int64_t n = cnt[b];
+  const int64_t s0 = (int64_t)b * region, d0 = off[b];
+  for (int64_t k = threadIdx.x; k < n; k += kBlock) {
+    const int64_t i = s0 + k, o = d0 + k;
+    for (int c = 0; c < src.ncols; c++) {
+      if (!((amask >> c) & 1u)) continue;
+      switch (src.types[c]) {
+        case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT:
+          ((uint32_t*)dst.col[c])[o] = ((const uint32_t*)src.col[c])[i];
+          break;
+        case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)dst.col[c])[o] = ((const uint64_t*)src.col[c])[i]; break;
+        case SHD_T_BOOL: ((uint8_t*)dst.col[c])[o] = ((const uint8_t*)src.col[c])[i]; break;
+      }
+      dst.nul[c][o] = src.nul[c][i];
+    }
+    dst.ts[o] = src.ts[i];
+    dst.key[o] = src.key[i];
+    dst.seq[o] = src.seq[i];
+    dst.pend[o] = src.pend[i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_region_pairs(const uint32_t* __restrict__ sj, const uint32_t* __restrict__ si,
+                                                         uint32_t* __restrict__ dj, uint32_t* __restrict__ di,
+                                                         int64_t region, const uint32_t* __restrict__ cnt,
+                                                         const uint32_t* __restrict__ off) {
+  const int b = blockIdx.x;
+  const int64_t n = cnt[b];
+  const int64_t s0 = (int64_t)b * region, d0 = off[b];
+  for (int64_t k = threadIdx.x; k < n; k += kBlock) {
+    dj[d0 + k] = sj[s0 + k];
+    di[d0 + k] = si[s0 + k];
   }
 }
 
 }  // namespace
+
+void launch_region_compact(const SpillCols& src, const SpillCols& dst, uint32_t amask, int64_t region, int nblk,
+                           const uint32_t* ocnt, const uint32_t* ooff, const uint32_t* sj, const uint32_t* si,
+                           uint32_t* dj, uint32_t* di, const uint32_t* mcnt, const uint32_t* moff, hipStream_t s) {
+  hipLaunchKernelGGL(k_region_rows, dim3(nblk), dim3(kBlock), 0, s, src, dst, amask, region, ocnt, ooff);
+  SHD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_region_pairs, dim3(nblk), dim3(kBlock), 0, s, sj, si, dj, di, region, mcnt, moff);
+  SHD_CHECK_LAUNCH();
+}
 
 int group_walk_blocks(int ngroups) { return ngroups < 8192 ? ngroups : 8192; }
 

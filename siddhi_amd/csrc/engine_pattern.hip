@@ -1282,6 +1282,13 @@ struct GatherArgs {
   int64_t* dseq;
   uint32_t amask;   // k_gather_list: stream-A columns to copy
   const uint32_t* obase;   // k_gather_list: first output row (device word; null: 0)
+  // k_gather_list: the partial's time from the sorted positions (32-bit
+  // offsets from tbase, or 64-bit) and the stream-A attribute that IS the
+  // partition key (from the sorted key; -1: none) -- only the other masked
+  // attributes are row gathers
+  const int32_t* sts32;
+  const int64_t* sts64;
+  int key_attr;
   uint32_t* dpush;         // dormant rows: the push index they became dormant in
   uint32_t push_idx;
   // new-list / pending-list placement of each carried partial (export_replay)
@@ -1402,27 +1409,40 @@ __global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __rest
     const int64_t o = obase + oi;
     const int64_t r = pv_row(spv[p]);
     // one uniform column table per branch (carried rows / pushed rows)
+    const uint64_t kk = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
+    const bool sts = a.sts32 || a.sts64;
     if (r < x.C) {
       for (int c = 0; c < a.ncols; c++) {
         if (!((a.amask >> c) & 1u)) continue;
+        if (c == a.key_attr) {
+          store_col(a.dcol[c], a.types[c], o, kk);
+          a.dnul[c][o] = 0;
+          continue;
+        }
         const Val v = col_load(x.carry, r, c);
         store_col(a.dcol[c], a.types[c], o, v.b);
         a.dnul[c][o] = (uint8_t)v.null;
       }
-      a.dts[o] = gld(x.carry.ts, r);
+      if (!sts) a.dts[o] = gld(x.carry.ts, r);
       a.dseq[o] = x.carry_seq[r];
     } else {
       const int64_t br = r - x.C;
       for (int c = 0; c < a.ncols; c++) {
         if (!((a.amask >> c) & 1u)) continue;
+        if (c == a.key_attr) {
+          store_col(a.dcol[c], a.types[c], o, kk);
+          a.dnul[c][o] = 0;
+          continue;
+        }
         const Val v = col_load(x.batch, br, c);
         store_col(a.dcol[c], a.types[c], o, v.b);
         a.dnul[c][o] = (uint8_t)v.null;
       }
-      a.dts[o] = gld(x.batch.ts, br);
+      if (!sts) a.dts[o] = gld(x.batch.ts, br);
       a.dseq[o] = x.seq0 + br;
     }
-    a.dkey[o] = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
+    if (sts) a.dts[o] = a.sts64 ? a.sts64[p] : gld(x.batch.ts, 0) + (int64_t)a.sts32[p];
+    a.dkey[o] = kk;
     a.dpend[o] = (uint8_t)(((pst[p] & PS_PEND) || (r < x.C && a.pend_old[r])) ? 1 : 0);
     if (a.dpush) a.dpush[o] = a.push_idx;
   }
@@ -1704,18 +1724,27 @@ struct PatternEngine : Engine {
   uint32_t push_idx = 0;      // pushes that updated lp
   static constexpr uint64_t kLpMax = 1ull << 27;
   DevBuf d_scnt, d_soff, d_dlist;
-  CarryTable fresh;            // sorted LDS walk: this push's dormant partials, written by the walk
+  CarryTable fresh;            // sorted LDS walk: the open partials, per block region
+  DevBuf d_mjs, d_mis, d_bo, d_bm, d_boo, d_bmo;   // its match pairs per region, region counts / offsets
+  int64_t region = 0;
   bool dorm_direct = false;    // this push: fresh holds them (finish copies instead of gathering)
   bool open_direct = false;    // this push: the walk wrote the next carry table (finish skips the gather)
+  bool match_direct = false;   // this push: the walk wrote the (e2 row, e1 row) pairs (finish skips k_emit_pairs)
+  // sorted times of this push's positions (finish: carried partials' times)
+  const int32_t* fin_sts32 = nullptr;
+  const int64_t* fin_sts64 = nullptr;
   // this push (sort_push -> finish)
   bool spill_now = false;
   uint32_t n_dorm = 0, n_surv = 0;
   int64_t stile = 0;
   int nst = 0;
 
+  // opt-in (SHD_SPILL=1): on P3 the dormant table's gather + compaction
+  // (1.08 ms / step) cost more than sorting the carried rows (r03k: 15.6 vs
+  // 17.2 G events/s), so by default every open partial is carried
   bool spill_plan() const {
     return partitioned && logical != 2 && W != INT64_MAX && !type_key64(key_type[0]) && !type_key64(key_type[1]) &&
-           !getenv("SHD_NO_SPILL");
+           getenv("SHD_SPILL") && !getenv("SHD_NO_SPILL");
   }
   SpillCols spill_cols(CarryTable& t) const {
     SpillCols c{};
@@ -2023,8 +2052,11 @@ struct PatternEngine : Engine {
   void push(const Staged& b) override {
     if (b.n <= 0) return;
     spill_now = false;
+    fin_sts32 = nullptr;
+    fin_sts64 = nullptr;
     dorm_direct = false;
     open_direct = false;
+    match_direct = false;
     int la = 0;
     int64_t t_last_probe = 0;
     if (bucket_candidate(b, la, t_last_probe) && bucket_push(b, la, t_last_probe)) return;
@@ -2476,8 +2508,11 @@ struct PatternEngine : Engine {
   static constexpr int kLdsBits = 16;
   bool lds_skip = false;
   bool lds_candidate(const PrepAgg& pg, int64_t n_ext, bool key64) const {
-    if (lds_skip || !partitioned || logical != 0 || key64 || pg.ovf || pg.kmin > pg.kmax || getenv("SHD_NO_LDSWALK") ||
-        getenv("SHD_GROUP"))
+    // opt-in (SHD_LDSWALK=1): measured slower than the full key sort + forward
+    // scan on P3 (r03k: the walk is latency-bound at 1.6 ms per 50M-row push
+    // against 0.4 ms for the third sort pass + scan it replaces)
+    if (lds_skip || !partitioned || logical != 0 || key64 || pg.ovf || pg.kmin > pg.kmax || !getenv("SHD_LDSWALK") ||
+        getenv("SHD_NO_LDSWALK") || getenv("SHD_GROUP"))
       return false;
     const double nk = std::min<double>((double)(1 << kLdsBits), (double)(pg.kmax - pg.kmin) + 1.0);
     return (double)n_ext / nk <= 0.75 * lds_walk_cap();
@@ -2505,29 +2540,37 @@ struct PatternEngine : Engine {
     sa.within = W;
     sa.partitioned = 1;
     sa.prune = 0;   // partitioned: every open partial is carried (per-key expiry)
+    const int nwalk = std::min(1 << kLdsBits, 8192);
     if (!getenv("SHD_CARRY_GATHER")) {
-      // the walk writes the open partials straight into the next carry table
-      // (every candidate, carried or opened by this push, may stay open)
-      const int64_t cap = C + (int64_t)pg.n_cand;
-      CarryTable& nt = carry[cur ^ 1];
-      nt.reserve(cap, typesA);
+      // the walk writes the open partials (carry rows) and the matches
+      // straight out, each block into its own region, compacted below
+      const int64_t cands = C + (int64_t)pg.n_cand;
+      region = ceil_div(cands, nwalk) * 5 / 4 + 1024;
+      fresh.reserve(region * nwalk, typesA);
       carry[cur].pend.reserve(std::max<int64_t>(C, 1));
+      d_mjs.reserve((size_t)region * nwalk * 4);
+      d_mis.reserve((size_t)region * nwalk * 4);
+      d_bo.reserve((size_t)nwalk * 4);
+      d_bm.reserve((size_t)nwalk * 4);
+      d_boo.reserve((size_t)nwalk * 4);
+      d_bmo.reserve((size_t)nwalk * 4);
       sa.direct = 1;
       sa.direct_val = PS_OPEN;
-      sa.fresh = spill_cols(nt);
+      sa.fresh = spill_cols(fresh);
       sa.fresh.push = nullptr;
       sa.amask = carry_mask;
-      sa.fresh_n = reinterpret_cast<unsigned int*>(d_agg.as<char>() + 144);
-      sa.fresh_cap = cap;
       sa.carry_pend = carry[cur].pend.as<uint8_t>();
-      SHD_HIP(hipMemsetAsync(d_agg.as<char>() + 144, 0, 4, s));
+      sa.mj = d_mjs.as<uint32_t>();
+      sa.mi = d_mis.as<uint32_t>();
+      sa.region = region;
+      sa.blk_open = d_bo.as<uint32_t>();
+      sa.blk_match = d_bm.as<uint32_t>();
     }
     const int64_t t_end = (int64_t)pg.ts_max;
     sa.t_end = t_end;
     const int ngroups = 1 << kLdsBits;
     d_gbeg.reserve((size_t)ngroups * 4);
     d_gend.reserve((size_t)ngroups * 4);
-    const int nwalk = std::min(ngroups, 8192);
     const int nblk = grid_for(n_ext, 1, 4096);
     const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
     const int ntile = (int)ceil_div(n_ext, tile);
@@ -2536,26 +2579,46 @@ struct PatternEngine : Engine {
     d_boff.reserve((size_t)3 * ntile * 4);
     launch_lds_walk(dev_args(sa), sa.f2.fp.ok != 0, n_ext, kLdsBits, skey32, spv, sts32, d_gbeg.as<uint32_t>(),
                     d_gend.as<uint32_t>(), d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), nwalk, s);
-    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
-                       d_bcnt.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
+    if (!sa.direct) {
+      hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
+                         d_bcnt.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+    }
     ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
     hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
     uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    if (!sa.direct) {
+      scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
+      scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
+    } else {   // region counts -> offsets (totals: matches, open partials)
+      scan_exclusive_u32(d_bm.as<uint32_t>(), d_bmo.as<uint32_t>(), nwalk, d_mo, d_scan, s);
+      scan_exclusive_u32(d_bo.as<uint32_t>(), d_boo.as<uint32_t>(), nwalk, d_mo + 1, d_scan, s);
+    }
     mark("compact");
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 84, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 88, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     ScanOut so;
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];
     const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    open_direct = sa.direct && h_agg.as<uint32_t>()[36] == n_open;
-    if (so.hbm_walks) return false;   // a group beyond the LDS capacity
+    if (so.hbm_walks) return false;   // a group beyond the LDS capacity / a full region
+    if (sa.direct) {
+      carry[cur ^ 1].reserve(n_open, typesA);
+      d_pj.reserve((size_t)std::max<uint32_t>(m, 1) * 4);
+      d_pi.reserve((size_t)std::max<uint32_t>(m, 1) * 4);
+      SpillCols dst = spill_cols(carry[cur ^ 1]);
+      dst.push = nullptr;
+      launch_region_compact(sa.fresh, dst, carry_mask, region, nwalk, (const uint32_t*)d_bo.as<uint32_t>(),
+                            (const uint32_t*)d_boo.as<uint32_t>(), (const uint32_t*)d_mjs.as<uint32_t>(),
+                            (const uint32_t*)d_mis.as<uint32_t>(), d_pj.as<uint32_t>(), d_pi.as<uint32_t>(),
+                            (const uint32_t*)d_bm.as<uint32_t>(), (const uint32_t*)d_bmo.as<uint32_t>(), s);
+      mark("carry");
+    }
+    open_direct = sa.direct != 0;
+    match_direct = sa.direct != 0;
     if (so.violation) throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
     if (so.pruned) {
       have_horizon = true;
@@ -2980,6 +3043,8 @@ struct PatternEngine : Engine {
       have_horizon = true;
       horizon = std::max(horizon, t_end);
     }
+    fin_sts32 = sts32;
+    fin_sts64 = sts64;
     finish(b, x, n_ext, tile, ntile, spv, skey32, skey64, sorted64, keyed, grouped, key64, m, n_open, so, t_end,
            pg.n_cand);
   }
@@ -3001,11 +3066,13 @@ struct PatternEngine : Engine {
         d_se1.reserve((int64_t)m * 4);
         d_sot.reserve((int64_t)m * 4);
       }
-      hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
-                         (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
-                         tile, logical, (const int32_t*)d_mother.as<int32_t>(), d_pj.as<uint32_t>(),
-                         d_pi.as<uint32_t>(), d_se1.as<uint32_t>(), d_sot.as<int32_t>());
-      SHD_CHECK_LAUNCH();
+      if (!match_direct) {
+        hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                           (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
+                           tile, logical, (const int32_t*)d_mother.as<int32_t>(), d_pj.as<uint32_t>(),
+                           d_pi.as<uint32_t>(), d_se1.as<uint32_t>(), d_sot.as<int32_t>());
+        SHD_CHECK_LAUNCH();
+      }
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
       if (logical) bits++;   // + processor order
@@ -3080,6 +3147,15 @@ struct PatternEngine : Engine {
       }
       if (logical != 2 && !getenv("SHD_CARRY_SERIAL")) {
         ga.amask = carry_mask;
+        if (grouped && !getenv("SHD_GATHER_ROWS")) {
+          ga.sts32 = fin_sts32;
+          ga.sts64 = fin_sts64;
+          // the partition key attribute of stream A, a 32-bit plain column (sorted key == its value)
+          ga.key_attr = (partitioned && !sorted64 && key_col[0] >= 0 &&
+                         (key_type[0] == SHD_T_STRING || key_type[0] == SHD_T_INT)) ? key_col[0] : -1;
+        } else {
+          ga.key_attr = -1;
+        }
         d_olist.reserve((size_t)n_open * 4);
         hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
                            (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_olist.as<uint32_t>(),
@@ -3143,6 +3219,7 @@ struct PatternEngine : Engine {
         gd.dpend = dst.pend.as<uint8_t>();
         gd.pend_old = carry[cur].pend.as<uint8_t>();
         gd.amask = carry_mask;
+        gd.key_attr = -1;
         gd.obase = reinterpret_cast<const uint32_t*>(d_agg.as<char>() + 140);   // survivors come first
         gd.dpush = dst.push.as<uint32_t>();
         gd.push_idx = push_idx + 1;

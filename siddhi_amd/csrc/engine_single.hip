@@ -1609,6 +1609,411 @@ __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- chunked window walk
+// Window aggregates without a global group sort (dense group ids, at most
+// kWcMaxG groups).  The op stream of the push (item x added at position x;
+// item i expired at position e[i], before that position's add -- the
+// reference's LengthWindowProcessor / TimeWindowProcessor order) is cut into
+// chunks of whole InputHandler calls (<= kWcItems adds; the carried items
+// [0, C) form their own add-only chunks).  A chunk's ops are two contiguous
+// item ranges: its adds and the items expiring at its positions (e is
+// non-decreasing).
+//   k_wc_delta: per chunk, the ops sorted by group in LDS (counting sort,
+//     arrival order restored inside a group), folded per group -> the
+//     chunk's change of every group's window state (sum per channel in
+//     double-double, non-null count, item count);
+//   k_wc_scan1..3: prefix over the chunks -> every group's state at the
+//     start of every chunk (and after the push: the group tables);
+//   k_wc_emit: per chunk again, each group folded from its start state; at
+//     the last add of every (call, group) run the run record k_emit reads
+//     (the same record k_seg_emit writes), written at the run's first item.
+// A group's window state is a running sum of the items inside the window
+// (the reference's `sum += v; sum -= v`, SumAttributeAggregatorExecutor.java
+// :184-198) kept in double-double: within 1e-9 relative of the reference,
+// like the segmented scans.
+constexpr int kWcItems = 4096;          // adds per chunk (whole calls)
+constexpr int kWcOps = 8192;            // adds + expires per chunk
+constexpr int kWcMaxG = 2048;           // dense group ids [0, kWcMaxG)
+constexpr int kWcThreads = 512;
+constexpr int kWcSeg = 64;              // chunks per scan segment
+
+template <int NC>
+struct WcAcc {
+  double s[NC];     // window sum per channel (double-double hi only in the table)
+  int32_t nn[NC];   // non-null operands in the window
+  int32_t cnt;      // items in the window
+};
+
+struct WcArgs {
+  int64_t C, total;
+  int G;
+  int nagg;
+  int kind[kMaxAggs];
+  int type[kMaxAggs];
+  int chan[kMaxAggs];
+  const uint64_t* ikey;      // group id per item (dense)
+  const uint32_t* e;         // expiry position per item (kInf: none)
+  const int64_t* cp;         // chunk k: positions [cp[k], cp[k+1])
+  const int64_t* ce;         // chunk k: expiring items [ce[k], ce[k+1])
+  uint64_t* rec;             // run records (k_emit<true>)
+  uint8_t* first;
+  double* dsum;              // group tables [nagg][nkeys]: the window state after the push
+  int64_t* gcnt;
+  int64_t nkeys;
+  unsigned int* flag;        // a chunk with more than kWcOps ops
+};
+
+// chunk item ranges: K_c carried chunks of kWcItems items, then one chunk per
+// F calls (first item of a call: lower bound of its index in icall[C, total))
+__global__ void k_wc_bounds(const WcArgs* __restrict__ ap, int kc, int K, int F, int ncalls, const int32_t* icall,
+                            int64_t* cp, int64_t* ce) {
+  const WcArgs& a = *ap;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= K; k += gridDim.x * blockDim.x) {
+    int64_t p;
+    if (k < kc) p = (int64_t)k * kWcItems;
+    else if (k == K) p = a.total;
+    else {
+      const int c = (k - kc) * F;
+      if (c >= ncalls) p = a.total;
+      else {
+        int64_t lo = a.C, hi = a.total;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (icall[mid] >= c) hi = mid;
+          else lo = mid + 1;
+        }
+        p = lo;
+      }
+    }
+    if (k < kc && p > a.C) p = a.C;
+    cp[k] = p;
+    // first item expiring at or after position p
+    int64_t lo = 0, hi = a.total;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)a.e[mid] >= p) hi = mid;
+      else lo = mid + 1;
+    }
+    ce[k] = lo;
+  }
+}
+
+// a chunk with more ops than fit in LDS -> flag (the host keeps the segmented scans)
+__global__ void k_wc_check(const int64_t* cp, const int64_t* ce, int K, unsigned int* flag) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x)
+    if ((cp[k + 1] - cp[k]) + (ce[k + 1] - ce[k]) > kWcOps || cp[k + 1] < cp[k]) atomicOr(flag, 1u);
+}
+
+// Load chunk k's ops into LDS sorted by group (arrival order inside a group:
+// position, expire before add, then item).  Returns the op count (0 and the
+// flag set when it exceeds kWcOps).  sop: op codes (item | add << 31) in
+// group order; gs: group starts [G + 1].
+template <int NC>
+__device__ int wc_load_sorted(const WcArgs& a, int k, uint32_t* op, uint32_t* ordk, uint16_t* grp, uint32_t* cnt,
+                              uint32_t* gs, uint16_t* tmp, uint32_t* sop, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t P0 = a.cp[k], P1 = a.cp[k + 1], E0 = a.ce[k], E1 = a.ce[k + 1];
+  const int na = (int)(P1 - P0), nx = (int)(E1 - E0);
+  const int nops = na + nx;
+  if (nops > kWcOps) {
+    if (tid == 0) atomicOr(a.flag, 1u);
+    return 0;
+  }
+  for (int g = tid; g < a.G; g += kWcThreads) cnt[g] = 0;
+  __syncthreads();
+  for (int i = tid; i < nops; i += kWcThreads) {
+    uint32_t item, code, ord;
+    if (i < nx) {   // expire of item E0 + i at position e[...]
+      item = (uint32_t)(E0 + i);
+      const int64_t pos = (int64_t)a.e[item];
+      code = item;
+      ord = ((uint32_t)(2 * (pos - P0)) << 14) | (uint32_t)i;
+    } else {
+      item = (uint32_t)(P0 + (i - nx));
+      code = item | 0x80000000u;
+      ord = ((uint32_t)(2 * (item - P0) + 1) << 14) | (uint32_t)(i - nx);
+    }
+    const uint32_t g = (uint32_t)a.ikey[item];
+    op[i] = code;
+    ordk[i] = ord;
+    grp[i] = (uint16_t)g;
+    tmp[i] = (uint16_t)atomicAdd(&cnt[g], 1u);
+  }
+  __syncthreads();
+  // group starts: exclusive scan of cnt[0, G)
+  {
+    constexpr int kPer = kWcMaxG / kWcThreads;
+    uint32_t c[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      const int g = tid * kPer + j;
+      c[j] = g < a.G ? cnt[g] : 0u;
+      sum += c[j];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = inc - sum;
+    for (int kk = 0; kk < w; kk++) pre += wsum[kk];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      const int g = tid * kPer + j;
+      if (g < a.G) gs[g] = pre;
+      pre += c[j];
+    }
+    if (tid == kWcThreads - 1) gs[a.G] = pre;
+  }
+  __syncthreads();
+  // unordered placement, then the arrival rank inside the group
+  for (int i = tid; i < nops; i += kWcThreads) sop[gs[grp[i]] + tmp[i]] = (uint32_t)i;
+  __syncthreads();
+  for (int i = tid; i < nops; i += kWcThreads) {
+    const uint32_t g = grp[i];
+    const int b0 = (int)gs[g], b1 = (int)gs[g + 1];
+    const uint32_t my = ordk[i];
+    int rank = 0;
+    for (int y = b0; y < b1; y++) rank += ordk[sop[y]] < my ? 1 : 0;
+    tmp[b0 + rank] = (uint16_t)i;   // tmp is free again: the group-ordered op indices
+  }
+  __syncthreads();
+  return nops;
+}
+
+template <int NC>
+__device__ __forceinline__ void wc_apply(const SegItem<NC>& it, bool add, DD (&s)[NC], int32_t (&nn)[NC], int32_t& cnt) {
+  const uint32_t m = it.w >> 30;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!((m >> c) & 1u)) continue;
+    s[c] = dd_add(s[c], DD{add ? it.v[c] : -it.v[c], 0.0});
+    nn[c] += add ? 1 : -1;
+  }
+  cnt += add ? 1 : -1;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kWcThreads) void k_wc_delta(const WcArgs* __restrict__ ap, const SegItem<NC>* items,
+                                                        WcAcc<NC>* table) {
+  const WcArgs& a = *ap;
+  __shared__ uint32_t op[kWcOps], ordk[kWcOps], sop[kWcOps];
+  __shared__ uint16_t grp[kWcOps], tmp[kWcOps];
+  __shared__ uint32_t cnt[kWcMaxG], gs[kWcMaxG + 1];
+  __shared__ uint32_t wsum[kWcThreads / 64];
+  const int k = blockIdx.x;
+  const int nops = wc_load_sorted<NC>(a, k, op, ordk, grp, cnt, gs, tmp, sop, wsum);
+  for (int g = threadIdx.x; g < a.G; g += kWcThreads) {
+    DD s[NC];
+    int32_t nn[NC];
+    int32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      s[j] = DD{0.0, 0.0};
+      nn[j] = 0;
+    }
+    if (nops) {
+      for (int y = (int)gs[g]; y < (int)gs[g + 1]; y++) {
+        const uint32_t code = op[tmp[y]];
+        wc_apply<NC>(items[code & 0x7FFFFFFFu], (code >> 31) != 0, s, nn, c);
+      }
+    }
+    WcAcc<NC> r;
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      r.s[j] = s[j].hi;
+      r.nn[j] = nn[j];
+    }
+    r.cnt = c;
+    table[(int64_t)k * a.G + g] = r;
+  }
+}
+
+// prefix over the chunks: per (segment of kWcSeg chunks, group) totals; per
+// group the segments' exclusive prefix (+ the state after the push -> the
+// group tables); per (segment, group) the chunk-start states in place
+template <int NC>
+__global__ void k_wc_scan1(const WcArgs* __restrict__ ap, int K, const WcAcc<NC>* table, WcAcc<NC>* seg) {
+  const WcArgs& a = *ap;
+  const int nseg = (K + kWcSeg - 1) / kWcSeg;
+  const int64_t nt = (int64_t)nseg * a.G;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += (int64_t)gridDim.x * blockDim.x) {
+    const int sg = (int)(t / a.G), g = (int)(t % a.G);
+    DD s[NC];
+    WcAcc<NC> r{};
+#pragma unroll
+    for (int j = 0; j < NC; j++) s[j] = DD{0.0, 0.0};
+    const int k1 = min(K, (sg + 1) * kWcSeg);
+    for (int k = sg * kWcSeg; k < k1; k++) {
+      const WcAcc<NC> d = table[(int64_t)k * a.G + g];
+#pragma unroll
+      for (int j = 0; j < NC; j++) {
+        s[j] = dd_add(s[j], DD{d.s[j], 0.0});
+        r.nn[j] += d.nn[j];
+      }
+      r.cnt += d.cnt;
+    }
+#pragma unroll
+    for (int j = 0; j < NC; j++) r.s[j] = s[j].hi;
+    seg[t] = r;
+  }
+}
+
+template <int NC>
+__global__ void k_wc_scan2(const WcArgs* __restrict__ ap, int K, WcAcc<NC>* seg) {
+  const WcArgs& a = *ap;
+  const int nseg = (K + kWcSeg - 1) / kWcSeg;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < a.G; g += gridDim.x * blockDim.x) {
+    DD s[NC];
+    int32_t nn[NC];
+    int32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      s[j] = DD{0.0, 0.0};
+      nn[j] = 0;
+    }
+    for (int sg = 0; sg < nseg; sg++) {
+      WcAcc<NC>& x = seg[(int64_t)sg * a.G + g];
+      const WcAcc<NC> d = x;
+#pragma unroll
+      for (int j = 0; j < NC; j++) {
+        x.s[j] = s[j].hi;
+        x.nn[j] = nn[j];
+        s[j] = dd_add(s[j], DD{d.s[j], 0.0});
+        nn[j] += d.nn[j];
+      }
+      x.cnt = c;
+      c += d.cnt;
+    }
+    // the window state after the push -> group tables (as k_seg_emit's seg_end)
+    for (int j = 0; j < a.nagg; j++) {
+      const int ch = a.chan[j];
+      const int32_t nnw = ch >= 0 ? nn[ch] : 0;
+      a.dsum[j * a.nkeys + g] = (ch >= 0 && nnw) ? s[ch].hi : 0.0;
+      a.gcnt[j * a.nkeys + g] = ch >= 0 ? (int64_t)nnw : (int64_t)c;
+    }
+  }
+}
+
+template <int NC>
+__global__ void k_wc_scan3(const WcArgs* __restrict__ ap, int K, WcAcc<NC>* table, const WcAcc<NC>* seg) {
+  const WcArgs& a = *ap;
+  const int nseg = (K + kWcSeg - 1) / kWcSeg;
+  const int64_t nt = (int64_t)nseg * a.G;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += (int64_t)gridDim.x * blockDim.x) {
+    const int sg = (int)(t / a.G), g = (int)(t % a.G);
+    const WcAcc<NC> b = seg[t];
+    DD s[NC];
+    int32_t nn[NC];
+    int32_t c = b.cnt;
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      s[j] = DD{b.s[j], 0.0};
+      nn[j] = b.nn[j];
+    }
+    const int k1 = min(K, (sg + 1) * kWcSeg);
+    for (int k = sg * kWcSeg; k < k1; k++) {
+      WcAcc<NC>& x = table[(int64_t)k * a.G + g];
+      const WcAcc<NC> d = x;
+#pragma unroll
+      for (int j = 0; j < NC; j++) {
+        x.s[j] = s[j].hi;
+        x.nn[j] = nn[j];
+        s[j] = dd_add(s[j], DD{d.s[j], 0.0});
+        nn[j] += d.nn[j];
+      }
+      x.cnt = c;
+      c += d.cnt;
+    }
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(kWcThreads) void k_wc_emit(const WcArgs* __restrict__ ap, const SegItem<NC>* items,
+                                                       const WcAcc<NC>* table) {
+  const WcArgs& a = *ap;
+  __shared__ uint32_t op[kWcOps], ordk[kWcOps], sop[kWcOps];
+  __shared__ uint16_t grp[kWcOps], tmp[kWcOps];
+  __shared__ uint32_t cnt[kWcMaxG], gs[kWcMaxG + 1];
+  __shared__ uint32_t wsum[kWcThreads / 64];
+  const int k = blockIdx.x;
+  const int nops = wc_load_sorted<NC>(a, k, op, ordk, grp, cnt, gs, tmp, sop, wsum);
+  if (!nops) return;
+  for (int g = threadIdx.x; g < a.G; g += kWcThreads) {
+    const int y0 = (int)gs[g], y1 = (int)gs[g + 1];
+    if (y0 == y1) continue;
+    const WcAcc<NC> st = table[(int64_t)k * a.G + g];
+    DD s[NC];
+    int32_t nn[NC];
+    int32_t c = st.cnt;
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      s[j] = DD{st.s[j], 0.0};
+      nn[j] = st.nn[j];
+    }
+    // run ends, backwards: an add ends its (call, group) run unless the
+    // group's next add has the same call (ordk: free after the sort)
+    {
+      uint32_t next_call = 0xFFFFFFFFu;
+      for (int y = y1 - 1; y >= y0; y--) {
+        const uint32_t i = tmp[y];
+        const uint32_t code = op[i];
+        if (!(code >> 31)) continue;
+        const uint32_t call = items[code & 0x7FFFFFFFu].w & 0x3FFFFFFFu;
+        ordk[i] = call != next_call ? 1u : 0u;
+        next_call = call;
+      }
+    }
+    int64_t xf = -1;      // first item of the current (call, group) run
+    uint32_t rcall = 0;   // its call (+1)
+    for (int y = y0; y < y1; y++) {
+      const uint32_t code = op[tmp[y]];
+      const uint32_t x = code & 0x7FFFFFFFu;
+      const bool add = (code >> 31) != 0;
+      const SegItem<NC> it = items[x];
+      wc_apply<NC>(it, add, s, nn, c);
+      if (!add || (int64_t)x < a.C) continue;
+      const uint32_t call = it.w & 0x3FFFFFFFu;
+      if (xf < 0 || call != rcall) {
+        xf = x;
+        rcall = call;
+      }
+      if (!ordk[tmp[y]]) continue;   // not the run's last add
+      uint64_t vals[kMaxAggs];
+      uint32_t nul = 0;
+      for (int j = 0; j < a.nagg; j++) {
+        const int ch = a.chan[j];
+        uint64_t ob = 0;
+        bool on = false;
+        if (a.kind[j] == SHD_AGG_COUNT) {
+          ob = (uint64_t)c;
+        } else {
+          const int32_t nnw = nn[ch];
+          const double v = s[ch].hi;
+          if (a.kind[j] == SHD_AGG_SUM) {
+            const bool xn = (((it.w >> 30) >> ch) & 1u) == 0;
+            on = xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0);
+            ob = on ? 0ull : p_f64(v);
+          } else {
+            on = nnw == 0;
+            ob = on ? 0ull : p_f64(__ddiv_rn(v, (double)nnw));
+          }
+        }
+        vals[j] = ob;
+        nul |= on ? 1u << j : 0u;
+      }
+      uint64_t* r = a.rec + xf * run_rec_words(a.nagg);
+      r[0] = (uint64_t)x | ((uint64_t)nul << 32);
+      for (int j = 0; j < a.nagg; j++) r[1 + j] = vals[j];
+      a.first[xf] = 1;
+      xf = -1;
+    }
+  }
+}
+
 __global__ void k_first_counts(const uint8_t* first, int64_t C, int64_t total, uint32_t* cnt) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total - C; t += (int64_t)gridDim.x * blockDim.x)
     cnt[t] = first[C + t] ? 1u : 0u;
@@ -2263,6 +2668,102 @@ struct SingleEngine : Engine {
     mark("seg_window");
   }
 
+  // Chunked window walk (k_wc_*): dense group ids in [64, kWcMaxG], at most
+  // two aggregated expressions, calls of at most kWcItems events.  false:
+  // not this push's path (nothing written yet): the segmented scans run.
+  DevBuf wc_cp, wc_ce, wc_table, wc_seg;
+  template <int NC>
+  bool wc_kernels(int64_t total, int G, int64_t cap, int64_t ncalls, int F, int kc, int K) {
+    hipStream_t s = stream;
+    SegArgs sa{};
+    sa.nch = NC;
+    for (int c = 0; c < NC; c++) {
+      sa.ch_agg[c] = nch ? ch_agg[c] : 0;
+      sa.ch_type[c] = nch ? ch_type[c] : SHD_T_DOUBLE;
+    }
+    sa.nagg = nagg;
+    sa.cap = cap;
+    sa.C = C;
+    sa.total = total;
+    WcArgs wa{};
+    wa.C = C;
+    wa.total = total;
+    wa.G = G;
+    wa.nagg = nagg;
+    for (int g = 0; g < nagg; g++) {
+      wa.kind[g] = plan.aggs[g].kind;
+      wa.type[g] = plan.aggs[g].type;
+      wa.chan[g] = chan_of[g];
+    }
+    wc_cp.reserve((size_t)(K + 1) * 8);
+    wc_ce.reserve((size_t)(K + 1) * 8);
+    wa.ikey = ikey[cur].as<uint64_t>();
+    wa.e = e_exp.as<uint32_t>();
+    wa.cp = wc_cp.as<int64_t>();
+    wa.ce = wc_ce.as<int64_t>();
+    rec.reserve((size_t)cap * run_rec_words(nagg) * 8);
+    wa.rec = rec.as<uint64_t>();
+    wa.first = first.as<uint8_t>();
+    wa.dsum = g_dsum.as<double>();
+    wa.gcnt = g_cnt.as<int64_t>();
+    wa.nkeys = g_nkeys;
+    unsigned int* d_flag = (unsigned int*)(d_tot.as<uint64_t>() + 7);
+    SHD_HIP(hipMemsetAsync(d_flag, 0, 4, s));
+    wa.flag = d_flag;
+    const WcArgs* d_wa = dev_args(wa);
+    hipLaunchKernelGGL(k_wc_bounds, dim3(grid_for(K + 1)), dim3(kBlock), 0, s, d_wa, kc, K, F, (int)ncalls,
+                       (const int32_t*)icall.as<int32_t>(), wc_cp.as<int64_t>(), wc_ce.as<int64_t>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_wc_check, dim3(grid_for(K)), dim3(kBlock), 0, s, (const int64_t*)wc_cp.as<int64_t>(),
+                       (const int64_t*)wc_ce.as<int64_t>(), K, d_flag);
+    SHD_CHECK_LAUNCH();
+    SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 7, d_flag, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    if (h_tot.as<uint32_t>()[14]) return false;   // a chunk beyond the LDS capacity
+    seg_items.reserve((size_t)total * sizeof(SegItem<NC>));
+    hipLaunchKernelGGL(k_seg_pack<NC>, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(sa),
+                       (const uint64_t*)iargv[cur].as<uint64_t>(), (const uint8_t*)iargn[cur].as<uint8_t>(),
+                       (const uint32_t*)e_exp.as<uint32_t>(), (const int32_t*)icall.as<int32_t>(),
+                       (SegItem<NC>*)seg_items.as<char>());
+    SHD_CHECK_LAUNCH();
+    const SegItem<NC>* items = (const SegItem<NC>*)seg_items.as<char>();
+    wc_table.reserve((size_t)K * G * sizeof(WcAcc<NC>));
+    const int nseg = (K + kWcSeg - 1) / kWcSeg;
+    wc_seg.reserve((size_t)nseg * G * sizeof(WcAcc<NC>));
+    WcAcc<NC>* table = (WcAcc<NC>*)wc_table.as<char>();
+    WcAcc<NC>* seg = (WcAcc<NC>*)wc_seg.as<char>();
+    hipLaunchKernelGGL(k_wc_delta<NC>, dim3(K), dim3(kWcThreads), 0, s, d_wa, items, table);
+    SHD_CHECK_LAUNCH();
+    mark("wc_delta");
+    const int64_t nt = (int64_t)nseg * G;
+    hipLaunchKernelGGL(k_wc_scan1<NC>, dim3(grid_for(nt)), dim3(kBlock), 0, s, d_wa, K, (const WcAcc<NC>*)table, seg);
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_wc_scan2<NC>, dim3(grid_for(G)), dim3(kBlock), 0, s, d_wa, K, seg);
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_wc_scan3<NC>, dim3(grid_for(nt)), dim3(kBlock), 0, s, d_wa, K, table, (const WcAcc<NC>*)seg);
+    SHD_CHECK_LAUNCH();
+    mark("wc_scan");
+    hipLaunchKernelGGL(k_wc_emit<NC>, dim3(K), dim3(kWcThreads), 0, s, d_wa, items, (const WcAcc<NC>*)table);
+    SHD_CHECK_LAUNCH();
+    mark("wc_emit");
+    return true;
+  }
+
+  bool agg_chunked(int64_t total, uint64_t kmax, int64_t cap, int64_t ncalls) {
+    if (getenv("SHD_NO_WCHUNK") || !gdense || (wkind != SHD_W_LENGTH && wkind != SHD_W_TIME) || nch > 2 ||
+        kmax + 1 > (uint64_t)kWcMaxG || kmax + 1 < 64 || total >= (int64_t)INT32_MAX)
+      return false;
+    int64_t maxcall = 0;
+    for (size_t c = 0; c + 1 < h_offs.size(); c++) maxcall = std::max<int64_t>(maxcall, h_offs[c + 1] - h_offs[c]);
+    if (maxcall <= 0 || maxcall > kWcItems || ncalls <= 0) return false;
+    const int F = (int)std::max<int64_t>(1, kWcItems / maxcall);
+    const int kc = (int)ceil_div(C, kWcItems);
+    const int K = kc + (int)ceil_div(ncalls, F);
+    const int G = (int)kmax + 1;
+    ensure_groups(G);
+    return nch <= 1 ? wc_kernels<1>(total, G, cap, ncalls, F, kc, K) : wc_kernels<2>(total, G, cap, ncalls, F, kc, K);
+  }
+
   void agg_segscan(int64_t total, uint64_t kmax, int64_t cap) {
     hipStream_t s = stream;
     okey32.reserve(total * 4);
@@ -2454,7 +2955,7 @@ struct SingleEngine : Engine {
     first.reserve(cap);
     if (total > 0) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
     if (seg_mode && total > 0) {
-      agg_segscan(total, kmax, cap);
+      if (!agg_chunked(total, kmax, cap, ncalls)) agg_segscan(total, kmax, cap);
     } else if (nops > 0) {
       okey.reserve(nops * 8);
       oref.reserve(nops * 4);

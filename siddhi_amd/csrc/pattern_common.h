@@ -145,16 +145,26 @@ struct ScanArgs {
   uint32_t* lp;
   uint64_t lp_base;
   uint32_t push_idx;
-  // sorted LDS walk: dormant partials written straight into `fresh` (rows
-  // reserved per round with one atomic on fresh_n; beyond fresh_cap: not
-  // written, the host gathers them instead)
+  // sorted LDS walk: open partials (or dormant ones) written straight into
+  // `fresh` and matches into mj / mi, each block into its own region of
+  // `region` rows (block b: rows [b * region, ...), reserved per round from a
+  // block-local count; counts to blk_open / blk_match; a full region counts as
+  // an overflow and the host redoes the push) -- compacted afterwards
   int direct;
+  int64_t region;
+  uint32_t* blk_open;
+  uint32_t* blk_match;
   uint32_t direct_val;   // PS_OPEN (carry table) or PS_DORM (dormant staging table)
   SpillCols fresh;
   uint32_t amask;
   unsigned int* fresh_n;
   int64_t fresh_cap;
   const uint8_t* carry_pend;   // pending-list flags of the carried rows
+  // ... and the matches as (e2 row, e1 row) pairs (reserved like the carry
+  // rows; null: per-position outcome bytes / match rows instead)
+  uint32_t* mj;
+  uint32_t* mi;
+  unsigned int* m_n;
   int64_t t_end;        // latest event time of this push
   // hashed buckets (0: positions are sorted by the full key): positions are
   // grouped by the low bits of key_bucket_mix(key), keys of one bucket
@@ -364,6 +374,9 @@ int lds_walk_cap();
 void launch_lds_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, uint32_t* skey, uint32_t* spv,
                      const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row, uint8_t* pst,
                      ScanOut* blk, int nblk, hipStream_t s);
+void launch_region_compact(const SpillCols& src, const SpillCols& dst, uint32_t amask, int64_t region, int nblk,
+                           const uint32_t* ocnt, const uint32_t* ooff, const uint32_t* sj, const uint32_t* si,
+                           uint32_t* dj, uint32_t* di, const uint32_t* mcnt, const uint32_t* moff, hipStream_t s);
 void launch_group_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, const uint32_t* skey,
                        const uint32_t* spv, const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row,
                        uint8_t* pst, ScanOut* blk, hipStream_t s);

@@ -153,8 +153,8 @@ def test_grouped_lds_walk(hip_available, monkeypatch, path, parts):
     if path == "sort":
         monkeypatch.setenv("SHD_NO_GROUP", "1")
         monkeypatch.setenv("SHD_NO_LDSWALK", "1")
-    elif path == "ldswalk":   # the default: sorted LDS walk (engine_group.hip k_lds_walk)
-        pass
+    elif path == "ldswalk":   # the sorted LDS walk (engine_group.hip k_lds_walk, opt-in)
+        monkeypatch.setenv("SHD_LDSWALK", "1")
     else:   # the opt-in grouped walk carries every open partial (no dormant table)
         monkeypatch.setenv("SHD_GROUP", "force" if path == "group-oversized" else "1")
         monkeypatch.setenv("SHD_NO_SPILL", "1")
@@ -300,8 +300,8 @@ def test_partition_keys_far_from_zero(hip_available, monkeypatch, parts, lds):
     app = ("define stream S (k int, p double); partition with (k of S) begin "
            "@info(name='q') from every e1=S[p>40] -> e2=S[p>e1.p*1.02] within 30 milliseconds "
            "select e1.k as k, e1.p as p1, e2.p as p2 insert into O; end;")
-    if not lds:
-        monkeypatch.setenv("SHD_NO_LDSWALK", "1")
+    if lds:
+        monkeypatch.setenv("SHD_LDSWALK", "1")
     qp, _ = compile_single_query(app)
     rng = np.random.default_rng(12)
     n = 120_000
@@ -348,10 +348,11 @@ def test_dormant_partials(hip_available, monkeypatch, back):
 
 
 P3_PATH_ENVS = {
-    "ldswalk": {},
-    "forward-scan": {"SHD_NO_LDSWALK": "1"},
-    "forward-scan-carry-all": {"SHD_NO_LDSWALK": "1", "SHD_NO_SPILL": "1"},
-    "ldswalk-carry-all": {"SHD_NO_SPILL": "1"},
+    "ldswalk": {"SHD_LDSWALK": "1"},
+    "forward-scan": {},
+    "forward-scan-carry-all": {"SHD_NO_SPILL": "1"},
+    "ldswalk-carry-all": {"SHD_LDSWALK": "1", "SHD_NO_SPILL": "1"},
+    "ldswalk-gather": {"SHD_LDSWALK": "1", "SHD_CARRY_GATHER": "1"},
 }
 
 
@@ -359,9 +360,9 @@ P3_PATH_ENVS = {
 @pytest.mark.parametrize("shape", ["sparse", "dense"])
 @pytest.mark.parametrize("parts", [1, 4])
 def test_p3_paths(hip_available, monkeypatch, path, shape, parts):
-    """Partitioned P3 on each device path -- the sorted LDS walk (default) or
-    the full key sort + forward scan, with dormant partials or carrying every
-    open partial -- over sparse (the bench's 10 events / key / `within`
+    """Partitioned P3 on each device path -- the full key sort + forward scan
+    (default) with dormant partials (SHD_SPILL) or carrying every open
+    partial, or the sorted LDS walk (SHD_LDSWALK) -- over sparse (the bench's 10 events / key / `within`
     fraction) and dense keys, in one push or four: equal to the oracle."""
     for k, v in P3_PATH_ENVS[path].items():
         monkeypatch.setenv(k, v)
