@@ -331,26 +331,16 @@ struct DExprSet {
   int nins, nconsts;
 };
 
-// Expression program placement.  Staging the program into LDS at kernel start
-// (every lane decodes the same uniform instruction stream) was measured to
-// fault on the MI355X pool in the single-stream kernels (k_filter: memory
-// aperture violation for any batch size, while the identical kernels reading
-// the program from global memory pass: scripts/probe_filter.py, DESIGN.md
-// "LDS program staging").  The program therefore stays in global memory,
-// where the uniform instruction reads are served by the scalar/L1 caches;
-// stage_prog keeps the call sites and reserves no LDS.  Plans larger than
-// the former LDS store are still rejected at load (DevExprTable::upload).
+// Expression program placement: the program stays in global memory (the
+// uniform instruction reads are served by the scalar / L1 caches).  Staging
+// it into LDS at kernel start was measured to fault on the MI355X pool in the
+// single-stream kernels (k_filter: memory aperture violation for any batch
+// size, while the identical kernels reading the program from global memory
+// pass: scripts/probe_filter.py, DESIGN.md "LDS program staging").  Plans
+// larger than kLdsIns / kLdsConsts are still rejected at load
+// (DevExprTable::upload).
 constexpr int kLdsIns = 256;
 constexpr int kLdsConsts = 64;
-struct LdsProg {
-  int4 ins[1];
-};
-
-template <int NT = kBlock>
-__device__ __forceinline__ DExprSet stage_prog(const DExprSet& g, LdsProg& s) {
-  (void)s;
-  return g;
-}
 
 // ---------------------------------------------------------------- fast predicates
 // Filter chains whose bytecode is a conjunction of comparisons between simple

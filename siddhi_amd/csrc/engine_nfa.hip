@@ -1419,7 +1419,6 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
                                                         const NfaRunArgs* __restrict__ ap) {
   __shared__ NfaProg sprog;
   __shared__ NfaLayout slay;
-  __shared__ LdsProg prog;
   {
     const int* src = reinterpret_cast<const int*>(gprog);
     int* dst = reinterpret_cast<int*>(&sprog);
@@ -1429,7 +1428,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
     for (int i = threadIdx.x; i < (int)(sizeof(NfaLayout) / 4); i += kLaneBlock) d2[i] = s2[i];
   }
   const NfaRunArgs& a = *ap;
-  const DExprSet es = stage_prog<kLaneBlock>(a.es, prog);   // contains the barrier
+  __syncthreads();   // the program / layout copies above are complete
+  const DExprSet es = a.es;
   const int64_t lane_id = (int64_t)blockIdx.x * kLaneBlock + threadIdx.x;
   if (lane_id >= a.nlanes) return;
   int64_t seg, slot;
@@ -1624,8 +1624,7 @@ __device__ __forceinline__ uint64_t canon_key(Val v, int type) {
 __global__ __launch_bounds__(kBlock) void k_nfa_keys(const KeyArgs* __restrict__ ap, int64_t n, int64_t stride,
                                                      uint64_t* key, uint32_t* keyed, unsigned long long* kmax) {
   const KeyArgs& a = *ap;
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   unsigned long long m = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     BatchCtx cx{&a.batch, i};

@@ -725,8 +725,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
                                                            uint8_t* __restrict__ pst, uint32_t* __restrict__ bcnt,
                                                            ScanOut* __restrict__ blk, int slot0) {
   const ScanArgs& a = *ap;
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   uint64_t steps = 0, pruned = 0;
   uint32_t viol = 0, nm = 0, no = 0;
   const int64_t t0 = (int64_t)blockIdx.x * tile;
@@ -1238,8 +1237,7 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
                                                     int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq,
                                                     int32_t* o_sidx) {
   const ProjArgs& a = *ap;
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   const ExtRows& x = a.x;
   for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < m; k = m) {
     int64_t j = pj[k], i = pi[k];

@@ -148,8 +148,7 @@ struct FilterArgs {
 __global__ __launch_bounds__(kBlock) void k_filter(const FilterArgs* __restrict__ ap, int64_t n, uint8_t* flags, uint32_t* cnt,
                                                    uint64_t* pkey) {
   const FilterArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     RowCtx cx{&cs, i, nullptr, nullptr};
@@ -204,8 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_project_rows(const ProjArgs* __restr
                                                          int64_t* o_ts, uint64_t* o_vals, uint8_t* o_nul,
                                                          int64_t* o_seq) {
   const ProjArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
@@ -253,8 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
                                                        int32_t* ievrow, int32_t* icall, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
@@ -2045,8 +2042,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const EmitArgs* __restrict__ ap
                                                  int64_t* o_chunk, int32_t* o_type, int64_t* o_ts, uint64_t* o_vals,
                                                  uint8_t* o_nul, int64_t* o_seq) {
   const EmitArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  __shared__ LdsProg prog;
-  const DExprSet es = stage_prog(a.es, prog);
+  const DExprSet es = a.es;
   const ColSet& cs = a.cs;
   for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < nnew; t0 = nnew) {
     if (!fcnt[t0]) continue;
@@ -2750,7 +2746,13 @@ struct SingleEngine : Engine {
   }
 
   bool agg_chunked(int64_t total, uint64_t kmax, int64_t cap, int64_t ncalls) {
-    if (getenv("SHD_NO_WCHUNK") || !gdense || (wkind != SHD_W_LENGTH && wkind != SHD_W_TIME) || nch > 2 ||
+    // group ids: dense dictionary ids (string / bool attribute) or the group
+    // dictionary's dense ids -- either way in [0, kmax]
+    // opt-in (SHD_WCHUNK=1): on W2 the per-chunk workgroups (144 KB of LDS:
+    // one per CU) are latency-bound -- r03m: 13.5 ms of delta + emit per
+    // 100 M events against 10.4 ms for the group sort + segmented scans
+    if (!getenv("SHD_WCHUNK") || getenv("SHD_NO_WCHUNK") || ngk == 0 || (wkind != SHD_W_LENGTH && wkind != SHD_W_TIME) ||
+        nch > 2 ||
         kmax + 1 > (uint64_t)kWcMaxG || kmax + 1 < 64 || total >= (int64_t)INT32_MAX)
       return false;
     int64_t maxcall = 0;

@@ -158,3 +158,33 @@ def test_range_guard_falls_back_to_exact_fold(hip_available, shape):
                 col[np.isnan(col)] = np.nan
             return rows[:3] + (v,) + rows[4:]
         assert_rows_agg(canon(dev), canon(ora), qp, exact=True)
+
+
+CHUNK_APPS = [a for a in APPS if a[0] in ("sparse-groups", "length-1", "time-short", "typed-channels",
+                                           "one-group-groupby")] + [
+    ("w2-length-shape", "from S[d > 20.0]#window.length(700) select k, avg(d) as a, sum(d) as s, count() as c "
+                        "group by k insert into O;"),
+    ("long-window", "from S#window.length(9000) select k, sum(d) as s, count() as c group by k insert into O;"),
+]
+
+
+@pytest.mark.parametrize("name,app", CHUNK_APPS, ids=[a[0] for a in CHUNK_APPS])
+@pytest.mark.parametrize("keys", [64, 700, 2000])
+@pytest.mark.parametrize("call", [1, 97, 1024])
+def test_chunked_window_walk(hip_available, monkeypatch, name, app, keys, call):
+    """Dense group ids in [64, 2048]: the chunked window walk (opt-in, k_wc_*: per-chunk
+    group sort in LDS, chunk-start states from a prefix over chunks, carried
+    items in their own chunks) against the oracle at rtol 1e-9, and against
+    the segmented scans (SHD_NO_WCHUNK) -- calls of one event, of 97 and of
+    1024, windows longer than a chunk, null operands, typed channels."""
+    monkeypatch.setenv("SHD_WCHUNK", "1")   # the chunked walk is opt-in
+    qp, _ = compile_single_query("@app:playback " + SCHEMA + "@info(name='q') " + app)
+    m = 3000 if call == 1 else 20000
+    batches = make_batches(23 + keys, 4, m, keys, call=call)
+    ora = run_oracle(qp, batches)
+    dev, _, kind = run_device(qp, batches)
+    assert kind == 2 and len(ora[2]) > 0
+    assert_rows_agg(dev, ora, qp, exact=False)
+    monkeypatch.setenv("SHD_NO_WCHUNK", "1")
+    seg, _, _ = run_device(qp, batches)
+    assert_rows_agg(dev, seg, qp, exact=False)
