@@ -482,13 +482,23 @@ def main():
                                 co.astype(np.int64), True)
                 else:
                     # RCCL all-to-all: every event to its key's owner, arrival order restored by seq
-                    (rs, rp, rv, rt), rseq, _ = ex.route([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b],
-                                                         seqs[a:b], world)
+                    if os.environ.get("SHD_ROUTE_TORCH"):
+                        # round-2 routing (torch owner sort + sequence sort), for comparison
+                        (rs, rp, rv, rt), rseq, _ = ex.route([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b],
+                                                             seqs[a:b], world)
+                        co = ex.call_offsets_from_seq(rseq, 1024).numpy() if rs.numel() else None
+                    else:
+                        # HIP bucket scatter -> all-to-all -> per-call merge (csrc/route.hip); the
+                        # micro-batch spans global seqs [a * world, b * world) (round-robin shares)
+                        lo = (a * world) // 1024 * 1024
+                        nb = -(-(b * world - lo) // 1024)
+                        (rs, rp, rv, rt), rseq, co, _ = ex.route_device(
+                            [sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b], seqs[a:b], world, lo, 1024, nb,
+                            device=local)
                     m = rs.numel()
                     routed_total[0] += m
                     if m == 0:
                         continue
-                    co = ex.call_offsets_from_seq(rseq, 1024).numpy()   # (host copy: orders torch's stream)
                     torch.cuda.current_stream().synchronize()   # routed columns complete before the engine's stream reads them
                     dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
                                 he.SHD_MEM_DEVICE, co.astype(np.int64), True)

@@ -171,6 +171,38 @@ int shd_query_stream(shd_query* q, void** stream);
  * entries of ns[] and stage names (static strings) to names[]; *n = count. */
 int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int* n);
 
+/* Key-owner re-route of a micro-batch across ranks (replaces the
+ * reference's in-process PartitionStreamReceiver.send fan-out to per-key state,
+ * C/partition/PartitionStreamReceiver.java:262-283, when keys are sharded over
+ * GPUs).  All buffers are device memory, all work is queued on `stream`
+ * (hipStream_t), nothing synchronises.  Rows travel packed: the 8-byte columns,
+ * then the 4-byte columns two per 8-byte word, the last 4-byte slot holding
+ * seq - seq_lo; shd_route_words gives the words per row.  One calling thread
+ * per device at a time (the bucket pass keeps a per-device scratch buffer).
+ *
+ * shd_route_bucket: owner(i) = fmix32(low 32 bits of key[i]) % world; rows are
+ * written to send[] grouped by owner, each group in batch order (stable), and
+ * counts[o] (device int64[world]) = rows for owner o.  cols[c] holds
+ * widths[c] (4 or 8) bytes per row; seq[i] - seq_lo must lie in [0, 2^32).
+ *
+ * shd_route_merge: recv[] holds the rows of `world` senders, sender s's rows at
+ * [seg_off[s], seg_off[s+1]) (device int64[world+1], seg_off[world] = m), each
+ * in its sender's order.  The global stream's InputHandler calls are the
+ * blocks of `block` sequence numbers from seq_lo (seq_lo a multiple of block
+ * in the global numbering); every row must fall in one of the `nblocks`
+ * blocks.  Writes the rows in increasing sequence order to out_cols (widths as
+ * sent) and out_seq (int64), block_off[b] (device int64[nblocks+1]) = first
+ * output row of block b (block_off[nblocks] = m), and err[0] (device int32) = 1
+ * when a row is outside the blocks or a block holds more rows than sequence
+ * numbers.  start: device scratch of (nblocks + 1) * world int64. */
+int shd_route_words(int ncols, const int* widths, int* words);
+int shd_route_bucket(shd_ctx* ctx, void* stream, int64_t n, int world, const void* key, int key_width, int ncols,
+                     const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
+                     int64_t* counts);
+int shd_route_merge(shd_ctx* ctx, void* stream, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m,
+                    int64_t seq_lo, int64_t block, int64_t nblocks, int ncols, void* const* out_cols,
+                    const int* widths, int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err);
+
 const char* shd_last_error(void);
 
 #ifdef __cplusplus

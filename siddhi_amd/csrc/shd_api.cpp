@@ -603,6 +603,16 @@ void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, c
 
 }  // namespace
 
+namespace shd {
+int route_words(int ncols, const int* widths);
+void route_bucket(int device, hipStream_t s, int64_t n, int world, const void* key, int key_width, int ncols,
+                  const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
+                  int64_t* counts);
+void route_merge(hipStream_t s, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m, int64_t seq_lo,
+                 int64_t block, int64_t nblocks, int ncols, void* const* out_cols, const int* widths,
+                 int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err);
+}  // namespace shd
+
 extern "C" {
 
 const char* shd_last_error(void) { return g_err.c_str(); }
@@ -638,6 +648,38 @@ int shd_ctx_create(const int* device_ids, int n, shd_ctx** out) {
 int shd_ctx_destroy(shd_ctx* ctx) {
   delete ctx;
   return SHD_OK;
+}
+
+int shd_route_words(int ncols, const int* widths, int* words) {
+  return guarded([&]() -> int {
+    if (!words || (ncols > 0 && !widths)) return fail(SHD_E_ARG, "null pointer");
+    *words = route_words(ncols, widths);
+    return SHD_OK;
+  });
+}
+
+int shd_route_bucket(shd_ctx* ctx, void* stream, int64_t n, int world, const void* key, int key_width, int ncols,
+                     const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
+                     int64_t* counts) {
+  return guarded([&]() -> int {
+    if (!ctx || (ncols > 0 && (!cols || !widths))) return fail(SHD_E_ARG, "null pointer");
+    SHD_HIP(hipSetDevice(ctx->device));
+    route_bucket(ctx->device, (hipStream_t)stream, n, world, key, key_width, ncols, cols, widths, seq, seq_lo, send,
+                 counts);
+    return SHD_OK;
+  });
+}
+
+int shd_route_merge(shd_ctx* ctx, void* stream, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m,
+                    int64_t seq_lo, int64_t block, int64_t nblocks, int ncols, void* const* out_cols,
+                    const int* widths, int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err) {
+  return guarded([&]() -> int {
+    if (!ctx || (ncols > 0 && (!out_cols || !widths))) return fail(SHD_E_ARG, "null pointer");
+    SHD_HIP(hipSetDevice(ctx->device));
+    route_merge((hipStream_t)stream, world, recv, seg_off, m, seq_lo, block, nblocks, ncols, out_cols, widths,
+                out_seq, start, block_off, err);
+    return SHD_OK;
+  });
 }
 
 int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {

@@ -16,6 +16,14 @@ query's output depends on.
 
 Columns travel as one packed int64 matrix (one collective for all columns):
 int32 / uint32 ids widen to int64, float64 travels as its bit pattern.
+
+On the GPU (`route_device`) both local passes are HIP kernels behind the
+C-ABI (`shd_route_bucket` / `shd_route_merge`, siddhi_amd/csrc/route.hip): a
+stable bucket-by-owner scatter straight into the packed send buffer, and a
+merge that puts the received rows back into global arrival order one
+InputHandler call per workgroup (no sort), unpacking the columns and yielding
+the call boundaries on the way.  4-byte columns and the sequence number travel
+as 4-byte halves of a word (P3: 32 bytes per event instead of 40).
 """
 from __future__ import annotations
 
@@ -170,3 +178,94 @@ def call_offsets_from_seq(seq: torch.Tensor, call_size: int) -> torch.Tensor:
     starts = torch.nonzero(torch.cat([torch.ones(1, dtype=torch.bool, device=seq.device),
                                       call[1:] != call[:-1]])).flatten()
     return torch.cat([starts.to(torch.int64).cpu(), torch.tensor([n], dtype=torch.int64)])
+
+
+# ---------------------------------------------------------------- HIP routing
+def _widths(cols):
+    w = []
+    for c in cols:
+        if c.element_size() not in (4, 8) or not c.is_contiguous():
+            raise ValueError("route_device: contiguous 4- or 8-byte columns only")
+        w.append(c.element_size())
+    return w
+
+
+def bucket(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int, seq_lo: int,
+           device: int = 0):
+    """shd_route_bucket on torch's current stream: (send words [n * words] int64,
+    counts [world] int64 device, words per row)."""
+    import ctypes
+    from siddhi_amd import hip_engine as he
+    lib, ctx = he.load_library(), he.context(device)
+    n = seq.numel()
+    widths = _widths(cols)
+    wa = (ctypes.c_int * max(len(cols), 1))(*widths)
+    words = ctypes.c_int()
+    he._check(lib.shd_route_words(len(cols), wa, ctypes.byref(words)))
+    send = torch.empty(max(n, 1) * words.value, dtype=torch.int64, device=seq.device)
+    counts = torch.empty(world, dtype=torch.int64, device=seq.device)
+    ptrs = (ctypes.c_void_p * max(len(cols), 1))(*[c.data_ptr() for c in cols])
+    if key.dtype not in (torch.int32, torch.int64) or not key.is_contiguous() or not seq.is_contiguous():
+        raise ValueError("route_device: contiguous int32/int64 key and int64 seq")
+    stream = torch.cuda.current_stream(seq.device).cuda_stream
+    he._check(lib.shd_route_bucket(ctx, stream, n, world, key.data_ptr(), key.element_size(), len(cols), ptrs, wa,
+                                   seq.data_ptr(), int(seq_lo), send.data_ptr(), counts.data_ptr()))
+    return send[:n * words.value], counts, words.value
+
+
+def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtype], world: int, seq_lo: int,
+          call_size: int, nblocks: int, device: int = 0):
+    """shd_route_merge on torch's current stream: the received rows of `world`
+    senders (sender s's recv_counts[s] rows in turn) in global sequence order.
+    Returns (columns, seq, call offsets as a host int64 array)."""
+    import ctypes
+    import numpy as np
+    from siddhi_amd import hip_engine as he
+    lib, ctx = he.load_library(), he.context(device)
+    dev = recv.device
+    seg_off = torch.zeros(world + 1, dtype=torch.int64, device=dev)
+    seg_off[1:] = torch.cumsum(recv_counts, 0)
+    m = int(seg_off[-1].item())
+    outs = [torch.empty(m, dtype=dt, device=dev) for dt in dtypes]
+    widths = _widths(outs)
+    wa = (ctypes.c_int * max(len(outs), 1))(*widths)
+    ptrs = (ctypes.c_void_p * max(len(outs), 1))(*[c.data_ptr() for c in outs])
+    out_seq = torch.empty(m, dtype=torch.int64, device=dev)
+    start = torch.empty((nblocks + 1) * world, dtype=torch.int64, device=dev)
+    block_off = torch.empty(nblocks + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    he._check(lib.shd_route_merge(ctx, stream, world, recv.data_ptr(), seg_off.data_ptr(), m, int(seq_lo),
+                                  int(call_size), int(nblocks), len(outs), ptrs, wa, out_seq.data_ptr(),
+                                  start.data_ptr(), block_off.data_ptr(), err.data_ptr()))
+    bo = block_off.cpu().numpy()
+    if int(err.cpu()[0]) != 0:
+        raise ValueError("route_device: received rows outside the micro-batch's calls (seq_lo / nblocks)")
+    co = np.unique(bo)
+    if len(co) == 0 or co[0] != 0:
+        co = np.concatenate([[0], co])
+    return outs, out_seq, co.astype(np.int64)
+
+
+def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int, seq_lo: int,
+                 call_size: int, nblocks: int, group: Optional[dist.ProcessGroup] = None, device: int = 0):
+    """route() on the GPU with the HIP bucket / merge passes around ONE RCCL
+    all-to-all (plus the all-to-all of the per-owner counts, whose host copy
+    sizes the exchange).  The micro-batch's events hold sequence numbers in
+    [seq_lo, seq_lo + nblocks * call_size) with seq_lo a multiple of call_size
+    (the global stream's InputHandler calls).  Returns (columns, seq, host call
+    offsets, stats) in increasing sequence order."""
+    dtypes = [c.dtype for c in cols]
+    send, counts, words = bucket(cols, key, seq, world, seq_lo, device)
+    if world > 1:
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts, group=group)
+        cs, rcs = counts.tolist(), recv_counts.tolist()
+        recv = torch.empty(sum(rcs) * words, dtype=torch.int64, device=send.device)
+        dist.all_to_all_single(recv, send, [c * words for c in rcs], [c * words for c in cs], group=group)
+        rank = dist.get_rank(group)
+        stats = {"sent": sum(cs) - cs[rank], "received": sum(rcs) - rcs[rank]}
+    else:
+        recv, recv_counts, stats = send, counts, {"sent": 0, "received": 0}
+    outs, rseq, co = merge(recv, recv_counts, dtypes, world, seq_lo, call_size, nblocks, device)
+    return outs, rseq, co, stats
