@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${TAG:-r03n}
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_route.py -x -v -rs --timeout 120 --timeout-method thread \
+timeout -k 10 400 python3 -u -m pytest ${TESTS:-tests/test_gpu_route.py} -x -v -rs --timeout 120 --timeout-method thread \
   > gpurun_out/route_$T.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/route_$T.log; exit 1; }
 tail -3 gpurun_out/route_$T.log
 timeout -k 10 300 python3 -u bench.py --input roundrobin --steps 3 --warmup 1 --cpu-sample 0 \

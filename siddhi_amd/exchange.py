@@ -214,9 +214,10 @@ def bucket(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world
 
 
 def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtype], world: int, seq_lo: int,
-          call_size: int, nblocks: int, device: int = 0):
+          call_size: int, nblocks: int, device: int = 0, m: Optional[int] = None):
     """shd_route_merge on torch's current stream: the received rows of `world`
     senders (sender s's recv_counts[s] rows in turn) in global sequence order.
+    m: total rows when the caller knows it (saves a device read).
     Returns (columns, seq, call offsets as a host int64 array)."""
     import ctypes
     import numpy as np
@@ -225,21 +226,24 @@ def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtyp
     dev = recv.device
     seg_off = torch.zeros(world + 1, dtype=torch.int64, device=dev)
     seg_off[1:] = torch.cumsum(recv_counts, 0)
-    m = int(seg_off[-1].item())
+    if m is None:
+        m = int(seg_off[-1].item())
     outs = [torch.empty(m, dtype=dt, device=dev) for dt in dtypes]
     widths = _widths(outs)
     wa = (ctypes.c_int * max(len(outs), 1))(*widths)
     ptrs = (ctypes.c_void_p * max(len(outs), 1))(*[c.data_ptr() for c in outs])
     out_seq = torch.empty(m, dtype=torch.int64, device=dev)
     start = torch.empty((nblocks + 1) * world, dtype=torch.int64, device=dev)
-    block_off = torch.empty(nblocks + 1, dtype=torch.int64, device=dev)
-    err = torch.empty(1, dtype=torch.int32, device=dev)
+    # call offsets and the error flag (last word) come back in ONE device -> host copy
+    tail = torch.empty(nblocks + 2, dtype=torch.int64, device=dev)
+    block_off, err = tail[:nblocks + 1], tail[nblocks + 1:].view(torch.int32)
     stream = torch.cuda.current_stream(dev).cuda_stream
     he._check(lib.shd_route_merge(ctx, stream, world, recv.data_ptr(), seg_off.data_ptr(), m, int(seq_lo),
                                   int(call_size), int(nblocks), len(outs), ptrs, wa, out_seq.data_ptr(),
                                   start.data_ptr(), block_off.data_ptr(), err.data_ptr()))
-    bo = block_off.cpu().numpy()
-    if int(err.cpu()[0]) != 0:
+    th = tail.cpu().numpy()
+    bo = th[:nblocks + 1]
+    if int(th[nblocks + 1:].view(np.int32)[0]) != 0:
         raise ValueError("route_device: received rows outside the micro-batch's calls (seq_lo / nblocks)")
     co = np.unique(bo)
     if len(co) == 0 or co[0] != 0:
@@ -267,5 +271,6 @@ def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor,
         stats = {"sent": sum(cs) - cs[rank], "received": sum(rcs) - rcs[rank]}
     else:
         recv, recv_counts, stats = send, counts, {"sent": 0, "received": 0}
-    outs, rseq, co = merge(recv, recv_counts, dtypes, world, seq_lo, call_size, nblocks, device)
+    outs, rseq, co = merge(recv, recv_counts, dtypes, world, seq_lo, call_size, nblocks, device,
+                           m=recv.numel() // words if world > 1 else seq.numel())
     return outs, rseq, co, stats

@@ -218,6 +218,18 @@ class InputHandler:
         self._rt._send_columns(self.stream_id, batch)
 
 
+def _duration_ms(text: str) -> int:
+    """'100 millisecond' / '2 sec' / '500' (ms) -> milliseconds."""
+    parts = str(text).strip().split()
+    n = int(float(parts[0]))
+    if len(parts) == 1:
+        return n
+    unit = qc._time_unit(parts[1])
+    if unit is None:
+        raise ValueError("unknown time unit in %r" % text)
+    return n * unit
+
+
 class SiddhiAppRuntime:
     """io.siddhi.core.SiddhiAppRuntime"""
 
@@ -230,6 +242,16 @@ class SiddhiAppRuntime:
         if ann is not None and ann.elements:
             self.name = ann.elements[0][1]
         self.playback = app.annotation("app:playback") is not None
+        # @app:playback(idle.time = '100 millisecond', increment = '2 sec'): the
+        # heartbeat that moves playback time while no events arrive
+        # (TimestampGeneratorImpl.setIdleTime / setIncrementInMilliseconds)
+        self.idle_time = self.idle_increment = None
+        if self.playback:
+            pa = app.annotation("app:playback")
+            it, inc = pa.get("idle.time"), pa.get("increment")
+            if it is not None and inc is not None:
+                self.idle_time, self.idle_increment = _duration_ms(it), _duration_ms(inc)
+        self._event_time = None   # TimestampGeneratorImpl.lastEventTimestamp (playback)
         self.stream_types: Dict[str, List[int]] = {
             s: [pl.TYPE_CODE[t] for _, t in sd.attrs] for s, sd in app.streams.items()}
         self.queries: List[_QueryRuntime] = []
@@ -385,8 +407,21 @@ class SiddhiAppRuntime:
             raise RuntimeError("Siddhi app '%s' is not running" % self.name)
         t = int(ts)
         self._last_wall = max(self._last_wall, t)
+        if self._event_time is None or t > self._event_time:
+            self._event_time = t
         for q in self.queries:
             self._deliver(q, q.engine.set_time(t))
+
+    def idle(self, ms: int):
+        """`ms` of wall-clock time pass with no events on a playback app: its
+        heartbeat moves the app time by `increment` once per `idle.time`
+        (TimestampGeneratorImpl.TimeInjector.run, C/util/timestamp/
+        TimestampGeneratorImpl.java:168-184: each injection re-arms the
+        heartbeat for another idle period).  No-op without idle.time."""
+        if not self.playback or self.idle_time is None or self._event_time is None:
+            return
+        for _ in range(int(ms) // max(self.idle_time, 1)):
+            self.advanceTime(self._event_time + self.idle_increment)
 
     # -- internals
     def _wall_clock(self):
@@ -414,6 +449,8 @@ class SiddhiAppRuntime:
             return
         # setCurrentTimestamp(last ts): every query's due timers first
         t = int(batch.ts[-1])
+        if self._event_time is None or t > self._event_time:
+            self._event_time = t
         for q in self.queries:
             self._deliver(q, q.engine.set_time(t))
         self._junction(stream_id, batch)
