@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 180 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs --timeout 180 --timeout-method thread -p no:cacheprovider \
     ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu_$TAG.log

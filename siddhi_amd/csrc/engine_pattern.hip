@@ -243,7 +243,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
                                                 int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
                                                 int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
                                                 uint64_t& steps, uint32_t& viol, uint32_t& fm, int64_t& ra,
-                                                int64_t& rb) {
+                                                int64_t& rb, int64_t q1 = -1) {
   uint8_t st = ST_OPEN;
   bool stop = false, first = true;
   int it = 0;
@@ -331,7 +331,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
             // partner processor on this same event (LogicalPostStateProcessor.java:59-86)
             int32_t br = -1;
             if (!(fm & 1u)) {
-              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second, q};
+              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second, q, q1};
               if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
                 fm |= 1u;
                 ra = r2;
@@ -339,7 +339,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
               }
             }
             if (br < 0 && !(fm & 2u)) {
-              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first, q};
+              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first, q, q1};
               if (FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx)) {
                 fm |= 2u;
                 rb = r2;
@@ -357,6 +357,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
           }
           PairCtx cx{&a.x, r, r2, a.s_first};
           cx.q2 = q;
+          cx.q1 = q1;
           bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
           int32_t br = 0;
           if (!hit && a.logical) {
@@ -521,10 +522,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_bpos(const ExtRows* __restric
   const ExtRows& x = *xp;
   for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_ext; p += (int64_t)gridDim.x * kBlock) {
     const int64_t r = pv_row(spv[p]);
-    if (r < x.C) continue;
+    // carried rows are e1 partials: only their e1-side operands (apos_mask)
+    const uint32_t m = r < x.C ? x.apos_mask : (x.bpos_mask | x.apos_mask);
     for (int c = 0; c < x.batch.ncols; c++) {
-      if (!((x.bpos_mask >> c) & 1u)) continue;
-      const Val v = col_load(x.batch, r - x.C, c);
+      if (!((m >> c) & 1u)) continue;
+      const Val v = r < x.C ? col_load(x.carry, r, c) : col_load(x.batch, r - x.C, c);
       switch (x.bpos.type[c]) {
         case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)x.bpos.col[c])[p] = (uint32_t)v.b; break;
         case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)x.bpos.col[c])[p] = v.b; break;
@@ -609,11 +611,13 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       if (cand && !(fm & 1u)) {
         PairCtx cx{&a.x, r, r2, a.s_first};
         cx.q2 = q;
+        cx.q1 = p;
         ha = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
       }
       if (cand && !(fm & 2u)) {
         PairCtx cx{&a.x, r, r2, a.s_second};
         cx.q2 = q;
+        cx.q1 = p;
         hb = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
       }
       const uint64_t am = __ballot(ha), bm = __ballot(hb);
@@ -655,6 +659,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       const int64_t r2 = pv_row(pq);
       PairCtx cx{&a.x, r, r2, a.s_first};
       cx.q2 = q;
+      cx.q1 = p;
       hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
       int32_t br = 0;
       if (!hit && a.logical) {
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       int64_t ra = -1, rb = -1;
       if (a.logical == 2) and_carried(a, pv_row(pvp), fm, ra, rb);
       const uint8_t st = walk_partial<false, FAST, 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true,
-                                                      j, steps, viol, fm, ra, rb);
+                                                      j, steps, viol, fm, ra, rb, p);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
         out = PS_MATCH;
@@ -793,7 +798,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       uint32_t fm = 0;
       int64_t ra = -1, rb = -1;
       const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 64>(
-          a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j, steps, viol, fm, ra, rb);
+          a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j, steps, viol, fm, ra, rb, p);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
         out = PS_MATCH;
@@ -1687,6 +1692,7 @@ struct PatternEngine : Engine {
   std::vector<int> typesB;   // AND: schema of the operand events carried with half-filled partials
   bool and_indep = false;    // AND: neither operand filter reads the partner's slot
   uint32_t bpos_mask = 0;    // e2-side attributes read by the operand filters (ExtRows::bpos)
+  uint32_t apos_mask = 0;    // e1-side attributes read by the operand filters (ExtRows::apos_mask)
   DevBuf d_bpos[kMaxCols], d_bpos_nul[kMaxCols];
   int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
@@ -2956,10 +2962,16 @@ struct PatternEngine : Engine {
     // position order once, so the walks load them coalesced; worth its pass
     // only when walks are long (SHD_NO_BPOS: off, SHD_BPOS: always when dense)
     if (grouped && rmode != 0 && isB && bpos_mask && !getenv("SHD_NO_BPOS") && (e_key >= 8.0 || getenv("SHD_BPOS"))) {
+      // e1 operands position-major too (same stream schema, columns the carry keeps)
+      uint32_t apos = getenv("SHD_NO_APOS") ? 0u : (apos_mask & carry_mask);
+      for (int c = 0; c < kMaxCols; c++)
+        if (((apos >> c) & 1u) && (c >= b.cs.ncols || c >= (int)typesA.size() || typesA[c] != b.cs.type[c]))
+          apos &= ~(1u << c);
       sa.x.bpos = b.cs;
       sa.x.bpos.n = n_ext;
+      sa.x.apos_mask = apos;
       for (int c = 0; c < b.cs.ncols; c++) {
-        if (!((bpos_mask >> c) & 1u)) continue;
+        if (!(((bpos_mask | apos) >> c) & 1u)) continue;
         d_bpos[c].reserve(n_ext * type_size(b.cs.type[c]));
         d_bpos_nul[c].reserve(n_ext);
         sa.x.bpos.col[c] = d_bpos[c].p;
@@ -3361,6 +3373,11 @@ std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, con
     };
     scan(b.filters, b.state_id);
     if (c) scan(c->filters, c->state_id);
+    for (const std::vector<int>* fs : {&b.filters, c ? &c->filters : nullptr})
+      if (fs)
+        for (int f : *fs)
+          for (auto& in : p.exprs[f])
+            if (in.op == SHD_OP_LOAD && in.a == 0 && (in.c & 0xFFFF) < kMaxCols) e->apos_mask |= 1u << (in.c & 0xFFFF);
   }
   for (auto& o : p.outputs) e->outs.push_back(o.second);
   e->partitioned = !p.part_keys.empty();

@@ -47,6 +47,10 @@ struct ExtRows {
   // the 64 positions a wave steps over load coalesced instead of one row each
   ColSet bpos;
   uint32_t bpos_mask;
+  // e1-side attributes the filters read, in the same position-major columns
+  // (carried rows included): a walk reads its partial's own operands at its
+  // start position, coalesced, instead of one random row load per step
+  uint32_t apos_mask;
   __device__ __forceinline__ const ColSet& cs(int64_t r) const { return r < C ? carry : (r < C + batch.n ? batch : half); }
   __device__ __forceinline__ int64_t row(int64_t r) const { return r < C ? r : (r < C + batch.n ? r - C : r - C - batch.n); }
   __device__ __forceinline__ int64_t ts(int64_t r) const {
@@ -76,6 +80,7 @@ struct PairCtx {
   int64_t r3 = -1;        // logical AND: the partner operand's row (state s3)
   int s3 = -1;
   int64_t q2 = -1;        // sorted position of r2 (walks; -1 in the projection)
+  int64_t q1 = -1;        // sorted position of r1 (walks from a known start position)
   __device__ __forceinline__ int64_t slot(int st, int idx) const {
     int64_t r = st == 0 ? r1 : (st == s2 ? r2 : (st == s3 ? r3 : -1));
     if (r < 0) return -1;
@@ -93,6 +98,7 @@ struct PairCtx {
     // branch on the row's table instead of selecting a per-lane ColSet
     // pointer: each branch reads a wave-uniform column table (scalar loads)
     if (st == s2 && q2 >= 0 && ((x->bpos_mask >> attr) & 1u)) return col_load(x->bpos, q2, attr);
+    if (st == 0 && q1 >= 0 && ((x->apos_mask >> attr) & 1u)) return col_load(x->bpos, q1, attr);
     if (r < x->C) return col_load(x->carry, r, attr);
     if (r < x->C + x->batch.n) return col_load(x->batch, r - x->C, attr);
     return col_load(x->half, r - x->C - x->batch.n, attr);
