@@ -90,6 +90,15 @@ def gen_roundrobin_columns(torch, n, keys_total, delta, rank, world, dev):
     return sym, price, vol, ts, seq
 
 
+def align_rr(batch, world, call=1024):
+    """Largest micro-batch <= batch (at least one unit) whose cuts a * world are
+    multiples of the call size: round-robin micro-batches then hold whole
+    InputHandler calls (a call split over two pushes would see two clock moves)."""
+    import math
+    unit = call // math.gcd(call, world)
+    return max(unit, batch // unit * unit)
+
+
 def alg_bytes_pattern(c, n):
     """B_ev = 20 + 16*P + 24*f_new + 32*m per event."""
     P = c["partial_scans"] / max(n, 1)
@@ -107,13 +116,23 @@ def alg_bytes_window(c, n, n_out):
 def pmc_summary(cfg_name):
     """Newest committed rocprofv3 PMC summary of this config (profiles/rNN_pmc_<config>.json,
     written by scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes with the
-    gfx950 corrections): per-kernel HBM bytes and times of one push."""
+    gfx950 corrections): per-kernel HBM bytes and times of one push.  Only a summary
+    taken on the running sources (its "build" = buildinfo.source_hash()) is used;
+    otherwise (None, reason) and the line's traffic stays null."""
     import glob
+    from siddhi_amd.buildinfo import source_hash
+    want = source_hash()
+    newest = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % cfg_name)), reverse=True):
         d = json.load(open(f))
-        if "push" in d and "kernels" in d:
-            return d, os.path.relpath(f, ROOT)
-    return None, None
+        if "push" not in d or "kernels" not in d:
+            continue
+        rel = os.path.relpath(f, ROOT)
+        if d.get("build") == want:
+            return d, rel
+        newest = newest or rel
+    return None, ("no PMC summary of build %s (newest %s is of other sources)" % (want, newest) if newest
+                  else "no PMC summary of build %s" % want)
 
 
 def cpu_baseline(cfg_name, app, keys, delta, sample):
@@ -463,6 +482,11 @@ def main():
         he.context(local)
         dq = he.DeviceQuery(qp.ir, device=local)
         batch = min(args.batch, n)
+        if seqs is not None:
+            # a micro-batch [a, b) of this rank's round-robin share spans global
+            # seqs [a * world, b * world): cut on InputHandler call boundaries
+            # (multiples of 1024 global seqs), so no call straddles two pushes
+            batch = align_rr(batch, world)
         cuts = list(range(0, n, batch)) + [n]
         offs_all = wl.call_offsets(n)
 
@@ -512,6 +536,8 @@ def main():
 
         for sb in [int(x) for x in args.sweep_batches.split(",") if x]:
             # micro-batch size sweep (diagnostic): same data, same query
+            if seqs is not None:
+                sb = align_rr(sb, world)
             sc = list(range(0, n, sb)) + [n]
             run_step(cuts=sc)
             torch.cuda.synchronize()
@@ -599,6 +625,9 @@ def main():
         pmc, psrc = pmc_summary(args.config)
         traffic = None
         kern = None
+        pmc_note = None
+        if not pmc:
+            pmc_note, psrc = psrc, None
         if pmc:
             traffic = round(pmc["push"]["hbm_bytes_per_event"] * n)
             top = sorted(pmc["kernels"].items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["dispatches_per_push"])[:5]
@@ -611,7 +640,7 @@ def main():
                 "alg_bytes_per_event": round(bytes_step / n, 2),
                 "scope": "whole push pipeline per step (wall clock)",
                 "device_achieved": round(dev_ach, 1), "device_frac": round(dev_ach / HBM_PEAK_GBS, 4),
-                "pmc_source": psrc, "kernels": kern}
+                "pmc_source": psrc, "pmc_note": pmc_note, "kernels": kern}
     matches_per_s = counters["matches"] * world * args.steps / elapsed
 
     cpu = None
@@ -650,6 +679,8 @@ def main():
         if pattern and isinstance(item, qc.Partition) and args.cpu_threads > 0:
             cpu_mt = cpu_baseline_parallel(args.config, app, keys, delta, min(4 * sample, n), args.cpu_threads)
 
+    from siddhi_amd.buildinfo import source_hash
+    build_id = source_hash()
     if rank == 0:
         line = {
             "metric": "events/sec ingested + matches/sec (partitioned pattern, 1\u20138 GPU); % HBM peak",
@@ -664,6 +695,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
+            "build": build_id,
             "config": {"workload": args.config, "events_per_gpu": n,
                        ("keys_total" if mode == "roundrobin" else "keys_per_gpu"): keys, "delta_ms": delta,
                        "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world,

@@ -75,9 +75,12 @@ typedef struct shd_batch {
   int32_t use_base_seq;         /* 1: base_seq is given (0, the zero-initialised
                                    default: the query continues its own count) */
   int64_t base_seq;             /* arrival index of the batch's first event in the
-                                   whole stream (a key-sharded rank receives a
-                                   subset): shd_out.in_seq of this batch's rows is
-                                   then global; must not go back (SHD_E_ARG)     */
+                                   whole stream when the batch is a CONTIGUOUS
+                                   slice of it: shd_out.in_seq = base_seq + row
+                                   is then global; must not go back (SHD_E_ARG).
+                                   Rows re-routed by key (shd_route_merge) are not
+                                   contiguous: map in_seq through out_seq
+                                   (exchange.merge_outputs)                    */
 } shd_batch;
 
 /* Output rows of a query since the last poll, in reference order.  Rows with
@@ -177,13 +180,14 @@ int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int*
  * GPUs).  All buffers are device memory, all work is queued on `stream`
  * (hipStream_t), nothing synchronises.  Rows travel packed: the 8-byte columns,
  * then the 4-byte columns two per 8-byte word, the last 4-byte slot holding
- * seq - seq_lo; shd_route_words gives the words per row.  One calling thread
- * per device at a time (the bucket pass keeps a per-device scratch buffer).
+ * seq - seq_lo; shd_route_words gives the words per row.  Scratch is
+ * caller-owned (device memory): calls on different streams may overlap.
  *
  * shd_route_bucket: owner(i) = fmix32(low 32 bits of key[i]) % world; rows are
  * written to send[] grouped by owner, each group in batch order (stable), and
  * counts[o] (device int64[world]) = rows for owner o.  cols[c] holds
  * widths[c] (4 or 8) bytes per row; seq[i] - seq_lo must lie in [0, 2^32).
+ * scratch: device buffer of shd_route_bucket_scratch(n, world) bytes.
  *
  * shd_route_merge: recv[] holds the rows of `world` senders, sender s's rows at
  * [seg_off[s], seg_off[s+1]) (device int64[world+1], seg_off[world] = m), each
@@ -196,9 +200,10 @@ int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int*
  * when a row is outside the blocks or a block holds more rows than sequence
  * numbers.  start: device scratch of (nblocks + 1) * world int64. */
 int shd_route_words(int ncols, const int* widths, int* words);
+int shd_route_bucket_scratch(int64_t n, int world, size_t* bytes);
 int shd_route_bucket(shd_ctx* ctx, void* stream, int64_t n, int world, const void* key, int key_width, int ncols,
                      const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
-                     int64_t* counts);
+                     int64_t* counts, void* scratch);
 int shd_route_merge(shd_ctx* ctx, void* stream, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m,
                     int64_t seq_lo, int64_t block, int64_t nblocks, int ncols, void* const* out_cols,
                     const int* widths, int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err);

@@ -1782,7 +1782,9 @@ struct Engine {
     int64_t count = 0;
     std::deque<Ev*> q;
     int64_t lastTimestamp = INT64_MIN;
-    std::multiset<int64_t> notify;
+    // Scheduler.SchedulerState.toNotifyQueue: a FIFO (LinkedBlockingQueue),
+    // peeked / polled at its head (C/util/Scheduler.java:113-209,330-332)
+    std::deque<int64_t> notify;
     // aggregator states per group key
     std::map<std::vector<std::pair<uint64_t, uint8_t>>, GroupAgg> groups;
   };
@@ -1992,12 +1994,16 @@ struct Engine {
           c->type = EXPIRED;
           ks->q.push_back(c);
           if (ks->lastTimestamp < c->ts) {
-            ks->notify.insert(c->ts + window_param);
+            ks->notify.push_back(c->ts + window_param);
             ks->lastTimestamp = c->ts;
           }
           out.push_back(e);
         }
       }
+      // PartitionStateHolder.returnState (C/util/snapshot/state/PartitionStateHolder.java:50-69):
+      // a partition's window state whose queue emptied is dropped, so its
+      // lastTimestamp starts over (TimeWindowProcessor.WindowState.canDestroy :219-221)
+      if (partitioned && ks->q.empty()) ks->lastTimestamp = INT64_MIN;
     }
     return out;
   }
@@ -2063,17 +2069,17 @@ struct Engine {
     std::vector<std::pair<int64_t, KeySingle*>> due;
     if (partitioned) {
       for (auto& kv : single_keys)
-        if (!kv.second->notify.empty() && *kv.second->notify.begin() <= t)
-          due.push_back({*kv.second->notify.begin(), kv.second.get()});
-    } else if (single_global && !single_global->notify.empty() && *single_global->notify.begin() <= t) {
-      due.push_back({*single_global->notify.begin(), single_global.get()});
+        if (!kv.second->notify.empty() && kv.second->notify.front() <= t)
+          due.push_back({kv.second->notify.front(), kv.second.get()});
+    } else if (single_global && !single_global->notify.empty() && single_global->notify.front() <= t) {
+      due.push_back({single_global->notify.front(), single_global.get()});
     }
     std::stable_sort(due.begin(), due.end(), [](auto& a, auto& b) { return a.first < b.first; });
     for (auto& d : due) {
       KeySingle* ks = d.second;
-      while (!ks->notify.empty() && *ks->notify.begin() - now <= 0) {
-        int64_t nt = *ks->notify.begin();
-        ks->notify.erase(ks->notify.begin());
+      while (!ks->notify.empty() && ks->notify.front() - now <= 0) {
+        int64_t nt = ks->notify.front();
+        ks->notify.pop_front();
         Ev* te = ev_arena.get();
         *te = Ev();
         te->type = TIMER;

@@ -15,7 +15,12 @@ per-push totals (all kernels of a push).
 import argparse
 import csv
 import json
+import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from siddhi_amd.buildinfo import source_hash  # noqa: E402
 
 PEAK_GBS = 8000.0
 
@@ -66,6 +71,9 @@ def main():
         tot_b += (fb + wb) * per_push
         tot_us += us * per_push
     out = {
+        # the libsiddhi_hip sources these counters were taken on (bench.py
+        # uses the traffic only when its own tree hashes the same)
+        "build": source_hash(),
         "source": {"trace": a.trace, "fetch": a.fetch, "write": a.write},
         "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
         "events_per_push": a.events,

@@ -231,6 +231,9 @@ std::unique_ptr<Engine> make_logical_pattern_engine(const Plan& p, std::string& 
 // `every e1=A[f1] -> not A[fx] for T` (engine_absent.hip)
 std::unique_ptr<Engine> make_absent_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why);
+// keyed exact window engine: EXPIRED output, `having`, partitioned windows /
+// aggregates (engine_window.hip)
+std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why);
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why);
 // list_hint: expected partials per key at once (sizes the per-key lists of an
 // unpartitioned plan; 0 = defaults)

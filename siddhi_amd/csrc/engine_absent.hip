@@ -306,9 +306,13 @@ __global__ void k_abs_due(const int64_t* __restrict__ ts, int64_t C, int64_t T, 
   }
 }
 
-__global__ void k_call_last_ts(const int64_t* __restrict__ ts, const int64_t* __restrict__ ends, int nc,
+// last event time of every call (INT64_MIN for an empty call: nothing is read)
+__global__ void k_call_last_ts(const int64_t* __restrict__ ts, const int64_t* __restrict__ offs, int nc,
                                int64_t* __restrict__ out) {
-  for (int c = blockIdx.x * kBlock + threadIdx.x; c < nc; c += gridDim.x * kBlock) out[c] = ts[ends[c] - 1];
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < nc; c += gridDim.x * kBlock) {
+    const int64_t a = offs[c], b = offs[c + 1];
+    out[c] = b > a ? ts[b - 1] : INT64_MIN;
+  }
 }
 
 struct AbsTable {
@@ -453,10 +457,10 @@ struct AbsentEngine : Engine {
     int64_t now_after = now;
     if (b.advance_time) {
       const int nc = (int)b.call_offsets.size() - 1;
-      d_ends.reserve((size_t)nc * 8);
+      d_ends.reserve((size_t)(nc + 1) * 8);
       d_last.reserve((size_t)nc * 8);
       h_last.reserve((size_t)nc * 8);
-      SHD_HIP(hipMemcpyAsync(d_ends.p, b.call_offsets.data() + 1, (size_t)nc * 8, hipMemcpyHostToDevice, s));
+      SHD_HIP(hipMemcpyAsync(d_ends.p, b.call_offsets.data(), (size_t)(nc + 1) * 8, hipMemcpyHostToDevice, s));
       hipLaunchKernelGGL(k_call_last_ts, dim3(grid_for(nc)), dim3(kBlock), 0, s, b.cs.ts,
                          (const int64_t*)d_ends.as<int64_t>(), nc, d_last.as<int64_t>());
       SHD_CHECK_LAUNCH();

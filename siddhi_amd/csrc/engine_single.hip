@@ -25,6 +25,8 @@
 #include <cstdlib>
 
 #include "engine.h"
+#include "gdict.h"
+#include "agg.h"
 
 namespace shd {
 
@@ -33,7 +35,6 @@ namespace {
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kAddBit = 0x80000000u;
 constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
-constexpr int kMaxGroupAttrs = 4;
 // segmented scans only while every operand seen so far is finite and the
 // non-zero magnitudes span at most 2^kSegMaxExpSpan (k_operand_stats)
 constexpr uint32_t kSegMaxExpSpan = 30;
@@ -56,45 +57,6 @@ struct RowCtx {
     return v;
   }
 };
-
-__device__ __forceinline__ uint64_t canon_key(Val v, int type) {
-  if (type == SHD_T_FLOAT) return p_f64((double)v_f32(v.b));
-  return v.b;
-}
-
-// One group-by value as a canonical word: two values share a word exactly
-// when String.valueOf prints them alike (the reference's group key is that
-// text, C/query/selector/GroupByKeyGenerator.java:63-73): a null string is the
-// string "null" (its dictionary id), every NaN is one NaN, 0.0 and -0.0 stay
-// apart; other nulls set isnull (word 0).
-__device__ __forceinline__ uint64_t group_word(Val v, int type, int64_t null_str_id, bool& isnull) {
-  isnull = false;
-  if (v.null) {
-    if (type == SHD_T_STRING && null_str_id >= 0) return (uint64_t)null_str_id;
-    isnull = true;
-    return 0;
-  }
-  switch (type) {
-    case SHD_T_FLOAT: {
-      const float f = v_f32(v.b);
-      return f != f ? 0x7fc00000ull : (uint64_t)(uint32_t)v.b;
-    }
-    case SHD_T_DOUBLE: {
-      const double d = __longlong_as_double((long long)v.b);
-      return d != d ? 0x7ff8000000000000ull : v.b;
-    }
-    case SHD_T_INT:
-    case SHD_T_BOOL:
-    case SHD_T_STRING: return (uint64_t)(uint32_t)v.b;
-    default: return v.b;
-  }
-}
-
-__host__ __device__ __forceinline__ uint64_t gdict_mix(uint64_t z) {   // splitmix64 finaliser
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 
 // ---------------------------------------------------------------- calls / time
 // call_of[i] for every event; call_last_ts[c]
@@ -300,129 +262,7 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
   }
 }
 
-// ---------------------------------------------------------------- group dictionary
-// Group keys that are not dense ids (numeric / multi-attribute / nullable
-// non-string keys) map to dense group ids through an open-addressing table on
-// the device: tag (hash with bit 63 set, 0 = empty; its low bits are the home slot), id, the key words and null mask.
-// Lookups are read-only; a push with unseen keys inserts them in a second
-// phase (misses compacted, sorted by hash, one leader per distinct key, CAS
-// insertion of distinct keys -- no thread ever waits on another), then looks
-// the missed items up again.
-constexpr uint64_t kTagBit = 1ull << 63;
-struct GDict {
-  unsigned long long* tag;
-  uint32_t* id;
-  uint64_t* kw;     // [nk][cap]
-  uint8_t* kn;
-  uint64_t cap;     // power of two
-  int nk;
-};
-
-__device__ __forceinline__ bool gdict_find(const GDict& d, uint64_t h, const uint64_t* key, int64_t kstride,
-                                           int64_t ki, uint8_t nul, uint32_t& id) {
-  const unsigned long long tg = (unsigned long long)(h | kTagBit);
-  uint64_t slot = h & (d.cap - 1);
-  for (uint64_t probe = 0; probe < d.cap; probe++) {
-    const unsigned long long t = d.tag[slot];
-    if (t == 0ull) return false;
-    if (t == tg && d.kn[slot] == nul) {
-      bool eq = true;
-      for (int g = 0; g < d.nk; g++) eq = eq && d.kw[(uint64_t)g * d.cap + slot] == key[(int64_t)g * kstride + ki];
-      if (eq) {
-        id = d.id[slot];
-        return true;
-      }
-    }
-    slot = (slot + 1) & (d.cap - 1);
-  }
-  return false;
-}
-
-// Group id of new item i (or a miss flag): ikey[C + i].
-__global__ __launch_bounds__(kBlock) void k_gdict_lookup(GDict d, int64_t n, const uint64_t* gh, const uint64_t* gkw,
-                                                         const uint8_t* gkn, int64_t gstride, int64_t C,
-                                                         uint64_t* ikey, uint32_t* miss) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
-    uint32_t id;
-    const bool hit = gdict_find(d, gh[i], gkw, gstride, i, gkn[i], id);
-    if (hit) ikey[C + i] = id;
-    miss[i] = hit ? 0u : 1u;
-  }
-}
-
-// Second look-up over the compacted misses (all present after the insert).
-__global__ __launch_bounds__(kBlock) void k_gdict_relookup(GDict d, int64_t nm, const uint32_t* midx, const uint64_t* gh,
-                                                           const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
-                                                           int64_t C, uint64_t* ikey) {
-  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nm; j = nm) {
-    const int64_t i = midx[j];
-    uint32_t id = 0xFFFFFFFFu;
-    gdict_find(d, gh[i], gkw, gstride, i, gkn[i], id);
-    ikey[C + i] = id;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_gdict_compact(const uint32_t* miss, const uint32_t* moff, int64_t n,
-                                                          const uint64_t* gh, uint32_t* midx, uint64_t* mh) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
-    if (!miss[i]) continue;
-    midx[moff[i]] = (uint32_t)i;
-    mh[moff[i]] = gh[i];
-  }
-}
-
-// Leaders among the hash-sorted misses: the first of each distinct key (an
-// equal-hash run is searched back for an equal key; such runs hold one key
-// unless 64-bit hashes collide).
-__global__ __launch_bounds__(kBlock) void k_gdict_leaders(int64_t nm, const uint64_t* sh, const uint32_t* sidx,
-                                                          const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
-                                                          int nk, uint32_t* lead) {
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nm; p = nm) {
-    const int64_t i = sidx[p];
-    bool leader = true;
-    for (int64_t q = p - 1; q >= 0 && sh[q] == sh[p]; q--) {
-      const int64_t j = sidx[q];
-      bool eq = gkn[j] == gkn[i];
-      for (int g = 0; g < nk && eq; g++) eq = gkw[(int64_t)g * gstride + j] == gkw[(int64_t)g * gstride + i];
-      if (eq) {
-        leader = false;
-        break;
-      }
-    }
-    lead[p] = leader ? 1u : 0u;
-  }
-}
-
-// CAS insertion of distinct keys (the leaders): ids base + leader rank.
-__global__ __launch_bounds__(kBlock) void k_gdict_insert(GDict d, int64_t nm, const uint64_t* sh, const uint32_t* sidx,
-                                                         const uint32_t* lead, const uint32_t* lrank,
-                                                         const uint64_t* gkw, const uint8_t* gkn, int64_t gstride,
-                                                         uint32_t base) {
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nm; p = nm) {
-    if (!lead[p]) continue;
-    const int64_t i = sidx[p];
-    const uint64_t h = sh[p];
-    const unsigned long long tg = (unsigned long long)(h | kTagBit);
-    uint64_t slot = h & (d.cap - 1);
-    while (atomicCAS(&d.tag[slot], 0ull, tg) != 0ull) slot = (slot + 1) & (d.cap - 1);
-    d.id[slot] = base + lrank[p];
-    d.kn[slot] = gkn[i];
-    for (int g = 0; g < d.nk; g++) d.kw[(uint64_t)g * d.cap + slot] = gkw[(int64_t)g * gstride + i];
-  }
-}
-
-// Table growth: re-insert every entry of `o` into the empty table `d`.
-__global__ __launch_bounds__(kBlock) void k_gdict_rehash(GDict o, GDict d) {
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < o.cap; s = o.cap) {
-    const unsigned long long tg = o.tag[s];
-    if (tg == 0ull) continue;
-    uint64_t slot = (uint64_t)tg & (d.cap - 1);
-    while (atomicCAS(&d.tag[slot], 0ull, tg) != 0ull) slot = (slot + 1) & (d.cap - 1);
-    d.id[slot] = o.id[s];
-    d.kn[slot] = o.kn[s];
-    for (int g = 0; g < d.nk; g++) d.kw[(uint64_t)g * d.cap + slot] = o.kw[(uint64_t)g * o.cap + s];
-  }
-}
+// ---------------------------------------------------------------- group dictionary (gdict.h)
 
 // Range guard of the segmented-scan mode: over the new items' double / float
 // operands of the scanned channels, flags[0] |= 1 for a non-finite value,
@@ -668,13 +508,6 @@ __global__ void k_head_list(const uint32_t* head, const uint32_t* hoff, int64_t 
     if (head[i]) hl[hoff[i]] = (uint32_t)i;
 }
 
-__device__ __forceinline__ int64_t java_d2l(double d) {
-  if (d != d) return 0;
-  if (d >= 9.2233720368547758e18) return INT64_MAX;
-  if (d <= -9.2233720368547758e18) return INT64_MIN;
-  return (int64_t)d;
-}
-
 struct FoldArgs {
   int nagg;
   int kind[kMaxAggs];
@@ -686,77 +519,6 @@ struct FoldArgs {
   int64_t* cnt;
   int64_t nkeys;
 };
-
-// One aggregator step on a CURRENT (add) or EXPIRED (remove) event: the
-// reference's incremental executors, Sum/Avg/CountAttributeAggregatorExecutor
-// (.../selector/attribute/aggregator/*.java: processAdd / processRemove).
-// ob/on: the aggregator's value after the step (on = null).  avg: ob is the
-// running sum and the count is the state c; the division value / count happens
-// at emission (k_emit) for the rows that are emitted, not in the sequential fold.
-__device__ __forceinline__ void agg_step(int kind, int type, bool add, uint64_t xb, bool xn, double& d, int64_t& l,
-                                         int64_t& c, uint64_t& ob, bool& on) {
-  ob = 0;
-  on = true;
-  switch (kind) {
-    case SHD_AGG_COUNT:
-      c += add ? 1 : -1;
-      ob = (uint64_t)c;
-      on = false;
-      break;
-    case SHD_AGG_SUM:
-      if (type == SHD_T_INT || type == SHD_T_LONG) {
-        if (xn) {
-          if (c != 0) { ob = (uint64_t)l; on = false; }
-          break;
-        }
-        int64_t x = type == SHD_T_INT ? (int64_t)v_i32(xb) : (int64_t)xb;
-        if (add) {
-          l = (int64_t)((uint64_t)l + (uint64_t)x);
-          c++;
-          ob = (uint64_t)l;
-          on = false;
-        } else {
-          l = java_d2l(__dsub_rn((double)l, (double)x));
-          c--;
-          if (c != 0) { ob = (uint64_t)l; on = false; }
-        }
-      } else {
-        if (xn) {
-          if (type == SHD_T_DOUBLE && c != 0) { ob = p_f64(d); on = false; }
-          break;
-        }
-        double x = type == SHD_T_FLOAT ? (double)v_f32(xb) : v_f64(xb);
-        if (add) {
-          d = __dadd_rn(d, x);
-          c++;
-          ob = p_f64(d);
-          on = false;
-        } else {
-          d = __dsub_rn(d, x);
-          c--;
-          if (c != 0) { ob = p_f64(d); on = false; }
-        }
-      }
-      break;
-    case SHD_AGG_AVG: {
-      if (xn) {
-        if (c != 0) { ob = p_f64(d); on = false; }
-        break;
-      }
-      double x;
-      switch (type) {
-        case SHD_T_INT: x = (double)v_i32(xb); break;
-        case SHD_T_LONG: x = (double)(int64_t)xb; break;
-        case SHD_T_FLOAT: x = (double)v_f32(xb); break;
-        default: x = v_f64(xb);
-      }
-      if (add) { c++; d = __dadd_rn(d, x); }
-      else { c--; d = __dsub_rn(d, x); }
-      if (c != 0) { ob = p_f64(d); on = false; }
-      break;
-    }
-  }
-}
 
 // One lane per group segment: the reference's sequential add/remove order
 // (short segments: many groups, few operations each).
@@ -2110,11 +1872,8 @@ struct SingleEngine : Engine {
   int ngk = 0;
   int gk_expr[kMaxGroupAttrs] = {}, gk_col[kMaxGroupAttrs] = {}, gk_type[kMaxGroupAttrs] = {};
   bool gdense = false;
-  DevBuf gd_tag, gd_id, gd_kw, gd_kn;
-  uint64_t gd_cap = 0;
-  int64_t gd_count = 0;
-  DevBuf g_kw, g_kn, g_h, g_miss, g_moff, g_midx, g_mh, g_midx_alt, g_mh_alt, g_lead, g_lrank, g_ctr;
-  PinnedBuf h_ctr;
+  GroupDict gd;                      // group ids of non-dense keys
+  DevBuf g_kw, g_kn, g_h;            // per new item: key words, null mask, hash
   std::vector<int> outs;
   std::vector<int> types;
   int nagg = 0;
@@ -2132,6 +1891,9 @@ struct SingleEngine : Engine {
   // segmented-scan mode (default for count / sum(double|float) / avg)
   bool seg_ok = false, seg_mode = false;
   bool seg_unsafe = false;   // a non-finite or wide-range operand was seen: exact fold from then on
+  // running operand statistics of every push since reset (k_operand_stats):
+  // the window can hold items of earlier pushes, so the span covers them all
+  uint32_t op_emax = 0, op_emin = 0xFFFFFFFFu;
   bool seg_pref = true;      // the mode asked for (option / default), restored by reset()
   DevBuf d_chmeta;
   PinnedBuf h_chmeta;
@@ -2167,95 +1929,18 @@ struct SingleEngine : Engine {
       SHD_HIP(hipMemsetAsync(g_lsum.p, 0, g_lsum.cap, stream));
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
-    gd_count = 0;
-    if (gd_cap) SHD_HIP(hipMemsetAsync(gd_tag.p, 0, gd_cap * 8, stream));
+    gd.reset(stream);
     seg_unsafe = false;
+    op_emax = 0;
+    op_emin = 0xFFFFFFFFu;
     seg_mode = seg_ok && seg_pref;
   }
 
-  GDict gdict() {
-    return GDict{gd_tag.as<unsigned long long>(), gd_id.as<uint32_t>(), gd_kw.as<uint64_t>(), gd_kn.as<uint8_t>(), gd_cap,
-                 ngk};
-  }
-
-  // Table with room for `need` entries at load <= 1/2 (rehash on growth).
-  void gdict_reserve(int64_t need) {
-    uint64_t cap = gd_cap ? gd_cap : 1024;
-    while ((int64_t)(cap / 2) < need) cap *= 2;
-    if (cap == gd_cap) return;
-    DevBuf t, i, k, n;
-    t.reserve(cap * 8);
-    i.reserve(cap * 4);
-    k.reserve((size_t)std::max(ngk, 1) * cap * 8);
-    n.reserve(cap);
-    SHD_HIP(hipMemsetAsync(t.p, 0, cap * 8, stream));
-    GDict nd{t.as<unsigned long long>(), i.as<uint32_t>(), k.as<uint64_t>(), n.as<uint8_t>(), cap, ngk};
-    if (gd_cap && gd_count) {
-      hipLaunchKernelGGL(k_gdict_rehash, dim3(grid_cover((int64_t)gd_cap)), dim3(kBlock), 0, stream, gdict(), nd);
-      SHD_CHECK_LAUNCH();
-    }
-    SHD_HIP(hipStreamSynchronize(stream));
-    std::swap(gd_tag.p, t.p); std::swap(gd_tag.cap, t.cap);
-    std::swap(gd_id.p, i.p); std::swap(gd_id.cap, i.cap);
-    std::swap(gd_kw.p, k.p); std::swap(gd_kw.cap, k.cap);
-    std::swap(gd_kn.p, n.p); std::swap(gd_kn.cap, n.cap);
-    gd_cap = cap;
-  }
-
-  // Dense group ids of the m new items [C, C + m) (dictionary mode): look up,
-  // insert the keys never seen before, look the misses up again.
+  // Dense group ids of the m new items [C, C + m) (dictionary mode).
   void gdict_assign(int64_t m, int64_t gstride) {
-    if (m <= 0) return;
-    hipStream_t s = stream;
-    gdict_reserve(1);
-    g_miss.reserve(m * 4);
-    g_moff.reserve(m * 4);
-    g_ctr.reserve(64);
-    h_ctr.reserve(64);
-    hipLaunchKernelGGL(k_gdict_lookup, dim3(grid_cover(m)), dim3(kBlock), 0, s, gdict(), m,
-                       (const uint64_t*)g_h.as<uint64_t>(), (const uint64_t*)g_kw.as<uint64_t>(),
-                       (const uint8_t*)g_kn.as<uint8_t>(), gstride, C, ikey[cur].as<uint64_t>(), g_miss.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    scan_exclusive_u32(g_miss.as<uint32_t>(), g_moff.as<uint32_t>(), m, g_ctr.as<uint32_t>(), d_scan, s);
-    SHD_HIP(hipMemcpyAsync(h_ctr.p, g_ctr.p, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    const int64_t nm = h_ctr.as<uint32_t>()[0];
-    if (nm == 0) return;
-    g_midx.reserve(nm * 4);
-    g_mh.reserve(nm * 8);
-    g_midx_alt.reserve(nm * 4);
-    g_mh_alt.reserve(nm * 8);
-    hipLaunchKernelGGL(k_gdict_compact, dim3(grid_cover(m)), dim3(kBlock), 0, s, (const uint32_t*)g_miss.as<uint32_t>(),
-                       (const uint32_t*)g_moff.as<uint32_t>(), m, (const uint64_t*)g_h.as<uint64_t>(),
-                       g_midx.as<uint32_t>(), g_mh.as<uint64_t>());
-    SHD_CHECK_LAUNCH();
-    bool in_alt = false;
-    radix_sort_pairs_u64(g_mh.as<uint64_t>(), g_midx.as<uint32_t>(), g_mh_alt.as<uint64_t>(), g_midx_alt.as<uint32_t>(),
-                         nm, 64, d_sort, s, in_alt);
-    const uint64_t* sh = in_alt ? g_mh_alt.as<uint64_t>() : g_mh.as<uint64_t>();
-    const uint32_t* sidx = in_alt ? g_midx_alt.as<uint32_t>() : g_midx.as<uint32_t>();
-    g_lead.reserve(nm * 4);
-    g_lrank.reserve(nm * 4);
-    hipLaunchKernelGGL(k_gdict_leaders, dim3(grid_cover(nm)), dim3(kBlock), 0, s, nm, sh, sidx,
-                       (const uint64_t*)g_kw.as<uint64_t>(), (const uint8_t*)g_kn.as<uint8_t>(), gstride, ngk,
-                       g_lead.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    scan_exclusive_u32(g_lead.as<uint32_t>(), g_lrank.as<uint32_t>(), nm, g_ctr.as<uint32_t>() + 1, d_scan, s);
-    SHD_HIP(hipMemcpyAsync(h_ctr.as<uint32_t>() + 1, g_ctr.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    const int64_t nu = h_ctr.as<uint32_t>()[1];
-    if (gd_count + nu >= (int64_t)0xFFFFFFF0ll) throw Error(SHD_E_CAPACITY, "more than 2^32 group-by keys");
-    gdict_reserve(gd_count + nu);
-    hipLaunchKernelGGL(k_gdict_insert, dim3(grid_cover(nm)), dim3(kBlock), 0, s, gdict(), nm, sh, sidx,
-                       (const uint32_t*)g_lead.as<uint32_t>(), (const uint32_t*)g_lrank.as<uint32_t>(),
-                       (const uint64_t*)g_kw.as<uint64_t>(), (const uint8_t*)g_kn.as<uint8_t>(), gstride,
-                       (uint32_t)gd_count);
-    SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_gdict_relookup, dim3(grid_cover(nm)), dim3(kBlock), 0, s, gdict(), nm, sidx,
-                       (const uint64_t*)g_h.as<uint64_t>(), (const uint64_t*)g_kw.as<uint64_t>(),
-                       (const uint8_t*)g_kn.as<uint8_t>(), gstride, C, ikey[cur].as<uint64_t>());
-    SHD_CHECK_LAUNCH();
-    gd_count += nu;
+    gd.nk = std::max(ngk, 1);
+    gd.assign(m, g_h.as<uint64_t>(), g_kw.as<uint64_t>(), g_kn.as<uint8_t>(), gstride, ikey[cur].as<uint64_t>(), C,
+              stream);
   }
 
   // window contents (items [0, C) of slot `cur`) + dense per-group aggregates
@@ -2278,15 +1963,10 @@ struct SingleEngine : Engine {
       w.dev(g_cnt.p, gb);
     }
     w.put<int32_t>(seg_unsafe ? 1 : 0);
+    w.put<uint32_t>(op_emax);
+    w.put<uint32_t>(op_emin);
     // group dictionary (dictionary-mode group keys)
-    w.put<uint64_t>(gd_cap);
-    w.put<int64_t>(gd_count);
-    if (gd_cap) {
-      w.dev(gd_tag.p, gd_cap * 8);
-      w.dev(gd_id.p, gd_cap * 4);
-      w.dev(gd_kw.p, (size_t)std::max(ngk, 1) * gd_cap * 8);
-      w.dev(gd_kn.p, gd_cap);
-    }
+    gd.save(w);
   }
   void load_state(SnapR& r) override {
     const int64_t c0 = r.get<int64_t>();
@@ -2318,24 +1998,11 @@ struct SingleEngine : Engine {
     }
     if (nk > 0 || !g_nkeys) g_nkeys = nk;
     seg_unsafe = r.get<int32_t>() != 0;
+    op_emax = r.get<uint32_t>();
+    op_emin = r.get<uint32_t>();
     seg_mode = seg_ok && seg_pref && !seg_unsafe;
-    const uint64_t dcap = r.get<uint64_t>();
-    const int64_t dcount = r.get<int64_t>();
-    if (dcap & (dcap - 1)) throw Error(SHD_E_ARG, "snapshot of a different plan");
-    gd_count = 0;
-    if (gd_cap) SHD_HIP(hipMemsetAsync(gd_tag.p, 0, gd_cap * 8, stream));
-    if (dcap) {
-      gd_tag.reserve(dcap * 8);
-      gd_id.reserve(dcap * 4);
-      gd_kw.reserve((size_t)std::max(ngk, 1) * dcap * 8);
-      gd_kn.reserve(dcap);
-      r.dev_into(gd_tag.p, dcap * 8);
-      r.dev_into(gd_id.p, dcap * 4);
-      r.dev_into(gd_kw.p, (size_t)std::max(ngk, 1) * dcap * 8);
-      r.dev_into(gd_kn.p, dcap);
-      gd_cap = dcap;
-      gd_count = dcount;
-    }
+    gd.nk = std::max(ngk, 1);
+    gd.load(r, stream);
     counters.carry = C;
   }
 
@@ -2937,8 +2604,12 @@ struct SingleEngine : Engine {
       // over a wide magnitude range its rounding history shows in the result
       // (1e20 + 1 - 1e20 = 0): from the first such push on, this query keeps the
       // bit-exact sequential fold (the group tables carry over).
+      // the span is over every operand since reset (window items of earlier
+      // pushes included), not just this push's
       const uint32_t* fl = h_tot.as<uint32_t>() + 10;
-      const bool wide = fl[2] != 0xFFFFFFFFu && fl[1] > fl[2] + kSegMaxExpSpan;
+      op_emax = std::max(op_emax, fl[1]);
+      op_emin = std::min(op_emin, fl[2]);
+      const bool wide = op_emin != 0xFFFFFFFFu && op_emax > op_emin + kSegMaxExpSpan;
       if (fl[0] || wide) {
         seg_mode = false;
         seg_unsafe = true;
@@ -3086,14 +2757,17 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
     }
   }
   if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
-  if (p.having >= 0) { why = "having"; return nullptr; }
   for (auto& o : p.outputs) e->outs.push_back(o.second);
   if (e->outs.size() > (size_t)kMaxCols) { why = "too many outputs"; return nullptr; }
   e->nagg = (int)p.aggs.size();
   if (e->nagg > kMaxAggs) { why = "too many aggregators"; return nullptr; }
   e->partitioned = !p.part_keys.empty();
   bool needs_agg = e->nagg > 0 || !p.group_by.empty();
-  if (p.expired_on && (needs_agg || e->wkind != 0)) { why = "expired-event output from a window"; return nullptr; }
+  // EXPIRED output, `having`, no CURRENT output, aggregation inside a
+  // partition: the keyed exact window engine (engine_window.hip)
+  if ((p.expired_on && (needs_agg || e->wkind != 0)) || p.having >= 0 || !p.current_on ||
+      (!p.part_keys.empty() && (needs_agg || (e->wkind != 0 && p.expired_on))))
+    return make_window_x_engine(p, why);
   if (e->wkind != 0 && e->wparam <= 0 && e->wkind == SHD_W_LENGTH) { why = "length(0) window"; return nullptr; }
   e->agg_mode = needs_agg;
   // segmented-scan aggregation: count(), sum(double|float), avg(numeric); one
@@ -3126,7 +2800,6 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
   e->seg_pref = !getenv("SHD_EXACT_AGGREGATES");
   e->seg_mode = seg && e->seg_pref;
   if (e->partitioned) {
-    if (e->agg_mode) { why = "partitioned window/aggregation"; return nullptr; }
     e->key_expr = p.part_keys[0].second;
     e->key_col = plain_load_attr(p, e->key_expr);
     e->key_type = expr_result_type(p, e->key_expr, {});

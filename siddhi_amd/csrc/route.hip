@@ -24,6 +24,8 @@
 // Wire format (8-byte words per row): the 8-byte columns in column order, then
 // the 4-byte columns two per word, the last 4-byte slot holding the event's
 // sequence offset seq - seq_lo (< 2^32).
+#include <algorithm>
+
 #include "common.h"
 
 namespace shd {
@@ -299,23 +301,24 @@ RouteLayout layout(int ncols, const int* widths) {
   return L;
 }
 
-DevBuf& tile_counts(int device) {
-  static DevBuf bufs[64];
-  if (device < 0 || device >= 64) throw Error(SHD_E_ARG, "route: device id out of range");
-  return bufs[device];
-}
-
 }  // namespace
+
+// per-tile owner counts of the bucket pass (caller-owned, so concurrent
+// buckets on different streams never share scratch)
+int64_t route_bucket_scratch(int64_t n, int world) {
+  if (world < 1 || world > kRouteMaxWorld || n < 0) throw Error(SHD_E_ARG, "route: world 1..64, n >= 0");
+  return std::max<int64_t>(ceil_div(n, kRouteTile) * world, 1) * (int64_t)sizeof(uint32_t);
+}
 
 int route_words(int ncols, const int* widths) { return layout(ncols, widths).nwords; }
 
-void route_bucket(int device, hipStream_t s, int64_t n, int world, const void* key, int key_width, int ncols,
+void route_bucket(hipStream_t s, int64_t n, int world, const void* key, int key_width, int ncols,
                   const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
-                  int64_t* counts) {
+                  int64_t* counts, uint32_t* scratch) {
   if (world < 1 || world > kRouteMaxWorld) throw Error(SHD_E_ARG, "route: world must be 1..64");
   if (key_width != 4 && key_width != 8) throw Error(SHD_E_ARG, "route: key width must be 4 or 8 bytes");
   if (n < 0 || n >= (int64_t(1) << 32)) throw Error(SHD_E_ARG, "route: batch of 0 .. 2^32-1 rows");
-  if (!counts || (n > 0 && (!key || !seq || !send))) throw Error(SHD_E_ARG, "route: null buffer");
+  if (!counts || (n > 0 && (!key || !seq || !send || !scratch))) throw Error(SHD_E_ARG, "route: null buffer");
   RouteLayout L = layout(ncols, widths);
   for (int c = 0; c < ncols; c++) {
     if (n > 0 && !cols[c]) throw Error(SHD_E_ARG, "route: null column");
@@ -326,9 +329,7 @@ void route_bucket(int device, hipStream_t s, int64_t n, int world, const void* k
     return;
   }
   const int64_t ntiles = ceil_div(n, kRouteTile);
-  DevBuf& tc = tile_counts(device);
-  tc.reserve((size_t)(ntiles * world) * sizeof(uint32_t));
-  uint32_t* d_tc = tc.as<uint32_t>();
+  uint32_t* d_tc = scratch;   // [world][ntiles] (route_bucket_scratch bytes)
   hipLaunchKernelGGL(k_route_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, s, key, key_width == 8 ? 1 : 0, n, world,
                      ntiles, d_tc);
   SHD_CHECK_LAUNCH();

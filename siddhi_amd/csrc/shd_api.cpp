@@ -605,9 +605,10 @@ void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, c
 
 namespace shd {
 int route_words(int ncols, const int* widths);
-void route_bucket(int device, hipStream_t s, int64_t n, int world, const void* key, int key_width, int ncols,
+int64_t route_bucket_scratch(int64_t n, int world);
+void route_bucket(hipStream_t s, int64_t n, int world, const void* key, int key_width, int ncols,
                   const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
-                  int64_t* counts);
+                  int64_t* counts, uint32_t* scratch);
 void route_merge(hipStream_t s, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m, int64_t seq_lo,
                  int64_t block, int64_t nblocks, int ncols, void* const* out_cols, const int* widths,
                  int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err);
@@ -658,14 +659,22 @@ int shd_route_words(int ncols, const int* widths, int* words) {
   });
 }
 
+int shd_route_bucket_scratch(int64_t n, int world, size_t* bytes) {
+  return guarded([&]() -> int {
+    if (!bytes) return fail(SHD_E_ARG, "null pointer");
+    *bytes = (size_t)route_bucket_scratch(n, world);
+    return SHD_OK;
+  });
+}
+
 int shd_route_bucket(shd_ctx* ctx, void* stream, int64_t n, int world, const void* key, int key_width, int ncols,
                      const void* const* cols, const int* widths, const int64_t* seq, int64_t seq_lo, uint64_t* send,
-                     int64_t* counts) {
+                     int64_t* counts, void* scratch) {
   return guarded([&]() -> int {
     if (!ctx || (ncols > 0 && (!cols || !widths))) return fail(SHD_E_ARG, "null pointer");
     SHD_HIP(hipSetDevice(ctx->device));
-    route_bucket(ctx->device, (hipStream_t)stream, n, world, key, key_width, ncols, cols, widths, seq, seq_lo, send,
-                 counts);
+    route_bucket((hipStream_t)stream, n, world, key, key_width, ncols, cols, widths, seq, seq_lo, send, counts,
+                 (uint32_t*)scratch);
     return SHD_OK;
   });
 }

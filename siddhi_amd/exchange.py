@@ -102,6 +102,8 @@ def route(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world:
     if world == 1:
         order = _seq_order(seq)
         return [c[order] for c in cols], seq[order], {"sent": 0, "received": 0}
+    if world > 256:
+        raise ValueError("route: world %d > 256 (owners are bucketed with one 8-bit pass)" % world)
     owner = owner_of(key, world)
     # stable bucket order by owner: one 8-bit radix pass (world <= 256)
     _, order = torch.sort(owner.to(torch.uint8), stable=True)
@@ -207,9 +209,13 @@ def bucket(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world
     ptrs = (ctypes.c_void_p * max(len(cols), 1))(*[c.data_ptr() for c in cols])
     if key.dtype not in (torch.int32, torch.int64) or not key.is_contiguous() or not seq.is_contiguous():
         raise ValueError("route_device: contiguous int32/int64 key and int64 seq")
+    sb = ctypes.c_size_t()
+    he._check(lib.shd_route_bucket_scratch(n, world, ctypes.byref(sb)))
+    scratch = torch.empty((sb.value + 7) // 8, dtype=torch.int64, device=seq.device)
     stream = torch.cuda.current_stream(seq.device).cuda_stream
     he._check(lib.shd_route_bucket(ctx, stream, n, world, key.data_ptr(), key.element_size(), len(cols), ptrs, wa,
-                                   seq.data_ptr(), int(seq_lo), send.data_ptr(), counts.data_ptr()))
+                                   seq.data_ptr(), int(seq_lo), send.data_ptr(), counts.data_ptr(),
+                                   scratch.data_ptr()))
     return send[:n * words.value], counts, words.value
 
 

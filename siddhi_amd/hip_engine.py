@@ -27,7 +27,7 @@ ENGINE_NAMES = {1: "pattern-forward-scan", 2: "window-aggregate", 3: "filter-pro
 EXPORTED = ["shd_device_count", "shd_ctx_create", "shd_ctx_destroy", "shd_plan_load", "shd_plan_free",
             "shd_plan_engine", "shd_set_time", "shd_push", "shd_flush", "shd_poll", "shd_discard_output",
             "shd_reset", "shd_get_counters", "shd_query_stream", "shd_stage_times", "shd_snapshot", "shd_restore",
-            "shd_set_option", "shd_route_words", "shd_route_bucket", "shd_route_merge", "shd_last_error"]
+            "shd_set_option", "shd_route_words", "shd_route_bucket_scratch", "shd_route_bucket", "shd_route_merge", "shd_last_error"]
 
 
 class SiddhiHipError(RuntimeError):
@@ -90,7 +90,8 @@ def load_library(path: str = LIB_PATH):
         lib.shd_snapshot.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
         lib.shd_restore.argtypes = [P, P, ctypes.c_size_t]
         lib.shd_route_words.argtypes = [I, P, ctypes.POINTER(I)]
-        lib.shd_route_bucket.argtypes = [P, P, I64, I, P, I, I, P, P, P, I64, P, P]
+        lib.shd_route_bucket_scratch.argtypes = [I64, I, ctypes.POINTER(ctypes.c_size_t)]
+        lib.shd_route_bucket.argtypes = [P, P, I64, I, P, I, I, P, P, P, I64, P, P, P]
         lib.shd_route_merge.argtypes = [P, P, I, P, P, I64, I64, I64, I64, I, P, P, P, P, P, P]
         lib.shd_last_error.restype = ctypes.c_char_p
         for f in EXPORTED:

@@ -33,6 +33,7 @@ FILES = [
     "query/sequence/SequenceTestCase.java",
     "query/partition/PatternPartitionTestCase.java",
     "query/partition/SequencePartitionTestCase.java",
+    "query/partition/WindowPartitionTestCase.java",
     "query/window/LengthWindowTestCase.java",
     "query/window/TimeWindowTestCase.java",
     "query/GroupByTestCase.java",
@@ -481,6 +482,22 @@ def extract(name, body, line, fname):
                 expected.append({"n": "all" if ems[0][2] == "" else "first_of_each", "data": parse_values(ems[0][0])})
             except ValueError as e:
                 return None, str(e)
+    # StreamCallback bodies that count events and check the n-th one:
+    # `if (xCount == N) { assertEquals(V, event.getData()[K]); }` (a StreamCallback
+    # sees every event as CURRENT: InsertIntoStreamCallback.send :50-57)
+    nth = []
+    if cb_kind == "StreamCallback" and not tu:
+        if re.search(r"getData\(\)\[\d+\]\.equals\(", cbody):
+            return None, "data-dependent callback counters"
+        for cm_ in re.finditer(r"if \((\w+) == (\d+)\) \{\s*(?:AssertJUnit\.)?assertEquals\(([^,]+?),\s*"
+                               r"event\.getData\(\)\[(\d+)\]\);", cbody):
+            if not re.search(re.escape(cm_.group(1)) + r"\+\+", cbody):
+                continue
+            try:
+                nth.append({"n": int(cm_.group(2)), "col": int(cm_.group(4)),
+                            "value": parse_values(cm_.group(3))[0]})
+            except ValueError as e:
+                return None, str(e)
     count = None
     if tu:
         # the first count assertion after the callback (later ones follow more sends)
@@ -518,7 +535,10 @@ def extract(name, body, line, fname):
         if rm:
             removes = int(rm.group(1))
             break
-    if count is None and not expected and not cells:
+    if cb_kind == "StreamCallback" and count is None and removes is not None and "inEventCount++" not in cbody:
+        # a StreamCallback counter named removeEventCount counts every event it sees
+        count, removes = removes, None
+    if count is None and not expected and not cells and not nth:
         return None, "no expectations"
     return {
         "name": "%s.%s" % (os.path.basename(fname)[:-5], name),
@@ -530,6 +550,7 @@ def extract(name, body, line, fname):
         "expected_count": count,
         "expected_remove_count": removes,
         "expected_cells": cells,
+        "expected_nth": nth,
         "playback": "@app:playback" in app.replace(" ", "").lower() or "@app:playback" in app.lower(),
         "start_time": None if playback else T0,
     }, None

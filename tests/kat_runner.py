@@ -139,6 +139,16 @@ def check_case(case, col, rtol=0.0):
             d = ev.getData()
             if len(d) != len(exp["data"]) or not all(values_equal(e, a, rtol) for e, a in zip(exp["data"], d)):
                 errs.append("event %s: %r != expected %r" % (n, d, [_py(v)[1] for v in exp["data"]]))
+    for cell in case.get("expected_nth", []):
+        # the n-th event a counting StreamCallback sees, one column checked
+        if cell["n"] - 1 >= len(col.in_events):
+            errs.append("missing event #%d" % cell["n"])
+            continue
+        d = col.in_events[cell["n"] - 1].getData()
+        if cell["col"] >= len(d) or not values_equal(cell["value"], d[cell["col"]], rtol):
+            errs.append("event #%d col %d: %r != expected %r" % (cell["n"], cell["col"], d[cell["col"]] if
+                                                                  cell["col"] < len(d) else None,
+                                                                  _py(cell["value"])[1]))
     for cell in case.get("expected_cells", []):
         targets = [c[0][0] for c in col.chunks if c[0]] if cell["which"] == "first_of_each" else col.in_events
         for ev in targets:

@@ -160,6 +160,23 @@ def test_range_guard_falls_back_to_exact_fold(hip_available, shape):
         assert_rows_agg(canon(dev), canon(ora), qp, exact=True)
 
 
+def test_range_guard_spans_pushes(hip_available):
+    """one length window holds items of several pushes, each push
+    narrow in magnitude (1e20 in push 1, ~1 in push 2).  When the 1e20 items
+    expire the reference's running sum has lost the small operands
+    (1e20 + 1 - 1e20 = 0); the guard must see the span over all pushes, not
+    per push, and switch to the exact fold: rows within 1e-9 of the oracle
+    (without the cross-push span the scan gives the exact small sums where
+    the reference keeps its rounding residue: relative error ~1)."""
+    qp, _ = compile_single_query("@app:playback " + SCHEMA +
+                                 "from S#window.length(4000) select k, sum(d) as s, count() as c insert into O;")
+    batches = make_batches(91, 3, 3_000, 1, nulls=False)
+    batches[0][1].cols[4][:] = 1e20 + np.arange(3_000) * 1e6
+    ora = run_oracle(qp, batches)
+    dev, _, _ = run_device(qp, batches)
+    assert_rows_agg(dev, ora, qp, exact=False)
+
+
 CHUNK_APPS = [a for a in APPS if a[0] in ("sparse-groups", "length-1", "time-short", "typed-channels",
                                            "one-group-groupby")] + [
     ("w2-length-shape", "from S[d > 20.0]#window.length(700) select k, avg(d) as a, sum(d) as s, count() as c "
