@@ -2033,6 +2033,9 @@ struct Engine {
         r.nul.push_back(v.null);
       }
       bool on = (e->type == CURRENT && p.current_on) || (e->type == EXPIRED && p.expired_on);
+      // havingConditionExecutor (QuerySelector.java:176-178,292-293,338-339): over
+      // the event with its aggregator values, before the type check
+      if (on && p.having >= 0 && !eval_bool(p, p.having, cx)) on = false;
       if (!on) continue;
       if (group) {
         std::vector<std::pair<uint64_t, uint8_t>> gk = group_key(cx);

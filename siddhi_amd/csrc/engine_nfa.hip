@@ -148,8 +148,9 @@ struct NfaRunArgs {
   int64_t chunk_len;
   int64_t warm;
   int64_t c_exact;
-  uint64_t* hash_w;   // per lane: state hash after the warm-up (= before the first owned event)
-  uint64_t* hash_e;   // per lane: state hash after the last owned event
+  uint64_t* hash_w;   // per lane: state hashes after the warm-up (= before the first owned event), 2 words
+  uint64_t* hash_e;   // per lane: state hashes after the last owned event, 2 words
+  int hash1_zero;     // debug hook (SHD_NFA_HASH1_ZERO): the first hash always collides
   const int32_t* call_of;
   const int64_t* call_now;
   const uint8_t* call_changed;
@@ -258,12 +259,20 @@ struct Lane {
   // canonical ids carry the hash call's stamp in the high half (no clearing)
   __device__ uint32_t& cse(int i) { return ks.at<uint32_t>(Y.o_cse, i); }
   __device__ uint32_t& cev(int i) { return ks.at<uint32_t>(Y.o_cev, i); }
-  __device__ uint64_t state_hash() {
+  // Two independent 64-bit hashes over the same canonical walk (an FNV-style
+  // xor-multiply and a splitmix-style add-multiply-xorshift with other
+  // constants): a lane is accepted only when both agree, so a wrong warm-up
+  // state slips through only if it collides in both.
+  __device__ uint64_t state_hash(uint64_t& h2) {
     uint64_t h = 1469598103934665603ull;
+    uint64_t g = 0x6A09E667F3BCC909ull;
     auto mix = [&](uint64_t x) {
       h ^= x;
       h *= 1099511628211ull;
       h ^= h >> 29;
+      g += x + 0x9E3779B97F4A7C15ull;
+      g *= 0xBF58476D1CE4E5B9ull;
+      g ^= g >> 31;
     };
     uint32_t stamp = (misc(MISC_HSTAMP) + 1) & 0xFFFFu;
     if (stamp == 0) {   // wrapped: clear once
@@ -319,6 +328,7 @@ struct Lane {
     }
     mix(evret);
     mix(misc(MISC_SEEDED) != 0);
+    h2 = g;
     return h;
   }
 
@@ -1487,7 +1497,12 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
       if (row == ob) {
         L.quiet = false;
         NFA_PROF_T0(th);
-        if (!exact) a.hash_w[lane_id] = L.state_hash();
+        if (!exact) {
+          uint64_t h2;
+          const uint64_t h1 = L.state_hash(h2);
+          a.hash_w[2 * lane_id] = a.hash1_zero ? 0ull : h1;
+          a.hash_w[2 * lane_id + 1] = h2;
+        }
         NFA_PROF_ADDL(L, 5, th);
       } else if (row == wb) {
         L.quiet = true;
@@ -1508,7 +1523,12 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
       if (!L.ovf) L.fire_upto(a.ncalls - 1);
     }
     L.misc(MISC_EVRET) = L.evret;
-    a.hash_e[lane_id] = L.state_hash();
+    {
+      uint64_t h2;
+      const uint64_t h1 = L.state_hash(h2);
+      a.hash_e[2 * lane_id] = a.hash1_zero ? 0ull : h1;
+      a.hash_e[2 * lane_id + 1] = h2;
+    }
 #ifdef SHD_NFA_PROF
     for (int k = 0; k < kProfN; k++) atomicAdd(&a.ctl->prof[k], (unsigned long long)L.prof[k]);
 #endif
@@ -1564,7 +1584,62 @@ __global__ __launch_bounds__(kLaneBlock) void k_nfa_run(const NfaProg* __restric
 __global__ void k_win_check(const uint64_t* hw, const uint64_t* he, int64_t c0, int64_t nl, unsigned int* bad) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + (c0 > 1 ? c0 : 1); c < nl;
        c += (int64_t)gridDim.x * blockDim.x)
-    if (hw[c] != he[c - 1]) atomicAdd(bad, 1u);
+    if (hw[2 * c] != he[2 * (c - 1)] || hw[2 * c + 1] != he[2 * (c - 1) + 1]) atomicAdd(bad, 1u);
+}
+
+// ---------------------------------------------------------------- growth
+// One field of a layout change (grow on capacity overflow): elements (r, c) of
+// the old field, r < rows, c < cols, move to the same (r, c) of the new field
+// (element r * cols_old + c -> r * cols_new + c, lane-interleaved).  kind 1: a
+// free bitmap (the new handles [lo, hi) start free), 2: a mark bitmap (zero),
+// 3: the misc words (free-handle counters grow with their pools).
+struct RelayField {
+  int64_t off_old, off_new, rows, cols, cols_old, cols_new, words_old, lo, hi;
+  int sz, kind;
+};
+struct RelayArgs {
+  int nfield;
+  RelayField f[NfaLayout::kMaxFields];
+  int64_t blk_old, blk_new, nblocks;
+  int W;
+  int32_t dSE, dEV, dREC;
+};
+
+__global__ __launch_bounds__(kBlock) void k_nfa_relayout(const RelayArgs* __restrict__ ap, const char* __restrict__ src,
+                                                         char* __restrict__ dst) {
+  const RelayArgs& a = *ap;
+  const int64_t total = a.nblocks * a.W;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t = total) {
+    const int64_t b = t / a.W, k = t % a.W;
+    const char* sb = src + b * a.blk_old;
+    char* db = dst + b * a.blk_new;
+    for (int fi = 0; fi < a.nfield; fi++) {
+      const RelayField& f = a.f[fi];
+      if (f.kind == 2) continue;   // mark bitmaps: zero (the destination is zeroed)
+      if (f.kind == 1) {           // free bitmap: old words, then the new handles free
+        for (int64_t w = 0; w < f.cols_new; w++) {
+          uint64_t v = w < f.words_old ? *(const uint64_t*)(sb + f.off_old + (w * a.W + k) * 8) : 0ull;
+          const int64_t w0 = w * 64;
+          for (int bit = 0; bit < 64; bit++)
+            if (w0 + bit >= f.lo && w0 + bit < f.hi) v |= 1ull << bit;
+          *(uint64_t*)(db + f.off_new + (w * a.W + k) * 8) = v;
+        }
+        continue;
+      }
+      for (int64_t r = 0; r < f.rows; r++)
+        for (int64_t c = 0; c < f.cols; c++) {
+          const char* sp = sb + f.off_old + ((r * f.cols_old + c) * a.W + k) * f.sz;
+          char* dp = db + f.off_new + ((r * f.cols_new + c) * a.W + k) * f.sz;
+          for (int x = 0; x < f.sz; x++) dp[x] = sp[x];
+        }
+      if (f.kind == 3) {
+        uint32_t* m = (uint32_t*)(db + f.off_new);
+        m[MISC_FREE_SE * a.W + k] += (uint32_t)a.dSE;
+        m[MISC_FREE_EV * a.W + k] += (uint32_t)a.dEV;
+        m[MISC_FREE_REC * a.W + k] += (uint32_t)a.dREC;
+      }
+    }
+  }
 }
 
 // one key's state (every field of slot src) into slots [dst0, dst0 + ndst):
@@ -2062,6 +2137,16 @@ int env_int(const char* name, int def) {
 
 }  // namespace
 
+void layout_offsets(NfaLayout& Y);
+
+// Thrown by a push whose keys outgrew the per-key capacities (flags: OV_*):
+// the engine grows its layout from the pre-push state and runs the push again.
+struct NfaOverflow : Error {
+  unsigned flags;
+  int64_t rows;
+  NfaOverflow(unsigned f, int64_t r, const std::string& m) : Error(SHD_E_CAPACITY, m), flags(f), rows(r) {}
+};
+
 struct NfaEngine : Engine {
   NfaProg prog{};
   NfaLayout lay{};
@@ -2124,7 +2209,27 @@ struct NfaEngine : Engine {
   }
 
   // key blocks (all per-key NFA state) + key directory, byte for byte
+  void save_caps(SnapW& w) const {
+    w.put<int32_t>(lay.L); w.put<int32_t>(lay.SC); w.put<int32_t>(lay.EC); w.put<int32_t>(lay.RC);
+    w.put<int32_t>(lay.QC); w.put<int32_t>(lay.RETC); w.put<int32_t>(lay.WK);
+  }
+  // a snapshot taken after growth carries its (larger) capacities: adopt them
+  void load_caps(SnapR& r) {
+    NfaLayout ny = lay;
+    ny.L = r.get<int32_t>(); ny.SC = r.get<int32_t>(); ny.EC = r.get<int32_t>(); ny.RC = r.get<int32_t>();
+    ny.QC = r.get<int32_t>(); ny.RETC = r.get<int32_t>(); ny.WK = r.get<int32_t>();
+    if (ny.L < 1 || ny.L >= 65000 || ny.SC < 1 || ny.SC > 32768 || ny.EC < 1 || ny.EC > 65000 || ny.RC < 1 ||
+        ny.RC > 65000 || ny.QC < 1 || ny.QC >= 65000 || ny.RETC < 1 || ny.RETC > 65000 || ny.WK < 1)
+      throw Error(SHD_E_ARG, "snapshot of a different plan");
+    layout_offsets(ny);
+    if (ny.blk != lay.blk) {
+      state.release();
+      slot_cap = 0;
+    }
+    lay = ny;
+  }
   void save_state(SnapW& w) override {
+    save_caps(w);
     if (windowed) {   // the carried state: slot 0's block (+ the learned warm-up)
       w.put<int64_t>(win_warm);
       w.put<int64_t>(slot_cap > 0 ? 1 : 0);
@@ -2142,6 +2247,7 @@ struct NfaEngine : Engine {
     w.dev(ht_slot.p, (size_t)ht_cap * 4);
   }
   void load_state(SnapR& r) override {
+    load_caps(r);
     if (windowed) {
       const int64_t ww = r.get<int64_t>();
       if (ww < 0 || ww > ((int64_t)1 << 40)) throw Error(SHD_E_ARG, "snapshot of a different plan");
@@ -2398,7 +2504,162 @@ struct NfaEngine : Engine {
   }
 
   // One push (b != nullptr) or one time change (b == nullptr, time t).
+  // SHD_E_CAPACITY never reaches the caller while the handle space (16-bit
+  // handles) allows growth: a push that overflows a key's lists / pools is
+  // rerun from the pre-push state with the overflowed capacities doubled
+  // (the key blocks re-laid out on the device, k_nfa_relayout).
+  DevBuf backup;
+  int64_t backup_blocks = 0, backup_nslots = 0;
+  int64_t grows = 0;
   void run_push(const Staged* b, int64_t t_only) {
+    // the pre-push key blocks (window lanes: the carried state, slot 0's block)
+    backup_nslots = nslots;
+    const int64_t used = windowed ? std::min<int64_t>(slot_cap, 1) : nslots;
+    backup_blocks = used > 0 ? ceil_div(used, lay.W) : 0;
+    if (backup_blocks > 0) {
+      backup.reserve((size_t)backup_blocks * lay.blk);
+      SHD_HIP(hipMemcpyAsync(backup.p, state.p, (size_t)backup_blocks * lay.blk, hipMemcpyDeviceToDevice, stream));
+    }
+    for (;;) {
+      try {
+        run_push_once(b, t_only);
+        return;
+      } catch (NfaOverflow& o) {
+        grow(o.flags, o.rows, o.what());
+      }
+    }
+  }
+
+  void grow(unsigned ovf, int64_t rows, const char* msg) {
+    args_begin();   // the failed attempt's argument blocks are no longer read
+    NfaLayout ny = lay;
+    bool changed = false;
+    auto dbl = [&](int& v, int mx) {
+      const int nv = std::min(2 * v, mx);
+      if (nv > v) {
+        v = nv;
+        changed = true;
+      }
+    };
+    if (ovf & OV_LIST) {
+      dbl(ny.L, 64999);
+      ny.RETC = std::max(ny.RETC, std::min(ny.L * std::max(ny.npre, 1), 65000));
+    }
+    if (ovf & OV_SE) dbl(ny.SC, 32768);
+    if (ovf & OV_EV) dbl(ny.EC, 65000);
+    if (ovf & OV_REC) dbl(ny.RC, 65000);
+    if (ovf & OV_SCHED) dbl(ny.QC, 64999);
+    if (ovf & OV_RET) dbl(ny.RETC, 65000);
+    if (ovf & OV_WORK) dbl(ny.WK, 1 << 20);
+    if (rows > R) {
+      ensure_staging(2 * rows);
+      changed = true;
+    }
+    if (!changed) throw Error(SHD_E_CAPACITY, std::string(msg) + " (at the largest per-key capacities)");
+    grows++;
+    if (ny.L != lay.L || ny.SC != lay.SC || ny.EC != lay.EC || ny.RC != lay.RC || ny.QC != lay.QC ||
+        ny.RETC != lay.RETC || ny.WK != lay.WK) {
+      layout_offsets(ny);
+      relayout(ny);
+    } else if (backup_blocks > 0) {   // same layout (staging grew): back to the pre-push blocks
+      SHD_HIP(hipMemcpyAsync(state.p, backup.p, (size_t)backup_blocks * lay.blk, hipMemcpyDeviceToDevice, stream));
+    }
+    // keys first seen by the failed attempt are forgotten: the directory is
+    // rebuilt from the pre-push slots, the retry inserts them again
+    if (!windowed && partitioned && (nslots != backup_nslots || backup_blocks > 0)) {
+      nslots = backup_nslots;
+      if (ht_cap > 0) {
+        SHD_HIP(hipMemsetAsync(ht_state.p, 0, (size_t)ht_cap * 4, stream));
+        epoch++;
+        if (nslots > 0) {
+          hipLaunchKernelGGL(k_slot_rebuild, dim3(grid_for(nslots)), dim3(kBlock), 0, stream, (const char*)state.p,
+                             lay.blk, lay.W, lay.o_key, nslots, ht_state.as<uint32_t>(), ht_key.as<uint64_t>(),
+                             ht_slot.as<uint32_t>(), (uint64_t)(ht_cap - 1), epoch);
+          SHD_CHECK_LAUNCH();
+        }
+      }
+      // blocks of the forgotten slots start unseeded again
+      const int64_t keep_b = ceil_div(nslots, lay.W);
+      const size_t keep = (size_t)keep_b * lay.blk, all = (size_t)(slot_cap / lay.W) * lay.blk;
+      if (all > keep && backup_blocks == keep_b) {
+        // the pre-push blocks hold nslots slots; the partial block's later slots were unseeded before the push
+        SHD_HIP(hipMemsetAsync(state.as<char>() + keep, 0, all - keep, stream));
+      }
+    }
+    SHD_HIP(hipStreamSynchronize(stream));
+  }
+
+  // the pre-push blocks (backup) re-laid out for `ny` into a fresh state
+  // array; slots beyond them start zero (unseeded)
+  void relayout(const NfaLayout& ny) {
+    const NfaLayout& o = lay;
+    RelayArgs ra{};
+    auto add = [&](int64_t oo, int64_t on, int64_t rows, int64_t cols, int64_t cold, int64_t cnew, int sz, int kind,
+                   int64_t wold = 0, int64_t lo = 0, int64_t hi = 0) {
+      RelayField& f = ra.f[ra.nfield++];
+      f.off_old = oo; f.off_new = on; f.rows = rows; f.cols = cols; f.cols_old = cold; f.cols_new = cnew;
+      f.sz = sz; f.kind = kind; f.words_old = wold; f.lo = lo; f.hi = hi;
+    };
+    const int64_t nsch = std::max(o.nsched, 1);
+    add(o.o_pend, ny.o_pend, o.npre, o.L, o.L + 1, ny.L + 1, 2, 0);
+    add(o.o_pend_n, ny.o_pend_n, 1, o.npre, o.npre, ny.npre, 2, 0);
+    add(o.o_new, ny.o_new, o.npre, o.L, o.L + 1, ny.L + 1, 2, 0);
+    add(o.o_new_n, ny.o_new_n, 1, o.npre, o.npre, ny.npre, 2, 0);
+    add(o.o_flags, ny.o_flags, 1, o.npre, o.npre, ny.npre, 1, 0);
+    add(o.o_lst, ny.o_lst, 1, o.npre, o.npre, ny.npre, 8, 0);
+    add(o.o_sq, ny.o_sq, nsch, o.QC, o.QC, ny.QC, 8, 0);
+    add(o.o_sq_n, ny.o_sq_n, 1, nsch, nsch, nsch, 2, 0);
+    add(o.o_se_ev, ny.o_se_ev, o.SC, o.nstates, o.nstates, ny.nstates, 2, 0);
+    add(o.o_se_ts, ny.o_se_ts, 1, o.SC, o.SC + 1, ny.SC + 1, 8, 0);
+    add(o.o_se_type, ny.o_se_type, 1, o.SC, o.SC + 1, ny.SC + 1, 1, 0);
+    add(o.o_se_free, ny.o_se_free, 0, 0, o.sew, ny.sew, 8, 1, o.sew, o.SC, ny.SC);
+    add(o.o_se_mark, ny.o_se_mark, 0, 0, o.sew, ny.sew, 8, 2);
+    add(o.o_ev_rec, ny.o_ev_rec, 1, o.EC, o.EC + 1, ny.EC + 1, 2, 0);
+    add(o.o_ev_next, ny.o_ev_next, 1, o.EC, o.EC + 1, ny.EC + 1, 2, 0);
+    add(o.o_ev_free, ny.o_ev_free, 0, 0, o.evw, ny.evw, 8, 1, o.evw, o.EC, ny.EC);
+    add(o.o_ev_mark, ny.o_ev_mark, 0, 0, o.evw, ny.evw, 8, 2);
+    add(o.o_rec_ts, ny.o_rec_ts, 1, o.RC, o.RC + 1, ny.RC + 1, 8, 0);
+    add(o.o_rec_val, ny.o_rec_val, o.RC, o.ncols, o.ncols, ny.ncols, 8, 0);
+    add(o.o_rec_nul, ny.o_rec_nul, 1, o.RC, o.RC + 1, ny.RC + 1, 4, 0);
+    add(o.o_rec_free, ny.o_rec_free, 0, 0, o.recw, ny.recw, 8, 1, o.recw, o.RC, ny.RC);
+    add(o.o_rec_mark, ny.o_rec_mark, 0, 0, o.recw, ny.recw, 8, 2);
+    add(o.o_ret, ny.o_ret, 1, o.RETC, o.RETC + 1, ny.RETC + 1, 2, 0);
+    add(o.o_tmp, ny.o_tmp, 1, o.RETC, o.RETC + 1, ny.RETC + 1, 2, 0);
+    add(o.o_wk, ny.o_wk, 1, o.WK + 1, o.WK + 1, ny.WK + 1, 4, 0);
+    add(o.o_key, ny.o_key, 1, 1, 1, 1, 8, 0);
+    add(o.o_misc, ny.o_misc, 1, MISC_N, MISC_N, MISC_N, 4, 3);
+    add(o.o_cse, ny.o_cse, 1, o.SC + 1, o.SC + 1, ny.SC + 1, 4, 0);
+    add(o.o_cev, ny.o_cev, 1, o.EC + 1, o.EC + 1, ny.EC + 1, 4, 0);
+    ra.blk_old = o.blk;
+    ra.blk_new = ny.blk;
+    ra.nblocks = backup_blocks;
+    ra.W = o.W;
+    ra.dSE = ny.SC - o.SC;
+    ra.dEV = ny.EC - o.EC;
+    ra.dREC = ny.RC - o.RC;
+    const size_t bytes = (size_t)(slot_cap / o.W) * ny.blk;
+    DevBuf nb;
+    nb.reserve(std::max<size_t>(bytes, 1));
+    SHD_HIP(hipMemsetAsync(nb.p, 0, bytes, stream));
+    if (backup_blocks > 0) {
+      hipLaunchKernelGGL(k_nfa_relayout, dim3(grid_cover(backup_blocks * o.W)), dim3(kBlock), 0, stream,
+                         dev_args(ra), (const char*)backup.p, nb.as<char>());
+      SHD_CHECK_LAUNCH();
+      // the new layout's backup: a later overflow of the same push starts from it
+      DevBuf bk;
+      bk.reserve((size_t)backup_blocks * ny.blk);
+      SHD_HIP(hipMemcpyAsync(bk.p, nb.p, (size_t)backup_blocks * ny.blk, hipMemcpyDeviceToDevice, stream));
+      SHD_HIP(hipStreamSynchronize(stream));
+      std::swap(backup.p, bk.p);
+      std::swap(backup.cap, bk.cap);
+    }
+    SHD_HIP(hipStreamSynchronize(stream));
+    std::swap(state.p, nb.p);
+    std::swap(state.cap, nb.cap);
+    lay = ny;
+  }
+
+  void run_push_once(const Staged* b, int64_t t_only) {
     hipStream_t s = stream;
     h_up_used = 0;
     SHD_HIP(hipEventRecord(ev0, s));
@@ -2523,9 +2784,10 @@ struct NfaEngine : Engine {
         const int64_t c0 = std::min<int64_t>(nl, warm / chunk + 1);   // lanes with ob <= warm
         ensure_slots(nl + 1);   // may move the key blocks
         ra.state = state.as<char>();
-        d_hash.reserve(2 * nl * 8);
+        d_hash.reserve(4 * nl * 8);
         ra.hash_w = d_hash.as<uint64_t>();
-        ra.hash_e = d_hash.as<uint64_t>() + nl;
+        ra.hash_e = d_hash.as<uint64_t>() + 2 * nl;
+        ra.hash1_zero = getenv("SHD_NFA_HASH1_ZERO") != nullptr;
         ra.chunk_len = chunk;
         ra.warm = warm;
         ra.c_exact = c0;
@@ -2582,7 +2844,7 @@ struct NfaEngine : Engine {
                     "timers %d, returned %d, rows %lld/%lld); raise SHD_NFA_LIST / SHD_NFA_PARTIALS / "
                     "SHD_NFA_EVENTS / SHD_NFA_RECORDS / SHD_NFA_TIMERS and reset the query",
                     hc.overflow, lay.L, lay.SC, lay.EC, lay.RC, lay.QC, lay.RETC, (long long)hc.rows, (long long)R);
-      throw Error(SHD_E_CAPACITY, msg);
+      throw NfaOverflow(hc.overflow, (int64_t)hc.rows, msg);
     }
     const int64_t m = (int64_t)hc.rows;
     if (m > 0) order_rows(m, partitioned || (win && !win_one), timers, n);   // window lanes: merge by event order
@@ -2673,6 +2935,60 @@ struct NfaEngine : Engine {
 };
 
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why) { return make_nfa_engine(p, why, 0); }
+
+// Field offsets of a layout from its capacities (lane-interleaved blocks).
+void layout_offsets(NfaLayout& Y) {
+  Y.sew = (Y.SC + 1 + 63) / 64;
+  Y.evw = (Y.EC + 1 + 63) / 64;
+  Y.recw = (Y.RC + 1 + 63) / 64;
+  // 64 key states interleaved per block; SHD_NFA_INTERLEAVE=0 keeps one key
+  // state contiguous (measured slower on window lanes too: S4-seq 158 vs 182 M
+  // events/s, S4P-seqplus 190 vs 199 M)
+  Y.W = kLaneBlock;
+  if (const char* w = getenv("SHD_NFA_INTERLEAVE")) Y.W = w[0] == '0' ? 1 : kLaneBlock;
+  const int64_t falign = Y.W == 1 ? 16 : 256;
+  int64_t off = 0;
+  Y.nf = 0;
+  auto field = [&](int64_t count, int sz) {
+    int64_t o = off;
+    off += (count * Y.W * sz + falign - 1) & ~(falign - 1);
+    Y.f_off[Y.nf] = o;
+    Y.f_cnt[Y.nf] = count;
+    Y.f_sz[Y.nf] = sz;
+    Y.nf++;
+    return o;
+  };
+  Y.o_pend = field((int64_t)Y.npre * (Y.L + 1), 2);
+  Y.o_pend_n = field(Y.npre, 2);
+  Y.o_new = field((int64_t)Y.npre * (Y.L + 1), 2);
+  Y.o_new_n = field(Y.npre, 2);
+  Y.o_flags = field(Y.npre, 1);
+  Y.o_lst = field(Y.npre, 8);
+  Y.o_sq = field((int64_t)std::max(Y.nsched, 1) * Y.QC, 8);
+  Y.o_sq_n = field(std::max(Y.nsched, 1), 2);
+  Y.o_se_ev = field((int64_t)(Y.SC + 1) * Y.nstates, 2);
+  Y.o_se_ts = field(Y.SC + 1, 8);
+  Y.o_se_type = field(Y.SC + 1, 1);
+  Y.o_se_free = field(Y.sew, 8);
+  Y.o_se_mark = field(Y.sew, 8);
+  Y.o_ev_rec = field(Y.EC + 1, 2);
+  Y.o_ev_next = field(Y.EC + 1, 2);
+  Y.o_ev_free = field(Y.evw, 8);
+  Y.o_ev_mark = field(Y.evw, 8);
+  Y.o_rec_ts = field(Y.RC + 1, 8);
+  Y.o_rec_val = field((int64_t)(Y.RC + 1) * Y.ncols, 8);
+  Y.o_rec_nul = field(Y.RC + 1, 4);
+  Y.o_rec_free = field(Y.recw, 8);
+  Y.o_rec_mark = field(Y.recw, 8);
+  Y.o_ret = field(Y.RETC + 1, 2);
+  Y.o_tmp = field(Y.RETC + 1, 2);
+  Y.o_wk = field(Y.WK + 1, 4);
+  Y.o_key = field(1, 8);
+  Y.o_misc = field(MISC_N, 4);
+  Y.o_cse = field(Y.SC + 1, 4);
+  Y.o_cev = field(Y.EC + 1, 4);
+  Y.blk = off;
+}
 
 std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t list_hint) {
   if (p.kind != SHD_KIND_STATE) {
@@ -2895,56 +3211,7 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   Y.nstates = p.n_states;
   Y.npre = npre;
   Y.nsched = g.n_sched;
-  Y.sew = (Y.SC + 1 + 63) / 64;
-  Y.evw = (Y.EC + 1 + 63) / 64;
-  Y.recw = (Y.RC + 1 + 63) / 64;
-  // 64 key states interleaved per block; SHD_NFA_INTERLEAVE=0 keeps one key
-  // state contiguous (measured slower on window lanes too: S4-seq 158 vs 182 M
-  // events/s, S4P-seqplus 190 vs 199 M)
-  Y.W = kLaneBlock;
-  if (const char* w = getenv("SHD_NFA_INTERLEAVE")) Y.W = w[0] == '0' ? 1 : kLaneBlock;
-  const int64_t falign = Y.W == 1 ? 16 : 256;
-  int64_t off = 0;
-  Y.nf = 0;
-  auto field = [&](int64_t count, int sz) {
-    int64_t o = off;
-    off += (count * Y.W * sz + falign - 1) & ~(falign - 1);
-    Y.f_off[Y.nf] = o;
-    Y.f_cnt[Y.nf] = count;
-    Y.f_sz[Y.nf] = sz;
-    Y.nf++;
-    return o;
-  };
-  Y.o_pend = field((int64_t)npre * (Y.L + 1), 2);
-  Y.o_pend_n = field(npre, 2);
-  Y.o_new = field((int64_t)npre * (Y.L + 1), 2);
-  Y.o_new_n = field(npre, 2);
-  Y.o_flags = field(npre, 1);
-  Y.o_lst = field(npre, 8);
-  Y.o_sq = field((int64_t)std::max(g.n_sched, 1) * Y.QC, 8);
-  Y.o_sq_n = field(std::max(g.n_sched, 1), 2);
-  Y.o_se_ev = field((int64_t)(Y.SC + 1) * Y.nstates, 2);
-  Y.o_se_ts = field(Y.SC + 1, 8);
-  Y.o_se_type = field(Y.SC + 1, 1);
-  Y.o_se_free = field(Y.sew, 8);
-  Y.o_se_mark = field(Y.sew, 8);
-  Y.o_ev_rec = field(Y.EC + 1, 2);
-  Y.o_ev_next = field(Y.EC + 1, 2);
-  Y.o_ev_free = field(Y.evw, 8);
-  Y.o_ev_mark = field(Y.evw, 8);
-  Y.o_rec_ts = field(Y.RC + 1, 8);
-  Y.o_rec_val = field((int64_t)(Y.RC + 1) * Y.ncols, 8);
-  Y.o_rec_nul = field(Y.RC + 1, 4);
-  Y.o_rec_free = field(Y.recw, 8);
-  Y.o_rec_mark = field(Y.recw, 8);
-  Y.o_ret = field(Y.RETC + 1, 2);
-  Y.o_tmp = field(Y.RETC + 1, 2);
-  Y.o_wk = field(Y.WK + 1, 4);
-  Y.o_key = field(1, 8);
-  Y.o_misc = field(MISC_N, 4);
-  Y.o_cse = field(Y.SC + 1, 4);
-  Y.o_cev = field(Y.EC + 1, 4);
-  Y.blk = off;
+  layout_offsets(Y);
   return e;
 }
 

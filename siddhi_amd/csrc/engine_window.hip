@@ -929,6 +929,12 @@ struct WindowXEngine : Engine {
 
   int kind() const override { return ENG_WINDOW; }
 
+  // aggregates here always fold sequentially (bit-exact): the option is a no-op
+  void set_option(const std::string& key, int64_t v) override {
+    if (key == "exact_aggregates") return;
+    Engine::set_option(key, v);
+  }
+
   void reset() override {
     C = 0;
     np = 0;

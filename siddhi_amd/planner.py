@@ -500,8 +500,36 @@ def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta],
         if gt == T_STRING:
             plan.null_str_id = ec.dict.id("null")
     if sel.having is not None:
-        raise UnsupportedPlanException("having is outside the round-1 hot path")
+        if state_query:
+            raise UnsupportedPlanException("having over pattern / sequence output is outside the hot path")
+        # QuerySelector's having condition is parsed against the selector's
+        # output event (SelectorParser.parse, C/util/parser/SelectorParser.java:
+        # havingConditionExecutor over the output attributes): an attribute name
+        # of the select list stands for that output's expression
+        outs = {oa.name: oa.expr for oa in attrs}
+        hexpr = _subst_outputs(sel.having, outs)
+        eid, t = ec.compile(hexpr, cs, 0, allow_agg=True)
+        if t != T_BOOL:
+            raise SiddhiAppValidationException("having condition must be of type BOOL")
+        plan.having = eid
     return names, types
+
+
+def _subst_outputs(e, outs):
+    """Having AST with unqualified names of the select list replaced by their expressions."""
+    if isinstance(e, qc.Var):
+        if e.stream is None and e.index is None and e.attr in outs:
+            return outs[e.attr]
+        return e
+    if isinstance(e, qc.BinOp):
+        return qc.BinOp(e.op, _subst_outputs(e.left, outs), _subst_outputs(e.right, outs))
+    if isinstance(e, qc.Not):
+        return qc.Not(_subst_outputs(e.expr, outs))
+    if isinstance(e, qc.IsNull):
+        return qc.IsNull(_subst_outputs(e.expr, outs))
+    if isinstance(e, qc.Func):
+        return qc.Func(e.name, [_subst_outputs(a, outs) for a in e.args], e.namespace)
+    return e
 
 
 def _plan_state(app, q, dictionary, partition, extra_streams) -> QueryPlan:

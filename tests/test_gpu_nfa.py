@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from parity import assert_same_rows, compile_single_query, run_device, run_oracle, stock_batch
+from parity import assert_same_rows, compile_single_query, concat_rows, run_device, run_oracle, stock_batch
 from siddhi_amd import workloads as wl
 
 pytestmark = pytest.mark.gpu
@@ -118,24 +118,64 @@ def test_absent_timer_fires_on_set_time(hip_available):
     assert_same_rows(dev, ora)
 
 
-def test_capacity_overflow_is_reported(hip_available, monkeypatch):
-    """A per-key pending list that overflows raises SHD_E_CAPACITY (never drops)."""
-    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST, SiddhiHipError, SHD_E_CAPACITY
-    monkeypatch.setenv("SHD_NFA_LIST", "4")
+@pytest.mark.parametrize("caps", [{"SHD_NFA_LIST": "4"},
+                                  {"SHD_NFA_LIST": "2", "SHD_NFA_PARTIALS": "8", "SHD_NFA_EVENTS": "8",
+                                   "SHD_NFA_RECORDS": "8"}],
+                         ids=["lists", "lists-pools"])
+@pytest.mark.parametrize("shape", ["and", "seqplus-part"])
+def test_capacity_overflow_grows(hip_available, monkeypatch, caps, shape):
+    """A push whose keys outgrow the per-key lists / pools is rerun from the
+    pre-push state with the overflowed capacities doubled (grow,
+    never drop, never fail): started far too small, the rows still equal the
+    oracle's, over several pushes (the grown layout carries on) and a snapshot
+    taken after growth restores into a fresh query."""
+    from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
+    for k, v in caps.items():
+        monkeypatch.setenv(k, v)
     monkeypatch.setenv("SHD_NO_LOGICAL_SCAN", "1")   # the generic engine's pending lists
-    qp, _ = compile_single_query(wl.S4_APPS["and"])
-    sym, price, vol, ts = wl.stock_stream(5000, 1000, 1.0, seed_offset=2)
-    b = stock_batch(sym, price, vol, ts)
+    app = wl.S4_APPS["and"] if shape == "and" else wl.S4_PART_APPS["seqplus"]
+    qp, _ = compile_single_query(app)
+    sym, price, vol, ts = wl.stock_stream(8000, 40 if shape != "and" else 1000, 1.0, seed_offset=2)
+    batches = split(sym, price, vol, ts, 3, call=500)
+    ora = run_oracle(qp, batches)
+    assert len(ora[2]) > 0
     dq = DeviceQuery(qp.ir)
+    dev_parts = []
     try:
-        cols = [np.ascontiguousarray(x) for x in b.cols]
-        tts = np.ascontiguousarray(b.ts, np.int64)
-        with pytest.raises(SiddhiHipError) as ei:
-            dq.push_raw(0, b.n, tts.ctypes.data, [x.ctypes.data for x in cols], [0] * 3, SHD_MEM_HOST,
+        for j, (si, b) in enumerate(batches):
+            if j == 2:   # restore the grown state into a fresh query
+                image = dq.snapshot()
+                dq.close()
+                dq = DeviceQuery(qp.ir)
+                dq.restore(image)
+            cols = [np.ascontiguousarray(x) for x in b.cols]
+            tts = np.ascontiguousarray(b.ts, np.int64)
+            dq.push_raw(si, b.n, tts.ctypes.data, [x.ctypes.data for x in cols], [0] * 3, SHD_MEM_HOST,
                         b.call_offsets, True)
-        assert ei.value.code == SHD_E_CAPACITY
+            r = dq.poll()
+            if r is not None:
+                dev_parts.append(r)
     finally:
         dq.close()
+    assert_same_rows(concat_rows(dev_parts), ora)
+
+
+@pytest.mark.parametrize("name", ["seqplus", "not100"])
+def test_window_lane_hash_collision_is_caught(hip_available, monkeypatch, name):
+    """Debug hook SHD_NFA_HASH1_ZERO: the first of the two window-lane state
+    hashes collides for every lane, so a wrong warm-up state would pass it;
+    the second hash still rejects it (the push reruns with longer warm-ups)
+    and the rows equal the oracle's."""
+    monkeypatch.setenv("SHD_NFA_HASH1_ZERO", "1")
+    monkeypatch.setenv("SHD_NFA_CHUNK", "5")
+    monkeypatch.setenv("SHD_NO_ABSENT_SCAN", "1")
+    qp, _ = compile_single_query(WINDOW_SEQS[name] if name in WINDOW_SEQS else wl.S4_APPS[name])
+    sym, price, vol, ts = wl.stock_stream(20000, 50, 1.0, seed_offset=78)
+    batches = split(sym, price, vol, ts, 2, call=700)
+    ora = run_oracle(qp, batches)
+    dev, _, kind = run_device(qp, batches)
+    assert kind == ENGINE_NFA
+    assert_same_rows(dev, ora)
 
 
 WINDOW_SEQS = {

@@ -16,7 +16,7 @@ from isa_check import scan
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "siddhi_amd", "csrc")
-SOURCES = ["engine_pattern.hip", "engine_single.hip", "engine_nfa.hip", "primitives.hip", "engine_group.hip",
+SOURCES = ["engine_pattern.hip", "engine_single.hip", "engine_window.hip", "engine_nfa.hip", "primitives.hip", "engine_group.hip",
            "engine_absent.hip", "route.hip"]
 
 
@@ -26,8 +26,17 @@ def asm(tmp_path_factory):
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")
     out = tmp_path_factory.mktemp("isa")
+    hdrs = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    hdrs += [os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))]
+    newest_input = max(os.path.getmtime(h) for h in hdrs)
 
     def one(src):
+        # the build's own gfx950 assembly (Makefile: -save-temps=obj) when it is
+        # newer than the source and every header
+        kept = os.path.join(CSRC, "build", src.rsplit(".", 1)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s")
+        if os.path.exists(kept) and os.path.getmtime(kept) >= max(newest_input,
+                                                                  os.path.getmtime(os.path.join(CSRC, src))):
+            return kept
         dst = str(out / (src + ".s"))
         subprocess.check_call([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-x", "hip",
                                "--cuda-device-only", "-S", os.path.join(CSRC, src), "-o", dst],
