@@ -258,21 +258,31 @@ def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtyp
 
 
 def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int, seq_lo: int,
-                 call_size: int, nblocks: int, group: Optional[dist.ProcessGroup] = None, device: int = 0):
+                 call_size: int, nblocks: int, group: Optional[dist.ProcessGroup] = None, device: int = 0,
+                 stage_host: bool = False):
     """route() on the GPU with the HIP bucket / merge passes around ONE RCCL
     all-to-all (plus the all-to-all of the per-owner counts, whose host copy
     sizes the exchange).  The micro-batch's events hold sequence numbers in
     [seq_lo, seq_lo + nblocks * call_size) with seq_lo a multiple of call_size
     (the global stream's InputHandler calls).  Returns (columns, seq, host call
-    offsets, stats) in increasing sequence order."""
+    offsets, stats) in increasing sequence order.
+    stage_host: the two all-to-alls run on host copies (a gloo group, e.g. ranks
+    sharing one GPU in tests; RCCL needs one GPU per rank)."""
     dtypes = [c.dtype for c in cols]
     send, counts, words = bucket(cols, key, seq, world, seq_lo, device)
     if world > 1:
+        def a2a(out, inp, out_splits=None, in_splits=None):
+            if not stage_host:
+                dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+                return
+            ho = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
+            out.copy_(ho)
         recv_counts = torch.empty_like(counts)
-        dist.all_to_all_single(recv_counts, counts, group=group)
+        a2a(recv_counts, counts)
         cs, rcs = counts.tolist(), recv_counts.tolist()
         recv = torch.empty(sum(rcs) * words, dtype=torch.int64, device=send.device)
-        dist.all_to_all_single(recv, send, [c * words for c in rcs], [c * words for c in cs], group=group)
+        a2a(recv, send, [c * words for c in rcs], [c * words for c in cs])
         rank = dist.get_rank(group)
         stats = {"sent": sum(cs) - cs[rank], "received": sum(rcs) - rcs[rank]}
     else:

@@ -4,6 +4,8 @@ ranks; each rank's rows carry shd_out.in_seq, mapped to the global sequence
 and k-way merged (exchange.merge_outputs).  The merged rows -- order, values,
 timestamps and callback chunks -- must equal one device query over the whole
 stream and the CPU oracle.  Also: in_seq of every engine equals the oracle's."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -79,3 +81,82 @@ def test_in_seq_equals_oracle(hip_available, name, app, n, keys, delta):
     assert len(ora[2]) > 0
     assert len(dseq) == len(oseq)
     assert np.array_equal(dseq, oseq)
+
+
+N_RR, KEYS_RR, DELTA_RR, BATCH_RR = 200_000, 4000, 0.02, 30_720
+
+
+def _rr_rank(rank, world, path, outdir):
+    """One rank of the N > 1 bench path on a shared GPU: its round-robin share
+    of the global stream resident in HBM, each micro-batch re-routed by key
+    owner with the HIP bucket / merge passes (the all-to-all staged through host
+    tensors over gloo), pushed to this rank's P3 query."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for q in (root, os.path.join(root, "tests")):
+        if q not in sys.path:
+            sys.path.insert(0, q)
+    import torch.distributed as dist
+    from siddhi_amd import exchange as ex2
+    from siddhi_amd import hip_engine as he
+    from siddhi_amd import workloads as wl2
+    from parity import compile_single_query as csq
+    dist.init_process_group("gloo", init_method="file://" + path, rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    qp, _ = csq(wl2.P3_APP)
+    idx = np.arange(rank, N_RR, world, dtype=np.int64)
+    s, p, v, t = wl2.stock_stream_at(idx, KEYS_RR, DELTA_RR, seed_offset=0)
+    cols = [torch.from_numpy(s.astype(np.int32)).to(dev), torch.from_numpy(p).to(dev),
+            torch.from_numpy(v).to(dev), torch.from_numpy(t).to(dev)]
+    seq = torch.from_numpy(idx).to(dev)
+    dq = he.DeviceQuery(qp.ir)
+    parts, lseqs, routed = [], [], []
+    for a in range(0, len(idx), BATCH_RR):   # BATCH_RR * world: whole 1024-event calls
+        b = min(len(idx), a + BATCH_RR)
+        lo = (a * world) // 1024 * 1024
+        nb = -(-(b * world - lo) // 1024)
+        (rs, rp, rv, rt), rseq, co, _ = ex2.route_device([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo,
+                                                         1024, nb, stage_host=True)
+        torch.cuda.synchronize()
+        m = rs.numel()
+        if m == 0:
+            continue
+        dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
+                    he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+        routed.append(rseq.cpu().numpy())
+        r = dq.poll(with_seq=True)
+        if r is not None:
+            parts.append(r[:5])
+            lseqs.append(r[5])
+    dq.close()
+    gall = np.concatenate(routed) if routed else np.zeros(0, np.int64)
+    rows = concat_rows(parts)
+    lseq = np.concatenate(lseqs) if lseqs else np.zeros(0, np.int64)
+    np.savez(os.path.join(outdir, "r%d.npz" % rank), c=rows[0], ty=rows[1], ts=rows[2], v=rows[3], n=rows[4],
+             g=gall[lseq] if len(lseq) else np.zeros(0, np.int64))
+    dist.destroy_process_group()
+
+
+def test_roundrobin_route_device_world2_merges_to_single_engine(hip_available, tmp_path):
+    """The N > 1 bench path end to end (bench.py --input roundrobin): two ranks
+    on one GPU, HIP bucket -> all-to-all -> HIP merge -> P3 query per rank, rows
+    mapped to global sequence numbers and k-way merged (exchange.merge_outputs):
+    equal to one device query over the whole stream and to the CPU oracle."""
+    import tempfile
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_rr_rank, args=(world, tempfile.mktemp(dir=str(tmp_path)), str(tmp_path)), nprocs=world)
+    parts = []
+    for r in range(world):
+        z = np.load(os.path.join(str(tmp_path), "r%d.npz" % r))
+        parts.append(((z["c"], z["ty"], z["ts"], z["v"], z["n"]), z["g"]))
+    merged = ex.merge_outputs(parts)
+    qp, _ = compile_single_query(wl.P3_APP)
+    s, p, v, t = wl.stock_stream_at(np.arange(N_RR, dtype=np.int64), KEYS_RR, DELTA_RR, seed_offset=0)
+    whole = run_oracle(qp, [(0, stock_batch(s, p, v, t, 1024))])
+    one, _ = _device_rows_with_seq(qp, [(0, stock_batch(s, p, v, t, 1024))])
+    assert len(whole[2]) > 50
+    assert_same_rows(one, whole)
+    assert merged is not None
+    assert_same_rows(merged[:5], whole)

