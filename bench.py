@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--events", type=int, default=0, help="override events per GPU")
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=50_000_000, help="micro-batch size (events)")
+    ap.add_argument("--no-share", action="store_true", help="M5: every query scans alone (no shd_group)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads of the per-key parallel CPU baseline (partitioned configs; 0=skip)")
@@ -269,7 +270,7 @@ def run_multi(args, torch, dist, rank, world, local, dev):
     all queries over the stream, is fixed as N grows)."""
     from siddhi_amd import workloads as wl
     from siddhi_amd import hip_engine as he
-    from siddhi_amd.planner import StringDictionary, plan_query
+    from siddhi_amd.planner import StringDictionary, plan_query, plan_shared_leader, share_groups
     from siddhi_amd import query_compiler as qc
 
     app, n_def, k_def, delta = wl.CONFIGS[args.config]
@@ -278,44 +279,67 @@ def run_multi(args, torch, dist, rank, world, local, dev):
     qa = qc.parse(app)
     d = StringDictionary()
     wl.register_symbols(d, keys)
-    plans = [plan_query(qa, item, d) for item in qa.execution_order]
+    queries = list(qa.execution_order)
+    plans = [plan_query(qa, item, d) for item in queries]
     mine = [i for i in range(len(plans)) if i % world == rank]
     sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=0, key_base=0, dev=dev)
     torch.cuda.synchronize()
     he.context(local)
-    dqs = [he.DeviceQuery(plans[i].ir, device=local) for i in mine]
+    dqs = {i: he.DeviceQuery(plans[i].ir, device=local) for i in mine}
+    # query sharing: the P1 variants (same f2 / within, e1 threshold 60..84.5)
+    # run one forward scan per rank (shd_group_*); every other query alone
+    units = []      # (DeviceGroup | None, [query index])
+    grouped = set()
+    if not args.no_share:
+        for g in share_groups([queries[i] for i in mine]):
+            idx = [mine[k] for k in g]
+            lead = plan_shared_leader(qa, [queries[i] for i in idx], d)
+            units.append((he.DeviceGroup(lead.ir, [dqs[i] for i in idx], device=local), idx))
+            grouped.update(idx)
+    units += [(None, [i]) for i in mine if i not in grouped]
     # 100 queries each keep their own scratch: 10M-event micro-batches by default
     batch = min(args.batch if args.batch != 50_000_000 else 10_000_000, n)
     cuts = list(range(0, n, batch)) + [n]
     offs_all = wl.call_offsets(n)
 
     def run_step(collect=None):
-        for dq in dqs:
-            dq.reset()
+        for grp, idx in units:
+            if grp is not None:
+                grp.reset()
+            else:
+                dqs[idx[0]].reset()
         tot = {}
         for a, b in zip(cuts[:-1], cuts[1:]):
             lo = np.searchsorted(offs_all, a)
             hi = np.searchsorted(offs_all, b)
             co = (np.concatenate([[a], offs_all[lo:hi][offs_all[lo:hi] > a], [b]]) - a).astype(np.int64)
             cols = [sym.data_ptr() + 4 * a, price.data_ptr() + 8 * a, vol.data_ptr() + 8 * a]
-            for dq in dqs:   # junction fan-out in definition order
-                dq.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE, co, True)
-                dq.discard()
+            for grp, idx in units:   # junction fan-out
+                tgt = grp if grp is not None else dqs[idx[0]]
+                tgt.push_raw(0, b - a, ts.data_ptr() + 8 * a, cols, [0, 0, 0], he.SHD_MEM_DEVICE, co, True)
+                for i in idx:
+                    dqs[i].discard()
                 if collect is not None:
-                    for k, v in dq.stage_times().items():
+                    for k, v in tgt.stage_times().items():
                         tot[k] = tot.get(k, 0) + v
         if collect is not None:
             collect.append(tot)
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()
+    if rank == 0:
+        print("M5: warmup %.1f s (%d units, %d shared scans)" % (time.perf_counter() - tw, len(units),
+              sum(1 for g, _ in units if g is not None)), file=sys.stderr, flush=True)
     if dist:
         dist.barrier()
     stage_runs = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         run_step(stage_runs)
+        if rank == 0:
+            print("M5: step %d done at %.1f s" % (k, time.perf_counter() - t0), file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -324,9 +348,19 @@ def run_multi(args, torch, dist, rank, world, local, dev):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # algorithmic bytes of every owned query (pattern / window formulas of SURVEY.md §8d)
+    # algorithmic bytes (SURVEY.md §8d formulas): a shared scan counts the input
+    # record and its partial-match traffic once (the leader's P and f_new) plus
+    # every member's 32-byte output rows; a query alone counts its own formula
     bytes_step, matches = 0.0, 0
-    for i, dq in zip(mine, dqs):
+    for grp, idx in units:
+        if grp is not None:
+            c = grp.counters()
+            mem_matches = sum(dqs[i].counters()["matches"] for i in idx)
+            b_lead, _ = alg_bytes_pattern(dict(c, matches=0), c["events"])
+            bytes_step += b_lead + 32 * mem_matches
+            matches += mem_matches
+            continue
+        dq = dqs[idx[0]]
         c = dq.counters()
         matches += c["matches"]
         if dq.engine_kind in (1, 4):
@@ -341,15 +375,18 @@ def run_multi(args, torch, dist, rank, world, local, dev):
     if dist:
         dist.all_reduce(vals)
     bytes_all, matches_all = float(vals[0].item()), float(vals[1].item())
-    dominant = max(stages, key=stages.get) if stages else None
     roof = None
-    if dominant:
-        launches = (len(cuts) - 1) * len(dqs)
-        ach = (bytes_step / launches) / (stages[dominant] / launches * 1e-9) / 1e9
-        path = bytes_step / (sum(stages.values()) * 1e-9) / 1e9
+    if stages:
+        # frac as on the P3 line: the path's algorithmic bytes per step / the wall
+        # time of a step; device_*: / the HIP-event time of every push
+        ach = bytes_step / (elapsed / args.steps) / 1e9
+        dev_ach = bytes_step / (sum(stages.values()) * 1e-9) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_stage": dominant,
-                "path_achieved": round(path, 1), "path_frac": round(path / HBM_PEAK_GBS, 4)}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_event": round(bytes_step / n, 2),
+                "scope": "whole fan-out per step (wall clock), rank 0",
+                "device_achieved": round(dev_ach, 1), "device_frac": round(dev_ach / HBM_PEAK_GBS, 4),
+                "stage_top": max(stages, key=stages.get)}
     if rank == 0:
         line = {
             "metric": "events/sec ingested + matches/sec (partitioned pattern, 1–8 GPU); % HBM peak",
@@ -359,7 +396,8 @@ def run_multi(args, torch, dist, rank, world, local, dev):
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
             "config": {"workload": "M5", "queries": len(plans), "events": n, "keys": keys, "delta_ms": delta,
                        "micro_batch": batch, "call_size": 1024,
-                       "parallelism": "query-parallel x%d (broadcast input)" % world},
+                       "parallelism": "query-parallel x%d (broadcast input)" % world,
+                       "shared_scans": [len(idx) for grp, idx in units if grp is not None]},
             "query_events_per_s": round(n * len(plans) * args.steps / elapsed, 1),
             "matches_per_s": round(matches_all * args.steps / elapsed, 1),
             "algorithmic_bytes_per_step": round(bytes_all),
@@ -367,35 +405,61 @@ def run_multi(args, torch, dist, rank, world, local, dev):
             "roofline": roof,
             "cpu_baseline": None,
         }
-    prefix = None
+    for grp, _ in units:
+        if grp is not None:
+            grp.close()
+    for dq in dqs.values():
+        dq.close()
     if rank == 0 and args.cpu_sample != 0:
-        prefix = m5_parity_prefix(he, plans, sym, price, vol, ts, min(n, args.cpu_sample if args.cpu_sample > 0
-                                                                        else 20_000), keys, delta)
-        line["parity_prefix"] = prefix
+        sample = min(n, args.cpu_sample if args.cpu_sample > 0 else 200_000)
+        line["parity_prefix"], line["cpu_baseline"] = m5_parity_prefix(
+            he, qa, queries, plans, d, sym, price, vol, ts, sample, keys, delta, not args.no_share)
         print(json.dumps(line))
     elif rank == 0:
         print(json.dumps(line))
-    for dq in dqs:
-        dq.close()
 
 
-def m5_parity_prefix(he, plans, sym, price, vol, ts, prefix, keys, delta):
-    """Every M5 query (a fresh device query each) on the first `prefix` events
-    of the benchmark stream against the CPU oracle on the same events: pattern
-    rows bit-exact, window rows with doubles within 1e-9 relative."""
+def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, keys, delta, share):
+    """Every M5 query on the first `prefix` events of the benchmark stream, run
+    the way the timed loop runs it (the shared scans of shd_group included, one
+    push), against the CPU oracle on the same events: pattern rows bit-exact,
+    window rows with doubles within 1e-9 relative.  The oracle's own time over
+    the prefix (all queries, one core, one after the other) is the line's
+    cpu_baseline."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_engine import OracleQueryEngine
     from parity import assert_rows_agg, assert_same_rows, concat_rows
     from siddhi_amd import workloads as wl
+    from siddhi_amd.planner import plan_shared_leader, share_groups
     from siddhi_amd.runtime import ColumnBatch
     s, p, v, t = wl.stock_stream(prefix, keys, delta, seed_offset=0)
     offs = wl.call_offsets(prefix)
+    dqs = [he.DeviceQuery(qp.ir) for qp in plans]
+    groups = []
+    grouped = set()
+    if share:
+        for g in share_groups(queries):
+            groups.append(he.DeviceGroup(plan_shared_leader(qa, [queries[i] for i in g], d).ir, [dqs[i] for i in g]))
+            grouped.update(g)
+    cols = [sym.data_ptr(), price.data_ptr(), vol.data_ptr()]
+    for tgt in groups + [dqs[i] for i in range(len(dqs)) if i not in grouped]:
+        tgt.push_raw(0, prefix, ts.data_ptr(), cols, [0, 0, 0], he.SHD_MEM_DEVICE, offs.astype(np.int64), True)
+    devs = []
+    for dq in dqs:
+        r = dq.poll()
+        devs.append((concat_rows([r] if r is not None else []), dq.engine_kind == 2))
+    for g in groups:
+        g.close()
+    for dq in dqs:
+        dq.close()
     rows = 0
+    cpu_s = 0.0
     try:
-        for qp in plans:
+        for qp, (dev, window) in zip(plans, devs):
             eng = OracleQueryEngine(qp, None)
             parts = []
             cid = 0
+            t0 = time.perf_counter()
             for c in range(len(offs) - 1):
                 a, b = int(offs[c]), int(offs[c + 1])
                 sub = ColumnBatch(t[a:b], [s[a:b].astype(np.uint32), p[a:b], v[a:b]], [None, None, None])
@@ -403,23 +467,23 @@ def m5_parity_prefix(he, plans, sym, price, vol, ts, prefix, keys, delta):
                     k = len(ch.ts)
                     parts.append((np.full(k, cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
                     cid += 1
+            cpu_s += time.perf_counter() - t0
             eng.close()
+            print("M5 parity: %s oracle %.1f s" % (qp.name, cpu_s), file=sys.stderr, flush=True)
             ora = concat_rows(parts)
-            dq = he.DeviceQuery(qp.ir)
-            dq.push_raw(0, prefix, ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol.data_ptr()], [0, 0, 0],
-                        he.SHD_MEM_DEVICE, offs.astype(np.int64), True)
-            r = dq.poll()
-            window = dq.engine_kind == 2
-            dq.close()
-            dev = concat_rows([r] if r is not None else [])
             if window:
                 assert_rows_agg(dev, ora, qp, exact=False)
             else:
                 assert_same_rows(dev, ora)
             rows += len(dev[2])
-        return "equal (%d queries, %d events, %d rows)" % (len(plans), prefix, rows)
+        verdict = "equal (%d queries, %d shared, %d events, %d rows)" % (len(plans), len(grouped), prefix, rows)
     except AssertionError as e:
-        return "DIFFERENT: %s" % str(e).splitlines()[0]
+        verdict = "DIFFERENT: %s" % str(e).splitlines()[0]
+    cpu = {"value": round(prefix / cpu_s, 1) if cpu_s > 0 else None, "unit": "events/s", "cores": 1,
+           "kind": "port",
+           "sample": "the first %d stream events through all %d queries, one after the other (oracle C++ "
+                     "restatement, one core; polled per InputHandler call)" % (prefix, len(plans))}
+    return verdict, cpu
 
 
 def main():

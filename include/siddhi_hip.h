@@ -45,6 +45,7 @@ extern "C" {
 
 typedef struct shd_ctx shd_ctx;
 typedef struct shd_query shd_query;
+typedef struct shd_group shd_group;
 
 enum shd_status {
   SHD_OK = 0,
@@ -207,6 +208,36 @@ int shd_route_bucket(shd_ctx* ctx, void* stream, int64_t n, int world, const voi
 int shd_route_merge(shd_ctx* ctx, void* stream, int world, const uint64_t* recv, const int64_t* seg_off, int64_t m,
                     int64_t seq_lo, int64_t block, int64_t nblocks, int ncols, void* const* out_cols,
                     const int* widths, int64_t* out_seq, int64_t* start, int64_t* block_off, int32_t* err);
+
+/* Query groups: the queries a StreamJunction fans one stream out to
+ * (C/stream/StreamJunction.java:146-272) that differ only in the start
+ * state's filter -- `every e1=A[f1_g] -> e2=B[f2] within W` with the same f2,
+ * W, streams and partitioning -- run ONE forward scan.  Each partial of such a
+ * pattern meets the later events alone (ST/StreamPreStateProcessor.java:118-129,
+ * 326-403), so a leader plan whose e1 filter accepts every event any member's
+ * does (the host planner builds it as their disjunction) holds every member's
+ * partials with the member's outcome; a member's rows are the leader's matches
+ * whose e1 event passes the member's own f1, in the leader's order.
+ *
+ * shd_group_create: loads the leader IR on ctx and attaches 1..64 fresh member
+ * queries (pattern-engine plans; SHD_E_ARG when one differs from the leader in
+ * more than its e1 filter and its selector, or reads an e1 attribute the
+ * leader does not carry).  While grouped, members refuse shd_push / shd_reset /
+ * shd_snapshot / shd_restore / shd_plan_free; shd_poll, shd_get_counters
+ * (events and matches of the member; the shared scan's counters are the
+ * leader's) and shd_set_time work as usual.
+ * shd_group_push: one batch into every member (as shd_push on each would).
+ * When the leader has to hand over to the generic NFA engine (time going back
+ * inside a key), each member takes over the leader's open partials through its
+ * own NFA engine and the group runs its members one by one from then on.
+ * shd_group_leader: the leader query (counters, stage times; not pushable).
+ * shd_group_free: detaches and resets the members, frees the leader. */
+int shd_group_create(shd_ctx* ctx, const void* leader_ir, size_t len, shd_query* const* members, int n,
+                     shd_group** out);
+int shd_group_push(shd_group* g, const shd_batch* batch);
+int shd_group_reset(shd_group* g);
+int shd_group_leader(shd_group* g, shd_query** leader);
+int shd_group_free(shd_group* g);
 
 const char* shd_last_error(void);
 

@@ -193,6 +193,16 @@ struct Engine {
   virtual void export_replay(std::vector<Replay>&) {
     throw Error(SHD_E_UNSUPPORTED, "engine state cannot be handed over");
   }
+  // Query sharing (shd_group_*, the junction fan-out of StreamJunction.java:146-272
+  // to queries that differ only in their start-state filter): this engine
+  // becomes the leader of `members`, whose rows it derives from its own
+  // per-push results.  grouped: a leader or member -- pushes, resets and
+  // snapshots go through the group.
+  bool grouped = false;
+  virtual void group_attach(const std::vector<Engine*>&) {
+    throw Error(SHD_E_UNSUPPORTED, "this query's engine cannot lead a query group");
+  }
+  virtual void group_detach() {}
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column

@@ -1272,6 +1272,82 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
   }
 }
 
+// ---- query sharing (PatternEngine::group_emit)
+// Partials of `every e1=A[f1] -> e2=B[f2] within W` evolve independently: each
+// A event passing f1 opens one StateEvent and meets the later events alone
+// (StreamPreStateProcessor.java:118-129,326-403; nothing a partial does depends
+// on another).  A leader whose e1 filter accepts every event a member's does
+// (their disjunction) therefore holds every member partial, with the member's
+// outcome, and the member's matches are the leader's match pairs whose e1 row
+// passes the member's own f1 -- in the leader's (e2 event, creation) order.
+constexpr int kGroupMax = 64;
+constexpr int kGroupWaveItems = 8;   // pairs per lane: one wave covers 512 consecutive pairs
+
+struct GroupSelArgs {
+  ExtRows x;
+  int G;
+  DExprSet es[kGroupMax];
+  DFilters f1[kGroupMax];
+};
+
+// bit g of mask[k]: member g's f1 on the e1 row of pair k
+__global__ __launch_bounds__(kBlock) void k_group_mask(const GroupSelArgs* __restrict__ ap, const uint32_t* pi,
+                                                       int64_t m, uint64_t* __restrict__ mask) {
+  const GroupSelArgs& a = *ap;
+  for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < m; k = m) {
+    PairCtx cx{&a.x, (int64_t)pi[k], -1, 1, false, -1, -1};
+    uint64_t b = 0;
+    for (int g = 0; g < a.G; g++)
+      if (eval_filters(a.es[g], a.f1[g], cx)) b |= 1ull << g;
+    mask[k] = b;
+  }
+}
+
+// cnt[g * nw + w]: member g's pairs among wave w's 512 pairs.  SCATTER: the
+// same walk writes them, in pair order, from off[g * nw + w] on.
+template <bool SCATTER>
+__global__ __launch_bounds__(kBlock) void k_group_split(const uint64_t* __restrict__ mask, const uint32_t* pj,
+                                                        const uint32_t* pi, int64_t m, int G, int64_t nw,
+                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ gpj,
+                                                        uint32_t* __restrict__ gpi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  if (w >= nw) return;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t mk[kGroupWaveItems];
+  uint32_t vj[kGroupWaveItems], vi[kGroupWaveItems];
+  for (int s = 0; s < kGroupWaveItems; s++) {
+    const int64_t k = w * (64 * kGroupWaveItems) + s * 64 + lane;
+    mk[s] = k < m ? mask[k] : 0ull;
+    if (SCATTER) {
+      vj[s] = k < m ? pj[k] : 0u;
+      vi[s] = k < m ? pi[k] : 0u;
+    }
+  }
+  for (int g = 0; g < G; g++) {
+    uint32_t base = SCATTER ? cnt[(int64_t)g * nw + w] : 0u;
+    for (int s = 0; s < kGroupWaveItems; s++) {
+      const bool on = (mk[s] >> g) & 1ull;
+      const uint64_t bal = __ballot(on);
+      if (SCATTER && on) {
+        const uint32_t pos = base + (uint32_t)__popcll(bal & below);
+        gpj[pos] = vj[s];
+        gpi[pos] = vi[s];
+      }
+      base += (uint32_t)__popcll(bal);
+    }
+    if (!SCATTER && lane == 0) cnt[(int64_t)g * nw + w] = base;
+  }
+}
+
+// bases[g] = first pair of member g in the split lists, bases[G] = their total
+__global__ void k_group_bases(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, int G, int64_t nw,
+                              uint32_t* __restrict__ bases) {
+  const int g = threadIdx.x;
+  if (g < G) bases[g] = off[(int64_t)g * nw];
+  if (g == G) bases[G] = off[(int64_t)G * nw - 1] + cnt[(int64_t)G * nw - 1];
+}
+
 struct GatherArgs {
   ExtRows x;
   int ncols;
@@ -3093,27 +3169,32 @@ struct PatternEngine : Engine {
                            d_pi_alt.as<uint32_t>(), m, bits, d_sort, s, in_alt);
       const uint32_t* pj = in_alt ? d_pj_alt.as<uint32_t>() : d_pj.as<uint32_t>();
       const uint32_t* pi = in_alt ? d_pi_alt.as<uint32_t>() : d_pi.as<uint32_t>();
-      out.ensure(m, s);
-      ProjArgs pr{};
-      pr.x = x;
-      pr.es = dset();
-      pr.nout = (int)outs.size();
-      for (size_t c = 0; c < outs.size(); c++) pr.outs[c] = dexpr(outs[c]);
-      pr.multi = (sA == sB);
-      pr.logical = logical;
-      pr.s_first = s_first;
-      pr.s_second = s_second;
-      pr.se1 = d_se1.as<uint32_t>();
-      pr.sot = d_sot.as<int32_t>();
-      pr.chunk0 = chunk_seq;
-      pr.row0 = out.count;
-      hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
-                         out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq(),
-                         out.d_sidx());
-      SHD_CHECK_LAUNCH();
-      out.count += m;
-      if (sA != sB && !logical) chunk_seq += m;
-      mark("order_project");
+      if (!gmembers.empty()) {   // a group leader: its members' rows only
+        group_emit(b, x, pj, pi, m);
+        mark("order_project");
+      } else {
+        out.ensure(m, s);
+        ProjArgs pr{};
+        pr.x = x;
+        pr.es = dset();
+        pr.nout = (int)outs.size();
+        for (size_t c = 0; c < outs.size(); c++) pr.outs[c] = dexpr(outs[c]);
+        pr.multi = (sA == sB);
+        pr.logical = logical;
+        pr.s_first = s_first;
+        pr.s_second = s_second;
+        pr.se1 = d_se1.as<uint32_t>();
+        pr.sot = d_sot.as<int32_t>();
+        pr.chunk0 = chunk_seq;
+        pr.row0 = out.count;
+        hipLaunchKernelGGL(k_project, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(pr), pj, pi, (int64_t)m,
+                           out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(), out.d_nulls(), out.d_seq(),
+                           out.d_sidx());
+        SHD_CHECK_LAUNCH();
+        out.count += m;
+        if (sA != sB && !logical) chunk_seq += m;
+        mark("order_project");
+      }
     }
 
     // ---- carry the still-open partials
@@ -3268,9 +3349,142 @@ struct PatternEngine : Engine {
     counters.carry = C;
     counters.dormant = S;
     counters.kernel_ns = (int64_t)(ms * 1e6);
-      counters.partials += (int64_t)n_cand;
+    counters.partials += (int64_t)n_cand;
+    for (PatternEngine* g : gmembers) {
+      g->seq = seq;
+      if (b.advance_time && t_end > g->now) g->now = t_end;
+      g->counters.events += n;
+      g->counters.kernel_ns = 0;
+    }
   }
 
+  // ---- query sharing (shd_group_create): members whose plans differ from this
+  // one only in the e1 filter (and the output names); this engine's e1 filter
+  // accepts every event any member's does (the planner builds it as their
+  // disjunction).  A member's own state is never used while grouped: its open
+  // partials are the leader's whose A event passes its f1.
+  std::vector<PatternEngine*> gmembers;
+  DevBuf d_gmask, d_gcnt, d_goff, d_gscan, d_gpj, d_gpi, d_gbase;
+  PinnedBuf h_gbase;
+
+  static bool same_expr(const Plan& p, int e, const Plan& q, int f) {
+    if (e < 0 || f < 0) return e == f;
+    const auto& A = p.exprs[e];
+    const auto& B = q.exprs[f];
+    if (A.size() != B.size()) return false;
+    for (size_t i = 0; i < A.size(); i++) {
+      if (A[i].op != B[i].op || A[i].b != B[i].b || A[i].c != B[i].c) return false;
+      if (A[i].op == SHD_OP_CONST ? p.consts[A[i].a] != q.consts[B[i].a] : A[i].a != B[i].a) return false;
+    }
+    return true;
+  }
+
+  void group_attach(const std::vector<Engine*>& ms) override {
+    if (grouped) throw Error(SHD_E_ARG, "the leader already belongs to a group");
+    if (ms.empty() || ms.size() > (size_t)kGroupMax) throw Error(SHD_E_ARG, "a group holds 1..64 member queries");
+    if (logical != 0) throw Error(SHD_E_UNSUPPORTED, "query groups: logical patterns are not shared");
+    if (counters.events != 0 || C != 0 || S != 0) throw Error(SHD_E_ARG, "the group leader must be fresh");
+    std::vector<PatternEngine*> v;
+    for (Engine* e : ms) {
+      auto* m = dynamic_cast<PatternEngine*>(e);
+      if (!m || m == this || m->grouped) throw Error(SHD_E_ARG, "group member: not a free pattern-engine query");
+      for (PatternEngine* o : v)
+        if (o == m) throw Error(SHD_E_ARG, "group member listed twice");
+      bool ok = m->logical == 0 && m->sA == sA && m->sB == sB && m->W == W && m->partitioned == partitioned &&
+                m->implicit_key == implicit_key && m->typesA == typesA && m->f2.size() == f2.size() &&
+                m->plan.stream_types == plan.stream_types && (m->carry_mask & ~carry_mask) == 0;
+      for (int k = 0; ok && k < 2; k++)
+        ok = m->key_col[k] == key_col[k] && m->key_type[k] == key_type[k] &&
+             same_expr(plan, key_expr[k], m->plan, m->key_expr[k]);
+      for (size_t k = 0; ok && k < f2.size(); k++) ok = same_expr(plan, f2[k], m->plan, m->f2[k]);
+      if (!ok)
+        throw Error(SHD_E_ARG, "group member differs from the leader beyond the e1 filter and the selector");
+      if (m->counters.events != 0 || m->C != 0 || m->S != 0 || m->out.count != 0)
+        throw Error(SHD_E_ARG, "group members must be fresh (reset, no unpolled rows)");
+      v.push_back(m);
+    }
+    gmembers = v;
+    grouped = true;
+    for (PatternEngine* m : gmembers) m->grouped = true;
+  }
+
+  void group_detach() override {
+    for (PatternEngine* m : gmembers) m->grouped = false;
+    gmembers.clear();
+    grouped = false;
+  }
+
+  // this push's match pairs (sorted by e2 row, then creation) -> each member's
+  // output rows
+  void group_emit(const Staged& b, const ExtRows& x, const uint32_t* pj, const uint32_t* pi, uint32_t m) {
+    hipStream_t s = stream;
+    const int G = (int)gmembers.size();
+    if ((uint64_t)m * (uint64_t)G >= (1ull << 32))
+      throw Error(SHD_E_CAPACITY, "query group: too many matches in one push for 32-bit pair lists (split the batch)");
+    const int64_t per_wave = 64 * kGroupWaveItems;
+    const int64_t nw = ((int64_t)m + per_wave - 1) / per_wave;
+    GroupSelArgs ga{};
+    ga.x = x;
+    ga.G = G;
+    for (int g = 0; g < G; g++) {
+      ga.es[g] = gmembers[g]->dset();
+      ga.f1[g] = gmembers[g]->dfilters(gmembers[g]->f1);
+    }
+    d_gmask.reserve((size_t)m * 8);
+    d_gcnt.reserve((size_t)G * nw * 4);
+    d_goff.reserve((size_t)G * nw * 4);
+    d_gbase.reserve((size_t)(G + 1) * 4);
+    h_gbase.reserve((size_t)(G + 1) * 4);
+    hipLaunchKernelGGL(k_group_mask, dim3(grid_cover(m)), dim3(kBlock), 0, s, dev_args(ga), pi, (int64_t)m,
+                       d_gmask.as<uint64_t>());
+    SHD_CHECK_LAUNCH();
+    const int split_blocks = (int)((nw * 64 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_group_split<false>, dim3(split_blocks), dim3(kBlock), 0, s,
+                       (const uint64_t*)d_gmask.as<uint64_t>(), pj, pi, (int64_t)m, G, nw, d_gcnt.as<uint32_t>(),
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+    SHD_CHECK_LAUNCH();
+    scan_exclusive_u32(d_gcnt.as<uint32_t>(), d_goff.as<uint32_t>(), (int64_t)G * nw, nullptr, d_gscan, s);
+    hipLaunchKernelGGL(k_group_bases, dim3(1), dim3(128), 0, s, (const uint32_t*)d_goff.as<uint32_t>(),
+                       (const uint32_t*)d_gcnt.as<uint32_t>(), G, nw, d_gbase.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    SHD_HIP(hipMemcpyAsync(h_gbase.p, d_gbase.p, (size_t)(G + 1) * 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const uint32_t* base = h_gbase.as<uint32_t>();
+    const uint32_t total = base[G];
+    if (total == 0) return;
+    d_gpj.reserve((size_t)total * 4);
+    d_gpi.reserve((size_t)total * 4);
+    hipLaunchKernelGGL(k_group_split<true>, dim3(split_blocks), dim3(kBlock), 0, s,
+                       (const uint64_t*)d_gmask.as<uint64_t>(), pj, pi, (int64_t)m, G, nw, d_goff.as<uint32_t>(),
+                       d_gpj.as<uint32_t>(), d_gpi.as<uint32_t>());
+    SHD_CHECK_LAUNCH();
+    for (int g = 0; g < G; g++) {
+      PatternEngine& e = *gmembers[g];
+      const uint32_t mq = base[g + 1] - base[g];
+      if (mq == 0) continue;
+      e.out.ensure(mq, s);
+      ProjArgs pr{};
+      pr.x = x;
+      pr.es = e.dset();
+      pr.nout = (int)e.outs.size();
+      for (size_t c = 0; c < e.outs.size(); c++) pr.outs[c] = e.dexpr(e.outs[c]);
+      pr.multi = (sA == sB);
+      pr.logical = 0;
+      pr.s_first = e.s_first;
+      pr.s_second = e.s_second;
+      pr.chunk0 = e.chunk_seq;
+      pr.row0 = e.out.count;
+      hipLaunchKernelGGL(k_project, dim3(grid_cover(mq)), dim3(kBlock), 0, s, dev_args(pr),
+                         (const uint32_t*)d_gpj.as<uint32_t>() + base[g], (const uint32_t*)d_gpi.as<uint32_t>() + base[g],
+                         (int64_t)mq, e.out.d_chunk(), e.out.d_type(), e.out.d_ts(), e.out.d_vals(), e.out.d_nulls(),
+                         e.out.d_seq(), e.out.d_sidx());
+      SHD_CHECK_LAUNCH();
+      e.out.count += mq;
+      if (sA != sB) e.chunk_seq += mq;
+      e.counters.matches += mq;
+    }
+    (void)b;
+  }
 };
 
 std::unique_ptr<Engine> finish_pattern_engine(const Plan& p, const PNode& a, const PNode& b, const PNode* c,

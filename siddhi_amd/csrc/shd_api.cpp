@@ -527,10 +527,14 @@ void stage_host(hipStream_t s, PinnedBuf& pin, DevBuf& dts, DevBuf* dcol, DevBuf
 // by replaying the events that created them, carry over unpolled output and
 // the query's counters, then run the push there.  The query stays on the NFA
 // engine from then on.
-void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, const std::string& why) {
+// given: the open partials to replay (a dissolving query group hands its
+// leader's to every member); null: q's own engine exports them
+void switch_to_nfa(shd_query* q, const Staged& st, const shd_counters& before, const std::string& why,
+                   const std::vector<Replay>* given = nullptr) {
   Engine& old = *q->eng;
-  std::vector<Replay> parts;
-  old.export_replay(parts);
+  std::vector<Replay> own;
+  if (!given) old.export_replay(own);
+  const std::vector<Replay>& parts = given ? *given : own;
   int64_t nrep = 0;
   for (auto& r : parts) nrep += r.n;
   std::string w2;
@@ -726,6 +730,7 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
 }
 
 int shd_plan_free(shd_query* q) {
+  if (q && q->eng && q->eng->grouped) return fail(SHD_E_ARG, "query belongs to a group: free the group first");
   if (q) {
     if (q->eng && q->eng->stream) (void)hipStreamSynchronize(q->eng->stream);
     delete q;
@@ -754,58 +759,75 @@ int shd_set_time(shd_query* q, int64_t ts) {
   });
 }
 
+}  // extern "C"
+
+namespace {
+// shd_push's body: validate b against q's schema, stage it (host batches into
+// q's pinned staging + H2D on q's stream), push; a NeedNfa from the engine goes
+// to on_need_nfa with the staged batch and the counters before the push.
+template <class OnNfa>
+int push_batch(shd_query* q, const shd_batch* b, OnNfa&& on_need_nfa) {
+  Engine& e = *q->eng;
+  if (b->stream < 0 || b->stream >= (int)e.plan.stream_types.size()) return fail(SHD_E_ARG, "bad stream index");
+  const auto& types = e.plan.stream_types[b->stream];
+  if (b->ncols != (int)types.size()) return fail(SHD_E_ARG, "column count does not match the stream schema");
+  if ((int)types.size() > kMaxCols) return fail(SHD_E_UNSUPPORTED, "too many attributes");
+  if (b->n < 0 || (b->n > 0 && (!b->ts || !b->cols))) return fail(SHD_E_ARG, "bad batch");
+  if (b->n == 0) return SHD_OK;
+  // every column carries n value slots, null rows included (device kernels
+  // load the value and the null byte together)
+  for (int c = 0; c < b->ncols; c++)
+    if (!b->cols[c]) return fail(SHD_E_ARG, "null column pointer (null rows still need a value slot)");
+  SHD_HIP(hipSetDevice(q->ctx->device));
+  Staged st;
+  st.stream = b->stream;
+  st.n = b->n;
+  st.advance_time = b->advance_time != 0;
+  if (b->ncalls > 0 && b->call_offsets) {
+    st.call_offsets.assign(b->call_offsets, b->call_offsets + b->ncalls + 1);
+    if (st.call_offsets.front() != 0 || st.call_offsets.back() != b->n) return fail(SHD_E_ARG, "bad call offsets");
+  } else {
+    st.call_offsets = {0, b->n};
+  }
+  st.cs.ncols = b->ncols;
+  st.cs.n = b->n;
+  if (b->mem == SHD_MEM_DEVICE) {
+    st.cs.ts = b->ts;
+    for (int c = 0; c < b->ncols; c++) {
+      st.cs.col[c] = b->cols[c];
+      st.cs.nul[c] = b->nulls ? b->nulls[c] : nullptr;
+      st.cs.type[c] = (int8_t)types[c];
+    }
+  } else {
+    // Host batches: copy into library-owned pinned memory, then H2D on the
+    // query's stream.
+    stage_host(e.stream, q->pin, q->stage_ts, q->stage_col, q->stage_nul, b, types, st);
+  }
+  if (b->use_base_seq) {
+    if (b->base_seq < e.seq) return fail(SHD_E_ARG, "base_seq precedes events already pushed");
+    e.seq = b->base_seq;   // in_seq of this batch's rows = base_seq + row
+  }
+  const shd_counters before = e.counters;
+  e.args_begin();
+  try {
+    e.push(st);
+  } catch (NeedNfa& nf) {
+    on_need_nfa(st, before, nf);
+  }
+  q->eng->counters.kernel_ns_total += q->eng->counters.kernel_ns;
+  return SHD_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int shd_push(shd_query* q, const shd_batch* b) {
   return guarded([&]() -> int {
     if (!q || !b) return fail(SHD_E_ARG, "null argument");
-    Engine& e = *q->eng;
-    if (b->stream < 0 || b->stream >= (int)e.plan.stream_types.size()) return fail(SHD_E_ARG, "bad stream index");
-    const auto& types = e.plan.stream_types[b->stream];
-    if (b->ncols != (int)types.size()) return fail(SHD_E_ARG, "column count does not match the stream schema");
-    if ((int)types.size() > kMaxCols) return fail(SHD_E_UNSUPPORTED, "too many attributes");
-    if (b->n < 0 || (b->n > 0 && (!b->ts || !b->cols))) return fail(SHD_E_ARG, "bad batch");
-    if (b->n == 0) return SHD_OK;
-    // every column carries n value slots, null rows included (device kernels
-    // load the value and the null byte together)
-    for (int c = 0; c < b->ncols; c++)
-      if (!b->cols[c]) return fail(SHD_E_ARG, "null column pointer (null rows still need a value slot)");
-    SHD_HIP(hipSetDevice(q->ctx->device));
-    Staged st;
-    st.stream = b->stream;
-    st.n = b->n;
-    st.advance_time = b->advance_time != 0;
-    if (b->ncalls > 0 && b->call_offsets) {
-      st.call_offsets.assign(b->call_offsets, b->call_offsets + b->ncalls + 1);
-      if (st.call_offsets.front() != 0 || st.call_offsets.back() != b->n) return fail(SHD_E_ARG, "bad call offsets");
-    } else {
-      st.call_offsets = {0, b->n};
-    }
-    st.cs.ncols = b->ncols;
-    st.cs.n = b->n;
-    if (b->mem == SHD_MEM_DEVICE) {
-      st.cs.ts = b->ts;
-      for (int c = 0; c < b->ncols; c++) {
-        st.cs.col[c] = b->cols[c];
-        st.cs.nul[c] = b->nulls ? b->nulls[c] : nullptr;
-        st.cs.type[c] = (int8_t)types[c];
-      }
-    } else {
-      // Host batches: copy into library-owned pinned memory, then H2D on the
-      // query's stream.
-      stage_host(e.stream, q->pin, q->stage_ts, q->stage_col, q->stage_nul, b, types, st);
-    }
-    if (b->use_base_seq) {
-      if (b->base_seq < e.seq) return fail(SHD_E_ARG, "base_seq precedes events already pushed");
-      e.seq = b->base_seq;   // in_seq of this batch's rows = base_seq + row
-    }
-    const shd_counters before = e.counters;
-    e.args_begin();
-    try {
-      e.push(st);
-    } catch (NeedNfa& nf) {
+    if (q->eng->grouped) return fail(SHD_E_ARG, "query belongs to a group: push through shd_group_push");
+    return push_batch(q, b, [&](const Staged& st, const shd_counters& before, const NeedNfa& nf) {
       switch_to_nfa(q, st, before, nf.what());
-    }
-    q->eng->counters.kernel_ns_total += q->eng->counters.kernel_ns;
-    return SHD_OK;
+    });
   });
 }
 
@@ -875,6 +897,7 @@ int shd_discard_output(shd_query* q) {
 int shd_reset(shd_query* q) {
   return guarded([&]() -> int {
     if (!q) return fail(SHD_E_ARG, "null query");
+    if (q->eng->grouped) return fail(SHD_E_ARG, "query belongs to a group: reset through shd_group_reset");
     SHD_HIP(hipStreamSynchronize(q->eng->stream));
     q->eng->reset();
     return SHD_OK;
@@ -904,6 +927,7 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
   return guarded([&]() -> int {
     if (!q || !data || !len) return fail(SHD_E_ARG, "null argument");
     Engine& e = *q->eng;
+    if (e.grouped) return fail(SHD_E_UNSUPPORTED, "a grouped query has no state of its own to snapshot");
     SHD_HIP(hipStreamSynchronize(e.stream));
     if (e.out.count > 0) return fail(SHD_E_ARG, "snapshot with unpolled output rows");
     SnapW w;
@@ -944,6 +968,7 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
   return guarded([&]() -> int {
     if (!q || (!data && len)) return fail(SHD_E_ARG, "null argument");
     Engine& cur = *q->eng;
+    if (cur.grouped) return fail(SHD_E_ARG, "query belongs to a group: free the group before restoring it");
     SHD_HIP(hipStreamSynchronize(cur.stream));
     SnapR r;
     r.p = (const uint8_t*)data;
@@ -1007,4 +1032,98 @@ int shd_get_counters(shd_query* q, shd_counters* c) {
   return SHD_OK;
 }
 
+// ---- query groups (include/siddhi_hip.h)
+struct shd_group {
+  shd_query* leader = nullptr;          // owned: loaded from the leader IR
+  std::vector<shd_query*> members;      // caller-owned
+  bool dissolved = false;               // members run alone (after a NeedNfa hand-over)
+};
+
+int shd_group_create(shd_ctx* ctx, const void* leader_ir, size_t len, shd_query* const* members, int n,
+                     shd_group** out) {
+  return guarded([&]() -> int {
+    if (!ctx || !leader_ir || !members || n <= 0 || !out) return fail(SHD_E_ARG, "bad arguments");
+    shd_query* lq = nullptr;
+    int rc = shd_plan_load(ctx, leader_ir, len, &lq);
+    if (rc != SHD_OK) return rc;
+    std::unique_ptr<shd_query> own(lq);
+    std::vector<Engine*> es;
+    for (int i = 0; i < n; i++) {
+      if (!members[i]) return fail(SHD_E_ARG, "null member");
+      if (members[i]->ctx->device != ctx->device) return fail(SHD_E_ARG, "group member on another device");
+      SHD_HIP(hipStreamSynchronize(members[i]->eng->stream));
+      es.push_back(members[i]->eng.get());
+    }
+    lq->eng->group_attach(es);
+    auto* g = new shd_group();
+    g->leader = own.release();
+    g->members.assign(members, members + n);
+    *out = g;
+    return SHD_OK;
+  });
+}
+
+int shd_group_push(shd_group* g, const shd_batch* b) {
+  return guarded([&]() -> int {
+    if (!g || !b) return fail(SHD_E_ARG, "null argument");
+    if (g->dissolved) {
+      for (shd_query* q : g->members) {
+        int rc = push_batch(q, b, [&](const Staged& st, const shd_counters& before, const NeedNfa& nf) {
+          switch_to_nfa(q, st, before, nf.what());
+        });
+        if (rc != SHD_OK) return rc;
+      }
+      return SHD_OK;
+    }
+    shd_query* lq = g->leader;
+    return push_batch(lq, b, [&](const Staged& st, const shd_counters&, const NeedNfa& nf) {
+      // the leader's open partials, replayed into each member's generic NFA
+      // engine, rebuild exactly that member's (its f1 re-selects them); each
+      // member then takes this batch on its own and the group runs dissolved
+      SHD_HIP(hipStreamSynchronize(lq->eng->stream));
+      std::vector<Replay> parts;
+      lq->eng->export_replay(parts);
+      const int64_t seq = lq->eng->seq;
+      lq->eng->group_detach();
+      g->dissolved = true;
+      for (shd_query* q : g->members) {
+        q->eng->seq = seq;
+        const shd_counters before = q->eng->counters;
+        switch_to_nfa(q, st, before, nf.what(), &parts);
+        q->eng->counters.kernel_ns_total += q->eng->counters.kernel_ns;
+      }
+    });
+  });
+}
+
+int shd_group_reset(shd_group* g) {
+  return guarded([&]() -> int {
+    if (!g) return fail(SHD_E_ARG, "null group");
+    SHD_HIP(hipStreamSynchronize(g->leader->eng->stream));
+    g->leader->eng->reset();
+    for (shd_query* q : g->members) {
+      SHD_HIP(hipStreamSynchronize(q->eng->stream));
+      q->eng->reset();
+    }
+    return SHD_OK;
+  });
+}
+
+int shd_group_leader(shd_group* g, shd_query** leader) {
+  if (!g || !leader) return fail(SHD_E_ARG, "null argument");
+  *leader = g->leader;
+  return SHD_OK;
+}
+
+int shd_group_free(shd_group* g) {
+  if (!g) return SHD_OK;
+  (void)hipStreamSynchronize(g->leader->eng->stream);
+  g->leader->eng->group_detach();
+  for (shd_query* q : g->members) q->eng->reset();
+  delete g->leader;
+  delete g;
+  return SHD_OK;
+}
+
 }  // extern "C"
+

@@ -27,7 +27,9 @@ ENGINE_NAMES = {1: "pattern-forward-scan", 2: "window-aggregate", 3: "filter-pro
 EXPORTED = ["shd_device_count", "shd_ctx_create", "shd_ctx_destroy", "shd_plan_load", "shd_plan_free",
             "shd_plan_engine", "shd_set_time", "shd_push", "shd_flush", "shd_poll", "shd_discard_output",
             "shd_reset", "shd_get_counters", "shd_query_stream", "shd_stage_times", "shd_snapshot", "shd_restore",
-            "shd_set_option", "shd_route_words", "shd_route_bucket_scratch", "shd_route_bucket", "shd_route_merge", "shd_last_error"]
+            "shd_set_option", "shd_route_words", "shd_route_bucket_scratch", "shd_route_bucket", "shd_route_merge",
+            "shd_group_create", "shd_group_push", "shd_group_reset", "shd_group_leader", "shd_group_free",
+            "shd_last_error"]
 
 
 class SiddhiHipError(RuntimeError):
@@ -93,6 +95,11 @@ def load_library(path: str = LIB_PATH):
         lib.shd_route_bucket_scratch.argtypes = [I64, I, ctypes.POINTER(ctypes.c_size_t)]
         lib.shd_route_bucket.argtypes = [P, P, I64, I, P, I, I, P, P, P, I64, P, P, P]
         lib.shd_route_merge.argtypes = [P, P, I, P, P, I64, I64, I64, I64, I, P, P, P, P, P, P]
+        lib.shd_group_create.argtypes = [P, P, ctypes.c_size_t, P, I, ctypes.POINTER(P)]
+        lib.shd_group_push.argtypes = [P, ctypes.POINTER(ShdBatch)]
+        lib.shd_group_reset.argtypes = [P]
+        lib.shd_group_leader.argtypes = [P, ctypes.POINTER(P)]
+        lib.shd_group_free.argtypes = [P]
         lib.shd_last_error.restype = ctypes.c_char_p
         for f in EXPORTED:
             if f != "shd_last_error":
@@ -115,6 +122,36 @@ def context(device: int = 0):
         _check(lib.shd_ctx_create(dev, 1, ctypes.byref(ctx)))
         _ctx = ctx
     return _ctx
+
+
+def make_batch(stream, n, ts_ptr, col_ptrs, null_ptrs, mem=SHD_MEM_HOST, call_offsets=None, advance_time=True,
+               base_seq=None):
+    """An shd_batch over the given pointers, and the ctypes arrays it points
+    into (keep them alive until the push returns)."""
+    ncols = len(col_ptrs)
+    cols = (ctypes.c_void_p * max(ncols, 1))(*col_ptrs)
+    nulls = (ctypes.c_void_p * max(ncols, 1))(*null_ptrs)
+    b = ShdBatch()
+    b.stream = stream
+    b.mem = mem
+    b.n = n
+    b.ts = ts_ptr
+    b.ncols = ncols
+    b.cols = ctypes.cast(cols, ctypes.c_void_p)
+    b.nulls = ctypes.cast(nulls, ctypes.c_void_p)
+    co = None
+    if call_offsets is not None:
+        co = np.ascontiguousarray(call_offsets, np.int64)
+        b.ncalls = len(co) - 1
+        b.call_offsets = co.ctypes.data
+    else:
+        b.ncalls = 0
+        b.call_offsets = None
+    b.advance_time = 1 if advance_time else 0
+    if base_seq is not None:
+        b.use_base_seq = 1
+        b.base_seq = int(base_seq)
+    return b, (cols, nulls, co)
 
 
 class DeviceQuery:
@@ -151,29 +188,7 @@ class DeviceQuery:
                  call_offsets: np.ndarray = None, advance_time=True, base_seq=None):
         """shd_push.  base_seq: arrival index of the first event in the whole
         (sharded) stream, so that in_seq of the rows is global (shd_batch.base_seq)."""
-        ncols = len(col_ptrs)
-        cols = (ctypes.c_void_p * max(ncols, 1))(*col_ptrs)
-        nulls = (ctypes.c_void_p * max(ncols, 1))(*null_ptrs)
-        b = ShdBatch()
-        b.stream = stream
-        b.mem = mem
-        b.n = n
-        b.ts = ts_ptr
-        b.ncols = ncols
-        b.cols = ctypes.cast(cols, ctypes.c_void_p)
-        b.nulls = ctypes.cast(nulls, ctypes.c_void_p)
-        if call_offsets is not None:
-            co = np.ascontiguousarray(call_offsets, np.int64)
-            b.ncalls = len(co) - 1
-            b.call_offsets = co.ctypes.data
-        else:
-            co = None
-            b.ncalls = 0
-            b.call_offsets = None
-        b.advance_time = 1 if advance_time else 0
-        if base_seq is not None:
-            b.use_base_seq = 1
-            b.base_seq = int(base_seq)
+        b, keep = make_batch(stream, n, ts_ptr, col_ptrs, null_ptrs, mem, call_offsets, advance_time, base_seq)
         _check(self.lib.shd_push(self.q, ctypes.byref(b)))
 
     def set_time(self, t):
@@ -246,6 +261,64 @@ class DeviceQuery:
         s = ctypes.c_void_p()
         _check(self.lib.shd_query_stream(self.q, ctypes.byref(s)))
         return s.value
+
+
+class DeviceGroup:
+    """shd_group over fresh member DeviceQuery objects: one forward scan of the
+    leader plan (planner.share_pattern_queries) serves every member; poll the
+    members as usual.  Close the group before the members."""
+
+    def __init__(self, leader_ir: bytes, members: List[DeviceQuery], device: int = 0):
+        self.lib = load_library()
+        ctx = context(device)
+        self._ir = ctypes.create_string_buffer(leader_ir, len(leader_ir))
+        arr = (ctypes.c_void_p * len(members))(*[m.q.value for m in members])
+        g = ctypes.c_void_p()
+        _check(self.lib.shd_group_create(ctx, self._ir, len(leader_ir), arr, len(members), ctypes.byref(g)))
+        self.g = g
+        self.members = list(members)
+
+    def push_raw(self, stream, n, ts_ptr, col_ptrs, null_ptrs, mem=SHD_MEM_HOST, call_offsets=None,
+                 advance_time=True, base_seq=None):
+        b, keep = make_batch(stream, n, ts_ptr, col_ptrs, null_ptrs, mem, call_offsets, advance_time, base_seq)
+        _check(self.lib.shd_group_push(self.g, ctypes.byref(b)))
+
+    def reset(self):
+        _check(self.lib.shd_group_reset(self.g))
+
+    def _leader(self):
+        q = ctypes.c_void_p()
+        _check(self.lib.shd_group_leader(self.g, ctypes.byref(q)))
+        return q
+
+    def leader_engine_kind(self) -> int:
+        e = ctypes.c_int()
+        _check(self.lib.shd_plan_engine(self._leader(), ctypes.byref(e)))
+        return e.value
+
+    def counters(self) -> dict:
+        """The shared scan's counters (the leader query's)."""
+        c = ShdCounters()
+        _check(self.lib.shd_get_counters(self._leader(), ctypes.byref(c)))
+        return {f: getattr(c, f) for f, _ in ShdCounters._fields_}
+
+    def stage_times(self) -> dict:
+        ns = (ctypes.c_int64 * 16)()
+        names = (ctypes.c_char_p * 16)()
+        n = ctypes.c_int()
+        _check(self.lib.shd_stage_times(self._leader(), ns, names, 16, ctypes.byref(n)))
+        return {names[i].decode(): ns[i] for i in range(n.value)}
+
+    def close(self):
+        if self.g:
+            self.lib.shd_group_free(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class HipQueryEngine:

@@ -634,3 +634,104 @@ def classify_state_shape(plan: Plan, si: qc.StateInput) -> Dict:
             and not el.a.inner.absent and not el.b.absent:
         shape["every_a_then_b"] = True
     return shape
+
+
+# ---------------------------------------------------------------- query sharing
+# Queries on one StreamJunction (C/stream/StreamJunction.java:146-272) of the
+# form `every e1=A[f1] -> e2=B[f2] within W` that differ only in f1 (and in
+# their names / targets) share one forward scan on the device (shd_group_*,
+# include/siddhi_hip.h): the leader plan's e1 filter accepts every event any
+# member's does, and each member keeps the leader's matches whose e1 passes
+# its own f1.
+
+def _e1_site(q: qc.Query):
+    """The e1 StreamSE of an `every e1=A[..] -> e2=B[..]` pattern query, else None."""
+    si = q.input
+    if not isinstance(si, qc.StateInput) or si.kind != "pattern":
+        return None
+    el = si.element
+    if not isinstance(el, qc.NextSE) or not isinstance(el.b, qc.StreamSE) or not isinstance(el.a, qc.EverySE):
+        return None
+    a = el.a.inner
+    if not isinstance(a, qc.StreamSE) or a.absent or el.b.absent:
+        return None
+    return a
+
+
+def share_signature(q: qc.Query) -> Optional[str]:
+    """Equal for two queries iff they differ at most in the e1 filter, the
+    query name, annotations and the insert target (None: not shareable)."""
+    if _e1_site(q) is None or q.output_rate is not None:
+        return None
+    import copy
+    q2 = copy.deepcopy(q)
+    q2.name, q2.target, q2.annotations = None, "", []
+    _e1_site(q2).filters = []
+    return repr(q2)
+
+
+_NUMERIC = ("int", "long", "float", "double")
+
+
+def _threshold(fs):
+    """(op, var, const) when the filter list is one `attr op constant` with op in > >= < <=."""
+    if len(fs) != 1:
+        return None
+    f = fs[0]
+    if (isinstance(f, qc.BinOp) and f.op in (">", ">=", "<", "<=") and isinstance(f.left, qc.Var)
+            and f.left.index is None and isinstance(f.right, qc.Const) and f.right.type in _NUMERIC):
+        return f.op, f.left, f.right
+    return None
+
+
+def leader_e1_filters(filter_lists: List[list]) -> list:
+    """e1 filters accepting every event any of the lists accepts: one bound
+    when all are `attr > c` (or >=, <, <=) on the same attribute, else the
+    disjunction of each member's conjunction."""
+    if any(len(fs) == 0 for fs in filter_lists):
+        return []
+    th = [_threshold(fs) for fs in filter_lists]
+    if all(t is not None for t in th) and len({(t[0], repr(t[1])) for t in th}) == 1:
+        op = th[0][0]
+        pick = min if op in (">", ">=") else max
+        c = pick((t[2] for t in th), key=lambda k: k.value)
+        return [qc.BinOp(op, th[0][1], c)]
+    conj = []
+    for fs in filter_lists:
+        e = fs[0]
+        for f in fs[1:]:
+            e = qc.BinOp("and", e, f)
+        conj.append(e)
+    e = conj[0]
+    for c in conj[1:]:
+        e = qc.BinOp("or", e, c)
+    return [e]
+
+
+def share_groups(queries: List[qc.Query], max_members: int = 64) -> List[List[int]]:
+    """Indices of shareable queries, grouped (>= 2 members, at most max_members each)."""
+    by: Dict[str, List[int]] = {}
+    for i, q in enumerate(queries):
+        sig = share_signature(q)
+        if sig is not None:
+            by.setdefault(sig, []).append(i)
+    out = []
+    for idx in by.values():
+        for k in range(0, len(idx), max_members):
+            part = idx[k:k + max_members]
+            if len(part) >= 2:
+                out.append(part)
+    return out
+
+
+def plan_shared_leader(app: qc.SiddhiApp, members: List[qc.Query], dictionary: StringDictionary,
+                       partition: Optional[qc.Partition] = None) -> QueryPlan:
+    """The leader plan of a group of shareable queries (share_groups)."""
+    import copy
+    sigs = {share_signature(q) for q in members}
+    if len(sigs) != 1 or None in sigs:
+        raise UnsupportedPlanException("queries differ beyond the e1 filter: not shareable")
+    lead = copy.deepcopy(members[0])
+    lead.name = "shared(%s)" % ",".join(str(q.name) for q in members)
+    _e1_site(lead).filters = leader_e1_filters([_e1_site(q).filters for q in members])
+    return plan_query(app, lead, dictionary, partition)
