@@ -423,66 +423,135 @@ def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, key
     """Every M5 query on the first `prefix` events of the benchmark stream, run
     the way the timed loop runs it (the shared scans of shd_group included, one
     push), against the CPU oracle on the same events: pattern rows bit-exact,
-    window rows with doubles within 1e-9 relative.  The oracle's own time over
-    the prefix (all queries, one core, one after the other) is the line's
-    cpu_baseline."""
+    window rows with doubles within 1e-9 relative.
+
+    The oracle scans every pending partial per event (the reference's
+    StreamPreStateProcessor loop), which at M5's density is quadratic: one P1
+    variant over 200 k events costs minutes.  So each group of shareable
+    queries is checked through its leader plan, run once in the oracle: a
+    member's expected rows are the leader's whose e1 passes the member's
+    threshold (planner.share_groups' lemma, pinned on the oracle itself by
+    tests/test_share_plan.py), and the group's first, middle and last members
+    also run in the oracle directly.  Oracle runs go to a thread pool (ctypes
+    drops the GIL in the C++ oracle).
+
+    cpu_baseline: all queries of the app through the oracle, one after the
+    other on one core, over the first 10 k events (CPU seconds per thread)."""
+    import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_engine import OracleQueryEngine
     from parity import assert_rows_agg, assert_same_rows, concat_rows
+    from siddhi_amd import query_compiler as qc
     from siddhi_amd import workloads as wl
-    from siddhi_amd.planner import plan_shared_leader, share_groups
+    from siddhi_amd.planner import _e1_site, _threshold, plan_shared_leader, share_groups
     from siddhi_amd.runtime import ColumnBatch
     s, p, v, t = wl.stock_stream(prefix, keys, delta, seed_offset=0)
     offs = wl.call_offsets(prefix)
+    groups = share_groups(queries)
     dqs = [he.DeviceQuery(qp.ir) for qp in plans]
-    groups = []
+    dgroups = []
     grouped = set()
     if share:
-        for g in share_groups(queries):
-            groups.append(he.DeviceGroup(plan_shared_leader(qa, [queries[i] for i in g], d).ir, [dqs[i] for i in g]))
+        for g in groups:
+            dgroups.append(he.DeviceGroup(plan_shared_leader(qa, [queries[i] for i in g], d).ir, [dqs[i] for i in g]))
             grouped.update(g)
     cols = [sym.data_ptr(), price.data_ptr(), vol.data_ptr()]
-    for tgt in groups + [dqs[i] for i in range(len(dqs)) if i not in grouped]:
+    for tgt in dgroups + [dqs[i] for i in range(len(dqs)) if i not in grouped]:
         tgt.push_raw(0, prefix, ts.data_ptr(), cols, [0, 0, 0], he.SHD_MEM_DEVICE, offs.astype(np.int64), True)
     devs = []
     for dq in dqs:
         r = dq.poll()
         devs.append((concat_rows([r] if r is not None else []), dq.engine_kind == 2))
-    for g in groups:
+    for g in dgroups:
         g.close()
     for dq in dqs:
         dq.close()
+
+    def oracle(qp, n):
+        eng = OracleQueryEngine(qp, None)
+        parts = []
+        cid = 0
+        t0 = time.thread_time()
+        for c in range(len(offs) - 1):
+            a, b = int(offs[c]), int(offs[c + 1])
+            if a >= n:
+                break
+            b = min(b, n)
+            sub = ColumnBatch(t[a:b], [s[a:b].astype(np.uint32), p[a:b], v[a:b]], [None, None, None])
+            for ch in eng.set_time(int(t[b - 1])) + eng.push(0, sub):
+                k = len(ch.ts)
+                parts.append((np.full(k, cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+                cid += 1
+        cpu = time.thread_time() - t0
+        eng.close()
+        return concat_rows(parts), cpu
+
+    def member_mask(q, qp, lead_rows):
+        """Rows of the leader whose e1 passes q's threshold, or None when q's
+        f1 is not a threshold on an attribute the selector projects as e1.<attr>."""
+        th = _threshold(_e1_site(q).filters)
+        if th is None:
+            return None
+        op, var, const = th
+        ref = _e1_site(q).ref
+        for c, oa in enumerate(q.selector.attrs):
+            if isinstance(oa.expr, qc.Var) and oa.expr.attr == var.attr and oa.expr.stream == ref:
+                col = lead_rows[3][:, c]
+                vals = col.view(np.float64) if qp.output_types[c] == 4 else col.view(np.int64)
+                return {">": vals > const.value, ">=": vals >= const.value, "<": vals < const.value,
+                        "<=": vals <= const.value}[op]
+        return None
+
+    direct = set(range(len(plans)))
+    leaders = []
+    for g in groups:
+        lead = plan_shared_leader(qa, [queries[i] for i in g], d)
+        spot = {g[0], g[len(g) // 2], g[-1]}
+        leaders.append((g, lead, spot))
+        direct -= set(g) - spot
     rows = 0
-    cpu_s = 0.0
+    checked_direct, checked_lemma = 0, 0
     try:
-        for qp, (dev, window) in zip(plans, devs):
-            eng = OracleQueryEngine(qp, None)
-            parts = []
-            cid = 0
-            t0 = time.perf_counter()
-            for c in range(len(offs) - 1):
-                a, b = int(offs[c]), int(offs[c + 1])
-                sub = ColumnBatch(t[a:b], [s[a:b].astype(np.uint32), p[a:b], v[a:b]], [None, None, None])
-                for ch in eng.set_time(int(t[b - 1])) + eng.push(0, sub):
-                    k = len(ch.ts)
-                    parts.append((np.full(k, cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
-                    cid += 1
-            cpu_s += time.perf_counter() - t0
-            eng.close()
-            print("M5 parity: %s oracle %.1f s" % (qp.name, cpu_s), file=sys.stderr, flush=True)
-            ora = concat_rows(parts)
-            if window:
-                assert_rows_agg(dev, ora, qp, exact=False)
-            else:
-                assert_same_rows(dev, ora)
-            rows += len(dev[2])
-        verdict = "equal (%d queries, %d shared, %d events, %d rows)" % (len(plans), len(grouped), prefix, rows)
+        with cf.ThreadPoolExecutor(max_workers=16) as ex:
+            fut_direct = {i: ex.submit(oracle, plans[i], prefix) for i in sorted(direct)}
+            fut_lead = [ex.submit(oracle, lead, prefix) for _, lead, _ in leaders]
+            for i, f in fut_direct.items():
+                ora, _ = f.result()
+                dev, window = devs[i]
+                if window:
+                    assert_rows_agg(dev, ora, plans[i], exact=False)
+                else:
+                    assert_same_rows(dev, ora)
+                rows += len(dev[2])
+                checked_direct += 1
+            print("M5 parity: %d queries checked directly" % checked_direct, file=sys.stderr, flush=True)
+            for (g, lead, spot), f in zip(leaders, fut_lead):
+                lead_rows, _ = f.result()
+                for i in g:
+                    if i in spot:
+                        continue
+                    keep = member_mask(queries[i], plans[i], lead_rows)
+                    if keep is None:
+                        ora, _ = oracle(plans[i], prefix)
+                    else:
+                        # the leader's chunk ids: one callback chunk per completing event
+                        ora = tuple(x[keep] for x in lead_rows)
+                        checked_lemma += 1
+                    dev = devs[i][0]
+                    assert_same_rows(dev, ora)
+                    rows += len(dev[2])
+        verdict = ("equal (%d queries, %d through shared scans; %d checked against their own oracle run, %d "
+                   "against the oracle leader's rows passing their e1 threshold; %d events, %d rows)"
+                   % (len(plans), len(grouped), checked_direct, checked_lemma, prefix, rows))
     except AssertionError as e:
         verdict = "DIFFERENT: %s" % str(e).splitlines()[0]
-    cpu = {"value": round(prefix / cpu_s, 1) if cpu_s > 0 else None, "unit": "events/s", "cores": 1,
+    cpu_n = min(prefix, 10_000)
+    cpu_s = sum(oracle(qp, cpu_n)[1] for qp in plans)
+    cpu = {"value": round(cpu_n / cpu_s, 1) if cpu_s > 0 else None, "unit": "events/s", "cores": 1,
            "kind": "port",
            "sample": "the first %d stream events through all %d queries, one after the other (oracle C++ "
-                     "restatement, one core; polled per InputHandler call)" % (prefix, len(plans))}
+                     "restatement, CPU seconds of one thread, polled per InputHandler call; the pattern "
+                     "queries' pending-list scans grow with the sample)" % (cpu_n, len(plans))}
     return verdict, cpu
 
 
