@@ -38,6 +38,7 @@ constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
 // segmented scans only while every operand seen so far is finite and the
 // non-zero magnitudes span at most 2^kSegMaxExpSpan (k_operand_stats)
 constexpr uint32_t kSegMaxExpSpan = 30;
+constexpr int kMaxChan = 4;                   // distinct aggregated expressions (segmented scans)
 
 struct RowCtx {
   const ColSet* cs;
@@ -204,7 +205,57 @@ struct ItemArgs {
   uint64_t* gh;
   int64_t gstride;            // words per group attribute in gkw (>= new items)
   int64_t C;
+  int time_window;            // the item's time and call time are read (k_expiry) only by time windows
 };
+
+// Window item t (new item number inew = t - C) from event i.
+__device__ __forceinline__ void make_item(const ItemArgs& a, int64_t i, int64_t inew, const int32_t* call_of,
+                                          const int64_t* call_now, uint64_t* ikey, int64_t* its, uint64_t* iargv,
+                                          uint8_t* iargn, int32_t* ievrow, int32_t* icall, int64_t* inow,
+                                          int64_t cap) {
+  const DExprSet es = a.es;
+  const ColSet& cs = a.cs;
+  const int64_t t = a.C + inew;
+  RowCtx cx{&cs, i, nullptr, nullptr};
+  uint64_t k = 0;
+  if (a.ngroup) {
+    // GroupByKeyGenerator.constructEventKey: String.valueOf of every value
+    // joined -- canonical words with the same identifications (group_word)
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    uint8_t nm = 0;
+    for (int g = 0; g < a.ngroup; g++) {
+      Val kv = a.group_col[g] >= 0 ? col_load(cs, i, a.group_col[g])
+                                   : eval_expr(es.ins + a.group[g].off, a.group[g].len, es.consts, cx);
+      bool isnull = false;
+      const uint64_t w = group_word(kv, a.group_type[g], a.null_str_id, isnull);
+      if (a.dense) {
+        k = isnull ? 2u : w;   // bool null: its own group (the text "null")
+      } else {
+        a.gkw[(int64_t)g * a.gstride + inew] = w;
+        nm |= (uint8_t)((isnull ? 1u : 0u) << g);
+        h = gdict_mix(h ^ gdict_mix(w + 0x632BE59BD9B4E019ull * (uint64_t)(g + 1)));
+      }
+    }
+    if (!a.dense) {
+      h = gdict_mix(h ^ ((uint64_t)nm << 56));
+      a.gkn[inew] = nm;
+      a.gh[inew] = h;
+    }
+  }
+  ikey[t] = k;
+  if (a.time_window) its[t] = cs.ts[i];
+  for (int g = 0; g < a.nagg; g++) {
+    if (!a.has_arg[g]) continue;   // count(): no operand (agg_step never reads it)
+    const Val v = a.arg_col[g] >= 0 ? col_load(cs, i, a.arg_col[g])
+                                    : eval_expr(es.ins + a.agg_arg[g].off, a.agg_arg[g].len, es.consts, cx);
+    iargv[g * cap + t] = v.b;
+    iargn[g * cap + t] = (uint8_t)v.null;
+  }
+  ievrow[t] = (int32_t)i;
+  const int32_t c = call_of[i];
+  icall[t] = c;
+  if (a.time_window) inow[t] = call_now[c];
+}
 
 // New window items (one per filtered event), appended after the carried ones.
 __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restrict__ ap, int64_t n, const uint32_t* cnt, const uint32_t* off,
@@ -213,52 +264,167 @@ __global__ __launch_bounds__(kBlock) void k_make_items(const ItemArgs* __restric
                                                        int32_t* ievrow, int32_t* icall, int64_t* inow, int64_t cap,
                                                        uint32_t* null_key_flag) {
   const ItemArgs& a = *ap;   // args live in device memory (Engine::dev_args)
-  const DExprSet es = a.es;
-  const ColSet& cs = a.cs;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) {
     if (!cnt[i]) continue;
-    int64_t t = a.C + off[i];
-    RowCtx cx{&cs, i, nullptr, nullptr};
-    uint64_t k = 0;
-    if (a.ngroup) {
-      // GroupByKeyGenerator.constructEventKey: String.valueOf of every value
-      // joined -- canonical words with the same identifications (group_word)
-      uint64_t h = 0x9E3779B97F4A7C15ull;
-      uint8_t nm = 0;
-      for (int g = 0; g < a.ngroup; g++) {
-        Val kv = a.group_col[g] >= 0 ? col_load(cs, i, a.group_col[g])
-                                     : eval_expr(es.ins + a.group[g].off, a.group[g].len, es.consts, cx);
-        bool isnull = false;
-        const uint64_t w = group_word(kv, a.group_type[g], a.null_str_id, isnull);
-        if (a.dense) {
-          k = isnull ? 2u : w;   // bool null: its own group (the text "null")
-        } else {
-          a.gkw[(int64_t)g * a.gstride + off[i]] = w;
-          nm |= (uint8_t)((isnull ? 1u : 0u) << g);
-          h = gdict_mix(h ^ gdict_mix(w + 0x632BE59BD9B4E019ull * (uint64_t)(g + 1)));
+    make_item(a, i, off[i], call_of, call_now, ikey, its, iargv, iargn, ievrow, icall, inow, cap);
+  }
+}
+
+// Look-back status words: a device-coherent plain load (no read-modify-write:
+// many workgroups poll the same words, and atomics on one line serialise in L2)
+__device__ __forceinline__ uint64_t cw_status_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Filter + window items in one pass (aggregate queries outside partitions):
+// tiles of kFiTile events in arrival order; a tile's passing events become
+// items at the tile's offset, found by a decoupled look-back over the tiles
+// (each tile publishes its count first).  Also: the first item of every
+// InputHandler call (citem, for the call-window path), the largest new group
+// id, and the range guard's operand statistics (k_operand_stats).
+constexpr int kFiPer = 8;
+constexpr int kFiTile = kBlock * kFiPer;
+
+struct FusedArgs {
+  FilterArgs f;
+  ItemArgs it;
+  const int32_t* call_of;
+  const int64_t* call_now;
+  uint64_t* ikey;
+  int64_t* its;
+  uint64_t* iargv;
+  uint8_t* iargn;
+  int32_t* ievrow;
+  int32_t* icall;
+  int64_t* inow;
+  int64_t cap;
+  uint64_t* status;     // [tiles] look-back words (zeroed)
+  uint32_t* citem;      // [ncalls + 1]
+  int ncalls;
+  uint32_t* m_out;      // new items
+  unsigned long long* kmax_out;
+  int nch;              // range guard channels (0: none)
+  int ch_agg[kMaxChan];
+  int ch_f32[kMaxChan];
+  uint32_t* opstats;    // [3]: non-finite flag, max / min binary exponent
+  int probe;            // timing experiments (SHD_FI_PROBE): 1 = no look-back wait, 2 = no item writes
+};
+
+__global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __restrict__ ap, int64_t n) {
+  const FusedArgs& a = *ap;
+  const FilterArgs& fa = a.f;
+  __shared__ uint32_t wcnt[kFiPer][kBlock / 64];
+  __shared__ uint32_t tbase;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kFiTile;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t bal[kFiPer];
+  for (int j = 0; j < kFiPer; j++) {
+    const int64_t i = base + j * kBlock + threadIdx.x;
+    bool pass = false;
+    if (i < n) {
+      RowCtx cx{&fa.cs, i, nullptr, nullptr};
+      pass = eval_filters(fa.es, fa.filters, cx);
+    }
+    bal[j] = __ballot(pass);
+    if (lane == 0) wcnt[j][w] = (uint32_t)__popcll(bal[j]);
+  }
+  __syncthreads();
+  constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
+  if (threadIdx.x < 64) {
+    uint32_t local = 0;
+    for (int j = 0; j < kFiPer; j++)
+      for (int k = 0; k < kBlock / 64; k++) local += wcnt[j][k];
+    const int c = blockIdx.x;
+    if (lane == 0)
+      atomicExch((unsigned long long*)&a.status[c], (unsigned long long)((c == 0 ? kInc : kAgg) | local));
+    uint64_t tb = 0;
+    for (int top = (a.probe & 1) ? -1 : c - 1; top >= 0;) {
+      const int j = top - lane;
+      const uint64_t st = j >= 0 ? cw_status_load(&a.status[j]) : kInc;
+      if (__any((st >> 62) == 0)) {   // an earlier, running workgroup has not published yet
+        __builtin_amdgcn_s_sleep(4);
+        continue;
+      }
+      const uint64_t incl = __ballot((st >> 62) == 2);
+      const int stop = incl ? __ffsll((long long)incl) - 1 : 64;
+      uint64_t v = lane <= stop && j >= 0 ? (st & kVal) : 0ull;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      tb += v;
+      if (incl) break;
+      top -= 64;
+    }
+    if (lane == 0) {
+      if (c > 0) atomicExch((unsigned long long*)&a.status[c], (unsigned long long)(kInc | (tb + local)));
+      tbase = (uint32_t)tb;
+      if (base + kFiTile >= n) {   // the last tile: the push's item count, trailing empty calls
+        const uint32_t m = (uint32_t)(tb + local);
+        *a.m_out = m;
+        const int c0 = n > 0 ? a.call_of[n - 1] + 1 : 0;
+        for (int cc = c0; cc <= a.ncalls; cc++) a.citem[cc] = (uint32_t)(a.it.C + m);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t pre = tbase;
+  uint64_t kmax = 0;
+  uint32_t nf = 0, emax = 0, emin = 0xFFFFFFFFu;
+  for (int j = 0; j < kFiPer; j++) {
+    uint32_t before_w = 0, tot_j = 0;
+    for (int k = 0; k < kBlock / 64; k++) {
+      before_w += k < w ? wcnt[j][k] : 0u;
+      tot_j += wcnt[j][k];
+    }
+    const int64_t i = base + j * kBlock + threadIdx.x;
+    const uint32_t pos = pre + before_w + (uint32_t)__popcll(bal[j] & below);   // items before event i
+    if (i < n) {
+      // first event of one or more calls (empty calls share their start event)
+      const int32_t ci = a.call_of[i];
+      const int32_t cp = i > 0 ? a.call_of[i - 1] : -1;
+      for (int cc = cp + 1; cc <= ci; cc++) a.citem[cc] = (uint32_t)(a.it.C + pos);
+      if (((bal[j] >> lane) & 1ull) && !(a.probe & 2)) {
+        make_item(a.it, i, pos, a.call_of, a.call_now, a.ikey, a.its, a.iargv, a.iargn, a.ievrow, a.icall, a.inow,
+                  a.cap);
+        const int64_t t = a.it.C + pos;
+        kmax = a.ikey[t] > kmax ? a.ikey[t] : kmax;
+        for (int ch = 0; ch < a.nch; ch++) {
+          const int g = a.ch_agg[ch];
+          if (a.iargn[(int64_t)g * a.cap + t]) continue;
+          const uint64_t b = a.iargv[(int64_t)g * a.cap + t];
+          const double d = a.ch_f32[ch] ? (double)__uint_as_float((uint32_t)b) : __longlong_as_double((long long)b);
+          if (!(d - d == 0.0)) {   // Inf or NaN
+            nf = 1;
+            continue;
+          }
+          if (d == 0.0) continue;
+          const uint32_t e = (uint32_t)((__double_as_longlong(d) >> 52) & 0x7FF);
+          emax = e > emax ? e : emax;
+          emin = e < emin ? e : emin;
         }
       }
-      if (!a.dense) {
-        h = gdict_mix(h ^ ((uint64_t)nm << 56));
-        a.gkn[off[i]] = nm;
-        a.gh[off[i]] = h;
-      }
     }
-    ikey[t] = k;
-    its[t] = cs.ts[i];
-    for (int g = 0; g < a.nagg; g++) {
-      Val v;
-      v.b = 0;
-      v.null = 1;
-      if (a.has_arg[g])
-        v = a.arg_col[g] >= 0 ? col_load(cs, i, a.arg_col[g])
-                              : eval_expr(es.ins + a.agg_arg[g].off, a.agg_arg[g].len, es.consts, cx);
-      iargv[g * cap + t] = v.b;
-      iargn[g * cap + t] = (uint8_t)v.null;
+    pre += tot_j;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t km = __shfl_xor(kmax, o, 64);
+    kmax = km > kmax ? km : kmax;
+    nf |= __shfl_xor(nf, o, 64);
+    const uint32_t x = __shfl_xor(emax, o, 64), y = __shfl_xor(emin, o, 64);
+    emax = x > emax ? x : emax;
+    emin = y < emin ? y : emin;
+  }
+  // one word each for the whole push: an atomic only when this wave would
+  // change it (atomics on one address serialise in L2; the words settle fast)
+  if (lane == 0) {
+    if (kmax > cw_status_load((const uint64_t*)a.kmax_out)) atomicMax(a.kmax_out, (unsigned long long)kmax);
+    if (a.nch) {
+      if (nf && !__hip_atomic_load(&a.opstats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(&a.opstats[0], 1u);
+      if (emax > __hip_atomic_load(&a.opstats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&a.opstats[1], emax);
+      if (emin < __hip_atomic_load(&a.opstats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(&a.opstats[2], emin);
     }
-    ievrow[t] = (int32_t)i;
-    icall[t] = call_of[i];
-    inow[t] = call_now[call_of[i]];
   }
 }
 
@@ -885,7 +1051,6 @@ __global__ __launch_bounds__(kBlock) void k_fold_wave_d(const FoldArgs* __restri
 // Counts are exact integers.
 constexpr int kSegPer = 8;                    // positions per thread
 constexpr int kSegTile = kBlock * kSegPer;    // positions per tile (workgroup)
-constexpr int kMaxChan = 4;                   // distinct aggregated expressions
 
 struct DD {
   double hi, lo;
@@ -1365,6 +1530,530 @@ __global__ __launch_bounds__(kBlock) void k_seg_emit(const SegArgs* __restrict__
     r[0] = (uint64_t)x | ((uint64_t)nul << 32);
     for (int j = 0; j < a.nagg; j++) r[1 + j] = vals[j];
     first[xf] = 1;
+  }
+}
+
+// ---------------------------------------------------------------- call windows
+// Window aggregates per InputHandler call, without a global group sort (group
+// by, windows no longer than a few calls -- config W2-length).  The rows a call
+// emits are its groups' states after their last add of the call
+// (QuerySelector.processInBatchGroupBy, QuerySelector.java:315-373); group g's
+// state after item x is the set of its items q <= x that have not expired by
+// x (e[q] > x; LengthWindowProcessor / TimeWindowProcessor expire in FIFO
+// order before each add, so e is non-decreasing and every item of the call
+// sees a window inside [lb, x] with lb = first q with e[q] > the call's first
+// item).  One workgroup per call:
+//   1. the call's group ids go into an LDS hash table (first / last item of
+//      each group in the call);
+//   2. every item q of the region [lb, call end) whose group is in the table
+//      and lies in that group's window (q <= x_g, e[q] > x_g) is counted and
+//      listed under its group;
+//   3. one thread per group folds its listed items (double-double sums per
+//      channel, non-null counts) into the run record k_emit reads -- the same
+//      record k_seg_emit writes, at the run's first item.
+// The region is read from L2 by ~(L + call items) / call items neighbouring
+// workgroups; nothing is sorted in HBM.  Sums in double-double: within 1e-9
+// relative of the reference's running `sum += v; sum -= v`
+// (SumAttributeAggregatorExecutor.java:184-198), like the segmented scans.
+constexpr int kCwCall = 1024;          // items (events) per call
+constexpr uint32_t kCwEmpty = 0xFFFFFFFFu;
+
+struct CwArgs {
+  int nch;
+  int ch_agg[kMaxChan];
+  int ch_type[kMaxChan];
+  int nagg;
+  int kind[kMaxAggs];
+  int type[kMaxAggs];
+  int chan[kMaxAggs];
+  int64_t cap;
+  int64_t C;
+  int64_t total;
+  int64_t wlen;            // length window: e[q] = q + wlen (kInf past the items)
+  const uint64_t* ikey;
+  const uint32_t* e;
+  const uint64_t* iargv;
+  const uint8_t* iargn;
+  const uint32_t* citem;   // [ncalls + 1]: first item of each call (absolute)
+  const uint32_t* clb;     // [ncalls]: first item of the call's region
+  // group tables after the push (k_cw_gtables)
+  double* dsum;
+  int64_t* cnt;
+  int64_t nkeys;
+  // direct emission (k_cw<.., EMIT>): k_emit's inputs
+  ColSet cs;
+  DExprSet es;
+  DExpr outs[kMaxCols];
+  int32_t okind[kMaxCols];
+  int32_t oarg[kMaxCols];
+  int nout;
+  const int32_t* ievrow;
+  int64_t row0, chunk0, seq0;
+  int64_t* o_chunk;
+  int32_t* o_type;
+  int64_t* o_ts;
+  uint64_t* o_vals;
+  uint8_t* o_nul;
+  int64_t* o_seq;
+  int32_t* o_sidx;
+  uint64_t* status;     // [ncalls] look-back words (zeroed before the launch)
+  uint64_t* nrows;      // rows of the push (written by the last call)
+  int probe;            // timing experiments (SHD_CW_PROBE)
+};
+
+__device__ __forceinline__ double cw_operand(const CwArgs& a, int c, int64_t q, bool& nul) {
+  const int g = a.ch_agg[c];
+  const uint64_t b = a.iargv[(int64_t)g * a.cap + q];
+  nul = a.iargn[(int64_t)g * a.cap + q] != 0;
+  switch (a.ch_type[c]) {   // Number.doubleValue() of the operand
+    case SHD_T_INT: return (double)v_i32(b);
+    case SHD_T_LONG: return (double)(int64_t)b;
+    case SHD_T_FLOAT: return (double)v_f32(b);
+    default: return v_f64(b);
+  }
+}
+
+// first item of every call (from the event -> item offsets of k_filter's scan)
+__global__ void k_cw_citem(const int64_t* __restrict__ offs, const uint32_t* __restrict__ off, int64_t n, int64_t m,
+                           int64_t C, int ncalls, uint32_t* __restrict__ citem) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c <= ncalls; c += gridDim.x * blockDim.x) {
+    const int64_t ev = offs[c];
+    citem[c] = (uint32_t)(C + (ev < n ? (int64_t)off[ev] : m));
+  }
+}
+
+// first item of each call's region (binary search over the non-decreasing e)
+// and the largest call / region, for the host's choice of path
+__global__ void k_cw_regions(const uint32_t* __restrict__ e, const uint32_t* __restrict__ citem, int ncalls,
+                             uint32_t* __restrict__ clb, uint32_t* __restrict__ maxes) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < ncalls; c += gridDim.x * blockDim.x) {
+    const uint32_t s = citem[c], t = citem[c + 1];
+    uint32_t lo = 0, hi = s;   // first q in [0, s] with e[q] > s (q = s qualifies: e[s] > s)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (e[mid] > s) hi = mid;
+      else lo = mid + 1;
+    }
+    clb[c] = lo;
+    if (t - s > __hip_atomic_load(&maxes[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&maxes[0], t - s);
+    if (t - lo > __hip_atomic_load(&maxes[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&maxes[1], t - lo);
+  }
+}
+
+// block-wide exclusive prefix of n <= CAP values in LDS (in place)
+template <int CAP>
+__device__ __forceinline__ void cw_block_exclusive(uint32_t* v, int n, uint32_t* wsum) {
+  constexpr int per = CAP / kBlock;
+  uint32_t x[per], run = 0;
+  for (int j = 0; j < per; j++) {
+    const int i = threadIdx.x * per + j;
+    x[j] = i < n ? v[i] : 0u;
+    run += x[j];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = inc - run;
+  for (int k = 0; k < w; k++) pre += wsum[k];
+  for (int j = 0; j < per; j++) {
+    const int i = threadIdx.x * per + j;
+    if (i < n) v[i] = pre;
+    pre += x[j];
+  }
+  __syncthreads();
+}
+
+// One (call, group) row: the group's window items (list[l0, l0 + n_in),
+// region-relative) folded per channel in double-double, the aggregators'
+// values after item x (k_seg_emit's formulas), the selector's outputs.
+template <int NC>
+__device__ __forceinline__ void cw_fold_emit(const CwArgs& a, int c, uint32_t lb, const uint16_t* list, uint32_t l0,
+                                             uint32_t n_in, uint32_t x, int64_t row) {
+  DD acc[NC];
+  int32_t nn[NC];
+#pragma unroll
+  for (int ch = 0; ch < NC; ch++) {
+    acc[ch] = DD{0.0, 0.0};
+    nn[ch] = 0;
+  }
+  for (uint32_t j = 0; j < ((a.probe & 2) ? 0u : n_in); j++) {
+    const int64_t q = (int64_t)lb + list[l0 + j];
+#pragma unroll
+    for (int ch = 0; ch < NC; ch++) {
+      bool nul;
+      const double v = cw_operand(a, ch, q, nul);
+      if (!nul) {
+        acc[ch] = dd_add(acc[ch], DD{v, 0.0});
+        nn[ch]++;
+      }
+    }
+  }
+  uint64_t av[kMaxAggs];
+  uint8_t an[kMaxAggs];
+  for (int j = 0; j < a.nagg; j++) {
+    const int ch = a.chan[j];
+    uint64_t ob = 0;
+    bool on = false;
+    if (a.kind[j] == SHD_AGG_COUNT) {
+      ob = (uint64_t)n_in;
+    } else {
+      double v = 0.0;
+      int32_t nnw = 0;
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+        if (k == ch) {
+          v = acc[k].hi;   // the double-double sum rounded (dd_add keeps hi = round(hi + lo))
+          nnw = nn[k];
+        }
+      if (a.kind[j] == SHD_AGG_SUM) {
+        // a null operand leaves the sum (null once nothing is left; float sums: null)
+        bool xn;
+        (void)cw_operand(a, ch, x, xn);
+        on = xn && !(a.type[j] == SHD_T_DOUBLE && nnw != 0);
+        ob = on ? 0ull : p_f64(v);
+      } else {
+        // avg = value / count (AvgAttributeAggregatorExecutor: value / count as double)
+        on = nnw == 0;
+        ob = on ? 0ull : p_f64(__ddiv_rn(v, (double)nnw));
+      }
+    }
+    av[j] = ob;
+    an[j] = on ? 1 : 0;
+  }
+  const int64_t ev = a.ievrow[x];
+  RowCtx cx{&a.cs, ev, av, an};
+  for (int k = 0; k < a.nout; k++) {
+    Val v;
+    if (a.okind[k] == 1) {
+      v = col_load(a.cs, ev, a.oarg[k]);
+    } else if (a.okind[k] == 2) {
+      v.b = av[a.oarg[k]];
+      v.null = an[a.oarg[k]];
+    } else {
+      v = eval_expr(a.es.ins + a.outs[k].off, a.outs[k].len, a.es.consts, cx);
+    }
+    a.o_vals[row * a.nout + k] = v.b;
+    a.o_nul[row * a.nout + k] = (uint8_t)v.null;
+  }
+  a.o_ts[row] = a.cs.ts[ev];
+  a.o_type[row] = 0;
+  a.o_seq[row] = a.seq0 + ev;   // the group's last event of the call
+  a.o_chunk[row] = a.chunk0 + c;
+  a.o_sidx[row] = 0;
+}
+
+// Direct-mapped variant for small dense group ids (g < GCAP, config W2's
+// symbols): per-group LDS arrays indexed by the id -- no hash table -- and the
+// call's row base from k_cw_count + a scan instead of the look-back.
+// k_cw_count: distinct groups of every call (an LDS bitmap per call).
+template <int GCAP>
+__global__ __launch_bounds__(kBlock) void k_cw_count(const CwArgs* __restrict__ ap, int ncalls, uint32_t* cnt) {
+  const CwArgs& a = *ap;
+  __shared__ uint32_t bits[GCAP / 32];
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int c = blockIdx.x;
+  if (c >= ncalls) return;
+  const uint32_t s = a.citem[c], t = a.citem[c + 1];
+  for (int i = threadIdx.x; i < GCAP / 32; i += kBlock) bits[i] = 0;
+  __syncthreads();
+  for (uint32_t q = s + threadIdx.x; q < t; q += kBlock) {
+    const uint32_t g = (uint32_t)a.ikey[q];
+    atomicOr(&bits[g >> 5], 1u << (g & 31));
+  }
+  __syncthreads();
+  uint32_t v = 0;
+  for (int i = threadIdx.x; i < GCAP / 32; i += kBlock) v += __popc(bits[i]);
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int k = 0; k < kBlock / 64; k++) tot += wsum[k];
+    cnt[c] = tot;
+  }
+}
+
+template <int NC, int RC, int CALLCAP, int GCAP, bool LEN>
+__global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__ ap, int ncalls,
+                                                      const uint32_t* __restrict__ rbase) {
+  constexpr bool kStage = RC <= 2048;
+  constexpr int kExpN = (kStage && !LEN) ? RC : 1;
+  const CwArgs& a = *ap;
+  __shared__ uint32_t sfirst[GCAP], slast[GCAP], scnt[GCAP];
+  __shared__ uint16_t qslot[RC];
+  // staged group ids; after the region pass, the window lists (u16)
+  __shared__ uint32_t rkey[kStage ? RC : (RC + 1) / 2];
+  __shared__ uint32_t rexp[kExpN];
+  __shared__ uint32_t srank[CALLCAP];   // first-seen rank of the call's items
+  __shared__ uint32_t wsum[kBlock / 64];
+  uint16_t* list = reinterpret_cast<uint16_t*>(rkey);
+  uint32_t* soff = scnt;                // list offsets, in place of the counts (kept in registers below)
+  const int c = blockIdx.x;
+  if (c >= ncalls) return;
+  const uint32_t s = a.citem[c], t = a.citem[c + 1];
+  if (s == t) return;
+  const uint32_t lb = a.clb[c];
+  const int nr = (int)(t - lb);
+  const int rs = (int)(s - lb);
+  for (int g = threadIdx.x; g < GCAP; g += kBlock) {
+    sfirst[g] = 0xFFFFFFFFu;
+    slast[g] = 0;
+    scnt[g] = 0;
+  }
+  if (kStage)
+    for (int r = threadIdx.x; r < nr; r += kBlock) {
+      rkey[r] = (uint32_t)a.ikey[lb + r];
+      if (!LEN) rexp[r] = a.e[lb + r];
+    }
+  __syncthreads();
+  auto key_at = [&](int r) -> uint32_t { return kStage ? rkey[r] : (uint32_t)a.ikey[lb + r]; };
+  auto exp_of = [&](int r) -> uint32_t {
+    const uint32_t q = lb + r;
+    if (LEN) return (int64_t)q + a.wlen < a.total ? (uint32_t)(q + a.wlen) : kInf;
+    return kStage ? rexp[r] : a.e[q];
+  };
+  for (int r = rs + threadIdx.x; r < nr; r += kBlock) {
+    const uint32_t g = key_at(r);
+    atomicMin(&sfirst[g], lb + r);
+    atomicMax(&slast[g], lb + r);
+  }
+  __syncthreads();
+  // region items inside their group's window; first items of the call's groups
+  for (int r = threadIdx.x; r < nr; r += kBlock) {
+    const uint32_t q = lb + r;
+    const uint32_t g = key_at(r);
+    uint16_t sl = 0xFFFF;
+    const uint32_t x = slast[g];
+    if (sfirst[g] != 0xFFFFFFFFu && q <= x && exp_of(r) > x) {
+      sl = (uint16_t)g;
+      atomicAdd(&scnt[g], 1u);
+    }
+    qslot[r] = sl;
+    if (r >= rs) srank[r - rs] = sfirst[g] == q ? 1u : 0u;
+  }
+  __syncthreads();
+  // the counts of the call's groups, kept by the thread of the group's first item
+  uint32_t my_n[CALLCAP / kBlock];
+  for (int k = 0; k < CALLCAP / kBlock; k++) {
+    const int r = rs + threadIdx.x + k * kBlock;
+    my_n[k] = r < nr && srank[r - rs] ? scnt[key_at(r)] : 0u;
+  }
+  __syncthreads();
+  cw_block_exclusive<GCAP>(soff, GCAP, wsum);   // scnt -> list offsets
+  cw_block_exclusive<CALLCAP>(srank, nr - rs, wsum);
+  // (after the offsets: the group ids are still staged, the lists overwrite them next)
+  uint32_t my_g[CALLCAP / kBlock];
+  for (int k = 0; k < CALLCAP / kBlock; k++) {
+    const int r = rs + threadIdx.x + k * kBlock;
+    my_g[k] = r < nr ? key_at(r) : 0u;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nr; r += kBlock) {
+    const uint16_t g = qslot[r];
+    if (g != 0xFFFF) list[atomicAdd(&soff[g], 1u)] = (uint16_t)r;
+  }
+  __syncthreads();
+  const int64_t base = a.row0 + (int64_t)rbase[c];
+  for (int k = 0; k < CALLCAP / kBlock; k++) {
+    const int r = rs + threadIdx.x + k * kBlock;
+    if (r >= nr || !my_n[k] || (a.probe & 4)) continue;
+    const uint32_t g = my_g[k];
+    // soff[g] now ends the group's list
+    cw_fold_emit<NC>(a, c, lb, list, soff[g] - my_n[k], my_n[k], slast[g], base + srank[r - rs]);
+  }
+}
+
+// The call's rows are written here, in first-seen order, at row0 + the rows
+// of all earlier calls (single-pass decoupled look-back over the calls: each
+// workgroup publishes its row count as soon as its groups are known).
+// CALLCAP: items per call (hash table of 2 * CALLCAP slots); RC: region items.
+// LDS: 38 KB at (512, 2048) -- four workgroups per CU.
+template <int NC, int RC, int CALLCAP, bool LEN>
+__global__ __launch_bounds__(kBlock) void k_cw(const CwArgs* __restrict__ ap, int ncalls) {
+  // small regions are staged in LDS (group id, and the expiry unless a length
+  // window gives it as q + L; one coalesced pass); larger ones are read from
+  // global memory (L2)
+  constexpr bool kStage = RC <= 2048;
+  constexpr int kStageN = kStage ? RC : 1;
+  constexpr int kExpN = (kStage && !LEN) ? RC : 1;
+  constexpr int kHash = 2 * CALLCAP;
+  const CwArgs& a = *ap;
+  __shared__ uint32_t hkey[kHash];
+  __shared__ uint16_t hidx[kHash];
+  // per group of the call: first / last item, items in its window, list offset
+  __shared__ uint32_t sfirst[CALLCAP], slast[CALLCAP], scnt[CALLCAP], soff[CALLCAP];
+  __shared__ uint16_t qslot[RC];
+  // staged group ids; after the region pass, the window lists (u16)
+  __shared__ uint32_t rkey[kStage ? RC : (RC + 1) / 2];
+  __shared__ uint32_t rexp[kExpN];
+  __shared__ uint32_t srank[CALLCAP];   // first-seen rank of the call's items
+  __shared__ uint32_t nslots;
+  __shared__ uint64_t sbase;
+  __shared__ uint32_t wsum[kBlock / 64];
+  uint16_t* list = reinterpret_cast<uint16_t*>(rkey);
+  const int c = blockIdx.x;
+  if (c >= ncalls) return;
+  const uint32_t s = a.citem[c], t = a.citem[c + 1];
+  const uint32_t lb = s == t ? s : a.clb[c];
+  const int nr = (int)(t - lb);
+  for (int h = threadIdx.x; h < kHash; h += kBlock) hkey[h] = kCwEmpty;
+  if (threadIdx.x == 0) nslots = 0;
+  if (kStage)
+    for (int r = threadIdx.x; r < nr; r += kBlock) {
+      rkey[r] = (uint32_t)a.ikey[lb + r];
+      if (!LEN) rexp[r] = a.e[lb + r];
+    }
+  __syncthreads();
+  auto exp_of = [&](int r) -> uint32_t {
+    const uint32_t q = lb + r;
+    if (LEN) return (int64_t)q + a.wlen < a.total ? (uint32_t)(q + a.wlen) : kInf;
+    return kStage ? rexp[r] : a.e[q];
+  };
+  auto key_at = [&](int r) -> uint32_t { return kStage ? rkey[r] : (uint32_t)a.ikey[lb + r]; };
+  auto hash = [&](uint32_t k) -> uint32_t { return key_bucket_mix(k) & (kHash - 1); };
+  // 1. the call's groups: the thread that claims a hash slot numbers it
+  const int rs = (int)(s - lb);
+  for (int r = rs + threadIdx.x; r < nr; r += kBlock) {
+    const uint32_t k = key_at(r);
+    uint32_t h = hash(k);
+    for (;;) {
+      const uint32_t old = atomicCAS(&hkey[h], kCwEmpty, k);
+      if (old == kCwEmpty) {
+        const uint32_t i = atomicAdd(&nslots, 1u);
+        hidx[h] = (uint16_t)i;
+        sfirst[i] = 0xFFFFFFFFu;
+        slast[i] = 0;
+        scnt[i] = 0;
+        break;
+      }
+      if (old == k) break;
+      h = (h + 1) & (kHash - 1);
+    }
+  }
+  __syncthreads();
+  constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
+  if (threadIdx.x == 0) {
+    // publish this call's row count at once; the look-back for the earlier
+    // calls' rows waits until the fold needs it
+    const uint64_t local = nslots;
+    atomicExch((unsigned long long*)&a.status[c], (unsigned long long)((c == 0 ? kInc : kAgg) | local));
+  }
+  // one wave reads 64 predecessors' words per step: the nearest inclusive
+  // prefix ends the walk, aggregates before it add up
+  auto look_back = [&]() {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const uint64_t local = nslots;
+    uint64_t base = 0;
+    for (int top = (a.probe & 1) ? -1 : c - 1; top >= 0;) {
+      const int j = top - lane;
+      uint64_t st = j >= 0 ? cw_status_load(&a.status[j]) : kInc;
+      if (__any((st >> 62) == 0)) {   // an earlier, running workgroup has not published yet
+        __builtin_amdgcn_s_sleep(4);
+        continue;
+      }
+      const uint64_t incl = __ballot((st >> 62) == 2);
+      const int stop = incl ? __ffsll((long long)incl) - 1 : 64;   // nearest inclusive word
+      uint64_t v = lane <= stop && j >= 0 ? (st & kVal) : 0ull;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      base += v;
+      if (incl) break;
+      top -= 64;
+    }
+    if (lane == 0) {
+      if (c > 0) atomicExch((unsigned long long*)&a.status[c], (unsigned long long)(kInc | (base + local)));
+      if (c == ncalls - 1) *a.nrows = base + local;
+      sbase = base;
+    }
+  };
+  // the look-back runs at once (short chains: every workgroup resolves its
+  // prefix right after publishing its count)
+  look_back();
+  if (s == t) return;   // an empty call: its zero rows are published, the chain continues through it
+  auto find = [&](uint32_t k) -> int {
+    uint32_t h = hash(k);
+    for (;;) {
+      const uint32_t x = hkey[h];
+      if (x == k) return hidx[h];
+      if (x == kCwEmpty) return -1;
+      h = (h + 1) & (kHash - 1);
+    }
+  };
+  for (int r = rs + threadIdx.x; r < nr; r += kBlock) {
+    const int i = find(key_at(r));
+    atomicMin(&sfirst[i], lb + r);
+    atomicMax(&slast[i], lb + r);
+  }
+  __syncthreads();
+  // 2. region items inside their group's window
+  for (int r = threadIdx.x; r < nr; r += kBlock) {
+    const uint32_t q = lb + r;
+    const int i = find(key_at(r));
+    uint16_t sl = 0xFFFF;
+    if (i >= 0) {
+      const uint32_t x = slast[i];
+      if (q <= x && exp_of(r) > x) {
+        sl = (uint16_t)i;
+        atomicAdd(&scnt[i], 1u);
+      }
+    }
+    qslot[r] = sl;
+  }
+  __syncthreads();
+  // first-seen order of the groups (LinkedHashMap insertion order): the rank
+  // of each group's first item among the call's first items
+  for (int r = threadIdx.x; r < nr - rs; r += kBlock) srank[r] = 0;
+  for (int i = threadIdx.x; i < (int)nslots; i += kBlock) soff[i] = scnt[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)nslots; i += kBlock) srank[sfirst[i] - s] = 1;
+  cw_block_exclusive<CALLCAP>(soff, (int)nslots, wsum);
+  cw_block_exclusive<CALLCAP>(srank, nr - rs, wsum);
+  // lists: soff[i] advances to the end of group i's list
+  for (int r = threadIdx.x; r < nr; r += kBlock) {
+    const uint16_t i = qslot[r];
+    if (i != 0xFFFF) list[atomicAdd(&soff[i], 1u)] = (uint16_t)r;
+  }
+  __syncthreads();
+  // 3. one thread per group: fold the window, write the row
+  for (int i = threadIdx.x; i < (int)nslots; i += kBlock) {
+    if (a.probe & 4) continue;
+    const uint32_t xf = sfirst[i];
+    cw_fold_emit<NC>(a, c, lb, list, soff[i] - scnt[i], scnt[i], slast[i],
+                     a.row0 + (int64_t)sbase + srank[xf - s]);
+  }
+}
+
+// group tables after the push: the groups of items [q0, q1) are reset (!ADD),
+// or those items, if still in the window (never expired: e == kInf), add in
+template <bool ADD>
+__global__ __launch_bounds__(kBlock) void k_cw_gtables(const CwArgs* __restrict__ ap, int64_t q0, int64_t q1) {
+  const CwArgs& a = *ap;
+  for (int64_t q = q0 + (int64_t)blockIdx.x * kBlock + threadIdx.x; q < q1; q += (int64_t)gridDim.x * kBlock) {
+    const uint32_t g = (uint32_t)a.ikey[q];
+    for (int j = 0; j < a.nagg; j++) {
+      const int64_t at = (int64_t)j * a.nkeys + g;
+      if (!ADD) {
+        a.dsum[at] = 0.0;
+        a.cnt[at] = 0;
+        continue;
+      }
+      if (a.e[q] != kInf) continue;
+      const int ch = a.chan[j];
+      if (ch < 0) {
+        atomicAdd((unsigned long long*)&a.cnt[at], 1ull);
+        continue;
+      }
+      bool nul;
+      const double v = cw_operand(a, ch, q, nul);
+      if (nul) continue;
+      atomicAdd(&a.dsum[at], v);
+      atomicAdd((unsigned long long*)&a.cnt[at], 1ull);
+    }
   }
 }
 
@@ -1930,6 +2619,8 @@ struct SingleEngine : Engine {
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
     }
     gd.reset(stream);
+    kmax_seen = 0;
+    kmax_known = true;
     seg_unsafe = false;
     op_emax = 0;
     op_emin = 0xFFFFFFFFu;
@@ -2003,6 +2694,7 @@ struct SingleEngine : Engine {
     seg_mode = seg_ok && seg_pref && !seg_unsafe;
     gd.nk = std::max(ngk, 1);
     gd.load(r, stream);
+    kmax_known = false;
     counters.carry = C;
   }
 
@@ -2042,8 +2734,8 @@ struct SingleEngine : Engine {
     d_flags.reserve(n);
     d_cnt.reserve(n * 4);
     d_off.reserve(n * 4);
-    d_tot.reserve(64);
-    h_tot.reserve(64);
+    d_tot.reserve(128);
+    h_tot.reserve(128);
     if (partitioned) d_pkey.reserve(n * 8);
     FilterArgs fa{};
     fa.cs = b.cs;
@@ -2055,16 +2747,22 @@ struct SingleEngine : Engine {
       fa.key_col = key_col;
       fa.key_type = key_type;
     }
-    const FilterArgs* d_fa = dev_args(fa);
-    if (std::getenv("SHD_DEBUG_ARGS")) debug_filter_args(d_fa, fa, n);
-    hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, d_fa, n, d_flags.as<uint8_t>(),
-                       d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
-    SHD_CHECK_LAUNCH();
-    uint32_t* d_m = (uint32_t*)d_tot.p;
-    scan_exclusive_u32(d_cnt.as<uint32_t>(), d_off.as<uint32_t>(), n, d_m, d_scan, s);
-    mark("filter");
-    if (!agg_mode) push_filter(b, ncalls, n);
-    else push_agg(b, ncalls, n);
+    // aggregate queries (never inside a partition here: those run on the
+    // keyed window engine) filter and build their items in one pass
+    if (agg_mode && !partitioned && !getenv("SHD_NO_FUSED_ITEMS")) {
+      push_agg_fused(b, ncalls, n, fa);
+    } else {
+      const FilterArgs* d_fa = dev_args(fa);
+      if (std::getenv("SHD_DEBUG_ARGS")) debug_filter_args(d_fa, fa, n);
+      hipLaunchKernelGGL(k_filter, dim3(grid_cover(n)), dim3(kBlock), 0, s, d_fa, n, d_flags.as<uint8_t>(),
+                         d_cnt.as<uint32_t>(), d_pkey.as<uint64_t>());
+      SHD_CHECK_LAUNCH();
+      uint32_t* d_m = (uint32_t*)d_tot.p;
+      scan_exclusive_u32(d_cnt.as<uint32_t>(), d_off.as<uint32_t>(), n, d_m, d_scan, s);
+      mark("filter");
+      if (!agg_mode) push_filter(b, ncalls, n);
+      else push_agg(b, ncalls, n);
+    }
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -2433,6 +3131,166 @@ struct SingleEngine : Engine {
     return nch <= 1 ? wc_kernels<1>(total, G, cap, ncalls, F, kc, K) : wc_kernels<2>(total, G, cap, ncalls, F, kc, K);
   }
 
+  // Call-window path (k_cw): group by, a length / time window whose region
+  // per call fits the LDS lists, calls of at most kCwCall events.
+  static constexpr int kCwRegionMax = 8192;
+  DevBuf d_cw_citem, d_cw_clb;
+  bool callwin_candidate(int64_t ncalls, int64_t total) const {
+    if (!seg_mode || ngk == 0 || partitioned || nch > kMaxChan || (wkind != SHD_W_LENGTH && wkind != SHD_W_TIME) ||
+        total >= (int64_t)UINT32_MAX - 1 || ncalls <= 0 || getenv("SHD_NO_CALLWIN"))
+      return false;
+    for (size_t c = 0; c + 1 < h_offs.size(); c++)
+      if (h_offs[c + 1] - h_offs[c] > kCwCall) return false;
+    return true;
+  }
+
+  template <int NC>
+  void callwin_launch(const CwArgs* d_ca, int64_t ncalls, uint32_t call, uint32_t region) {
+    const dim3 g((unsigned)ncalls), bl(kBlock);
+    const bool len = wkind == SHD_W_LENGTH;
+    if (region <= 2048 && call <= 512) {
+      if (len) hipLaunchKernelGGL((k_cw<NC, 2048, 512, true>), g, bl, 0, stream, d_ca, (int)ncalls);
+      else hipLaunchKernelGGL((k_cw<NC, 2048, 512, false>), g, bl, 0, stream, d_ca, (int)ncalls);
+    } else if (region <= 2048) {
+      if (len) hipLaunchKernelGGL((k_cw<NC, 2048, kCwCall, true>), g, bl, 0, stream, d_ca, (int)ncalls);
+      else hipLaunchKernelGGL((k_cw<NC, 2048, kCwCall, false>), g, bl, 0, stream, d_ca, (int)ncalls);
+    } else {
+      hipLaunchKernelGGL((k_cw<NC, kCwRegionMax, kCwCall, false>), g, bl, 0, stream, d_ca, (int)ncalls);
+    }
+    SHD_CHECK_LAUNCH();
+  }
+
+  static constexpr int kCwDirectG = 1024;   // direct-mapped groups (dense ids below this)
+  DevBuf d_cw_status, d_cw_cnt, d_cw_base;
+
+  template <int NC, int RC, int CALLCAP>
+  void callwin_direct_launch(const CwArgs* d_ca, int64_t ncalls) {
+    const dim3 g((unsigned)ncalls), bl(kBlock);
+    const uint32_t* base = d_cw_base.as<uint32_t>();
+    if (wkind == SHD_W_LENGTH)
+      hipLaunchKernelGGL((k_cw_direct<NC, RC, CALLCAP, kCwDirectG, true>), g, bl, 0, stream, d_ca, (int)ncalls, base);
+    else
+      hipLaunchKernelGGL((k_cw_direct<NC, RC, CALLCAP, kCwDirectG, false>), g, bl, 0, stream, d_ca, (int)ncalls, base);
+    SHD_CHECK_LAUNCH();
+  }
+  template <int NC>
+  void callwin_direct(const CwArgs* d_ca, int64_t ncalls, uint32_t call, uint32_t region) {
+    if (region <= 2048 && call <= 512) callwin_direct_launch<NC, 2048, 512>(d_ca, ncalls);
+    else if (region <= 2048) callwin_direct_launch<NC, 2048, kCwCall>(d_ca, ncalls);
+    else callwin_direct_launch<NC, kCwRegionMax, kCwCall>(d_ca, ncalls);
+  }
+  // the call-window fold + the rows of every call (no run records / k_emit)
+  void agg_callwin(const Staged& b, int64_t total, int64_t cap, int64_t ncalls, int64_t X, uint32_t call,
+                   uint32_t region, uint64_t kmax) {
+    hipStream_t s = stream;
+    const int64_t m = total - C;
+    CwArgs ca{};
+    ca.nch = std::max(nch, 1);
+    for (int c = 0; c < ca.nch; c++) {
+      ca.ch_agg[c] = nch ? ch_agg[c] : 0;
+      ca.ch_type[c] = nch ? ch_type[c] : SHD_T_DOUBLE;
+    }
+    ca.nagg = nagg;
+    for (int g = 0; g < nagg; g++) {
+      ca.kind[g] = plan.aggs[g].kind;
+      ca.type[g] = plan.aggs[g].type;
+      ca.chan[g] = chan_of[g];
+    }
+    ca.cap = cap;
+    ca.C = C;
+    ca.total = total;
+    ca.wlen = wparam;
+    ca.probe = getenv("SHD_CW_PROBE") ? atoi(getenv("SHD_CW_PROBE")) : 0;
+    ca.ikey = ikey[cur].as<uint64_t>();
+    ca.e = e_exp.as<uint32_t>();
+    ca.iargv = iargv[cur].as<uint64_t>();
+    ca.iargn = iargn[cur].as<uint8_t>();
+    ca.citem = d_cw_citem.as<uint32_t>();
+    ca.clb = d_cw_clb.as<uint32_t>();
+    ca.dsum = g_dsum.as<double>();
+    ca.cnt = g_cnt.as<int64_t>();
+    ca.nkeys = g_nkeys;
+    // rows: at most one per new item
+    out.ensure(std::max<int64_t>(m, 1), s);
+    ca.cs = b.cs;
+    ca.es = dset();
+    ca.nout = (int)outs.size();
+    for (size_t c = 0; c < outs.size(); c++) {
+      ca.outs[c] = dexpr(outs[c]);
+      const auto& code = plan.exprs[outs[c]];
+      ca.okind[c] = 0;
+      if (code.size() == 1 && code[0].op == SHD_OP_LOAD) {
+        ca.okind[c] = 1;
+        ca.oarg[c] = code[0].c & 0xFFFF;
+      } else if (code.size() == 1 && code[0].op == SHD_OP_AGG && code[0].a >= 0 && code[0].a < nagg) {
+        ca.okind[c] = 2;
+        ca.oarg[c] = code[0].a;
+      }
+    }
+    ca.ievrow = ievrow.as<int32_t>();
+    ca.row0 = out.count;
+    ca.chunk0 = chunk_seq;
+    ca.seq0 = seq;
+    ca.o_chunk = out.d_chunk();
+    ca.o_type = out.d_type();
+    ca.o_ts = out.d_ts();
+    ca.o_vals = out.d_vals();
+    ca.o_nul = out.d_nulls();
+    ca.o_seq = out.d_seq();
+    ca.o_sidx = out.d_sidx();
+    d_cw_status.reserve((size_t)ncalls * 8);
+    SHD_HIP(hipMemsetAsync(d_cw_status.p, 0, (size_t)ncalls * 8, s));
+    ca.status = d_cw_status.as<uint64_t>();
+    ca.nrows = d_tot.as<uint64_t>() + 9;
+    const CwArgs* d_ca = dev_args(ca);
+    if (kmax < (uint64_t)kCwDirectG && !getenv("SHD_CW_HASH")) {
+      // rows per call (distinct groups) -> each call's first row
+      d_cw_cnt.reserve((size_t)ncalls * 4);
+      d_cw_base.reserve((size_t)ncalls * 4);
+      hipLaunchKernelGGL(k_cw_count<kCwDirectG>, dim3((unsigned)ncalls), dim3(kBlock), 0, s, d_ca, (int)ncalls,
+                         d_cw_cnt.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      scan_exclusive_u32(d_cw_cnt.as<uint32_t>(), d_cw_base.as<uint32_t>(), ncalls, (uint32_t*)(d_tot.as<uint64_t>() + 9),
+                         d_scan, s);
+      SHD_HIP(hipMemsetAsync(d_tot.as<uint32_t>() + 19, 0, 4, s));   // (the row count's high word)
+      switch (ca.nch) {
+        case 1: callwin_direct<1>(d_ca, ncalls, call, region); break;
+        case 2: callwin_direct<2>(d_ca, ncalls, call, region); break;
+        case 3: callwin_direct<3>(d_ca, ncalls, call, region); break;
+        default: callwin_direct<4>(d_ca, ncalls, call, region); break;
+      }
+    } else {
+      switch (ca.nch) {
+        case 1: callwin_launch<1>(d_ca, ncalls, call, region); break;
+        case 2: callwin_launch<2>(d_ca, ncalls, call, region); break;
+        case 3: callwin_launch<3>(d_ca, ncalls, call, region); break;
+        default: callwin_launch<4>(d_ca, ncalls, call, region); break;
+      }
+    }
+    SHD_HIP(hipMemcpyAsync(h_tot.as<uint64_t>() + 9, d_tot.as<uint64_t>() + 9, 8, hipMemcpyDeviceToHost, s));
+    mark("call_window");
+    // the group tables: the window state after the push.  Only groups of the
+    // carried items (the state before the push) and of the final window can
+    // hold a non-empty state: those are reset, then the final window adds in
+    if (C > 0) {
+      hipLaunchKernelGGL(k_cw_gtables<false>, dim3(grid_for(C)), dim3(kBlock), 0, s, d_ca, (int64_t)0, C);
+      SHD_CHECK_LAUNCH();
+    }
+    if (total > X) {
+      hipLaunchKernelGGL(k_cw_gtables<false>, dim3(grid_for(total - X)), dim3(kBlock), 0, s, d_ca, X, total);
+      SHD_CHECK_LAUNCH();
+    }
+    if (total > X) {
+      hipLaunchKernelGGL(k_cw_gtables<true>, dim3(grid_for(total - X)), dim3(kBlock), 0, s, d_ca, X, total);
+      SHD_CHECK_LAUNCH();
+    }
+    mark("group_tables");
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t nrows = m > 0 ? (int64_t)h_tot.as<uint64_t>()[9] : 0;
+    out.count += nrows;
+    counters.matches += nrows;
+  }
+
   void agg_segscan(int64_t total, uint64_t kmax, int64_t cap) {
     hipStream_t s = stream;
     okey32.reserve(total * 4);
@@ -2478,17 +3336,10 @@ struct SingleEngine : Engine {
     }
   }
 
-  void push_agg(const Staged& b, int64_t ncalls, int64_t n) {
+  // the item slot `cur` holds the carry [0, C) and room for `total` items
+  void grow_items(int64_t total) {
     hipStream_t s = stream;
-    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    const int64_t m = h_tot.as<uint32_t>()[0];
-    const int64_t total = C + m;
-    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 5, 0, 8, s));
-    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 6, 0xFF, 8, s));
     if (total >= (int64_t)INT32_MAX) throw Error(SHD_E_CAPACITY, "window items exceed 2^31");
-    // items: carry slot `cur` already holds [0, C); build the new item set in slot `cur`
-    // (grow preserving the carry)
     if (icap[cur] < total) {
       int old = cur, nw = cur ^ 1;
       ensure_items(nw, total);
@@ -2508,6 +3359,10 @@ struct SingleEngine : Engine {
     ievrow.reserve(cap * 4);
     icall.reserve(cap * 4);
     inow.reserve(cap * 8);
+  }
+
+  // gstride: words per group attribute of the dictionary-mode key arrays (>= new items)
+  ItemArgs item_args(const Staged& b, int64_t gstride) {
     ItemArgs ia{};
     ia.cs = b.cs;
     ia.es = dset();
@@ -2529,15 +3384,30 @@ struct SingleEngine : Engine {
     ia.dense = gdense;
     ia.null_str_id = plan.null_str_id;
     if (ngk && !gdense) {
-      g_kw.reserve((size_t)ngk * std::max<int64_t>(m, 1) * 8);
-      g_kn.reserve(std::max<int64_t>(m, 1));
-      g_h.reserve(std::max<int64_t>(m, 1) * 8);
+      g_kw.reserve((size_t)ngk * gstride * 8);
+      g_kn.reserve(gstride);
+      g_h.reserve(gstride * 8);
       ia.gkw = g_kw.as<uint64_t>();
       ia.gkn = g_kn.as<uint8_t>();
       ia.gh = g_h.as<uint64_t>();
-      ia.gstride = std::max<int64_t>(m, 1);
+      ia.gstride = gstride;
     }
     ia.C = C;
+    ia.time_window = wkind == SHD_W_TIME;
+    return ia;
+  }
+
+  void push_agg(const Staged& b, int64_t ncalls, int64_t n) {
+    hipStream_t s = stream;
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t m = h_tot.as<uint32_t>()[0];
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 5, 0, 8, s));
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 6, 0xFF, 8, s));
+    // items: carry slot `cur` already holds [0, C); build the new item set in slot `cur`
+    grow_items(C + m);
+    const int64_t cap = icap[cur];
+    const ItemArgs ia = item_args(b, std::max<int64_t>(m, 1));
     hipLaunchKernelGGL(k_make_items, dim3(grid_cover(n)), dim3(kBlock), 0, s, dev_args(ia), n,
                        (const uint32_t*)d_cnt.as<uint32_t>(), (const uint32_t*)d_off.as<uint32_t>(),
                        (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_now.as<int64_t>(),
@@ -2547,6 +3417,66 @@ struct SingleEngine : Engine {
     SHD_CHECK_LAUNCH();
     if (ngk && !gdense) gdict_assign(m, std::max<int64_t>(m, 1));
     mark("window_items");
+    push_agg_tail(b, ncalls, n, m, false);
+  }
+
+  // filter + items in one pass (k_filter_items); the item arrays are sized
+  // for every event passing
+  DevBuf d_fi_status;
+  void push_agg_fused(const Staged& b, int64_t ncalls, int64_t n, const FilterArgs& fa) {
+    hipStream_t s = stream;
+    grow_items(C + n);
+    const int64_t cap = icap[cur];
+    FusedArgs fu{};
+    fu.f = fa;
+    fu.it = item_args(b, std::max<int64_t>(n, 1));
+    fu.call_of = d_call_of.as<int32_t>();
+    fu.call_now = d_now.as<int64_t>();
+    fu.ikey = ikey[cur].as<uint64_t>();
+    fu.its = its[cur].as<int64_t>();
+    fu.iargv = iargv[cur].as<uint64_t>();
+    fu.iargn = iargn[cur].as<uint8_t>();
+    fu.ievrow = ievrow.as<int32_t>();
+    fu.icall = icall.as<int32_t>();
+    fu.inow = inow.as<int64_t>();
+    fu.cap = cap;
+    const int64_t ntiles = ceil_div(n, kFiTile);
+    d_fi_status.reserve((size_t)ntiles * 8);
+    SHD_HIP(hipMemsetAsync(d_fi_status.p, 0, (size_t)ntiles * 8, s));
+    fu.status = d_fi_status.as<uint64_t>();
+    d_cw_citem.reserve((size_t)(ncalls + 1) * 4);
+    fu.citem = d_cw_citem.as<uint32_t>();
+    fu.ncalls = (int)ncalls;
+    fu.m_out = (uint32_t*)d_tot.p;
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 2, 0, 8, s));
+    fu.kmax_out = (unsigned long long*)(d_tot.as<uint64_t>() + 2);
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 5, 0, 8, s));
+    SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 6, 0xFF, 8, s));
+    fu.nch = seg_mode ? nch : 0;
+    for (int c = 0; c < nch; c++) {
+      fu.ch_agg[c] = ch_agg[c];
+      fu.ch_f32[c] = ch_type[c] == SHD_T_FLOAT;
+    }
+    fu.opstats = (uint32_t*)(d_tot.as<uint64_t>() + 5);
+    fu.probe = getenv("SHD_FI_PROBE") ? atoi(getenv("SHD_FI_PROBE")) : 0;
+    hipLaunchKernelGGL(k_filter_items, dim3((unsigned)ntiles), dim3(kBlock), 0, s, dev_args(fu), n);
+    SHD_CHECK_LAUNCH();
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 24, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const int64_t m = h_tot.as<uint32_t>()[0];
+    fused_kmax = h_tot.as<uint64_t>()[2];
+    if (ngk && !gdense) gdict_assign(m, std::max<int64_t>(n, 1));
+    mark("filter_items");
+    push_agg_tail(b, ncalls, n, m, true);
+  }
+  uint64_t fused_kmax = 0;     // largest group id of the push's new items (dense ids)
+  uint64_t kmax_seen = 0;      // largest dense group id since reset (an upper bound of the carried ones)
+  bool kmax_known = true;      // false after a restore: one reduction over the items
+
+  void push_agg_tail(const Staged& b, int64_t ncalls, int64_t n, int64_t m, bool fused) {
+    hipStream_t s = stream;
+    const int64_t total = C + m;
+    const int64_t cap = icap[cur];
     // expiry positions
     e_exp.reserve(std::max<int64_t>(total, 1) * 4);
     hipLaunchKernelGGL(k_expiry, dim3(grid_for(total)), dim3(kBlock), 0, s, wkind, wparam, C, total,
@@ -2575,9 +3505,12 @@ struct SingleEngine : Engine {
     hipLaunchKernelGGL(k_count_expired, dim3(grid_for(total, 4, 2048)), dim3(kBlock), 0, s,
                        (const uint32_t*)e_exp.as<uint32_t>(), total, d_x);
     SHD_CHECK_LAUNCH();
-    reduce_max_u64(ikey[cur].as<uint64_t>(), total, d_kmax, s);
+    // the largest group id: dense ids of a fused push come from k_filter_items
+    // (carried ids are bounded by the running maximum)
+    const bool kmax_fused = fused && (gdense || ngk == 0) && kmax_known;
+    if (!kmax_fused) reduce_max_u64(ikey[cur].as<uint64_t>(), total, d_kmax, s);
     const bool guard = seg_mode && nch > 0 && m > 0;
-    if (guard) {
+    if (guard && !fused) {
       d_chmeta.reserve(2 * kMaxChan * sizeof(int));
       int meta[2 * kMaxChan];
       for (int c = 0; c < nch; c++) {
@@ -2593,10 +3526,31 @@ struct SingleEngine : Engine {
                          (uint32_t*)(d_tot.as<uint64_t>() + 5));
       SHD_CHECK_LAUNCH();
     }
-    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 64, hipMemcpyDeviceToHost, s));
+    const bool cw_cand = callwin_candidate(ncalls, total);
+    if (cw_cand) {
+      d_cw_citem.reserve((size_t)(ncalls + 1) * 4);
+      d_cw_clb.reserve((size_t)std::max<int64_t>(ncalls, 1) * 4);
+      SHD_HIP(hipMemsetAsync(d_tot.as<uint64_t>() + 8, 0, 8, s));
+      if (!fused) {   // (k_filter_items wrote them)
+        hipLaunchKernelGGL(k_cw_citem, dim3(grid_for(ncalls + 1)), dim3(kBlock), 0, s,
+                           (const int64_t*)d_offs.as<int64_t>(), (const uint32_t*)d_off.as<uint32_t>(), n, m, C,
+                           (int)ncalls, d_cw_citem.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+      }
+      hipLaunchKernelGGL(k_cw_regions, dim3(grid_for(ncalls)), dim3(kBlock), 0, s,
+                         (const uint32_t*)e_exp.as<uint32_t>(), (const uint32_t*)d_cw_citem.as<uint32_t>(),
+                         (int)ncalls, d_cw_clb.as<uint32_t>(), (uint32_t*)(d_tot.as<uint64_t>() + 8));
+      SHD_CHECK_LAUNCH();
+    }
+    SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 72, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     const int64_t X = (int64_t)h_tot.as<uint64_t>()[1];
-    const uint64_t kmax = h_tot.as<uint64_t>()[2];
+    uint64_t kmax = h_tot.as<uint64_t>()[2];
+    if (kmax_fused) kmax = std::max(kmax_seen, fused_kmax);
+    kmax_seen = std::max(kmax_seen, kmax);
+    kmax_known = true;
+    const uint32_t cw_call = cw_cand ? h_tot.as<uint32_t>()[16] : 0u;
+    const uint32_t cw_region = cw_cand ? h_tot.as<uint32_t>()[17] : 0u;
     if (guard) {
       // Segmented scans reassociate the reference's running `sum += v; sum -= v`
       // (SumAttributeAggregatorExecutor.java:184-198).  With a non-finite
@@ -2625,9 +3579,16 @@ struct SingleEngine : Engine {
       resn.reserve(std::max(nagg, 1) * cap);
       last_of.reserve(cap * 4);
     }
+    // (a range-guard trip above cleared seg_mode: that push folds exactly)
+    const bool use_cw = seg_mode && total > 0 && cw_cand && cw_call <= (uint32_t)kCwCall &&
+                        cw_region <= (uint32_t)kCwRegionMax;
+    bool emitted = false;
     first.reserve(cap);
-    if (total > 0) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
-    if (seg_mode && total > 0) {
+    if (total > 0 && !use_cw) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
+    if (use_cw) {
+      agg_callwin(b, total, cap, ncalls, X, cw_call, cw_region, kmax);
+      emitted = true;
+    } else if (seg_mode && total > 0) {
       if (!agg_chunked(total, kmax, cap, ncalls)) agg_segscan(total, kmax, cap);
     } else if (nops > 0) {
       okey.reserve(nops * 8);
@@ -2717,7 +3678,7 @@ struct SingleEngine : Engine {
       mark("group_fold");
     }
     // emission: first-seen (call, group) rows in event order
-    if (m > 0) emit_rows(b, m, cap);
+    if (m > 0 && !emitted) emit_rows(b, m, cap);
     // carry: the unexpired suffix [X, total) becomes the new window contents
     int64_t keep = wkind == 0 ? 0 : total - X;
     if (keep > 0 && X > 0) {
