@@ -70,6 +70,24 @@ __global__ void k_call_of(const int64_t* offs, int ncalls, const int64_t* ts, in
 }
 
 // now[c] = max(now_prev, last_ts[0..c])  (TimestampGeneratorImpl only moves forward)
+// only the playback time after the push: now[ncalls - 1] = max(now_prev, every last_ts)
+__global__ __launch_bounds__(kBlock) void k_call_now_last(const int64_t* last_ts, int ncalls, int64_t now_prev,
+                                                          int64_t* now) {
+  __shared__ int64_t wmax[kBlock / 64];
+  int64_t v = now_prev;
+  for (int c = threadIdx.x; c < ncalls; c += kBlock) v = last_ts[c] > v ? last_ts[c] : v;
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; k++) v = wmax[k] > v ? wmax[k] : v;
+    now[ncalls - 1] = v;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_call_now(const int64_t* last_ts, int ncalls, int64_t now_prev,
                                                      int64_t* now) {
   __shared__ int64_t carry;
@@ -1624,15 +1642,20 @@ __global__ void k_cw_citem(const int64_t* __restrict__ offs, const uint32_t* __r
 
 // first item of each call's region (binary search over the non-decreasing e)
 // and the largest call / region, for the host's choice of path
-__global__ void k_cw_regions(const uint32_t* __restrict__ e, const uint32_t* __restrict__ citem, int ncalls,
-                             uint32_t* __restrict__ clb, uint32_t* __restrict__ maxes) {
+// (wlen > 0: a length window, e[q] = q + wlen)
+__global__ void k_cw_regions(const uint32_t* __restrict__ e, int64_t wlen, const uint32_t* __restrict__ citem,
+                             int ncalls, uint32_t* __restrict__ clb, uint32_t* __restrict__ maxes) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < ncalls; c += gridDim.x * blockDim.x) {
     const uint32_t s = citem[c], t = citem[c + 1];
     uint32_t lo = 0, hi = s;   // first q in [0, s] with e[q] > s (q = s qualifies: e[s] > s)
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (e[mid] > s) hi = mid;
-      else lo = mid + 1;
+    if (wlen > 0) {
+      lo = (int64_t)s + 1 > wlen ? (uint32_t)((int64_t)s + 1 - wlen) : 0u;
+    } else {
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (e[mid] > s) hi = mid;
+        else lo = mid + 1;
+      }
     }
     clb[c] = lo;
     if (t - s > __hip_atomic_load(&maxes[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&maxes[0], t - s);
@@ -2042,7 +2065,7 @@ __global__ __launch_bounds__(kBlock) void k_cw_gtables(const CwArgs* __restrict_
         a.cnt[at] = 0;
         continue;
       }
-      if (a.e[q] != kInf) continue;
+      if (a.wlen == 0 && a.e[q] != kInf) continue;   // (a length window: every item from X on stays)
       const int ch = a.chan[j];
       if (ch < 0) {
         atomicAdd((unsigned long long*)&a.cnt[at], 1ull);
@@ -2718,8 +2741,14 @@ struct SingleEngine : Engine {
                        (const int64_t*)d_offs.as<int64_t>(), (int)ncalls, b.cs.ts, d_call_of.as<int32_t>(),
                        d_last_ts.as<int64_t>());
     SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_call_now, dim3(1), dim3(kBlock), 0, stream, (const int64_t*)d_last_ts.as<int64_t>(),
-                       (int)ncalls, now, d_now.as<int64_t>());
+    // per-call times feed the time window's expiry; every other query only
+    // moves the clock to the push's latest call time
+    if (wkind == SHD_W_TIME)
+      hipLaunchKernelGGL(k_call_now, dim3(1), dim3(kBlock), 0, stream, (const int64_t*)d_last_ts.as<int64_t>(),
+                         (int)ncalls, now, d_now.as<int64_t>());
+    else
+      hipLaunchKernelGGL(k_call_now_last, dim3(1), dim3(kBlock), 0, stream, (const int64_t*)d_last_ts.as<int64_t>(),
+                         (int)ncalls, now, d_now.as<int64_t>());
     SHD_CHECK_LAUNCH();
   }
 
@@ -3155,7 +3184,8 @@ struct SingleEngine : Engine {
       if (len) hipLaunchKernelGGL((k_cw<NC, 2048, kCwCall, true>), g, bl, 0, stream, d_ca, (int)ncalls);
       else hipLaunchKernelGGL((k_cw<NC, 2048, kCwCall, false>), g, bl, 0, stream, d_ca, (int)ncalls);
     } else {
-      hipLaunchKernelGGL((k_cw<NC, kCwRegionMax, kCwCall, false>), g, bl, 0, stream, d_ca, (int)ncalls);
+      if (len) hipLaunchKernelGGL((k_cw<NC, kCwRegionMax, kCwCall, true>), g, bl, 0, stream, d_ca, (int)ncalls);
+      else hipLaunchKernelGGL((k_cw<NC, kCwRegionMax, kCwCall, false>), g, bl, 0, stream, d_ca, (int)ncalls);
     }
     SHD_CHECK_LAUNCH();
   }
@@ -3199,7 +3229,7 @@ struct SingleEngine : Engine {
     ca.cap = cap;
     ca.C = C;
     ca.total = total;
-    ca.wlen = wparam;
+    ca.wlen = wkind == SHD_W_LENGTH ? wparam : 0;
     ca.probe = getenv("SHD_CW_PROBE") ? atoi(getenv("SHD_CW_PROBE")) : 0;
     ca.ikey = ikey[cur].as<uint64_t>();
     ca.e = e_exp.as<uint32_t>();
@@ -3477,34 +3507,45 @@ struct SingleEngine : Engine {
     hipStream_t s = stream;
     const int64_t total = C + m;
     const int64_t cap = icap[cur];
-    // expiry positions
+    // expiry positions.  A length window's are x + L (kInf past the items):
+    // X = max(0, total - L) expire, and e is only materialised for the paths
+    // that read it (not the call-window path)
     e_exp.reserve(std::max<int64_t>(total, 1) * 4);
-    hipLaunchKernelGGL(k_expiry, dim3(grid_for(total)), dim3(kBlock), 0, s, wkind, wparam, C, total,
-                       (const int64_t*)its[cur].as<int64_t>(), (const int64_t*)inow.as<int64_t>(), e_exp.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    if (wkind == SHD_W_TIME) {
-      if (total <= (int64_t)kPmaxTile * 8) {
-        hipLaunchKernelGGL(k_prefix_max_u32, dim3(1), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total);
-        SHD_CHECK_LAUNCH();
-      } else {
-        const int64_t nt = ceil_div(total, kPmaxTile);
-        d_pmax.reserve(nt * 4);
-        hipLaunchKernelGGL(k_pmax_tiles, dim3((unsigned)nt), dim3(kBlock), 0, s, (const uint32_t*)e_exp.as<uint32_t>(),
-                           total, d_pmax.as<uint32_t>());
-        SHD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_pmax_scan, dim3(1), dim3(kBlock), 0, s, d_pmax.as<uint32_t>(), nt);
-        SHD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_pmax_apply, dim3((unsigned)nt), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total,
-                           (const uint32_t*)d_pmax.as<uint32_t>());
-        SHD_CHECK_LAUNCH();
+    const bool len_win = wkind == SHD_W_LENGTH;
+    bool e_ready = false;
+    auto make_expiry = [&]() {
+      hipLaunchKernelGGL(k_expiry, dim3(grid_for(total)), dim3(kBlock), 0, s, wkind, wparam, C, total,
+                         (const int64_t*)its[cur].as<int64_t>(), (const int64_t*)inow.as<int64_t>(),
+                         e_exp.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      if (wkind == SHD_W_TIME) {
+        if (total <= (int64_t)kPmaxTile * 8) {
+          hipLaunchKernelGGL(k_prefix_max_u32, dim3(1), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total);
+          SHD_CHECK_LAUNCH();
+        } else {
+          const int64_t nt = ceil_div(total, kPmaxTile);
+          d_pmax.reserve(nt * 4);
+          hipLaunchKernelGGL(k_pmax_tiles, dim3((unsigned)nt), dim3(kBlock), 0, s,
+                             (const uint32_t*)e_exp.as<uint32_t>(), total, d_pmax.as<uint32_t>());
+          SHD_CHECK_LAUNCH();
+          hipLaunchKernelGGL(k_pmax_scan, dim3(1), dim3(kBlock), 0, s, d_pmax.as<uint32_t>(), nt);
+          SHD_CHECK_LAUNCH();
+          hipLaunchKernelGGL(k_pmax_apply, dim3((unsigned)nt), dim3(kBlock), 0, s, e_exp.as<uint32_t>(), total,
+                             (const uint32_t*)d_pmax.as<uint32_t>());
+          SHD_CHECK_LAUNCH();
+        }
       }
-    }
+      e_ready = true;
+    };
     unsigned long long* d_x = (unsigned long long*)(d_tot.as<uint64_t>() + 1);
     uint64_t* d_kmax = d_tot.as<uint64_t>() + 2;
-    SHD_HIP(hipMemsetAsync(d_x, 0, 8, s));
-    hipLaunchKernelGGL(k_count_expired, dim3(grid_for(total, 4, 2048)), dim3(kBlock), 0, s,
-                       (const uint32_t*)e_exp.as<uint32_t>(), total, d_x);
-    SHD_CHECK_LAUNCH();
+    if (!len_win) {
+      make_expiry();
+      SHD_HIP(hipMemsetAsync(d_x, 0, 8, s));
+      hipLaunchKernelGGL(k_count_expired, dim3(grid_for(total, 4, 2048)), dim3(kBlock), 0, s,
+                         (const uint32_t*)e_exp.as<uint32_t>(), total, d_x);
+      SHD_CHECK_LAUNCH();
+    }
     // the largest group id: dense ids of a fused push come from k_filter_items
     // (carried ids are bounded by the running maximum)
     const bool kmax_fused = fused && (gdense || ngk == 0) && kmax_known;
@@ -3538,13 +3579,14 @@ struct SingleEngine : Engine {
         SHD_CHECK_LAUNCH();
       }
       hipLaunchKernelGGL(k_cw_regions, dim3(grid_for(ncalls)), dim3(kBlock), 0, s,
-                         (const uint32_t*)e_exp.as<uint32_t>(), (const uint32_t*)d_cw_citem.as<uint32_t>(),
-                         (int)ncalls, d_cw_clb.as<uint32_t>(), (uint32_t*)(d_tot.as<uint64_t>() + 8));
+                         (const uint32_t*)e_exp.as<uint32_t>(), len_win ? wparam : (int64_t)0,
+                         (const uint32_t*)d_cw_citem.as<uint32_t>(), (int)ncalls, d_cw_clb.as<uint32_t>(),
+                         (uint32_t*)(d_tot.as<uint64_t>() + 8));
       SHD_CHECK_LAUNCH();
     }
     SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 72, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    const int64_t X = (int64_t)h_tot.as<uint64_t>()[1];
+    const int64_t X = len_win ? std::max<int64_t>(0, total - wparam) : (int64_t)h_tot.as<uint64_t>()[1];
     uint64_t kmax = h_tot.as<uint64_t>()[2];
     if (kmax_fused) kmax = std::max(kmax_seen, fused_kmax);
     kmax_seen = std::max(kmax_seen, kmax);
@@ -3583,6 +3625,7 @@ struct SingleEngine : Engine {
     const bool use_cw = seg_mode && total > 0 && cw_cand && cw_call <= (uint32_t)kCwCall &&
                         cw_region <= (uint32_t)kCwRegionMax;
     bool emitted = false;
+    if (!use_cw && !e_ready) make_expiry();
     first.reserve(cap);
     if (total > 0 && !use_cw) SHD_HIP(hipMemsetAsync(first.p, 0, total, s));
     if (use_cw) {
