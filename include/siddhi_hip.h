@@ -122,10 +122,7 @@ typedef struct shd_counters {
                                    grouping (hashed buckets when below the key
                                    width), 0 when not partitioned              */
   int64_t kernel_ns_total;      /* device time of every push since load / reset  */
-  int64_t dormant;              /* pattern engine, partitioned: open partials that
-                                   only a push going back in time can still meet
-                                   (kept outside the carry until their key's next
-                                   event expires them)                          */
+  int64_t dormant;              /* reserved (0): every open partial is carried   */
 } shd_counters;
 
 int shd_device_count(int* n);

@@ -65,89 +65,6 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const PrepArgs* __restrict__
   prep_block_reduce<kBlock>(acc, blk, blockIdx.x);
 }
 
-// Fused prepare + one stable radix pass: k_bkt_hist counts the 256 digits of
-// every tile from the key column alone (plain 32-bit attribute keys),
-// k_bkt_scatter prepares the rows in registers (prep_row) and writes (key,
-// flags|row, ts32) straight to their digit positions -- the prepared rows never
-// make a round trip through HBM.  H: hashed buckets (key_bucket_mix, the
-// bucketed walk's layout); else the key's low byte (the first LSD pass of the
-// sort path's key sort, whose later passes run on digits of key - kbase with
-// kbase a multiple of 256).
-constexpr int kBktRounds = 16;   // rows per lane of a scatter tile (4096 rows / tile)
-
-__device__ __forceinline__ uint32_t bkt_key32(const PrepArgs& a, int64_t r) {
-  const ExtRows& x = a.x;
-  if (r < x.C) return (uint32_t)gld(a.carry_key, r);
-  const int64_t br = r - x.C;
-  const uint8_t* nul = x.batch.nul[a.key_col];
-  if (nul && gld(nul, br)) return 0u;
-  return gld((const uint32_t*)x.batch.col[a.key_col], br);
-}
-
-template <bool H, int R = kBktRounds>
-__global__ __launch_bounds__(kRsBlock) void k_bkt_hist(const PrepArgs* __restrict__ ap, int64_t n_ext,
-                                                       uint32_t* __restrict__ hist, int nb) {
-  const PrepArgs& a = *ap;
-  __shared__ uint32_t h[kRsWaves][256];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < kRsWaves * 256; i += kRsBlock) (&h[0][0])[i] = 0;
-  const int tile = rs_tile_of(blockIdx.x, nb);
-  const int64_t wb = (int64_t)tile * rs_tile(R) + (int64_t)w * 64 * R;
-  uint32_t k[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int64_t idx = wb + r * 64 + lane;
-    k[r] = bkt_key32(a, idx < n_ext ? idx : n_ext - 1);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < R; r++)
-    if (wb + r * 64 + lane < n_ext) atomicAdd(&h[w][rs_hdigit<H>(k[r], 0, 0u)], 1u);
-  __syncthreads();
-  if (tid < 256) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < kRsWaves; i++) c += h[i][tid];
-    hist[(int64_t)tid * nb + tile] = c;
-  }
-}
-
-template <bool FAST, bool H, int R = kBktRounds>
-__global__ __launch_bounds__(kRsBlock) void k_bkt_scatter(const PrepArgs* __restrict__ ap, int64_t n_ext,
-                                                          const uint32_t* __restrict__ hist,
-                                                          const uint32_t* __restrict__ offs,
-                                                          const uint32_t* __restrict__ dtotal, int nb,
-                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                          uint32_t* __restrict__ tout, PrepAgg* __restrict__ blk) {
-  const PrepArgs& a = *ap;
-  const DExprSet es = a.es;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tile = rs_tile_of(blockIdx.x, nb);
-  const int64_t t0 = (int64_t)tile * rs_tile(R);
-  const int64_t wb = t0 + (int64_t)w * 64 * R;
-  const uint32_t c = tid < 256 ? hist[(int64_t)tid * nb + tile] : 0u;
-  const uint32_t gr = tid < 256 ? offs[(int64_t)tid * nb + tile] : 0u;
-  const uint32_t dt = tid < 256 ? dtotal[tid] : 0u;
-  const int64_t tbase = a.x.batch.ts[0];
-  PrepAcc acc;
-  uint32_t k[R], v[R], x[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int64_t idx = wb + r * 64 + lane;
-    const bool ok = idx < n_ext;
-    const int64_t li = ok ? idx : n_ext - 1;
-    uint64_t kk;
-    uint32_t f;
-    int32_t t32;
-    prep_row<FAST>(a, es, li, tbase, ok, kk, f, t32, acc);
-    k[r] = (uint32_t)kk;
-    v[r] = (f << kRowBits) | (uint32_t)li;
-    x[r] = (uint32_t)t32;
-  }
-  rs_scatter_tile<uint32_t, R, true, H>(k, v, x, n_ext, t0, wb, 0, c, gr, dt, 0u, kout, vout, tout);
-  prep_block_reduce<kRsBlock>(acc, blk, tile);
-}
-
 __global__ __launch_bounds__(kBlock) void k_finish_prep(const PrepAgg* blk, int nblk, PrepAgg* out) {
   unsigned long long c = 0, km = 0, ov = 0, um = 0, kn = ULLONG_MAX;
   long long tmin = LLONG_MAX, tmax = LLONG_MIN, ctm = LLONG_MIN;
@@ -378,7 +295,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       q++;
     }
   }
-  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = a.spill ? ST_DORM : ST_PRUNED;
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
   return st;
 }
 
@@ -397,7 +314,7 @@ __device__ __forceinline__ void scan_block_reduce(uint64_t steps, uint64_t prune
   __shared__ ScanOut wpart[kBlock / 64];
   __shared__ uint32_t wcnt[2][kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
-    wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol, 0};
+    wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol};
     wcnt[0][threadIdx.x >> 6] = nm;
     wcnt[1][threadIdx.x >> 6] = no;
   }
@@ -499,14 +416,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
         if (a.logical == 2) match_row[p] = and_open_code(a, pv_row(pvp));   // carried half state unchanged
       } else if (st == ST_PRUNED) {
         pruned++;   // every later event is at or after t_end: it would expire this partial
-      } else if (st == ST_DORM) {
-        out = PS_DORM;
-        pruned++;
       }
     }
-    // the push index under the key of every event (dormant partials of that
-    // key, from earlier pushes, are expired by it)
-    if (a.lp && (pv_flags(pvp) & F_NEW) && !(pv_flags(pvp) & F_SKIP)) a.lp[k - a.lp_base] = a.push_idx;
     pst[p] = out;
   };
   const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
@@ -689,7 +600,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     first = false;
     q0 += 64;
   }
-  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = a.spill ? ST_DORM : ST_PRUNED;
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
   if (lane == 0) {
     steps += wsteps;
     if (wviol) viol = 1;
@@ -704,9 +615,6 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       no++;
       if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
     } else if (st == ST_PRUNED) {
-      pruned++;
-    } else if (st == ST_DORM) {
-      out = PS_DORM | PS_PEND;
       pruned++;
     }
     pst[p] = out;
@@ -763,9 +671,6 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
       } else if (st == ST_PRUNED) {
         pruned++;
-      } else if (st == ST_DORM) {
-        out = PS_DORM | PS_PEND;
-        pruned++;
       }
       pst[p] = out;
   };
@@ -809,9 +714,6 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
         no++;
       } else if (st == ST_PRUNED) {
         pruned++;
-      } else if (st == ST_DORM) {
-        out = PS_DORM | PS_PEND;
-        pruned++;
       } else if (st == ST_YIELD) {
         out = PS_CONT;
         match_row[p] = (int32_t)q;
@@ -843,243 +745,6 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
     }
   }
   scan_block_reduce(steps, pruned, viol, nm, no, blk, slot0 + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
-}
-
-// ---------------------------------------------------------------- bucketed time-local walk
-// Sparse keys under `within` (config P3: 10M keys, ~0.01 events of a key per
-// `within` span).  The push is split by ONE stable hashed pass into 256
-// buckets (low 8 bits of key_bucket_mix(key)); inside a bucket positions keep
-// arrival order, which is time order (checked: the push is globally
-// time-ordered and carried partials precede it).  A partial can only complete
-// or expire on an event at most `within` later, so a workgroup takes a chunk of
-// one bucket's positions plus the bucket events up to `within` past the
-// chunk's last one, stages them in LDS, groups them by key with a second hash
-// level in LDS (1024 sub-buckets), and resolves every partial of the chunk
-// against its own key's later events there:
-//   expiry  at the first same-key event with ts - tsi > within,
-//   match   at the first same-key B event inside `within` with f2 true,
-// whichever comes first (the sequential walk's outcome; a key's events are in
-// time order).  A partial whose key has no such event in the staged region is
-// open (the bucket ends there), retired (the region already reaches beyond
-// `within`: every later event would expire it, the horizon rule), or --
-// rarely, when the staged lookahead was too short -- walked on in HBM over
-// the bucket (walk_partial, hashed-bucket stepping).
-// Bytes: one read of the bucketed (key, ts32, flags|row) per position plus
-// the lookahead overlap, instead of the three LSD passes of a full key sort.
-constexpr int kBwThreads = 512;
-constexpr int kBwEntries = 4096;   // staged positions per chunk (owned + lookahead)
-constexpr int kBwSub = 1024;       // LDS sub-buckets (bits 8..17 of key_bucket_mix)
-constexpr int kBuckets = 256;
-
-struct BktArgs {
-  ScanArgs s;
-  const PrepAgg* pg;        // device: batch time range (t_end = ts_max)
-  const uint32_t* dtot;     // positions per bucket (digit totals of the hashed pass)
-  int ch;                   // owned positions per chunk
-  int la;                   // lookahead capacity (ch + la <= kBwEntries)
-  int g2;                   // workgroups per bucket
-};
-
-template <bool FAST>
-__global__ __launch_bounds__(kBwThreads) void k_bkt_walk(const BktArgs* __restrict__ ap, int64_t n_ext,
-                                                        const uint32_t* __restrict__ skey,
-                                                        const uint32_t* __restrict__ spv,
-                                                        const int32_t* __restrict__ sts,
-                                                        int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
-                                                        ScanOut* __restrict__ blk) {
-  const BktArgs& A = *ap;
-  const ScanArgs& a = A.s;
-  const DExprSet es = a.es;
-  __shared__ uint32_t lkey[kBwEntries];
-  __shared__ int32_t lts[kBwEntries];
-  __shared__ uint32_t lpv[kBwEntries];
-  __shared__ uint16_t lslot[kBwEntries];
-  __shared__ uint16_t lperm[kBwEntries];
-  __shared__ uint32_t cnt[kBwSub + 1];
-  __shared__ uint32_t wsum[kBwThreads / 64];
-  __shared__ int64_t sh_bounds[2];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // XCD-aware: consecutive workgroup ids land on different XCDs; give the
-  // workgroups of one XCD neighbouring buckets
-  const int b = (int)(blockIdx.x % kBuckets);
-  const int g = (int)(blockIdx.x / kBuckets);
-  if (tid < 64) {
-    // bucket b spans [sum of the totals of buckets < b, + its own total)
-    uint64_t pre = 0;
-    for (int d = lane; d < kBuckets; d += 64) pre += d < b ? A.dtot[d] : 0u;
-    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if (lane == 0) {
-      sh_bounds[0] = (int64_t)pre;
-      sh_bounds[1] = (int64_t)pre + A.dtot[b];
-    }
-  }
-  __syncthreads();
-  const int64_t bs = sh_bounds[0], be = sh_bounds[1];
-  const int64_t tbase = a.x.batch.ts[0];
-  const int64_t t_end = (int64_t)A.pg->ts_max;
-  const int64_t W = a.within;
-  const GlobalPos<false, false> ld{skey, nullptr, spv, sts, nullptr, tbase, 1};
-  uint64_t steps = 0, pruned = 0;
-  uint32_t viol = 0, hw = 0;
-  for (int64_t p0 = bs + (int64_t)g * A.ch; p0 < be; p0 += (int64_t)A.g2 * A.ch) {
-    const int64_t p1 = p0 + A.ch < be ? p0 + A.ch : be;
-    const int64_t pl = p1 + A.la < be ? p1 + A.la : be;
-    const int nown = (int)(p1 - p0), nreg = (int)(pl - p0);
-    {
-      // every load of the staged region issued before the first LDS store (one
-      // memory round trip per chunk, not one per 512 positions)
-      constexpr int kPer = kBwEntries / kBwThreads;
-      uint32_t rk[kPer], rp[kPer];
-      int32_t rt[kPer];
-#pragma unroll
-      for (int j = 0; j < kPer; j++) {
-        const int i = tid + j * kBwThreads;
-        const int64_t q = p0 + (i < nreg ? i : 0);
-        rk[j] = skey[q];
-        rt[j] = sts[q];
-        rp[j] = spv[q];
-      }
-      __syncthreads();   // the previous chunk's LDS readers are done
-#pragma unroll
-      for (int j = 0; j < kPer; j++) {
-        const int i = tid + j * kBwThreads;
-        if (i < nreg) {
-          lkey[i] = rk[j];
-          lts[i] = rt[j];
-          lpv[i] = rp[j];
-        }
-      }
-    }
-    for (int i = tid; i <= kBwSub; i += kBwThreads) cnt[i] = 0;
-    __syncthreads();
-    // events (batch rows with a key) go into their sub-bucket (unordered)
-    for (int i = tid; i < nreg; i += kBwThreads) {
-      const uint32_t f = pv_flags(lpv[i]);
-      if ((f & F_NEW) && !(f & F_SKIP)) {
-        const uint32_t d2 = (key_bucket_mix(lkey[i]) >> 8) & (kBwSub - 1);
-        lslot[i] = (uint16_t)atomicAdd(&cnt[d2], 1u);
-      }
-    }
-    __syncthreads();
-    {
-      // exclusive scan of the sub-bucket counts (two per thread)
-      const uint32_t c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
-      uint32_t inc = c0 + c1;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-      }
-      if (lane == 63) wsum[w] = inc;
-      __syncthreads();
-      uint32_t pre = inc - c0 - c1, tot = 0;
-#pragma unroll
-      for (int k = 0; k < kBwThreads / 64; k++) {
-        if (k < w) pre += wsum[k];
-        tot += wsum[k];
-      }
-      __syncthreads();
-      cnt[2 * tid] = pre;
-      cnt[2 * tid + 1] = pre + c0;
-      if (tid == 0) cnt[kBwSub] = tot;
-    }
-    __syncthreads();
-    for (int i = tid; i < nreg; i += kBwThreads) {
-      const uint32_t f = pv_flags(lpv[i]);
-      if ((f & F_NEW) && !(f & F_SKIP)) {
-        const uint32_t d2 = (key_bucket_mix(lkey[i]) >> 8) & (kBwSub - 1);
-        lperm[cnt[d2] + lslot[i]] = (uint16_t)i;
-      }
-    }
-    __syncthreads();
-    const int64_t treg = tbase + (int64_t)lts[nreg - 1];   // time of the last staged position
-    for (int li = tid; li < nown; li += kBwThreads) {
-      const uint32_t pv = lpv[li];
-      uint8_t out = PS_NONE;
-      if (pv_flags(pv) & F_CAND) {
-        const uint32_t k = lkey[li];
-        const int64_t tsi = tbase + (int64_t)lts[li];
-        const int64_t r = pv_row(pv);
-        const uint32_t d2 = (key_bucket_mix(k) >> 8) & (kBwSub - 1);
-        const int q0 = (int)cnt[d2], q1 = (int)cnt[d2 + 1];
-        int jd = kBwEntries, jm = kBwEntries;
-        for (int q = q0; q < q1; q++) {
-          const int e = lperm[q];
-          if (e <= li || lkey[e] != k) continue;
-          if (tbase + (int64_t)lts[e] - tsi > W) {
-            jd = e < jd ? e : jd;
-          } else if (e < jm && (pv_flags(lpv[e]) & F_B)) {
-            PairCtx cx{&a.x, r, (int64_t)pv_row(lpv[e]), a.s_first};
-            if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) jm = e;
-          }
-        }
-        const int term = jm < jd ? jm : jd;
-        for (int q = q0; q < q1; q++) {   // (partial, event) pairs the reference examines
-          const int e = lperm[q];
-          steps += (e > li && e <= term && lkey[e] == k) ? 1u : 0u;
-        }
-        if (jm < jd) {
-          out = PS_MATCH;
-          match_row[p0 + li] = (int32_t)pv_row(lpv[jm]);
-        } else if (jd < kBwEntries) {
-          out = PS_NONE;   // expired by a later event of its key
-        } else if (pl >= be) {
-          // no later event of its key in this push
-          if (a.prune && t_end - tsi > W) {
-            pruned++;
-          } else {
-            out = PS_OPEN;
-          }
-        } else if (treg - tsi > W) {
-          pruned++;   // every later event of the push is beyond `within` (t_end >= treg)
-        } else {
-          // lookahead too short: walk on over the bucket in HBM from pl
-          hw++;
-          int64_t q = pl;
-          uint32_t pq;
-          int64_t tq;
-          uint64_t kq;
-          ld(q, pq, tq, kq);
-          int32_t j = -1;
-          uint32_t fm = 0;
-          int64_t ra = -1, rb = -1;
-          uint64_t st2 = 0;
-          const uint8_t st = walk_partial<false, FAST, 4>(a, es, n_ext, ld, r, (uint64_t)k, tsi, q, pq, tq, kq, tsi,
-                                                          false, j, st2, viol, fm, ra, rb);
-          steps += st2;
-          if (st == ST_MATCH) {
-            out = PS_MATCH;
-            match_row[p0 + li] = j;
-          } else if (st == ST_OPEN) {
-            out = PS_OPEN;
-          } else if (st == ST_PRUNED) {
-            pruned++;
-          }
-        }
-      }
-      pst[p0 + li] = out;
-    }
-  }
-  // block partials of the scan counters (match / open counts: k_tile_count)
-  for (int o = 32; o > 0; o >>= 1) {
-    steps += __shfl_xor(steps, o, 64);
-    pruned += __shfl_xor(pruned, o, 64);
-    viol |= __shfl_xor(viol, o, 64);
-    hw += __shfl_xor(hw, o, 64);
-  }
-  __shared__ ScanOut wpart[kBwThreads / 64];
-  if (lane == 0) wpart[w] = ScanOut{steps, pruned, viol, hw};
-  __syncthreads();
-  if (tid == 0) {
-    ScanOut r = wpart[0];
-    for (int k = 1; k < kBwThreads / 64; k++) {
-      r.steps += wpart[k].steps;
-      r.pruned += wpart[k].pruned;
-      r.violation |= wpart[k].violation;
-      r.hbm_walks += wpart[k].hbm_walks;
-    }
-    blk[blockIdx.x] = r;
-  }
 }
 
 // Per-tile match / open counts of the outcome bytes (the compaction tiles of
@@ -1173,22 +838,20 @@ __device__ __forceinline__ void tile_compact(const uint8_t* __restrict__ pst, in
 
 __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int nblk, ScanOut* out) {
   unsigned long long st = 0, pr = 0;
-  uint32_t v = 0, hw = 0;
+  uint32_t v = 0;
 #pragma unroll 8
   for (int b = threadIdx.x; b < nblk; b += kBlock) {
     st += blk[b].steps;
     pr += blk[b].pruned;
     v |= blk[b].violation;
-    hw += blk[b].hbm_walks;
   }
   for (int o = 32; o > 0; o >>= 1) {
     st += __shfl_xor(st, o, 64);
     pr += __shfl_xor(pr, o, 64);
     v |= __shfl_xor(v, o, 64);
-    hw += __shfl_xor(hw, o, 64);
   }
   __shared__ ScanOut wpart[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{st, pr, v, hw};
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = ScanOut{st, pr, v};
   __syncthreads();
   if (threadIdx.x == 0) {
     ScanOut r = wpart[0];
@@ -1196,7 +859,6 @@ __global__ __launch_bounds__(kBlock) void k_finish_scan(const ScanOut* blk, int 
       r.steps += wpart[w].steps;
       r.pruned += wpart[w].pruned;
       r.violation |= wpart[w].violation;
-      r.hbm_walks += wpart[w].hbm_walks;
     }
     *out = r;
   }
@@ -1360,7 +1022,6 @@ struct GatherArgs {
   uint64_t* dkey;
   int64_t* dseq;
   uint32_t amask;   // k_gather_list: stream-A columns to copy
-  const uint32_t* obase;   // k_gather_list: first output row (device word; null: 0)
   // k_gather_list: the partial's time from the sorted positions (32-bit
   // offsets from tbase, or 64-bit) and the stream-A attribute that IS the
   // partition key (from the sorted key; -1: none) -- only the other masked
@@ -1368,8 +1029,6 @@ struct GatherArgs {
   const int32_t* sts32;
   const int64_t* sts64;
   int key_attr;
-  uint32_t* dpush;         // dormant rows: the push index they became dormant in
-  uint32_t push_idx;
   // new-list / pending-list placement of each carried partial (export_replay)
   uint8_t* dpend;
   const uint8_t* pend_old;
@@ -1482,10 +1141,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __rest
                                                         const uint64_t* __restrict__ skey64) {
   const GatherArgs& a = *ap;
   const ExtRows& x = a.x;
-  const int64_t obase = a.obase ? (int64_t)*a.obase : 0;
   for (int64_t oi = (int64_t)blockIdx.x * kBlock + threadIdx.x; oi < n_open; oi = n_open) {
     const int64_t p = olist[oi];
-    const int64_t o = obase + oi;
+    const int64_t o = oi;
     const int64_t r = pv_row(spv[p]);
     // one uniform column table per branch (carried rows / pushed rows)
     const uint64_t kk = !a.partitioned ? 0 : (a.key64 ? skey64[p] : (uint64_t)skey32[p]);
@@ -1523,106 +1181,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_list(const GatherArgs* __rest
     if (sts) a.dts[o] = a.sts64 ? a.sts64[p] : gld(x.batch.ts, 0) + (int64_t)a.sts32[p];
     a.dkey[o] = kk;
     a.dpend[o] = (uint8_t)(((pst[p] & PS_PEND) || (r < x.C && a.pend_old[r])) ? 1 : 0);
-    if (a.dpush) a.dpush[o] = a.push_idx;
-  }
-}
-
-// Per-tile count of one outcome value (the low 7 bits of pst): the compaction
-// tiles of k_open_list for dormant partials.
-__global__ __launch_bounds__(kBlock) void k_tile_count_val(const uint8_t* __restrict__ pst, int64_t n, int64_t tile,
-                                                           uint32_t val, uint32_t* __restrict__ bcnt) {
-  const int64_t t0 = (int64_t)blockIdx.x * tile;
-  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
-  uint32_t c = 0;
-  for (int64_t pb = t0 + (int64_t)threadIdx.x * 16; pb < t1; pb += kBlock * 16) {
-    const uint4 raw = *reinterpret_cast<const uint4*>(pst + pb);
-    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-    for (int i = 0; i < 16; i++) c += (pb + i < t1 && ((wv[i >> 2] >> ((i & 3) * 8)) & 127u) == val) ? 1u : 0u;
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  __shared__ uint32_t ws[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int k = 0; k < kBlock / 64; k++) t += ws[k];
-    bcnt[blockIdx.x] = t;
-  }
-}
-
-// ---------------------------------------------------------------- dormant partials
-// A dormant partial (PS_DORM) of key K, made dormant at push p, is alive while
-// no event of K came in a later push (lp[K - base] <= p): every such event is
-// at or after the time that made it dormant, more than `within` after the
-// partial, so it expired it (StreamPreStateProcessor.expireEvents :326-361,
-// per key: PartitionStateHolder).  Only a push going back in time can still
-// meet an alive one -- the NFA hand-over replays them.
-__device__ __forceinline__ bool spill_alive(const SpillCols& s, int64_t i, const uint32_t* lp, uint64_t lp_base,
-                                            uint64_t lp_n) {
-  const uint64_t k = s.key[i] - lp_base;
-  return k >= lp_n || lp[k] <= s.push[i];
-}
-
-__global__ __launch_bounds__(kBlock) void k_spill_count(SpillCols s, int64_t n, int64_t tile, const uint32_t* lp,
-                                                        uint64_t lp_base, uint64_t lp_n, uint32_t* __restrict__ bcnt) {
-  const int64_t t0 = (int64_t)blockIdx.x * tile;
-  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
-  uint32_t c = 0;
-  for (int64_t i = t0 + threadIdx.x; i < t1; i += kBlock) c += spill_alive(s, i, lp, lp_base, lp_n) ? 1u : 0u;
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  __shared__ uint32_t ws[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int k = 0; k < kBlock / 64; k++) t += ws[k];
-    bcnt[blockIdx.x] = t;
-  }
-}
-
-// Alive rows of src -> dst (order kept: per key in creation order).
-__global__ __launch_bounds__(kBlock) void k_spill_move(SpillCols src, SpillCols dst, int64_t n, int64_t tile,
-                                                       const uint32_t* lp, uint64_t lp_base, uint64_t lp_n,
-                                                       const uint32_t* __restrict__ boff) {
-  const int64_t t0 = (int64_t)blockIdx.x * tile;
-  const int64_t t1 = t0 + tile < n ? t0 + tile : n;
-  __shared__ uint32_t wsum[kBlock / 64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t base = boff[blockIdx.x];
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
-    const int64_t i = c0 + threadIdx.x;
-    const bool hit = i < t1 && spill_alive(src, i, lp, lp_base, lp_n);
-    const uint64_t m = __ballot(hit);
-    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < kBlock / 64; k++) {
-      pre += k < w ? wsum[k] : 0u;
-      tot += wsum[k];
-    }
-    if (hit) {
-      const int64_t o = base + pre + (uint32_t)__popcll(m & lt);
-      for (int c = 0; c < src.ncols; c++) {
-        switch (src.types[c]) {
-          case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT:
-            ((uint32_t*)dst.col[c])[o] = ((const uint32_t*)src.col[c])[i];
-            break;
-          case SHD_T_LONG: case SHD_T_DOUBLE: ((uint64_t*)dst.col[c])[o] = ((const uint64_t*)src.col[c])[i]; break;
-          case SHD_T_BOOL: ((uint8_t*)dst.col[c])[o] = ((const uint8_t*)src.col[c])[i]; break;
-        }
-        dst.nul[c][o] = src.nul[c][i];
-      }
-      dst.ts[o] = src.ts[i];
-      dst.key[o] = src.key[i];
-      dst.seq[o] = src.seq[i];
-      dst.pend[o] = src.pend[i];
-      dst.push[o] = src.push[i];
-    }
-    base += tot;
-    __syncthreads();
   }
 }
 
@@ -1632,7 +1190,6 @@ struct CarryTable {
   // the new list for the pending list (StreamPreStateProcessor.updateState);
   // 0: still in the new list (export_replay rebuilds the placement)
   DevBuf pend;
-  DevBuf push;   // dormant table: the push index a row became dormant in
   // logical AND: filled-operand bits and the held operand event (stream B)
   DevBuf half, bcol[kMaxCols], bnul[kMaxCols], bts, bseq;
   void reserve_b(int64_t n, const std::vector<int>& types) {
@@ -1789,110 +1346,12 @@ struct PatternEngine : Engine {
   int64_t t_last = INT64_MIN;   // time of the last event (arrival order) of the committed pushes
   int64_t last_b_seq = -1;      // arrival index of the last B-stream event (export_replay placement)
   static constexpr int64_t kPruneMinRows = 1 << 16;
-  // Dormant partials (partitioned plain / OR plans, PS_DORM): open partials
-  // that every event from the push's latest time on would expire wait here,
-  // outside the next pushes' sort, until their key's next event expires them
-  // (lp: the last push index per key) -- or a push going back in time hands
-  // them to the NFA engine (unspill + export_replay).  Rows are per key in
-  // creation order and older than any carried row of their key.
-  CarryTable spill[2];
-  int scur = 0;
-  int64_t S = 0;              // alive dormant partials (as of the last push)
-  bool spill_off = false;     // keys span too wide a range for the lp table: carry everything
-  DevBuf d_lp;                // push index of each key's last event, keys [lp_base, lp_base + lp_n)
-  uint64_t lp_base = 0, lp_n = 0;
-  uint32_t push_idx = 0;      // pushes that updated lp
-  static constexpr uint64_t kLpMax = 1ull << 27;
-  DevBuf d_scnt, d_soff, d_dlist;
-  CarryTable fresh;            // sorted LDS walk: the open partials, per block region
-  DevBuf d_mjs, d_mis, d_bo, d_bm, d_boo, d_bmo;   // its match pairs per region, region counts / offsets
-  int64_t region = 0;
-  bool dorm_direct = false;    // this push: fresh holds them (finish copies instead of gathering)
-  bool open_direct = false;    // this push: the walk wrote the next carry table (finish skips the gather)
-  bool match_direct = false;   // this push: the walk wrote the (e2 row, e1 row) pairs (finish skips k_emit_pairs)
   // sorted times of this push's positions (finish: carried partials' times)
   const int32_t* fin_sts32 = nullptr;
   const int64_t* fin_sts64 = nullptr;
-  // this push (sort_push -> finish)
-  bool spill_now = false;
-  uint32_t n_dorm = 0, n_surv = 0;
-  int64_t stile = 0;
-  int nst = 0;
-
-  // opt-in (SHD_SPILL=1): on P3 the dormant table's gather + compaction
-  // (1.08 ms / step) cost more than sorting the carried rows (r03k: 15.6 vs
-  // 17.2 G events/s), so by default every open partial is carried
-  bool spill_plan() const {
-    return partitioned && logical != 2 && W != INT64_MAX && !type_key64(key_type[0]) && !type_key64(key_type[1]) &&
-           getenv("SHD_SPILL") && !getenv("SHD_NO_SPILL");
-  }
-  SpillCols spill_cols(CarryTable& t) const {
-    SpillCols c{};
-    c.ncols = (int)typesA.size();
-    for (size_t i = 0; i < typesA.size(); i++) {
-      c.types[i] = (int32_t)typesA[i];
-      c.col[i] = t.col[i].p;
-      c.nul[i] = t.nul[i].as<uint8_t>();
-    }
-    c.ts = t.ts.as<int64_t>();
-    c.key = t.key.as<uint64_t>();
-    c.seq = t.seq.as<int64_t>();
-    c.pend = t.pend.as<uint8_t>();
-    c.push = t.push.as<uint32_t>();
-    return c;
-  }
-  // the lp table covers keys [kmin, kmax] (grown, zero-filled, old entries kept)
-  bool lp_cover(uint64_t kmin, uint64_t kmax) {
-    if (lp_n && kmin >= lp_base && kmax < lp_base + lp_n) return true;
-    const uint64_t lo = lp_n ? std::min(lp_base, kmin) : kmin;
-    const uint64_t hi = lp_n ? std::max(lp_base + lp_n - 1, kmax) : kmax;
-    if (hi - lo + 1 > kLpMax) return false;
-    const uint64_t nn = std::min<uint64_t>(kLpMax, (hi - lo + 1) + (hi - lo + 1) / 8 + 1024);
-    DevBuf nb;
-    nb.reserve(nn * 4);
-    SHD_HIP(hipMemsetAsync(nb.p, 0, nn * 4, stream));
-    if (lp_n)
-      SHD_HIP(hipMemcpyAsync(nb.as<uint32_t>() + (lp_base - lo), d_lp.p, lp_n * 4, hipMemcpyDeviceToDevice, stream));
-    SHD_HIP(hipStreamSynchronize(stream));
-    std::swap(d_lp.p, nb.p);
-    std::swap(d_lp.cap, nb.cap);
-    lp_base = lo;
-    lp_n = nn;
-    return true;
-  }
-  // dormant rows back into the carry, in front of the carried rows (exact:
-  // carrying every open partial is the reference's own state)
-  void unspill() {
-    if (S <= 0) return;
-    const int nxt = cur ^ 1;
-    CarryTable& d = carry[nxt];
-    CarryTable& sp = spill[scur];
-    const CarryTable& c = carry[cur];
-    d.reserve(S + C, typesA);
-    hipStream_t s = stream;
-    auto cp = [&](DevBuf& dst, const DevBuf& a, const DevBuf& b, size_t w) {
-      SHD_HIP(hipMemcpyAsync(dst.p, a.p, (size_t)S * w, hipMemcpyDeviceToDevice, s));
-      if (C > 0) SHD_HIP(hipMemcpyAsync(dst.as<char>() + (size_t)S * w, b.p, (size_t)C * w, hipMemcpyDeviceToDevice, s));
-    };
-    for (size_t i = 0; i < typesA.size(); i++) {
-      if (!((carry_mask >> i) & 1u)) continue;
-      cp(d.col[i], sp.col[i], c.col[i], type_size(typesA[i]));
-      cp(d.nul[i], sp.nul[i], c.nul[i], 1);
-    }
-    cp(d.ts, sp.ts, c.ts, 8);
-    cp(d.key, sp.key, c.key, 8);
-    cp(d.seq, sp.seq, c.seq, 8);
-    cp(d.pend, sp.pend, c.pend, 1);
-    SHD_HIP(hipStreamSynchronize(s));
-    cur = nxt;
-    C += S;
-    S = 0;
-    counters.carry = C;
-    counters.dormant = 0;
-  }
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
-      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_gbeg, d_gend, d_olist;
+      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_olist;
   // stream-A attributes read again after a partial is carried (state-0 loads
   // of f2 / f3 / the selector): only these columns are copied into the carry
   uint32_t carry_mask = ~0u;
@@ -1901,10 +1360,6 @@ struct PatternEngine : Engine {
   int kind() const override { return ENG_PATTERN; }
 
   void reset() override {
-    S = 0;
-    push_idx = 0;
-    lp_n = 0;
-    spill_off = false;
     C = 0;
     last_b_seq = -1;
     seq = 0;
@@ -1932,7 +1387,6 @@ struct PatternEngine : Engine {
   // partial is gone, it is replayed past the start state only (skip_start),
   // so it opens no partial the reference does not hold.
   void export_replay(std::vector<Replay>& parts) override {
-    unspill();
     SHD_HIP(hipStreamSynchronize(stream));
     const CarryTable& t = carry[cur];
     std::vector<int64_t> ts(C), sq(C);
@@ -2029,7 +1483,6 @@ struct PatternEngine : Engine {
 
   // open partials (carry table) + horizon guard
   void save_state(SnapW& w) override {
-    unspill();   // the snapshot holds every open partial as a carried one
     w.put<int64_t>(C);
     w.put<int32_t>(have_horizon ? 1 : 0);
     w.put<int64_t>(horizon);
@@ -2131,582 +1584,9 @@ struct PatternEngine : Engine {
 
   void push(const Staged& b) override {
     if (b.n <= 0) return;
-    spill_now = false;
     fin_sts32 = nullptr;
     fin_sts64 = nullptr;
-    dorm_direct = false;
-    open_direct = false;
-    match_direct = false;
-    int la = 0;
-    int64_t t_last_probe = 0;
-    if (bucket_candidate(b, la, t_last_probe) && bucket_push(b, la, t_last_probe)) return;
-    if (fused_group_push(b)) return;
     sort_push(b);
-  }
-
-  // The bucketed time-local walk (k_bkt_walk) fits pushes whose keys are
-  // sparse inside one `within` span: the bucket events of one span (E_b =
-  // events per span / 256 buckets) must fit the LDS lookahead next to a chunk.
-  // Decided from the batch's first / last timestamps (one 16-byte probe);
-  // whether the push really is time-ordered (and carried partials precede it)
-  // is checked on the device and the push is redone on the sort path if not.
-  // SHD_NO_BUCKET (or a forced SHD_HASH_BITS sort): off; SHD_BUCKET: on
-  // whenever legal (tests).
-  bool bucket_candidate(const Staged& b, int& la, int64_t& t_last_probe) {
-    const int slot = b.stream == sA ? 0 : 1;
-    // (the bucketed walk retires partials at the push horizon: unpartitioned
-    // plans grouped by an implicit key only, see `prune` in sort_push)
-    if (getenv("SHD_NO_BUCKET") || getenv("SHD_HASH_BITS") || logical != 0 || W == INT64_MAX || partitioned || !implicit_key ||
-        type_key64(key_type[slot]) || sA != sB)
-      return false;
-    const int64_t n_ext = C + b.n;
-    // measured on MI355X (P3, 50M-event pushes, profiles/r02a_*): the bucketed
-    // walk (1.26 ms) plus its pass (0.82 ms) lose to the exact key sort and
-    // forward scan (1.9 ms per push in all), so it runs only when forced
-    const bool forced = getenv("SHD_BUCKET") != nullptr;
-    if (!forced) return false;
-    h_agg.reserve(256);
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 208, b.cs.ts, 8, hipMemcpyDeviceToHost, stream));
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 216, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, stream));
-    SHD_HIP(hipStreamSynchronize(stream));
-    int64_t t0, t1;
-    std::memcpy(&t0, h_agg.as<char>() + 208, 8);
-    std::memcpy(&t1, h_agg.as<char>() + 216, 8);
-    if (t1 < t0) return false;
-    const double span = (double)(t1 - t0) + 1.0;
-    const double eb = std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span) / kBuckets;
-    const double need = eb + 4.0 * std::sqrt(eb) + 64.0;
-    if (need > kBwEntries / 2) return false;
-    la = (int)std::min<double>(kBwEntries / 2, std::ceil(need / 64.0) * 64.0);
-    t_last_probe = t1;
-    return true;
-  }
-
-  bool bucket_push(const Staged& b, int la, int64_t t_last_probe) {
-    const int64_t n = b.n;
-    const bool isA = b.stream == sA, isB = b.stream == sB;
-    const int64_t n_ext = C + n;
-    if (n_ext > (int64_t)kRowMask) throw Error(SHD_E_CAPACITY, "pattern batch + carried partials exceed 2^28 rows");
-    hipStream_t s = stream;
-    SHD_HIP(hipEventRecord(ev0, s));
-    stage_begin();
-    const int slot = isA ? 0 : 1;
-    d_pv.reserve(n_ext * 4);
-    d_ts.reserve(n_ext * 4);
-    d_k32.reserve(n_ext * 4);
-    d_match.reserve(n_ext * 4);
-    d_pst.reserve(n_ext + kCompactPad);
-    d_agg.reserve(256);
-    h_agg.reserve(256);
-    ExtRows x{};
-    x.carry = carry_cs();
-    x.batch = b.cs;
-    x.C = C;
-    x.seq0 = seq;
-    x.carry_seq = carry[cur].seq.as<int64_t>();
-    PrepArgs pa{};
-    pa.x = x;
-    pa.es = dset();
-    pa.f1 = dfilters(f1);
-    pa.is_a = isA;
-    pa.is_b = isB;
-    pa.partitioned = 1;
-    pa.null_skip = partitioned;
-    pa.key64 = 0;
-    if (key_expr[slot] >= 0) pa.key_expr = dexpr(key_expr[slot]);
-    pa.key_col = key_col[slot];
-    pa.key_type = key_type[slot];
-    pa.carry_key = carry[cur].key.as<uint64_t>();
-    PrepAgg init{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN, ULLONG_MAX};
-    PrepAgg* d_pa = d_agg.as<PrepAgg>();
-    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
-    std::memcpy(h_agg.p, &init, sizeof(init));
-    std::memset(h_agg.as<char>() + 64, 0, sizeof(ScanOut));
-    SHD_HIP(hipMemcpyAsync(d_agg.p, h_agg.p, 128, hipMemcpyHostToDevice, s));
-    const int nblk = grid_for(n_ext, 1, 4096);
-    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
-    const int ntile = (int)ceil_div(n_ext, tile);
-    const int g2 = (int)std::max<int64_t>(1, ceil_div(ceil_div(n_ext, kBuckets), kBwEntries - la));
-    const int nwalk = kBuckets * g2;
-    const int nbt = (int)ceil_div(n_ext, rs_tile(kBktRounds));   // fused scatter tiles
-    d_blk.reserve((size_t)std::max<int64_t>(std::max(3 * nblk, nbt), nwalk) *
-                  std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-    const PrepArgs* d_pa_args = dev_args(pa);
-    const bool fast1 = (!isA || pa.f1.fp.ok) && pa.key_col >= 0;
-    const uint32_t* skey32;
-    const uint32_t* spv;
-    const int32_t* sts32;
-    const uint32_t* dtot;
-    if (pa.key_col >= 0 && !getenv("SHD_BUCKET_UNFUSED")) {
-      // fused: hist of the key column, then prepare + scatter in one pass
-      d_k32_alt.reserve(n_ext * 4);
-      d_pv_alt.reserve(n_ext * 4);
-      d_ts_alt.reserve(n_ext * 4);
-      d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
-      uint32_t* hist = d_sort.as<uint32_t>();
-      uint32_t* offs = hist + (int64_t)nbt * 256;
-      uint32_t* tot = offs + (int64_t)nbt * 256;
-      hipLaunchKernelGGL(k_bkt_hist<true>, dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
-      SHD_CHECK_LAUNCH();
-      radix_digit_scan(hist, nbt, offs, tot, s);
-      if (fast1)
-        hipLaunchKernelGGL((k_bkt_scatter<true, true>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
-                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
-                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                           d_blk.as<PrepAgg>());
-      else
-        hipLaunchKernelGGL((k_bkt_scatter<false, true>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,
-                           (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,
-                           d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                           d_blk.as<PrepAgg>());
-      SHD_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
-      SHD_CHECK_LAUNCH();
-      skey32 = d_k32_alt.as<uint32_t>();
-      spv = d_pv_alt.as<uint32_t>();
-      sts32 = d_ts_alt.as<int32_t>();
-      dtot = tot;
-      mark("bucket_scatter");
-    } else {
-    if (fast1)
-      hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                         d_blk.as<PrepAgg>());
-    else
-      hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                         d_blk.as<PrepAgg>());
-    SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
-    SHD_CHECK_LAUNCH();
-    mark("prepare");
-    // one stable hashed pass: 256 buckets, arrival order inside a bucket
-    d_k32_alt.reserve(n_ext * 4);
-    d_pv_alt.reserve(n_ext * 4);
-    d_ts_alt.reserve(n_ext * 4);
-    bool in_alt = false;
-    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
-                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, 8, d_sort, s, in_alt, true, 0);
-    skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
-    spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
-    sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
-    dtot = radix_digit_totals(d_sort, n_ext);
-    mark("bucket_sort");
-    }
-    ScanArgs sa{};
-    sa.x = x;
-    sa.es = dset();
-    sa.f2 = dfilters(f2);
-    sa.logical = 0;
-    sa.s_first = s_first;
-    sa.s_second = s_second;
-    sa.within = W;
-    sa.partitioned = 1;
-    sa.prune = 1;
-    sa.hash_mask = kBuckets - 1;
-    sa.t_end = t_last_probe;   // the push is time-ordered (else redone): its last event is its latest
-    BktArgs ba{};
-    ba.s = sa;
-    ba.pg = d_pa;
-    ba.dtot = dtot;
-    ba.ch = kBwEntries - la;
-    ba.la = la;
-    ba.g2 = g2;
-    const BktArgs* d_ba = dev_args(ba);
-    if (sa.f2.fp.ok)
-      hipLaunchKernelGGL(k_bkt_walk<true>, dim3(nwalk), dim3(kBwThreads), 0, s, d_ba, n_ext, skey32, spv, sts32,
-                         d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>());
-    else
-      hipLaunchKernelGGL(k_bkt_walk<false>, dim3(nwalk), dim3(kBwThreads), 0, s, d_ba, n_ext, skey32, spv, sts32,
-                         d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>());
-    SHD_CHECK_LAUNCH();
-    d_bcnt.reserve((size_t)2 * ntile * 4);
-    d_boff.reserve((size_t)2 * ntile * 4);
-    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
-                       d_bcnt.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
-    SHD_CHECK_LAUNCH();
-    mark("bucket_walk");
-    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
-    mark("compact");
-    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 144, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    PrepAgg pg;
-    ScanOut so;
-    std::memcpy(&pg, h_agg.p, sizeof(pg));
-    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
-    const uint32_t m = h_agg.as<uint32_t>()[32];
-    const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    // the walk assumed a time-ordered push after its carried partials, 32-bit
-    // time offsets and no retirement horizon behind it: else redo on the sort path
-    if (pg.unmono || pg.ovf || (C > 0 && pg.carry_tmax > pg.ts_min) || (have_horizon && pg.ts_min < horizon) ||
-        so.violation)
-      return false;
-    const int64_t t_end = (int64_t)pg.ts_max;
-    if (so.pruned) {
-      have_horizon = true;
-      horizon = std::max(horizon, t_end);
-    }
-    counters.group_bits = 8;
-    if (getenv("SHD_DEBUG_BUCKET"))
-      fprintf(stderr, "bucket push: n_ext %lld la %d ch %d g2 %d hbm_walks %u pruned %llu steps %llu\n",
-              (long long)n_ext, la, kBwEntries - la, g2, so.hbm_walks, so.pruned, so.steps);
-    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
-    return true;
-  }
-
-  // rows per group (mean) up to which the grouped LDS walk is used: the walk
-  // stages 1024 rows of a group in LDS (larger groups walk in global memory)
-  static constexpr double kGroupMaxMean = 800.0;
-  static constexpr int kGroupBits = 16;
-
-  // Grouped LDS walk: hashed 16-bit key sort of the prepared rows (d_k32 /
-  // d_pv / d_ts), then one workgroup per group (engine_group.hip), then the
-  // shared compaction tail.  Exact for partitioned plans without retiring any
-  // partial; unpartitioned implicit grouping retires by global expiry (prune).
-  void group_push(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg, bool prune, bool isB) {
-    hipStream_t s = stream;
-    d_k32_alt.reserve(n_ext * 4);
-    d_pv_alt.reserve(n_ext * 4);
-    d_ts_alt.reserve(n_ext * 4);
-    bool in_alt = false;
-    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
-                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, kGroupBits, d_sort, s, in_alt, true,
-                           0);
-    const uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
-    const uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
-    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
-    mark("key_sort");
-    (void)isB;
-    group_walk_tail(b, x, n_ext, pg, prune, skey32, spv, sts32);
-  }
-
-  // f1's attributes when it is a fast predicate over at most two of them
-  // (the fused prepare preloads them): false otherwise
-  bool f1_attrs(const DFilters& f1, int& a0, int& a1) const {
-    a0 = a1 = -1;
-    if (!f1.fp.ok) return f1.n == 0;
-    auto add = [&](const FAtom& at) {
-      if (at.kind != FA_LOAD) return true;
-      if (at.st != 0) return false;
-      if (at.attr == a0 || at.attr == a1) return true;
-      if (a0 < 0) a0 = at.attr;
-      else if (a1 < 0) a1 = at.attr;
-      else return false;
-      return true;
-    };
-    for (int i = 0; i < f1.fp.n; i++) {
-      const FCmp& c = f1.fp.c[i];
-      if (!add(c.l.a) || !add(c.l.b) || !add(c.r.a) || !add(c.r.b)) return false;
-    }
-    return true;
-  }
-
-  // Partitioned plain pattern with a plain 32-bit key column and a fast f1:
-  // prepare fused into the first hashed pass (engine_group.hip
-  // k_prep_scatter), the second pass, then the grouped walk.  false: not this
-  // push's path (nothing changed): a timestamp offset beyond 32 bits.
-  bool group_hint = true;   // the last push's groups were small (rows / keys)
-  bool fused_group_push(const Staged& b) {
-    const int slot = b.stream == sA ? 0 : 1;
-    const bool isA = b.stream == sA, isB = b.stream == sB;
-    // opt-in (SHD_GROUP=1): measured slower than the key sort on P3 (r03c:
-    // group walk 3.5 ms, fused pass 1.0 ms per 50M-row push)
-    const char* gv = getenv("SHD_GROUP");   // "1": when groups are small; "force": always
-    const bool force = gv && std::strcmp(gv, "force") == 0;
-    if (!gv || !partitioned || logical != 0 || !(group_hint || force) || getenv("SHD_NO_GROUP") ||
-        (spill_plan() && !spill_off) ||
-        getenv("SHD_NO_FUSED_GROUP") ||
-        key_col[slot] < 0 || !(key_type[slot] == SHD_T_STRING || key_type[slot] == SHD_T_INT))
-      return false;
-    const int64_t n = b.n;
-    const int64_t n_ext = C + n;
-    if (n_ext > (int64_t)kRowMask) return false;
-    PrepArgs pa{};
-    pa.f1 = dfilters(f1);
-    int a0 = -1, a1 = -1;
-    if (isA && !f1_attrs(pa.f1, a0, a1)) return false;
-    hipStream_t s = stream;
-    SHD_HIP(hipEventRecord(ev0, s));
-    stage_begin();
-    d_k32.reserve(n_ext * 4);
-    d_pv.reserve(n_ext * 4);
-    d_ts.reserve(n_ext * 4);
-    d_k32_alt.reserve(n_ext * 4);
-    d_pv_alt.reserve(n_ext * 4);
-    d_ts_alt.reserve(n_ext * 4);
-    d_match.reserve(n_ext * 4);
-    d_pst.reserve(n_ext + kCompactPad);
-    d_agg.reserve(256);
-    h_agg.reserve(256);
-    ExtRows x{};
-    x.carry = carry_cs();
-    x.batch = b.cs;
-    x.C = C;
-    x.seq0 = seq;
-    x.carry_seq = carry[cur].seq.as<int64_t>();
-    pa.x = x;
-    pa.es = dset();
-    pa.is_a = isA;
-    pa.is_b = isB;
-    pa.partitioned = 1;
-    pa.null_skip = 1;
-    pa.key64 = 0;
-    pa.key_col = key_col[slot];
-    pa.key_type = key_type[slot];
-    pa.carry_key = carry[cur].key.as<uint64_t>();
-    const PrepArgs* d_pa_args = dev_args(pa);
-    const int nbt = prep_scatter_tiles(n_ext);
-    d_blk.reserve((size_t)std::max<int64_t>(nbt, group_walk_blocks(1 << kGroupBits)) *
-                  std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-    d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
-    uint32_t* hist = d_sort.as<uint32_t>();
-    uint32_t* offs = hist + (int64_t)nbt * 256;
-    uint32_t* tot = offs + (int64_t)nbt * 256;
-    hipLaunchKernelGGL((k_bkt_hist<true, kPrepRounds>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);
-    SHD_CHECK_LAUNCH();
-    radix_digit_scan(hist, nbt, offs, tot, s);
-    launch_prep_scatter(d_pa_args, n_ext, hist, offs, tot, nbt, a0, a1, d_k32_alt.as<uint32_t>(),
-                        d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), d_blk.as<PrepAgg>(), s);
-    PrepAgg* d_pa = d_agg.as<PrepAgg>();
-    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
-    SHD_CHECK_LAUNCH();
-    mark("prepare");
-    // second hashed pass: digit bits 8..15, alt -> primary
-    bool back = false;
-    radix_sort_triples_u32(d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                           d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), n_ext, kGroupBits, d_sort, s,
-                           back, true, 0, 8);
-    const bool in_alt = !back;
-    const uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
-    const uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
-    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
-    mark("key_sort");
-    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    PrepAgg pg;
-    std::memcpy(&pg, h_agg.p, sizeof(pg));
-    if (pg.ovf) return false;   // a timestamp more than 2^31 ms from the batch's first: the sort path
-    group_walk_tail(b, x, n_ext, pg, false, skey32, spv, sts32);
-    return true;
-  }
-
-  void group_walk_tail(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg, bool prune,
-                       const uint32_t* skey32, const uint32_t* spv, const int32_t* sts32) {
-    hipStream_t s = stream;
-    const int64_t n = b.n;
-    counters.group_bits = kGroupBits;
-    {
-      const double nk = pg.kmin <= pg.kmax ? std::min<double>(65536.0, (double)(pg.kmax - pg.kmin) + 1.0) : 1.0;
-      group_hint = (double)n_ext / nk <= kGroupMaxMean;
-    }
-    ScanArgs sa{};
-    sa.x = x;
-    sa.es = dset();
-    sa.f2 = dfilters(f2);
-    sa.logical = 0;
-    sa.s_first = s_first;
-    sa.s_second = s_second;
-    sa.within = W;
-    sa.partitioned = 1;
-    sa.prune = prune;
-    const int64_t t_end = (int64_t)pg.ts_max;
-    sa.t_end = t_end;
-    const int ngroups = 1 << kGroupBits;
-    d_gbeg.reserve((size_t)ngroups * 4);
-    d_gend.reserve((size_t)ngroups * 4);
-    const int nwalk = group_walk_blocks(ngroups);
-    const int nblk = grid_for(n_ext, 1, 4096);
-    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
-    const int ntile = (int)ceil_div(n_ext, tile);
-    d_blk.reserve((size_t)std::max<int64_t>(nwalk, 3 * nblk) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-    launch_group_walk(dev_args(sa), sa.f2.fp.ok != 0, n_ext, kGroupBits, skey32, spv, sts32, d_gbeg.as<uint32_t>(),
-                      d_gend.as<uint32_t>(), d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), s);
-    d_bcnt.reserve((size_t)2 * ntile * 4);
-    d_boff.reserve((size_t)2 * ntile * 4);
-    hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
-                       d_bcnt.as<uint32_t>());
-    SHD_CHECK_LAUNCH();
-    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
-    SHD_CHECK_LAUNCH();
-    mark("forward_scan");
-    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
-    scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
-    mark("compact");
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    ScanOut so;
-    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
-    const uint32_t m = h_agg.as<uint32_t>()[32];
-    const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    if (so.violation) throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
-    if (so.pruned) {
-      have_horizon = true;
-      horizon = std::max(horizon, t_end);
-    }
-    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
-  }
-
-  // Dormant partials of this push (per-tile counts + offsets at [2 ntile,
-  // 3 ntile), total at d_mo[2]) and the alive rows of the dormant table
-  // (offsets d_soff, total d_mo[3]): lp already holds this push's events.
-  void dormant_counts(int64_t n_ext, int64_t tile, int ntile, uint32_t* d_mo) {
-    hipStream_t s = stream;
-    hipLaunchKernelGGL(k_tile_count_val, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext,
-                       tile, (uint32_t)PS_DORM, d_bcnt.as<uint32_t>() + 2 * ntile);
-    SHD_CHECK_LAUNCH();
-    scan_exclusive_u32(d_bcnt.as<uint32_t>() + 2 * ntile, d_boff.as<uint32_t>() + 2 * ntile, ntile, d_mo + 2, d_scan, s);
-    if (S > 0) {
-      nst = grid_for(S, 1, 4096);
-      stile = ceil_div(ceil_div(S, nst), kBlock) * kBlock;
-      nst = (int)ceil_div(S, stile);
-      d_scnt.reserve((size_t)nst * 4);
-      d_soff.reserve((size_t)nst * 4);
-      hipLaunchKernelGGL(k_spill_count, dim3(nst), dim3(kBlock), 0, s, spill_cols(spill[scur]), S, stile,
-                         (const uint32_t*)d_lp.as<uint32_t>(), lp_base, lp_n, d_scnt.as<uint32_t>());
-      SHD_CHECK_LAUNCH();
-      scan_exclusive_u32(d_scnt.as<uint32_t>(), d_soff.as<uint32_t>(), nst, d_mo + 3, d_scan, s);
-    } else {
-      SHD_HIP(hipMemsetAsync(d_mo + 3, 0, 4, s));
-    }
-  }
-
-  // Sorted LDS walk (engine_group.hip k_lds_walk): a stable 16-bit hashed key
-  // sort (two passes instead of the full key's three), then per group the
-  // exact key order and the walks in LDS -- no forward-scan / resume passes
-  // over HBM.  Partitioned plain patterns with 32-bit keys and time offsets,
-  // groups of at most lds_walk_cap() rows (expected rows per group = rows /
-  // min(2^16, key range)).  false: some group was larger (nothing committed;
-  // the caller redoes the push on the full key sort).
-  static constexpr int kLdsBits = 16;
-  bool lds_skip = false;
-  bool lds_candidate(const PrepAgg& pg, int64_t n_ext, bool key64) const {
-    // opt-in (SHD_LDSWALK=1): measured slower than the full key sort + forward
-    // scan on P3 (r03k: the walk is latency-bound at 1.6 ms per 50M-row push
-    // against 0.4 ms for the third sort pass + scan it replaces)
-    if (lds_skip || !partitioned || logical != 0 || key64 || pg.ovf || pg.kmin > pg.kmax || !getenv("SHD_LDSWALK") ||
-        getenv("SHD_NO_LDSWALK") || getenv("SHD_GROUP"))
-      return false;
-    const double nk = std::min<double>((double)(1 << kLdsBits), (double)(pg.kmax - pg.kmin) + 1.0);
-    return (double)n_ext / nk <= 0.75 * lds_walk_cap();
-  }
-  bool lds_push(const Staged& b, const ExtRows& x, int64_t n_ext, const PrepAgg& pg) {
-    hipStream_t s = stream;
-    d_k32_alt.reserve(n_ext * 4);
-    d_pv_alt.reserve(n_ext * 4);
-    d_ts_alt.reserve(n_ext * 4);
-    bool in_alt = false;
-    radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), d_k32_alt.as<uint32_t>(),
-                           d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext, kLdsBits, d_sort, s, in_alt, true,
-                           0);
-    uint32_t* skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
-    uint32_t* spv = in_alt ? d_pv_alt.as<uint32_t>() : d_pv.as<uint32_t>();
-    const int32_t* sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
-    mark("key_sort");
-    ScanArgs sa{};
-    sa.x = x;
-    sa.es = dset();
-    sa.f2 = dfilters(f2);
-    sa.logical = 0;
-    sa.s_first = s_first;
-    sa.s_second = s_second;
-    sa.within = W;
-    sa.partitioned = 1;
-    sa.prune = 0;   // partitioned: every open partial is carried (per-key expiry)
-    const int nwalk = std::min(1 << kLdsBits, 8192);
-    if (!getenv("SHD_CARRY_GATHER")) {
-      // the walk writes the open partials (carry rows) and the matches
-      // straight out, each block into its own region, compacted below
-      const int64_t cands = C + (int64_t)pg.n_cand;
-      region = ceil_div(cands, nwalk) * 5 / 4 + 1024;
-      fresh.reserve(region * nwalk, typesA);
-      carry[cur].pend.reserve(std::max<int64_t>(C, 1));
-      d_mjs.reserve((size_t)region * nwalk * 4);
-      d_mis.reserve((size_t)region * nwalk * 4);
-      d_bo.reserve((size_t)nwalk * 4);
-      d_bm.reserve((size_t)nwalk * 4);
-      d_boo.reserve((size_t)nwalk * 4);
-      d_bmo.reserve((size_t)nwalk * 4);
-      sa.direct = 1;
-      sa.direct_val = PS_OPEN;
-      sa.fresh = spill_cols(fresh);
-      sa.fresh.push = nullptr;
-      sa.amask = carry_mask;
-      sa.carry_pend = carry[cur].pend.as<uint8_t>();
-      sa.mj = d_mjs.as<uint32_t>();
-      sa.mi = d_mis.as<uint32_t>();
-      sa.region = region;
-      sa.blk_open = d_bo.as<uint32_t>();
-      sa.blk_match = d_bm.as<uint32_t>();
-    }
-    const int64_t t_end = (int64_t)pg.ts_max;
-    sa.t_end = t_end;
-    const int ngroups = 1 << kLdsBits;
-    d_gbeg.reserve((size_t)ngroups * 4);
-    d_gend.reserve((size_t)ngroups * 4);
-    const int nblk = grid_for(n_ext, 1, 4096);
-    const int64_t tile = ceil_div(ceil_div(n_ext, nblk), kBlock) * kBlock;
-    const int ntile = (int)ceil_div(n_ext, tile);
-    d_blk.reserve((size_t)std::max<int64_t>(nwalk, 3 * nblk) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-    d_bcnt.reserve((size_t)3 * ntile * 4);
-    d_boff.reserve((size_t)3 * ntile * 4);
-    launch_lds_walk(dev_args(sa), sa.f2.fp.ok != 0, n_ext, kLdsBits, skey32, spv, sts32, d_gbeg.as<uint32_t>(),
-                    d_gend.as<uint32_t>(), d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), nwalk, s);
-    if (!sa.direct) {
-      hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext, tile,
-                         d_bcnt.as<uint32_t>());
-      SHD_CHECK_LAUNCH();
-    }
-    ScanOut* d_so = reinterpret_cast<ScanOut*>(d_agg.as<char>() + 64);
-    hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nwalk, d_so);
-    SHD_CHECK_LAUNCH();
-    mark("forward_scan");
-    uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
-    if (!sa.direct) {
-      scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
-      scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
-    } else {   // region counts -> offsets (totals: matches, open partials)
-      scan_exclusive_u32(d_bm.as<uint32_t>(), d_bmo.as<uint32_t>(), nwalk, d_mo, d_scan, s);
-      scan_exclusive_u32(d_bo.as<uint32_t>(), d_boo.as<uint32_t>(), nwalk, d_mo + 1, d_scan, s);
-    }
-    mark("compact");
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 88, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    ScanOut so;
-    std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
-    const uint32_t m = h_agg.as<uint32_t>()[32];
-    const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    if (so.hbm_walks) return false;   // a group beyond the LDS capacity / a full region
-    if (sa.direct) {
-      carry[cur ^ 1].reserve(n_open, typesA);
-      d_pj.reserve((size_t)std::max<uint32_t>(m, 1) * 4);
-      d_pi.reserve((size_t)std::max<uint32_t>(m, 1) * 4);
-      SpillCols dst = spill_cols(carry[cur ^ 1]);
-      dst.push = nullptr;
-      launch_region_compact(sa.fresh, dst, carry_mask, region, nwalk, (const uint32_t*)d_bo.as<uint32_t>(),
-                            (const uint32_t*)d_boo.as<uint32_t>(), (const uint32_t*)d_mjs.as<uint32_t>(),
-                            (const uint32_t*)d_mis.as<uint32_t>(), d_pj.as<uint32_t>(), d_pi.as<uint32_t>(),
-                            (const uint32_t*)d_bm.as<uint32_t>(), (const uint32_t*)d_bmo.as<uint32_t>(), s);
-      mark("carry");
-    }
-    open_direct = sa.direct != 0;
-    match_direct = sa.direct != 0;
-    if (so.violation) throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
-    if (so.pruned) {
-      have_horizon = true;
-      horizon = std::max(horizon, t_end);
-    }
-    counters.group_bits = kLdsBits;
-    finish(b, x, n_ext, tile, ntile, spv, skey32, nullptr, false, true, true, false, m, n_open, so, t_end, pg.n_cand);
-    return true;
   }
 
   void sort_push(const Staged& b) {
@@ -2776,65 +1656,17 @@ struct PatternEngine : Engine {
     d_blk.reserve((size_t)3 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!keyed || pa.key_col >= 0);
-    // partitioned plans with a plain 32-bit key column: prepare fused into the
-    // key sort's first LSD pass (the key's low byte) -- the prepared rows go
-    // straight to their first-pass positions instead of a round trip through HBM
-    // (SHD_HASH_BITS asks for hashed buckets: the unfused sort)
-    // Measured on MI355X (P3, 50 M-event pushes): 2.8 ms for the fused pass
-    // against 0.9 + 0.7 ms unfused (the fused scatter's per-row prepare
-    // serialises its loads), so it is opt-in (SHD_SORT_FUSED=1) until its
-    // loads are batched.
-    const bool fused1 = partitioned && !key64 && pa.key_col >= 0 && getenv("SHD_SORT_FUSED") &&
-                        !getenv("SHD_HASH_BITS");
-    if (fused1) {
-      const int fr = getenv("SHD_FUSE_ROUNDS") ? atoi(getenv("SHD_FUSE_ROUNDS")) : 8;
-      const int R1 = fr == 4 ? 4 : (fr == 16 ? 16 : 8);
-      const int nbt = (int)ceil_div(n_ext, rs_tile(R1));
-      if ((size_t)nbt * std::max(sizeof(PrepAgg), sizeof(ScanOut)) > d_blk.cap)
-        d_blk.reserve((size_t)std::max<int64_t>(3 * nblk, nbt) * std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-      d_k32_alt.reserve(n_ext * 4);
-      d_pv_alt.reserve(n_ext * 4);
-      d_ts_alt.reserve(n_ext * 4);
-      d_sort.reserve((size_t)(2 * (int64_t)nbt * 256 + 256) * 4);
-      uint32_t* hist = d_sort.as<uint32_t>();
-      uint32_t* offs = hist + (int64_t)nbt * 256;
-      uint32_t* tot = offs + (int64_t)nbt * 256;
-#define SHD_FUSED1(RR)                                                                                              \
-  do {                                                                                                              \
-    hipLaunchKernelGGL((k_bkt_hist<false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext, hist, nbt);      \
-    SHD_CHECK_LAUNCH();                                                                                             \
-    radix_digit_scan(hist, nbt, offs, tot, s);                                                                      \
-    if (fast1)                                                                                                      \
-      hipLaunchKernelGGL((k_bkt_scatter<true, false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,       \
-                         (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,                    \
-                         d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),                 \
-                         d_blk.as<PrepAgg>());                                                                      \
-    else                                                                                                            \
-      hipLaunchKernelGGL((k_bkt_scatter<false, false, RR>), dim3(nbt), dim3(kRsBlock), 0, s, d_pa_args, n_ext,      \
-                         (const uint32_t*)hist, (const uint32_t*)offs, (const uint32_t*)tot, nbt,                    \
-                         d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),                 \
-                         d_blk.as<PrepAgg>());                                                                      \
-    SHD_CHECK_LAUNCH();                                                                                             \
-  } while (0)
-      if (R1 == 4) SHD_FUSED1(4);
-      else if (R1 == 16) SHD_FUSED1(16);
-      else SHD_FUSED1(8);
-#undef SHD_FUSED1
-      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nbt, d_pa);
-      SHD_CHECK_LAUNCH();
-    } else {
-      if (fast1)
-        hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                           d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                           d_blk.as<PrepAgg>());
-      else
-        hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
-                           d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
-                           d_blk.as<PrepAgg>());
-      SHD_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
-      SHD_CHECK_LAUNCH();
-    }
+    if (fast1)
+      hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
+    else
+      hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
+                         d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
+                         d_blk.as<PrepAgg>());
+    SHD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
+    SHD_CHECK_LAUNCH();
     SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     PrepAgg pg;
@@ -2862,47 +1694,10 @@ struct PatternEngine : Engine {
     // (PartitionStateHolder: per-key pending lists), which may arrive in any
     // later push with any timestamp, so partitioned plans carry every open
     // partial until its key kills or completes it.
-    // partitioned: the same partials become dormant (PS_DORM) instead -- on
-    // the full key sort path; the sorted LDS walk carries every open partial
-    // (a per-event push-index write would be a random store there)
-    const bool lds = lds_candidate(pg, n_ext, key64);
-    bool spill_p = false;
-    if (!lds && spill_plan() && !spill_off) {
-      if (pg.kmin <= pg.kmax && !lp_cover(pg.kmin, pg.kmax)) spill_off = true;
-      else spill_p = S > 0 || n_ext >= kPruneMinRows || getenv("SHD_SPILL") != nullptr;
-    }
-    if (!spill_p && S > 0) {   // the dormant rows go back into the carry: redo the push with them
-      unspill();
-      sort_push(b);
-      return;
-    }
-    const bool prune = (n_ext >= kPruneMinRows && W != INT64_MAX && !partitioned) || spill_p;
-    if (lds) {
-      if (lds_push(b, x, n_ext, pg)) return;
-      lds_skip = true;   // redo this push on the full key sort
-      try {
-        sort_push(b);
-      } catch (...) {
-        lds_skip = false;
-        throw;
-      }
-      lds_skip = false;
-      return;
-    }
+    const bool prune = n_ext >= kPruneMinRows && W != INT64_MAX && !partitioned;
     // implicit grouping needs the reference's global expiry order to be the
     // per-key one: pushed rows time-ordered, carried partials before them
     const bool grouped = partitioned || (implicit_key && !pg.unmono && (C == 0 || pg.carry_tmax <= pg.ts_min));
-    // grouped LDS walk (engine_group.hip): a 16-bit hashed key sort (two
-    // passes) and the per-group walk in LDS, when the groups are small --
-    // expected rows per group = rows / min(2^16, keys of the push)
-    if (grouped && logical == 0 && !key64 && !pg.ovf && !spill_p && !getenv("SHD_NO_GROUP") && pg.kmin <= pg.kmax) {
-      const double nk = std::min<double>(65536.0, (double)(pg.kmax - pg.kmin) + 1.0);
-      const char* gv = getenv("SHD_GROUP");
-      if (gv && (std::strcmp(gv, "force") == 0 || (double)n_ext / nk <= kGroupMaxMean)) {
-        group_push(b, x, n_ext, pg, prune, isB);
-        return;
-      }
-    }
     uint32_t hash_mask = 0;
     counters.group_bits = 0;
     if (grouped) {
@@ -2913,14 +1708,7 @@ struct PatternEngine : Engine {
       int bits = 0;
       while (bits < 64 && (kmax >> bits)) bits++;
       uint32_t kbase = 0;
-      if (fused1) {
-        // the first pass sorted by the key's low byte: digits of key - kbase
-        // with kbase a multiple of 256 continue it
-        kbase = (uint32_t)(kmin & ~(uint64_t)255);
-        int rb = 0;
-        while (rb < 64 && ((kmax - kbase) >> rb)) rb++;
-        bits = std::max(rb, 8);
-      } else if (bits <= 32 && !type_key64(key_type[slot])) {
+      if (bits <= 32 && !type_key64(key_type[slot])) {
         int rb = 0;
         while (rb < 64 && ((kmax - kmin) >> rb)) rb++;
         if (rb < bits) {
@@ -2929,32 +1717,21 @@ struct PatternEngine : Engine {
         }
       }
       bool in_alt = false;
-      if (fused1) {
-        d_k32.reserve(n_ext * 4);
-        bool back = false;
-        radix_sort_triples_u32(d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(),
-                               d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(), n_ext, bits, d_sort, s,
-                               back, false, kbase, 8);
-        in_alt = !back;   // the first pass wrote the alt arrays
-        skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
-      } else {
-        if (bits <= 32) {
-          const int hb = hashed_bucket_bits(pg, n_ext, bits, prune && !partitioned);
-          if (hb > 0) {
-            bits = hb;
-            hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
-          }
-        }
-        d_pv_alt.reserve(n_ext * 4);
-        d_ts_alt.reserve(n_ext * 4);
-        if (key64 && bits <= 32) {
-          hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
-                             d_k32.as<uint32_t>(), n_ext);
-          SHD_CHECK_LAUNCH();
+      if (bits <= 32) {
+        const int hb = hashed_bucket_bits(pg, n_ext, bits, prune && !partitioned);
+        if (hb > 0) {
+          bits = hb;
+          hash_mask = hb >= 32 ? 0xFFFFFFFFu : ((1u << hb) - 1u);
         }
       }
-      if (fused1) {
-      } else if (bits <= 32) {
+      d_pv_alt.reserve(n_ext * 4);
+      d_ts_alt.reserve(n_ext * 4);
+      if (key64 && bits <= 32) {
+        hipLaunchKernelGGL(k_narrow_keys, dim3(grid_for(n_ext)), dim3(kBlock), 0, s, d_k64.as<uint64_t>(),
+                           d_k32.as<uint32_t>(), n_ext);
+        SHD_CHECK_LAUNCH();
+      }
+      if (bits <= 32) {
         d_k32_alt.reserve(n_ext * 4);
         radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
                                d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
@@ -2996,12 +1773,6 @@ struct PatternEngine : Engine {
     sa.partitioned = grouped;
     sa.prune = prune;
     sa.hash_mask = hash_mask;
-    if (spill_p) {
-      sa.spill = 1;
-      sa.lp = d_lp.as<uint32_t>();
-      sa.lp_base = lp_base;
-      sa.push_idx = push_idx + 1;
-    }
     const int64_t t_end = (int64_t)pg.ts_max;   // latest event of this push
     sa.t_end = t_end;
     const bool fast2 = sa.f2.fp.ok != 0 && (!logical || sa.f3.fp.ok != 0);
@@ -3110,8 +1881,6 @@ struct PatternEngine : Engine {
     uint32_t* d_mo = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 128);
     scan_exclusive_u32(d_bcnt.as<uint32_t>(), d_boff.as<uint32_t>(), ntile, d_mo, d_scan, s);
     scan_exclusive_u32(d_bcnt.as<uint32_t>() + ntile, d_boff.as<uint32_t>() + ntile, ntile, d_mo + 1, d_scan, s);
-    spill_now = spill_p;
-    if (spill_p) dormant_counts(n_ext, tile, ntile, d_mo);
     mark("compact");
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     // time of the push's last event in arrival order (NeedNfa hand-over: global expiry of unpartitioned plans)
@@ -3121,8 +1890,6 @@ struct PatternEngine : Engine {
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];
     const uint32_t n_open = h_agg.as<uint32_t>()[33];
-    n_dorm = spill_p ? h_agg.as<uint32_t>()[34] : 0u;
-    n_surv = spill_p ? h_agg.as<uint32_t>()[35] : 0u;
     if (so.violation)   // the generic NFA engine takes over (shd_push replays the open partials)
       throw NeedNfa("pattern engine: event timestamps decrease within a key under `within`");
     if (so.pruned) {
@@ -3152,13 +1919,11 @@ struct PatternEngine : Engine {
         d_se1.reserve((int64_t)m * 4);
         d_sot.reserve((int64_t)m * 4);
       }
-      if (!match_direct) {
-        hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
-                           (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
-                           tile, logical, (const int32_t*)d_mother.as<int32_t>(), d_pj.as<uint32_t>(),
-                           d_pi.as<uint32_t>(), d_se1.as<uint32_t>(), d_sot.as<int32_t>());
-        SHD_CHECK_LAUNCH();
-      }
+      hipLaunchKernelGGL(k_emit_pairs, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                         (const uint32_t*)d_boff.as<uint32_t>(), (const int32_t*)d_match.as<int32_t>(), spv, n_ext,
+                         tile, logical, (const int32_t*)d_mother.as<int32_t>(), d_pj.as<uint32_t>(),
+                         d_pi.as<uint32_t>(), d_se1.as<uint32_t>(), d_sot.as<int32_t>());
+      SHD_CHECK_LAUNCH();
       int bits = 0;
       while (bits < 32 && ((uint64_t)n_ext >> bits)) bits++;
       if (logical) bits++;   // + processor order
@@ -3200,7 +1965,7 @@ struct PatternEngine : Engine {
     // ---- carry the still-open partials
     int nxt = cur ^ 1;
     carry[nxt].reserve(n_open, typesA);
-    if (n_open > 0 && !open_direct) {
+    if (n_open > 0) {
       GatherArgs ga{};
       ga.x = x;
       ga.ncols = (int)typesA.size();
@@ -3263,70 +2028,6 @@ struct PatternEngine : Engine {
       SHD_CHECK_LAUNCH();
       mark("carry");
     }
-    // ---- dormant table: its alive rows, then this push's dormant partials
-    const int sn = scur ^ 1;
-    if (spill_now) {
-      CarryTable& dst = spill[sn];
-      const int64_t ns = (int64_t)n_surv + n_dorm;
-      dst.reserve(ns, typesA);
-      dst.push.reserve((size_t)std::max<int64_t>(ns, 1) * 4);
-      if (S > 0 && n_surv > 0) {
-        hipLaunchKernelGGL(k_spill_move, dim3(nst), dim3(kBlock), 0, s, spill_cols(spill[scur]), spill_cols(dst), S,
-                           stile, (const uint32_t*)d_lp.as<uint32_t>(), lp_base, lp_n,
-                           (const uint32_t*)d_soff.as<uint32_t>());
-        SHD_CHECK_LAUNCH();
-      }
-      if (n_dorm > 0 && dorm_direct) {
-        // the walk wrote them: append after the survivors
-        const int64_t o = n_surv;
-        auto cp = [&](DevBuf& d, const DevBuf& src, size_t w) {
-          SHD_HIP(hipMemcpyAsync(d.as<char>() + (size_t)o * w, src.p, (size_t)n_dorm * w, hipMemcpyDeviceToDevice, s));
-        };
-        for (size_t c = 0; c < typesA.size(); c++) {
-          if (!((carry_mask >> c) & 1u)) continue;
-          cp(dst.col[c], fresh.col[c], type_size(typesA[c]));
-          cp(dst.nul[c], fresh.nul[c], 1);
-        }
-        cp(dst.ts, fresh.ts, 8);
-        cp(dst.key, fresh.key, 8);
-        cp(dst.seq, fresh.seq, 8);
-        cp(dst.pend, fresh.pend, 1);
-        cp(dst.push, fresh.push, 4);
-      } else if (n_dorm > 0) {
-        GatherArgs gd{};
-        gd.x = x;
-        gd.ncols = (int)typesA.size();
-        gd.partitioned = 1;
-        gd.key64 = 0;
-        for (size_t c = 0; c < typesA.size(); c++) {
-          gd.types[c] = (int32_t)typesA[c];
-          gd.dcol[c] = dst.col[c].p;
-          gd.dnul[c] = dst.nul[c].as<uint8_t>();
-        }
-        gd.dts = dst.ts.as<int64_t>();
-        gd.dkey = dst.key.as<uint64_t>();
-        gd.dseq = dst.seq.as<int64_t>();
-        carry[cur].pend.reserve(std::max<int64_t>(C, 1));
-        gd.dpend = dst.pend.as<uint8_t>();
-        gd.pend_old = carry[cur].pend.as<uint8_t>();
-        gd.amask = carry_mask;
-        gd.key_attr = -1;
-        gd.obase = reinterpret_cast<const uint32_t*>(d_agg.as<char>() + 140);   // survivors come first
-        gd.dpush = dst.push.as<uint32_t>();
-        gd.push_idx = push_idx + 1;
-        d_dlist.reserve((size_t)n_dorm * 4);
-        // dormant offsets at [2 ntile, 3 ntile): k_open_list reads boff[ntile + tile]
-        hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
-                           (const uint32_t*)d_boff.as<uint32_t>() + ntile, n_ext, tile, d_dlist.as<uint32_t>(),
-                           (uint32_t)PS_DORM);
-        SHD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_gather_list, dim3(grid_cover((int64_t)n_dorm)), dim3(kBlock), 0, s, dev_args(gd),
-                           (const uint32_t*)d_dlist.as<uint32_t>(), (int64_t)n_dorm,
-                           (const uint8_t*)d_pst.as<uint8_t>(), spv, skey32, skey64);
-        SHD_CHECK_LAUNCH();
-      }
-      mark("dormant");
-    }
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -3334,11 +2035,6 @@ struct PatternEngine : Engine {
     SHD_HIP(hipEventElapsedTime(&ms, ev0, ev1));
     cur = nxt;
     C = n_open;
-    if (spill_now) {
-      scur = sn;
-      S = (int64_t)n_surv + n_dorm;
-      push_idx++;
-    }
     if (b.stream == sB) last_b_seq = seq + n - 1;
     seq += n;
     if (b.advance_time && t_end > now) now = t_end;
@@ -3347,7 +2043,6 @@ struct PatternEngine : Engine {
     counters.matches += m;
     counters.partial_scans += (int64_t)so.steps;
     counters.carry = C;
-    counters.dormant = S;
     counters.kernel_ns = (int64_t)(ms * 1e6);
     counters.partials += (int64_t)n_cand;
     for (PatternEngine* g : gmembers) {
@@ -3383,7 +2078,7 @@ struct PatternEngine : Engine {
     if (grouped) throw Error(SHD_E_ARG, "the leader already belongs to a group");
     if (ms.empty() || ms.size() > (size_t)kGroupMax) throw Error(SHD_E_ARG, "a group holds 1..64 member queries");
     if (logical != 0) throw Error(SHD_E_UNSUPPORTED, "query groups: logical patterns are not shared");
-    if (counters.events != 0 || C != 0 || S != 0) throw Error(SHD_E_ARG, "the group leader must be fresh");
+    if (counters.events != 0 || C != 0) throw Error(SHD_E_ARG, "the group leader must be fresh");
     std::vector<PatternEngine*> v;
     for (Engine* e : ms) {
       auto* m = dynamic_cast<PatternEngine*>(e);
@@ -3399,7 +2094,7 @@ struct PatternEngine : Engine {
       for (size_t k = 0; ok && k < f2.size(); k++) ok = same_expr(plan, f2[k], m->plan, m->f2[k]);
       if (!ok)
         throw Error(SHD_E_ARG, "group member differs from the leader beyond the e1 filter and the selector");
-      if (m->counters.events != 0 || m->C != 0 || m->S != 0 || m->out.count != 0)
+      if (m->counters.events != 0 || m->C != 0 || m->out.count != 0)
         throw Error(SHD_E_ARG, "group members must be fresh (reset, no unpolled rows)");
       v.push_back(m);
     }

@@ -1820,7 +1820,8 @@ __global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__
   if (c >= ncalls) return;
   const uint32_t s = a.citem[c], t = a.citem[c + 1];
   if (s == t) return;
-  const uint32_t lb = a.clb[c];
+  // (a length window: the region starts L - 1 items before the call)
+  const uint32_t lb = LEN ? ((int64_t)s + 1 > a.wlen ? (uint32_t)((int64_t)s + 1 - a.wlen) : 0u) : a.clb[c];
   const int nr = (int)(t - lb);
   const int rs = (int)(s - lb);
   for (int g = threadIdx.x; g < GCAP; g += kBlock) {
@@ -1922,7 +1923,7 @@ __global__ __launch_bounds__(kBlock) void k_cw(const CwArgs* __restrict__ ap, in
   const int c = blockIdx.x;
   if (c >= ncalls) return;
   const uint32_t s = a.citem[c], t = a.citem[c + 1];
-  const uint32_t lb = s == t ? s : a.clb[c];
+  const uint32_t lb = s == t ? s : (LEN ? ((int64_t)s + 1 > a.wlen ? (uint32_t)((int64_t)s + 1 - a.wlen) : 0u) : a.clb[c]);
   const int nr = (int)(t - lb);
   for (int h = threadIdx.x; h < kHash; h += kBlock) hkey[h] = kCwEmpty;
   if (threadIdx.x == 0) nslots = 0;
@@ -2721,6 +2722,63 @@ struct SingleEngine : Engine {
     counters.carry = C;
   }
 
+  // ---- query sharing (shd_group_create): window queries that differ only in
+  // the length of their length window share this engine's filter pass and
+  // items (it holds the longest window); each member's rows come from its own
+  // call-window fold over them.  The leader emits no rows of its own.
+  std::vector<SingleEngine*> wmembers;
+
+  static bool same_expr(const Plan& p, int e, const Plan& q, int f) {
+    if (e < 0 || f < 0) return e == f;
+    const auto& A = p.exprs[e];
+    const auto& B = q.exprs[f];
+    if (A.size() != B.size()) return false;
+    for (size_t i = 0; i < A.size(); i++) {
+      if (A[i].op != B[i].op || A[i].b != B[i].b || A[i].c != B[i].c) return false;
+      if (A[i].op == SHD_OP_CONST ? p.consts[A[i].a] != q.consts[B[i].a] : A[i].a != B[i].a) return false;
+    }
+    return true;
+  }
+
+  void group_attach(const std::vector<Engine*>& ms) override {
+    if (grouped) throw Error(SHD_E_ARG, "the leader already belongs to a group");
+    if (ms.empty() || ms.size() > 64) throw Error(SHD_E_ARG, "a group holds 1..64 member queries");
+    if (!agg_mode || !seg_mode || wkind != SHD_W_LENGTH || ngk == 0 || partitioned)
+      throw Error(SHD_E_UNSUPPORTED, "query groups: only length-window group-by aggregates share items");
+    if (counters.events != 0 || C != 0) throw Error(SHD_E_ARG, "the group leader must be fresh");
+    std::vector<SingleEngine*> v;
+    for (Engine* e : ms) {
+      auto* m = dynamic_cast<SingleEngine*>(e);
+      if (!m || m == this || m->grouped) throw Error(SHD_E_ARG, "group member: not a free window query");
+      for (SingleEngine* o : v)
+        if (o == m) throw Error(SHD_E_ARG, "group member listed twice");
+      bool ok = m->agg_mode && m->seg_mode && m->wkind == SHD_W_LENGTH && m->wparam <= wparam && !m->partitioned &&
+                m->plan.stream_types == plan.stream_types && m->filters.size() == filters.size() &&
+                m->ngk == ngk && m->gdense == gdense && m->nagg == nagg && m->outs.size() == outs.size() &&
+                m->nch == nch;
+      for (size_t k = 0; ok && k < filters.size(); k++) ok = same_expr(plan, filters[k], m->plan, m->filters[k]);
+      for (int k = 0; ok && k < ngk; k++)
+        ok = same_expr(plan, gk_expr[k], m->plan, m->gk_expr[k]) && gk_type[k] == m->gk_type[k];
+      for (int k = 0; ok && k < nagg; k++)
+        ok = plan.aggs[k].kind == m->plan.aggs[k].kind && plan.aggs[k].type == m->plan.aggs[k].type &&
+             same_expr(plan, plan.aggs[k].expr, m->plan, m->plan.aggs[k].expr) && chan_of[k] == m->chan_of[k];
+      if (!ok)
+        throw Error(SHD_E_ARG, "group member differs from the leader beyond its window length (or is longer)");
+      if (m->counters.events != 0 || m->C != 0 || m->out.count != 0)
+        throw Error(SHD_E_ARG, "group members must be fresh (reset, no unpolled rows)");
+      v.push_back(m);
+    }
+    wmembers = v;
+    grouped = true;
+    for (SingleEngine* m : wmembers) m->grouped = true;
+  }
+
+  void group_detach() override {
+    for (SingleEngine* m : wmembers) m->grouped = false;
+    wmembers.clear();
+    grouped = false;
+  }
+
   std::vector<int64_t> h_offs;   // lives until the next push (async H2D source)
   PinnedBuf h_last, h_offs_pin;
 
@@ -2809,6 +2867,8 @@ struct SingleEngine : Engine {
       if (last > now) now = last;
     }
     seq += n;
+    for (SingleEngine* q : wmembers)
+      if (now > q->now) q->now = now;
   }
 
   // Debug hook (SHD_DEBUG_ARGS=1): read the argument block back from the
@@ -3212,24 +3272,35 @@ struct SingleEngine : Engine {
   // the call-window fold + the rows of every call (no run records / k_emit)
   void agg_callwin(const Staged& b, int64_t total, int64_t cap, int64_t ncalls, int64_t X, uint32_t call,
                    uint32_t region, uint64_t kmax) {
+    callwin_rows(*this, b, total, cap, ncalls, X, call, region, kmax, true);
+  }
+
+  // The call-window rows of query `q` (this engine, or a member of its window
+  // group) over this engine's items: q's window length, group tables, output
+  // buffer and ids.  rows_known: k_cw_count's scan of the rows per call is
+  // still current (a group's members share it: the calls' distinct groups do
+  // not depend on the window).
+  void callwin_rows(SingleEngine& q, const Staged& b, int64_t total, int64_t cap, int64_t ncalls, int64_t X,
+                    uint32_t call, uint32_t region, uint64_t kmax, bool count_rows) {
     hipStream_t s = stream;
     const int64_t m = total - C;
+    q.ensure_groups((int64_t)kmax + 1);
     CwArgs ca{};
-    ca.nch = std::max(nch, 1);
+    ca.nch = std::max(q.nch, 1);
     for (int c = 0; c < ca.nch; c++) {
-      ca.ch_agg[c] = nch ? ch_agg[c] : 0;
-      ca.ch_type[c] = nch ? ch_type[c] : SHD_T_DOUBLE;
+      ca.ch_agg[c] = q.nch ? q.ch_agg[c] : 0;
+      ca.ch_type[c] = q.nch ? q.ch_type[c] : SHD_T_DOUBLE;
     }
-    ca.nagg = nagg;
-    for (int g = 0; g < nagg; g++) {
-      ca.kind[g] = plan.aggs[g].kind;
-      ca.type[g] = plan.aggs[g].type;
-      ca.chan[g] = chan_of[g];
+    ca.nagg = q.nagg;
+    for (int g = 0; g < q.nagg; g++) {
+      ca.kind[g] = q.plan.aggs[g].kind;
+      ca.type[g] = q.plan.aggs[g].type;
+      ca.chan[g] = q.chan_of[g];
     }
     ca.cap = cap;
     ca.C = C;
     ca.total = total;
-    ca.wlen = wkind == SHD_W_LENGTH ? wparam : 0;
+    ca.wlen = wkind == SHD_W_LENGTH ? q.wparam : 0;
     ca.probe = getenv("SHD_CW_PROBE") ? atoi(getenv("SHD_CW_PROBE")) : 0;
     ca.ikey = ikey[cur].as<uint64_t>();
     ca.e = e_exp.as<uint32_t>();
@@ -3237,37 +3308,37 @@ struct SingleEngine : Engine {
     ca.iargn = iargn[cur].as<uint8_t>();
     ca.citem = d_cw_citem.as<uint32_t>();
     ca.clb = d_cw_clb.as<uint32_t>();
-    ca.dsum = g_dsum.as<double>();
-    ca.cnt = g_cnt.as<int64_t>();
-    ca.nkeys = g_nkeys;
+    ca.dsum = q.g_dsum.as<double>();
+    ca.cnt = q.g_cnt.as<int64_t>();
+    ca.nkeys = q.g_nkeys;
     // rows: at most one per new item
-    out.ensure(std::max<int64_t>(m, 1), s);
+    q.out.ensure(std::max<int64_t>(m, 1), s);
     ca.cs = b.cs;
-    ca.es = dset();
-    ca.nout = (int)outs.size();
-    for (size_t c = 0; c < outs.size(); c++) {
-      ca.outs[c] = dexpr(outs[c]);
-      const auto& code = plan.exprs[outs[c]];
+    ca.es = q.dset();
+    ca.nout = (int)q.outs.size();
+    for (size_t c = 0; c < q.outs.size(); c++) {
+      ca.outs[c] = q.dexpr(q.outs[c]);
+      const auto& code = q.plan.exprs[q.outs[c]];
       ca.okind[c] = 0;
       if (code.size() == 1 && code[0].op == SHD_OP_LOAD) {
         ca.okind[c] = 1;
         ca.oarg[c] = code[0].c & 0xFFFF;
-      } else if (code.size() == 1 && code[0].op == SHD_OP_AGG && code[0].a >= 0 && code[0].a < nagg) {
+      } else if (code.size() == 1 && code[0].op == SHD_OP_AGG && code[0].a >= 0 && code[0].a < q.nagg) {
         ca.okind[c] = 2;
         ca.oarg[c] = code[0].a;
       }
     }
     ca.ievrow = ievrow.as<int32_t>();
-    ca.row0 = out.count;
-    ca.chunk0 = chunk_seq;
-    ca.seq0 = seq;
-    ca.o_chunk = out.d_chunk();
-    ca.o_type = out.d_type();
-    ca.o_ts = out.d_ts();
-    ca.o_vals = out.d_vals();
-    ca.o_nul = out.d_nulls();
-    ca.o_seq = out.d_seq();
-    ca.o_sidx = out.d_sidx();
+    ca.row0 = q.out.count;
+    ca.chunk0 = q.chunk_seq;
+    ca.seq0 = q.seq;
+    ca.o_chunk = q.out.d_chunk();
+    ca.o_type = q.out.d_type();
+    ca.o_ts = q.out.d_ts();
+    ca.o_vals = q.out.d_vals();
+    ca.o_nul = q.out.d_nulls();
+    ca.o_seq = q.out.d_seq();
+    ca.o_sidx = q.out.d_sidx();
     d_cw_status.reserve((size_t)ncalls * 8);
     SHD_HIP(hipMemsetAsync(d_cw_status.p, 0, (size_t)ncalls * 8, s));
     ca.status = d_cw_status.as<uint64_t>();
@@ -3275,14 +3346,16 @@ struct SingleEngine : Engine {
     const CwArgs* d_ca = dev_args(ca);
     if (kmax < (uint64_t)kCwDirectG && !getenv("SHD_CW_HASH")) {
       // rows per call (distinct groups) -> each call's first row
-      d_cw_cnt.reserve((size_t)ncalls * 4);
-      d_cw_base.reserve((size_t)ncalls * 4);
-      hipLaunchKernelGGL(k_cw_count<kCwDirectG>, dim3((unsigned)ncalls), dim3(kBlock), 0, s, d_ca, (int)ncalls,
-                         d_cw_cnt.as<uint32_t>());
-      SHD_CHECK_LAUNCH();
-      scan_exclusive_u32(d_cw_cnt.as<uint32_t>(), d_cw_base.as<uint32_t>(), ncalls, (uint32_t*)(d_tot.as<uint64_t>() + 9),
-                         d_scan, s);
-      SHD_HIP(hipMemsetAsync(d_tot.as<uint32_t>() + 19, 0, 4, s));   // (the row count's high word)
+      if (count_rows) {
+        d_cw_cnt.reserve((size_t)ncalls * 4);
+        d_cw_base.reserve((size_t)ncalls * 4);
+        hipLaunchKernelGGL(k_cw_count<kCwDirectG>, dim3((unsigned)ncalls), dim3(kBlock), 0, s, d_ca, (int)ncalls,
+                           d_cw_cnt.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+        scan_exclusive_u32(d_cw_cnt.as<uint32_t>(), d_cw_base.as<uint32_t>(), ncalls,
+                           (uint32_t*)(d_tot.as<uint64_t>() + 9), d_scan, s);
+        SHD_HIP(hipMemsetAsync(d_tot.as<uint32_t>() + 19, 0, 4, s));   // (the row count's high word)
+      }
       switch (ca.nch) {
         case 1: callwin_direct<1>(d_ca, ncalls, call, region); break;
         case 2: callwin_direct<2>(d_ca, ncalls, call, region); break;
@@ -3317,8 +3390,8 @@ struct SingleEngine : Engine {
     mark("group_tables");
     SHD_HIP(hipStreamSynchronize(s));
     const int64_t nrows = m > 0 ? (int64_t)h_tot.as<uint64_t>()[9] : 0;
-    out.count += nrows;
-    counters.matches += nrows;
+    q.out.count += nrows;
+    q.counters.matches += nrows;
   }
 
   void agg_segscan(int64_t total, uint64_t kmax, int64_t cap) {
@@ -3615,6 +3688,26 @@ struct SingleEngine : Engine {
       throw Error(SHD_E_CAPACITY, "more than 2^26 group-by keys in the dense group tables");
     ensure_groups((int64_t)kmax + 1);
     const int64_t nops = m + X;
+    if (!wmembers.empty()) {   // a window group's leader: its members' rows from these items, no rows of its own
+      if (!seg_mode)
+        throw Error(SHD_E_UNSUPPORTED, "query group: an operand outside the segmented scans' range (non-finite, "
+                                       "or magnitudes spanning more than 2^30): run these queries alone");
+      if (!(cw_cand && cw_call <= (uint32_t)kCwCall && cw_region <= (uint32_t)kCwRegionMax))
+        throw Error(SHD_E_UNSUPPORTED, "query group: a call above 1024 events or a window beyond the call-window "
+                                       "path: run these queries alone");
+      for (size_t k = 0; k < wmembers.size(); k++) {
+        SingleEngine& q = *wmembers[k];
+        const int64_t Xq = std::max<int64_t>(0, total - q.wparam);
+        callwin_rows(q, b, total, cap, ncalls, Xq, cw_call, cw_region, kmax, k == 0);
+        q.counters.events += n;
+        q.counters.carry = total - Xq;
+        q.chunk_seq += ncalls;
+        q.seq += n;
+      }
+      mark("members");
+      commit_carry(total, X, nops, ncalls);
+      return;
+    }
     if (!seg_mode) {   // (segmented-scan mode: packed run records instead)
       resv.reserve(std::max(nagg, 1) * cap * 8);
       resc.reserve(std::max(nagg, 1) * cap * 8);
@@ -3722,7 +3815,12 @@ struct SingleEngine : Engine {
     }
     // emission: first-seen (call, group) rows in event order
     if (m > 0 && !emitted) emit_rows(b, m, cap);
-    // carry: the unexpired suffix [X, total) becomes the new window contents
+    commit_carry(total, X, nops, ncalls);
+  }
+
+  // carry: the unexpired suffix [X, total) becomes the new window contents
+  void commit_carry(int64_t total, int64_t X, int64_t nops, int64_t ncalls) {
+    hipStream_t s = stream;
     int64_t keep = wkind == 0 ? 0 : total - X;
     if (keep > 0 && X > 0) {
       int nw = cur ^ 1;

@@ -1,8 +1,8 @@
-// pattern_common.h -- types shared by the pattern engine's translation units
-// (engine_pattern.hip: prepare / key sort / forward scan / compaction;
-// engine_group.hip: the grouped LDS walk): row flags, per-position outcomes,
-// extended-batch row addressing, the pair expression context and the scan
-// argument / counter blocks.  See engine_pattern.hip for the semantics.
+// pattern_common.h -- types of the pattern engine (engine_pattern.hip:
+// prepare / key sort / forward scan / compaction): row flags, per-position
+// outcomes, extended-batch row addressing, the pair expression context and
+// the scan argument / counter blocks.  See engine_pattern.hip for the
+// semantics.
 #pragma once
 #include "engine.h"
 
@@ -11,15 +11,11 @@ namespace pat {
 
 enum : uint32_t { F_CAND = 1, F_NEW = 2, F_B = 4, F_SKIP = 8 };
 // Per-position scan result (positions = key-sorted order when partitioned).
-enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5, ST_YIELD = 6,
-                 ST_DORM = 7 };
+enum : uint8_t { ST_NONE = 0, ST_OPEN = 1, ST_DEAD = 2, ST_MATCH = 3, ST_DEFER = 4, ST_PRUNED = 5, ST_YIELD = 6 };
 // per-position outcome stored by k_forward_scan for the compaction kernels
 // PS_CONT: a capped lane walk stopped before position match_row[p] (long
 // walk, continued by the wave-cooperative pass)
-// PS_DORM: open, but every event at or after the push's latest time would
-// expire it (ts - ts_i > within): a partitioned partial that waits for its
-// key's next event in the dormant table instead of the next push's sort
-enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3, PS_CONT = 4, PS_DORM = 5 };
+enum : uint8_t { PS_NONE = 0, PS_OPEN = 1, PS_MATCH = 2, PS_DEFER = 3, PS_CONT = 4 };
 // flag on PS_OPEN: the partial met a B event of its key after its creation,
 // so it sits in the pending list, not the new list (carried as CarryTable::pend)
 constexpr uint8_t PS_PEND = 0x80;
@@ -116,20 +112,6 @@ struct PairCtx {
   }
 };
 
-// A table of partials (dormant table rows): the A columns, time, key,
-// creation seq, pending-list flag, push index.
-struct SpillCols {
-  int ncols;
-  int32_t types[kMaxCols];
-  void* col[kMaxCols];
-  uint8_t* nul[kMaxCols];
-  int64_t* ts;
-  uint64_t* key;
-  int64_t* seq;
-  uint8_t* pend;
-  uint32_t* push;
-};
-
 struct ScanArgs {
   ExtRows x;
   DExprSet es;
@@ -143,34 +125,6 @@ struct ScanArgs {
   int64_t within;
   int partitioned;
   int prune;            // drop partials that can no longer match (horizon guard on later pushes)
-  // partitioned plans: such partials are not dropped but kept as dormant
-  // (PS_DORM); every event position stores the push index under its key
-  // (lp[key - lp_base]), which tells later pushes which dormant partials
-  // their key's events have expired
-  int spill;
-  uint32_t* lp;
-  uint64_t lp_base;
-  uint32_t push_idx;
-  // sorted LDS walk: open partials (or dormant ones) written straight into
-  // `fresh` and matches into mj / mi, each block into its own region of
-  // `region` rows (block b: rows [b * region, ...), reserved per round from a
-  // block-local count; counts to blk_open / blk_match; a full region counts as
-  // an overflow and the host redoes the push) -- compacted afterwards
-  int direct;
-  int64_t region;
-  uint32_t* blk_open;
-  uint32_t* blk_match;
-  uint32_t direct_val;   // PS_OPEN (carry table) or PS_DORM (dormant staging table)
-  SpillCols fresh;
-  uint32_t amask;
-  unsigned int* fresh_n;
-  int64_t fresh_cap;
-  const uint8_t* carry_pend;   // pending-list flags of the carried rows
-  // ... and the matches as (e2 row, e1 row) pairs (reserved like the carry
-  // rows; null: per-position outcome bytes / match rows instead)
-  uint32_t* mj;
-  uint32_t* mi;
-  unsigned int* m_n;
   int64_t t_end;        // latest event time of this push
   // hashed buckets (0: positions are sorted by the full key): positions are
   // grouped by the low bits of key_bucket_mix(key), keys of one bucket
@@ -183,7 +137,6 @@ struct ScanOut {
   unsigned long long steps;   // (partial, event) pairs examined
   unsigned long long pruned;  // open partials dropped by the horizon rule
   uint32_t violation;         // per-key timestamp decrease seen
-  uint32_t hbm_walks;         // bucketed walk: partials walked on in HBM (lookahead too short)
 };
 // Expression context of k_prepare: the pushed event as state 0 (stream-state
 // chain of one event), read from the uniform batch column table.
@@ -361,31 +314,6 @@ __device__ __forceinline__ void prep_block_reduce(PrepAcc acc, PrepAgg* blk, int
     blk[slot] = r;
   }
 }
-
-// Grouped LDS walk (engine_group.hip): rows sorted by the low `bits` bits of
-// key_bucket_mix(key); writes pst / match_row for every position and one
-// ScanOut per block (group_walk_blocks(1 << bits) of them) to blk.
-int group_walk_blocks(int ngroups);
-// Fused prepare + first hashed pass of the grouped walk (engine_group.hip).
-constexpr int kPrepRounds = 8;   // rows per lane of a fused tile (kRsBlock * 8 rows)
-int prep_scatter_tiles(int64_t n_ext);
-void launch_prep_scatter(const PrepArgs* d_args, int64_t n_ext, const uint32_t* hist, const uint32_t* offs,
-                         const uint32_t* dtot, int nb, int a0, int a1, uint32_t* kout, uint32_t* vout, uint32_t* tout,
-                         PrepAgg* blk, hipStream_t s);
-// Sorted LDS walk (engine_group.hip): rows sorted by the low `bits` bits of
-// key_bucket_mix(key); each group (<= lds_walk_cap() rows, else counted in
-// ScanOut::hbm_walks and left unresolved) is put in exact key order in place
-// (skey / spv) and walked; writes pst / match_row and one ScanOut per block.
-int lds_walk_cap();
-void launch_lds_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, uint32_t* skey, uint32_t* spv,
-                     const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row, uint8_t* pst,
-                     ScanOut* blk, int nblk, hipStream_t s);
-void launch_region_compact(const SpillCols& src, const SpillCols& dst, uint32_t amask, int64_t region, int nblk,
-                           const uint32_t* ocnt, const uint32_t* ooff, const uint32_t* sj, const uint32_t* si,
-                           uint32_t* dj, uint32_t* di, const uint32_t* mcnt, const uint32_t* moff, hipStream_t s);
-void launch_group_walk(const ScanArgs* d_args, bool fast, int64_t n_ext, int bits, const uint32_t* skey,
-                       const uint32_t* spv, const int32_t* sts, uint32_t* gbeg, uint32_t* gend, int32_t* match_row,
-                       uint8_t* pst, ScanOut* blk, hipStream_t s);
 
 }  // namespace pat
 }  // namespace shd

@@ -658,16 +658,38 @@ def _e1_site(q: qc.Query):
     return a
 
 
+def _length_window(q: qc.Query):
+    """The Window handler of a `from S[..]#window.length(L) ... group by` query, else None."""
+    si = q.input
+    if not isinstance(si, qc.SingleInput) or not q.selector.group_by or q.event_type != "current":
+        return None
+    wins = [h for h in si.handlers if isinstance(h, qc.Window)]
+    if len(wins) != 1 or wins[0].name != "length" or len(wins[0].params) != 1:
+        return None
+    if not isinstance(wins[0].params[0], qc.Const) or wins[0].params[0].type not in ("int", "long"):
+        return None
+    return wins[0]
+
+
 def share_signature(q: qc.Query) -> Optional[str]:
-    """Equal for two queries iff they differ at most in the e1 filter, the
-    query name, annotations and the insert target (None: not shareable)."""
-    if _e1_site(q) is None or q.output_rate is not None:
+    """Equal for two queries iff they can share one device pass (None: not
+    shareable): patterns that differ at most in the e1 filter, or length-window
+    group-by aggregates that differ at most in the window length -- beyond the
+    query name, annotations and the insert target."""
+    if q.output_rate is not None:
         return None
     import copy
-    q2 = copy.deepcopy(q)
-    q2.name, q2.target, q2.annotations = None, "", []
-    _e1_site(q2).filters = []
-    return repr(q2)
+    if _e1_site(q) is not None:
+        q2 = copy.deepcopy(q)
+        q2.name, q2.target, q2.annotations = None, "", []
+        _e1_site(q2).filters = []
+        return "pattern:" + repr(q2)
+    if _length_window(q) is not None:
+        q2 = copy.deepcopy(q)
+        q2.name, q2.target, q2.annotations = None, "", []
+        _length_window(q2).params = []
+        return "window:" + repr(q2)
+    return None
 
 
 _NUMERIC = ("int", "long", "float", "double")
@@ -726,12 +748,18 @@ def share_groups(queries: List[qc.Query], max_members: int = 64) -> List[List[in
 
 def plan_shared_leader(app: qc.SiddhiApp, members: List[qc.Query], dictionary: StringDictionary,
                        partition: Optional[qc.Partition] = None) -> QueryPlan:
-    """The leader plan of a group of shareable queries (share_groups)."""
+    """The leader plan of a group of shareable queries (share_groups): for
+    patterns, the members' query with the disjunction of their e1 filters;
+    for length windows, the member with the longest window (its items cover
+    every member's window)."""
     import copy
     sigs = {share_signature(q) for q in members}
     if len(sigs) != 1 or None in sigs:
-        raise UnsupportedPlanException("queries differ beyond the e1 filter: not shareable")
-    lead = copy.deepcopy(members[0])
+        raise UnsupportedPlanException("queries differ beyond the e1 filter / window length: not shareable")
+    if next(iter(sigs)).startswith("window:"):
+        lead = copy.deepcopy(max(members, key=lambda q: int(_length_window(q).params[0].value)))
+    else:
+        lead = copy.deepcopy(members[0])
+        _e1_site(lead).filters = leader_e1_filters([_e1_site(q).filters for q in members])
     lead.name = "shared(%s)" % ",".join(str(q.name) for q in members)
-    _e1_site(lead).filters = leader_e1_filters([_e1_site(q).filters for q in members])
     return plan_query(app, lead, dictionary, partition)

@@ -142,32 +142,21 @@ def test_timestamps_beyond_32bit_offsets(hip_available, within):
     assert_same_rows(dev, ora)
 
 
-@pytest.mark.parametrize("path", ["group", "sort", "group-oversized", "ldswalk"])
+@pytest.mark.parametrize("keys", [40, 100_000])
 @pytest.mark.parametrize("parts", [1, 3])
-def test_grouped_lds_walk(hip_available, monkeypatch, path, parts):
-    """Partitioned P3 on the grouped LDS walk (engine_group.hip: 16-bit hashed
-    key sort, every row of a key in one group, resolved in LDS -- nothing
-    retired) and on the full key sort, both equal to the oracle.
-    group-oversized: 40 keys, so every group exceeds the LDS capacity and
-    walks in global memory."""
-    if path == "sort":
-        monkeypatch.setenv("SHD_NO_GROUP", "1")
-        monkeypatch.setenv("SHD_NO_LDSWALK", "1")
-    elif path == "ldswalk":   # the sorted LDS walk (engine_group.hip k_lds_walk, opt-in)
-        monkeypatch.setenv("SHD_LDSWALK", "1")
-    else:   # the opt-in grouped walk carries every open partial (no dormant table)
-        monkeypatch.setenv("SHD_GROUP", "force" if path == "group-oversized" else "1")
-        monkeypatch.setenv("SHD_NO_SPILL", "1")
+def test_partitioned_key_sort(hip_available, keys, parts):
+    """Partitioned P3 on the full key sort + forward scan: 100k keys (17 key
+    bits) and 40 keys (every key holds thousands of rows), equal to the
+    oracle."""
     qp, _ = compile_single_query(wl.P3_APP)
-    # 100k keys: the full key sort covers 17 bits (distinct from the walk's 16)
-    n, keys = 300_000, (40 if path == "group-oversized" else 100_000)
+    n = 300_000
     sym, price, vol, ts = wl.stock_stream(n, keys, 0.01, seed_offset=77)
     batches = split(sym, price, vol, ts, parts)
     ora = run_oracle(qp, batches)
     dev, counters, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert (counters["group_bits"] == 16) == (path != "sort")
+    assert counters["group_bits"] == (17 if keys == 100_000 else 6)
 
 
 def test_hashed_grouping_needs_time_order(hip_available, monkeypatch):
@@ -290,18 +279,14 @@ def test_group_fold_long_segments(hip_available, monkeypatch, fold, name, app):
 
 
 @pytest.mark.parametrize("parts", [1, 3])
-@pytest.mark.parametrize("lds", [True, False])
-def test_partition_keys_far_from_zero(hip_available, monkeypatch, parts, lds):
+def test_partition_keys_far_from_zero(hip_available, parts):
     """Keys of a push span [kmin, kmax] far from 0 (one rank's key slice):
-    the full key sort covers only the bits of kmax - kmin (the sorted LDS
-    walk hashes the key: 16 bits either way); rows of null-key events
-    (dropped by PartitionStreamReceiver) sit anywhere in the sorted order and
-    are passed over by the walks."""
+    the full key sort covers only the bits of kmax - kmin; rows of null-key
+    events (dropped by PartitionStreamReceiver) sit anywhere in the sorted
+    order and are passed over by the walks."""
     app = ("define stream S (k int, p double); partition with (k of S) begin "
            "@info(name='q') from every e1=S[p>40] -> e2=S[p>e1.p*1.02] within 30 milliseconds "
            "select e1.k as k, e1.p as p1, e2.p as p2 insert into O; end;")
-    if lds:
-        monkeypatch.setenv("SHD_LDSWALK", "1")
     qp, _ = compile_single_query(app)
     rng = np.random.default_rng(12)
     n = 120_000
@@ -317,21 +302,16 @@ def test_partition_keys_far_from_zero(hip_available, monkeypatch, parts, lds):
     dev, counters, _ = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    assert counters["group_bits"] == (16 if lds else 15)
+    assert counters["group_bits"] == 15
 
 
 @pytest.mark.parametrize("back", [False, True])
-def test_dormant_partials(hip_available, monkeypatch, back):
-    """Partitioned P3 with sparse keys (the bench's shape): open partials that
-    every later event would expire (ts - ts_i > within from the push's latest
-    time on) wait in the dormant table -- outside the next pushes' sort -- until
-    an event of their key expires them (per-key expiry,
-    StreamPreStateProcessor.expireEvents :326-361).  With `back`, a last push
-    goes back in time: the live and the still-alive dormant partials are
-    handed to the NFA engine, and the ones a later event of their key expired
-    stay gone.  Equal to the oracle either way."""
-    monkeypatch.setenv("SHD_SPILL", "1")
-    monkeypatch.setenv("SHD_NO_LDSWALK", "1")   # the dormant table belongs to the full key sort path
+def test_sparse_keys_carry_and_go_back(hip_available, back):
+    """Partitioned P3 with sparse keys (the bench's shape): every open partial
+    is carried until an event of its key expires or completes it (per-key
+    expiry, StreamPreStateProcessor.expireEvents :326-361).  With `back`, a
+    last push goes back in time: the open partials are handed to the NFA
+    engine.  Equal to the oracle either way."""
     qp, _ = compile_single_query(wl.P3_APP)
     sym, price, vol, ts = wl.stock_stream(240_000, 60_000, 0.05, seed_offset=53)
     batches = split(sym, price, vol, ts, 6)
@@ -341,32 +321,16 @@ def test_dormant_partials(hip_available, monkeypatch, back):
     dev, counters, kind = run_device(qp, batches)
     assert len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    if back:
-        assert kind == 4
-    else:
-        assert kind == 1 and counters["dormant"] > counters["carry"] > 0
+    assert kind == (4 if back else 1)
+    if not back:
+        assert counters["carry"] > 0 and counters["dormant"] == 0
 
 
-P3_PATH_ENVS = {
-    "ldswalk": {"SHD_LDSWALK": "1"},
-    "forward-scan": {},
-    "forward-scan-carry-all": {"SHD_NO_SPILL": "1"},
-    "ldswalk-carry-all": {"SHD_LDSWALK": "1", "SHD_NO_SPILL": "1"},
-    "ldswalk-gather": {"SHD_LDSWALK": "1", "SHD_CARRY_GATHER": "1"},
-}
-
-
-@pytest.mark.parametrize("path", list(P3_PATH_ENVS))
 @pytest.mark.parametrize("shape", ["sparse", "dense"])
 @pytest.mark.parametrize("parts", [1, 4])
-def test_p3_paths(hip_available, monkeypatch, path, shape, parts):
-    """Partitioned P3 on each device path -- the full key sort + forward scan
-    (default) with dormant partials (SHD_SPILL) or carrying every open
-    partial, or the sorted LDS walk (SHD_LDSWALK) -- over sparse (the bench's 10 events / key / `within`
+def test_p3_shapes(hip_available, shape, parts):
+    """Partitioned P3 over sparse (the bench's 10 events / key / `within`
     fraction) and dense keys, in one push or four: equal to the oracle."""
-    for k, v in P3_PATH_ENVS[path].items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("SHD_SPILL", "1")
     qp, _ = compile_single_query(wl.P3_APP)
     n, keys, delta = (240_000, 60_000, 0.05) if shape == "sparse" else (200_000, 2_000, 0.002)
     sym, price, vol, ts = wl.stock_stream(n, keys, delta, seed_offset=71)
@@ -375,7 +339,3 @@ def test_p3_paths(hip_available, monkeypatch, path, shape, parts):
     dev, counters, kind = run_device(qp, batches)
     assert kind == 1 and len(ora[2]) > 0
     assert_same_rows(dev, ora)
-    if path.startswith("ldswalk"):
-        assert counters["group_bits"] == 16
-    if path.endswith("carry-all"):
-        assert counters["dormant"] == 0

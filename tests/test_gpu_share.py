@@ -1,10 +1,13 @@
-"""Query groups (shd_group_*): queries on one stream that differ only in the
-start state's filter run one forward scan; each member's rows must equal the
-CPU oracle's for that query alone, row for row and bit-exact (values, types,
-timestamps, callback chunks), across pushes (carried partials), for
-unpartitioned / partitioned / two-stream patterns, threshold families (one
-leader bound) and mixed filters (the leader's disjunction), and after the
-group dissolves into per-member NFA engines (time going back inside a key).
+"""Query groups (shd_group_*): pattern queries on one stream that differ only
+in the start state's filter run one forward scan; each member's rows must
+equal the CPU oracle's for that query alone, row for row and bit-exact
+(values, types, timestamps, callback chunks), across pushes (carried
+partials), for unpartitioned / partitioned / two-stream patterns, threshold
+families (one leader bound) and mixed filters (the leader's disjunction), and
+after the group dissolves into per-member NFA engines (time going back inside
+a key).  Length-window group-by aggregates that differ only in the window
+length share one filter pass and item buffer; each member's rows equal its own
+oracle run (doubles within 1e-9 relative).
 
 Reference: StreamJunction.sendEvent fan-out (C/stream/StreamJunction.java:146-272);
 per-partial independence of `every e1 -> e2` (ST/StreamPreStateProcessor.java:118-129,326-403)."""
@@ -155,6 +158,57 @@ def test_group_refusals(hip_available):
                 DeviceGroup(leader.ir, [dqs[0], odd])
         finally:
             odd.close()
+    finally:
+        for dq in dqs:
+            dq.close()
+
+
+WINDOW_LENGTHS = [1, 7, 60, 300, 1000]
+
+
+def window_app(lengths, alt_filter=None):
+    qs = []
+    for i, ln in enumerate(lengths):
+        f = alt_filter if (alt_filter and i == 1) else "p > 20.0"
+        qs.append("@info(name='w%d') from S[%s]#window.length(%d) select k, avg(p) as a, sum(p) as s, count() as c "
+                  "group by k insert into W%d;" % (i, f, ln, i))
+    return SCHEMA + " ".join(qs)
+
+
+@pytest.mark.parametrize("keys", [9, 40, 2000])
+def test_window_group_members_equal_oracle(hip_available, keys):
+    """Length-window group-by aggregates that differ only in the window length
+    share one filter pass and one item buffer (the leader holds the longest
+    window); each member's rows -- one per (call, group), first-seen order --
+    equal its own oracle run (doubles within 1e-9 relative, counts exact),
+    across pushes and calls of 64 events.  2000 keys: the hashed call-window
+    kernel; fewer: the direct-mapped one."""
+    from parity import assert_rows_agg
+    plans, leader = member_plans(window_app(WINDOW_LENGTHS))
+    batches = make_batches(21 + keys, 4, 6_000, keys)
+    dev, kinds, counters, shared = run_group(plans, leader, batches)
+    assert all(k == 2 for k in kinds)
+    for qp, d, c in zip(plans, dev, counters):
+        ora = run_oracle(qp, batches)
+        assert len(ora[2]) > 0
+        assert_rows_agg(d, ora, qp, exact=False)
+        assert c["matches"] == len(ora[2])
+    assert shared["events"] == counters[0]["events"]
+
+
+def test_window_group_refusals(hip_available):
+    from siddhi_amd.hip_engine import DeviceGroup, DeviceQuery, SiddhiHipError
+    plans, leader = member_plans(window_app(WINDOW_LENGTHS[:3]))
+    # a member whose filter differs from the leader's
+    other = [pl.plan_query(qc.parse(window_app(WINDOW_LENGTHS[:3], "p > 21.0")),
+                           list(qc.parse(window_app(WINDOW_LENGTHS[:3], "p > 21.0")).execution_order)[1],
+                           pl.StringDictionary())]
+    dqs = [DeviceQuery(plans[0].ir), DeviceQuery(other[0].ir)]
+    try:
+        with pytest.raises(SiddhiHipError):
+            DeviceGroup(leader.ir, dqs)
+        g = DeviceGroup(leader.ir, dqs[:1])   # a plain member is fine
+        g.close()
     finally:
         for dq in dqs:
             dq.close()

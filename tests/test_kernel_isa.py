@@ -16,7 +16,7 @@ from isa_check import scan
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "siddhi_amd", "csrc")
-SOURCES = ["engine_pattern.hip", "engine_single.hip", "engine_window.hip", "engine_nfa.hip", "primitives.hip", "engine_group.hip",
+SOURCES = ["engine_pattern.hip", "engine_single.hip", "engine_window.hip", "engine_nfa.hip", "primitives.hip",
            "engine_absent.hip", "route.hip"]
 
 

@@ -264,12 +264,10 @@ def test_restore_rejects_other_plan(hip_available):
 
 
 @pytest.mark.gpu
-def test_snapshot_restore_with_dormant_partials(hip_available, monkeypatch):
-    """A snapshot taken while the pattern engine holds dormant partials (P3,
-    sparse keys) restores them as carried partials; the rest of the stream then
-    gives the oracle's rows."""
-    monkeypatch.setenv("SHD_SPILL", "1")
-    monkeypatch.setenv("SHD_NO_LDSWALK", "1")
+def test_snapshot_restore_sparse_key_carry(hip_available):
+    """A snapshot taken while the pattern engine carries the open partials of
+    sparse keys (P3 shape) restores them; the rest of the stream then gives
+    the oracle's rows."""
     qp, _ = compile_single_query(wl.P3_APP)
     sym, price, vol, ts = wl.stock_stream(200_000, 20_000, 0.05, seed_offset=307)
     batches = _split(sym, price, vol, ts, 4)

@@ -16,9 +16,23 @@ def test_m5_pattern_variants_form_one_group():
     app = qc.parse(wl.M5_APP)
     qs = list(app.execution_order)
     groups = pl.share_groups(qs)
-    assert groups == [list(range(50))]          # the 50 P1 variants; the windows stay alone
+    # the 50 P1 variants, and the 50 W2-length variants (window lengths 100..5000)
+    assert groups == [list(range(50)), list(range(50, 100))]
     lf = pl.leader_e1_filters([pl._e1_site(qs[i]).filters for i in groups[0]])
     assert len(lf) == 1 and lf[0].op == ">" and lf[0].right.value == 60.0
+
+
+def test_window_leader_holds_the_longest_window():
+    app = qc.parse(wl.M5_APP)
+    qs = list(app.execution_order)
+    d = pl.StringDictionary()
+    wl.register_symbols(d, 10)
+    lead = pl.plan_shared_leader(app, qs[50:], d)
+    assert lead.plan.handlers[-1][-1] == 5000   # (kind, window kind, length)
+    # a different filter (or aggregate, or group-by) is another group
+    other = qc.parse(wl.M5_APP.replace("from StockStream[price>60]#window.length(400)",
+                                       "from StockStream[price>61]#window.length(400)"))
+    assert pl.share_signature(list(other.execution_order)[53]) != pl.share_signature(qs[52])
 
 
 def test_share_signature_separates_other_differences():
