@@ -45,14 +45,17 @@ def parse():
     ap.add_argument("--key-base", type=int, default=-1,
                     help="first key id of this rank's slice (default rank * keys; diagnostics)")
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
-    ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin"],
+    ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin", "slices"],
                     help="roundrobin: every rank holds a round-robin share of the global stream and events are "
-                         "re-routed to their key's owner with one RCCL all-to-all per micro-batch (default: "
-                         "prepartitioned, no data-path collective)")
+                         "re-routed to their key's owner with one RCCL all-to-all per micro-batch; slices "
+                         "(window configs): rank r holds slice r of one global stream and primes its query "
+                         "with the previous slice's tail (one RCCL send/recv per step); prepartitioned: "
+                         "independent per-rank streams, no data-path collective (default at N=1)")
     return ap.parse_args()
 
 
-def gen_device_columns(torch, n, keys, delta, seed_offset, key_base, dev):
+def gen_device_columns(torch, n, keys, delta, seed_offset, key_base, dev, start=0):
+    """Events [start, start + n) of the seeded StockStream, resident in HBM."""
     from siddhi_amd import workloads as wl
     sym = torch.empty(n, dtype=torch.int32, device=dev)
     price = torch.empty(n, dtype=torch.float64, device=dev)
@@ -61,7 +64,7 @@ def gen_device_columns(torch, n, keys, delta, seed_offset, key_base, dev):
     chunk = 5_000_000
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
-        s, p, v, t = wl.stock_stream(b - a, keys, delta, seed_offset=seed_offset, start=a)
+        s, p, v, t = wl.stock_stream(b - a, keys, delta, seed_offset=seed_offset, start=start + a)
         sym[a:b] = torch.from_numpy((s.astype(np.int64) + key_base).astype(np.int32))
         price[a:b] = torch.from_numpy(p)
         vol[a:b] = torch.from_numpy(v)
@@ -603,9 +606,15 @@ def main():
     # with an RCCL all-to-all per micro-batch; the prepartitioned measurement
     # (events arrive at their owner, keys_per_gpu each, no data-path
     # collective) runs alongside.  N = 1 is prepartitioned (nothing to route).
-    mode = args.input if args.input != "auto" else ("roundrobin" if world > 1 else "prepartitioned")
+    # Window configs (unpartitioned: one window over the whole stream) split the
+    # global stream by time instead: rank r holds slice r and primes its query with
+    # the previous slice's tail (exchange.py, "time slices with a halo").
+    mode = args.input if args.input != "auto" else (
+        "prepartitioned" if world == 1 else ("roundrobin" if pattern else "slices"))
     if mode == "roundrobin" and not pattern:
-        mode = "prepartitioned"   # window configs are unpartitioned: replicas
+        raise SystemExit("--input roundrobin re-routes by partition key; window configs use --input slices")
+    if mode == "slices" and pattern:
+        raise SystemExit("--input slices is for the (unpartitioned) window configs")
 
     def measure(mode):
         kb = None
@@ -614,6 +623,12 @@ def main():
             # rank r owns key slice r and its own events (no data-path collective)
             kb = args.key_base if args.key_base >= 0 else rank * keys
             sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=rank, key_base=kb, dev=dev)
+            seqs = None
+        elif mode == "slices":
+            # rank r holds events [r * n, (r + 1) * n) of ONE global stream over `keys` keys
+            kb = 0
+            sym, price, vol, ts = gen_device_columns(torch, n, keys, delta, seed_offset=0, key_base=0, dev=dev,
+                                                     start=rank * n)
             seqs = None
         else:
             # one global stream over `keys` keys in all, held round-robin; re-routed per micro-batch
@@ -632,10 +647,35 @@ def main():
         offs_all = wl.call_offsets(n)
 
         routed_total = [0]
+        take = [0]
+        cols4 = [sym, price, vol, ts]
+
+        def push_halo(halo):
+            """Prime the fresh query with the previous slice's tail; its rows are dropped."""
+            torch.cuda.current_stream().synchronize()   # received columns complete before the engine reads them
+            m = halo[3].numel()
+            dq.push_raw(0, m, halo[3].data_ptr(), [halo[0].data_ptr(), halo[1].data_ptr(), halo[2].data_ptr()],
+                        [0, 0, 0], he.SHD_MEM_DEVICE, wl.call_offsets(m), True)
+            dq.discard()
+
+        if mode == "slices" and world > 1:
+            window = ex.window_of(qp)
+            first_ts = int(ts[0].item())
+
+            def prime(halo):
+                dq.reset()
+                push_halo(halo)
+                return ex.halo_covers(window, dq.counters()["carry"], halo[3], first_ts)
+            take[0] = ex.halo_take(window, n, lambda k: ex.exchange_tail(cols4, k, rank, world), prime, device=dev)
 
         def run_step(collect=None, cuts=cuts):
             dq.reset()
             tot = {}
+            if take[0]:
+                # the halo: one RCCL send/recv pair per rank and step, inside the timed region
+                halo = ex.exchange_tail(cols4, take[0], rank, world)
+                if halo is not None:
+                    push_halo(halo)
             for a, b in zip(cuts[:-1], cuts[1:]):
                 if seqs is None:
                     # InputHandler calls of 1024 events inside the micro-batch
@@ -729,6 +769,7 @@ def main():
         total_events = n * world * args.steps
         value = total_events / elapsed
         return dict(sym=sym, price=price, vol=vol, ts=ts, seqs=seqs, kb=kb, dq=dq, calib=calib, counters=counters,
+                    halo=take[0],
                     stage_runs=stage_runs, elapsed=elapsed, ms_per_step=ms_per_step, value=value, batch=batch,
                     offs_all=offs_all, total_events=total_events)
 
@@ -838,9 +879,12 @@ def main():
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
             "build": build_id,
             "config": {"workload": args.config, "events_per_gpu": n,
-                       ("keys_total" if mode == "roundrobin" else "keys_per_gpu"): keys, "delta_ms": delta,
-                       "micro_batch": batch, "call_size": 1024, "parallelism": "key-sharded x%d" % world,
-                       "input": mode + (" (RCCL all-to-all re-route)" if mode == "roundrobin" else "")},
+                       ("keys_total" if mode in ("roundrobin", "slices") else "keys_per_gpu"): keys,
+                       "delta_ms": delta, "micro_batch": batch, "call_size": 1024,
+                       "parallelism": ("time-sliced x%d" if mode == "slices" else "key-sharded x%d") % world,
+                       "input": mode + {"roundrobin": " (RCCL all-to-all re-route)",
+                                        "slices": " (one global stream; RCCL send/recv of a %d-event halo per "
+                                                  "rank and step)" % M["halo"]}.get(mode, "")},
             "matches_per_s": round(matches_per_s, 1),
             "counters": {k: counters[k] for k in ("events", "matches", "partials", "partial_scans", "carry")},
             "derived": {k: round(v, 4) for k, v in derived.items()},

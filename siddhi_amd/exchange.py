@@ -290,3 +290,91 @@ def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor,
     outs, rseq, co = merge(recv, recv_counts, dtypes, world, seq_lo, call_size, nblocks, device,
                            m=recv.numel() // words if world > 1 else seq.numel())
     return outs, rseq, co, stats
+
+
+# ---------------------------------------------------------------------------
+# Time slices with a halo: unpartitioned window aggregates (configs W2-*).
+#
+# A window query without a partition holds ONE window over the whole stream
+# (LengthWindowProcessor / TimeWindowProcessor state is per query, C/query/
+# processor/stream/window/LengthWindowProcessor.java:106-142), so its events
+# cannot be split by key.  They split by time instead: rank r takes the
+# contiguous slice r of the global stream (cut on InputHandler-call
+# boundaries).  Everything the slice's rows depend on besides its own events is
+# the window content when the slice starts -- the last L filter-passing events
+# (length) or the events of the last T ms (time) -- and all of that lies in the
+# tail of slice r-1.  Rank r-1 sends that tail (the halo, one point-to-point
+# pair per rank and step: the only data-path exchange), rank r pushes it
+# through a fresh query first and drops its rows, then pushes its own slice:
+# from there on the query's state equals the one-engine state at that point
+# (length: the same L items; time: every item not yet expired), so rank r's
+# rows are exactly the one-engine rows of its calls, and the ranks' rows
+# concatenated in rank order are the whole stream's.  The halo's size is found
+# once (`halo_take`): double it until every rank's halo covers its window.
+# ---------------------------------------------------------------------------
+
+def window_of(qp) -> Optional[Tuple[str, int]]:
+    """("length", L) or ("time", T ms) of a single-stream window query (planner
+    Plan.handlers), None without a window."""
+    from . import planner as pl
+    for h in qp.plan.handlers:
+        if h[0] == pl.H_WINDOW:
+            return ("length" if h[1] == pl.W_LENGTH else "time", int(h[2]))
+    return None
+
+
+def exchange_tail(cols: List[torch.Tensor], take: int, rank: int, world: int,
+                  group: Optional[dist.ProcessGroup] = None) -> Optional[List[torch.Tensor]]:
+    """Rank r sends the last `take` rows of its slice to rank r+1 and receives
+    rank r-1's (None on rank 0).  `take` must be the same on every rank and at
+    most every rank's slice length; columns travel packed (pack())."""
+    dtypes = [c.dtype for c in cols]
+    if take <= 0 or world == 1:
+        return None
+    ops, recv = [], None
+    if rank + 1 < world:
+        ops.append(dist.P2POp(dist.isend, pack([c[-take:] for c in cols]), rank + 1, group))
+    if rank > 0:
+        recv = torch.empty((take, len(cols)), dtype=torch.int64, device=cols[0].device)
+        ops.append(dist.P2POp(dist.irecv, recv, rank - 1, group))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    return None if recv is None else unpack(recv, dtypes)
+
+
+def halo_covers(window: Tuple[str, int], carry: int, halo_ts: torch.Tensor, first_ts: int) -> bool:
+    """True when a halo leaves the window exactly as one engine has it before the
+    slice's first event.  length: the query holds L items after the halo
+    (counters.carry, the items its window carries).  time: with nondecreasing
+    timestamps, the halo's first event -- and so every event before it -- has
+    expired (ts + T - now <= 0, C/query/processor/stream/window/TimeWindowProcessor.java:144-145) before the
+    slice's first event arrives; the margin of one ms keeps it strict."""
+    kind, w = window
+    if kind == "length":
+        return carry >= w
+    ts = halo_ts
+    if ts.numel() == 0:
+        return False
+    mono = bool((ts[1:] >= ts[:-1]).all().item()) and int(ts[-1].item()) <= first_ts
+    return mono and int(ts[0].item()) + w < first_ts
+
+
+def halo_take(window: Tuple[str, int], n: int, exchange, prime, device=None,
+              group: Optional[dist.ProcessGroup] = None, start: int = 0) -> int:
+    """The halo size (events) every rank uses: the smallest power-of-two
+    multiple of `start` (default 2L for length windows, 4096 events for time)
+    at which every rank's halo covers its window.  exchange(take) -> the
+    received halo columns (None on rank 0); prime(halo) -> bool, the
+    halo_covers() verdict after pushing `halo` into a fresh query.  Raises when
+    a whole previous slice is not enough (the window reaches back past it)."""
+    take = min(n, start or (2 * window[1] if window[0] == "length" else 4096))
+    while True:
+        halo = exchange(take)
+        ok = True if halo is None else bool(prime(halo))
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()) == 0:
+            return take
+        if take >= n:
+            raise ValueError("window reaches back past the previous rank's whole slice (%d events)" % n)
+        take = min(n, take * 2)
