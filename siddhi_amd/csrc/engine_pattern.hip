@@ -152,6 +152,35 @@ struct GlobalPos {
   }
 };
 
+// Block skip: f2's threshold for partial (row r, sorted position q1) -- the
+// e1 side of comparison bs_ci (null: f2 can never pass).
+__device__ __forceinline__ Val skip_threshold(const ScanArgs& a, int64_t r, int64_t q1) {
+  const FCmp& c = a.f2.fp.c[a.bs_ci];
+  PairCtx cx{&a.x, r, -1, a.s_first};
+  cx.q1 = q1;
+  return fp_term(a.bs_side == 0 ? c.r : c.l, cx);
+}
+
+// True when a walk of key k (created at tsi, last step at prev) passes the
+// whole block without an outcome: every non-skip position is of key k, no
+// F_NEW event expires it or goes back in time, and no B event can pass f2.
+__device__ __forceinline__ bool block_skippable(const ScanArgs& a, const BlockSum& b, uint64_t k, int64_t tsi,
+                                                int64_t prev, Val thr) {
+  if (a.partitioned && !(b.flags & 4u) && (!(b.flags & 1u) || b.key != (uint32_t)k)) return false;
+  if (b.cnt && a.within != INT64_MAX) {
+    if (!(b.flags & 2u) || b.tfirst < prev || b.tlast - tsi > a.within) return false;
+  }
+  if (thr.null) return true;
+  const double t = v_f64(thr.b), v = b.v;
+  switch (a.bs_op) {
+    case SHD_OP_GT: return v <= t;
+    case SHD_OP_GE: return v < t;
+    case SHD_OP_LT: return v >= t;
+    case SHD_OP_LE: return v > t;
+  }
+  return false;
+}
+
 // WIN: positions are loaded WIN at a time (one round trip for WIN steps);
 // walks over hashed buckets step over a few other keys, and a wave waits for
 // its longest walk, so they fetch ahead.
@@ -164,6 +193,10 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
   uint8_t st = ST_OPEN;
   bool stop = false, first = true;
   int it = 0;
+  bool thr_ok = false;
+  Val thr;
+  thr.b = 0;
+  thr.null = 1;
   while (!stop && q < n_ext) {
     if constexpr (CAP > 0) {
       // CAP positions walked: yield before position q (nothing of it processed)
@@ -172,6 +205,22 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
         break;
       }
       it += WIN;
+    }
+    if constexpr (!DEFER) {
+      // long walks: whole 64-position blocks without an outcome are skipped
+      if (a.bsum && !first && !f2_now && (q & 63) == 0 && q + 64 <= n_ext) {
+        if (!thr_ok) {
+          thr = skip_threshold(a, r, q1);
+          thr_ok = true;
+        }
+        const BlockSum bs = a.bsum[q >> 6];
+        if (block_skippable(a, bs, k, tsi, prev, thr)) {
+          steps += bs.cnt;
+          if (bs.cnt) prev = bs.tlast;
+          q += 64;
+          continue;
+        }
+      }
     }
     uint32_t wp[WIN];
     int64_t wt[WIN];
@@ -448,6 +497,100 @@ __global__ __launch_bounds__(kBlock) void k_gather_bpos(const ExtRows* __restric
   }
 }
 
+// Block summaries for skipping walks (BlockSum): one wave per 64 sorted
+// positions (32-bit keys and timestamps).
+__global__ __launch_bounds__(kBlock) void k_block_sum(const ScanArgs* __restrict__ ap, int64_t n_ext,
+                                                     const uint32_t* __restrict__ skey32,
+                                                     const uint32_t* __restrict__ spv,
+                                                     const int32_t* __restrict__ sts32, BlockSum* __restrict__ out) {
+  const ScanArgs& a = *ap;
+  const ExtRows& x = a.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t nblk = (n_ext + 63) >> 6;
+  const int64_t tbase = x.batch.ts[0];
+  const int attr = a.bs_attr;
+  const bool usemax = a.bs_op == SHD_OP_GT || a.bs_op == SHD_OP_GE;
+  for (int64_t b = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; b < nblk;
+       b += ((int64_t)gridDim.x * kBlock) >> 6) {
+    const int64_t p = (b << 6) + lane;
+    const bool valid = p < n_ext;
+    const uint32_t pv = valid ? spv[p] : 0u;
+    const int64_t t = valid ? tbase + (int64_t)sts32[p] : 0;
+    const uint32_t key = (valid && a.partitioned) ? skey32[p] : 0u;
+    const uint32_t f = pv_flags(pv);
+    const bool keyed = valid && !(f & F_SKIP);
+    const bool nw = keyed && (f & F_NEW);
+    double dv = usemax ? -__builtin_inf() : __builtin_inf();
+    if (nw && (f & F_B)) {
+      const int64_t r = pv_row(pv);
+      const Val v = ((x.bpos_mask >> attr) & 1u) ? col_load(x.bpos, p, attr)
+                    : (r < x.C ? col_load(x.carry, r, attr) : col_load(x.batch, r - x.C, attr));
+      if (!v.null) {
+        const double d = v_f64(v.b);
+        if (d == d) dv = d;   // NaN never passes a comparison
+      }
+    }
+    dv = usemax ? wave_max(dv) : wave_min(dv);
+    const uint64_t km = __ballot(keyed), nm = __ballot(nw);
+    const uint32_t k0 = km ? __shfl(key, __ffsll((unsigned long long)km) - 1, 64) : 0u;
+    const bool uniform = __ballot(keyed && key != k0) == 0;
+    // running max of the earlier F_NEW times: a decrease breaks monotonicity
+    int64_t m = nw ? t : INT64_MIN;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = __shfl_up(m, o, 64);
+      if (lane >= o) m = u > m ? u : m;
+    }
+    int64_t before = __shfl_up(m, 1, 64);
+    if (lane == 0) before = INT64_MIN;
+    const bool mono = __ballot(nw && t < before) == 0;
+    const int64_t tfirst = nm ? __shfl(t, __ffsll((unsigned long long)nm) - 1, 64) : 0;
+    const int64_t tlast = __shfl(m, 63, 64);
+    if (lane == 0) {
+      BlockSum o;
+      o.key = k0;
+      o.cnt = (uint16_t)__popcll(nm);
+      o.flags = (uint8_t)((uniform ? 1u : 0u) | (mono ? 2u : 0u) | (km ? 0u : 4u));
+      o.pad = 0;
+      o.tfirst = tfirst;
+      o.tlast = tlast;
+      o.v = dv;
+      out[b] = o;
+    }
+  }
+}
+
+// The f2 comparison block skipping can answer from a block's max / min: a
+// double comparison (> >= < <=) between a plain e2 attribute (state s2, no
+// conversion) and a term free of e2.  Normalised to `e2.attr op threshold`.
+static bool block_skip_term(const FPred& fp, int s2, int& ci, int& side, int& op, int& attr) {
+  auto is_e2 = [&](const FTerm& t) {
+    return t.aop == 0 && t.a.kind == FA_LOAD && t.a.st == s2 && (t.a.idx == 0 || t.a.idx == SHD_IDX_CURRENT) &&
+           t.a.cvt_to < 0;
+  };
+  auto no_e2 = [&](const FTerm& t) {
+    auto ok = [&](const FAtom& x) { return x.kind != FA_LOAD || x.st == 0; };
+    return ok(t.a) && (t.aop == 0 || ok(t.b));
+  };
+  auto flip = [](int o) {
+    return o == SHD_OP_GT ? SHD_OP_LT : o == SHD_OP_LT ? SHD_OP_GT : o == SHD_OP_GE ? SHD_OP_LE : SHD_OP_GE;
+  };
+  for (int i = 0; i < fp.n && i < 4; i++) {
+    const FCmp& c = fp.c[i];
+    if (c.type != SHD_T_DOUBLE) continue;
+    if (c.op != SHD_OP_GT && c.op != SHD_OP_GE && c.op != SHD_OP_LT && c.op != SHD_OP_LE) continue;
+    if (is_e2(c.l) && no_e2(c.r)) {
+      ci = i, side = 0, op = c.op, attr = c.l.a.attr;
+      return true;
+    }
+    if (is_e2(c.r) && no_e2(c.l)) {
+      ci = i, side = 1, op = flip(c.op), attr = c.r.a.attr;
+      return true;
+    }
+  }
+  return false;
+}
+
 // Cooperative walk (resume MODE 2): the 64 lanes of a wave scan ONE deferred
 // partial's later positions 64 at a time (coalesced loads, f2 evaluated for all
 // of them at once) and ballot the first terminating position -- the same
@@ -487,9 +630,30 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
   if (a.logical == 2) and_carried(a, r, fm, ra, rb);
   uint64_t wsteps = 0;
   bool wviol = false;
+  bool thr_ok = false;
+  Val thr;
+  thr.b = 0;
+  thr.null = 1;
   while (q0 < n_ext) {
+    if (a.bsum && !first && (q0 & 63) == 0 && q0 + 64 <= n_ext) {
+      // a whole 64-position block without an outcome is skipped (block_skippable)
+      if (!thr_ok) {
+        thr = skip_threshold(a, r, p);
+        thr_ok = true;
+      }
+      const BlockSum bs = a.bsum[q0 >> 6];
+      if (block_skippable(a, bs, k, tsi, prev, thr)) {
+        wsteps += bs.cnt;
+        if (bs.cnt) prev = bs.tlast;
+        q0 += 64;
+        continue;
+      }
+    }
+    // with block skipping, rounds end on 64-position block boundaries
+    const int64_t qend = a.bsum ? ((q0 | 63) + 1) : q0 + 64;
     const int64_t q = q0 + lane;
-    const bool inb = q < n_ext;
+    const bool act = q < qend;
+    const bool inb = act && q < n_ext;
     uint32_t pq = 0;
     int64_t tq = 0;
     uint64_t kq = 0;
@@ -511,7 +675,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     before = before > prev ? before : prev;
     const bool vio = isnew && a.within != INT64_MAX && tq < before;
     const bool expire = isnew && !vio && tq - tsi > a.within;
-    const uint64_t stopm = __ballot(!inb || endkey || vio || expire);
+    const uint64_t stopm = __ballot(act && (!inb || endkey || vio || expire));
     const int sidx = stopm ? __ffsll((unsigned long long)stopm) - 1 : 64;
     bool hit = false;
     int32_t code = 0;
@@ -563,7 +727,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       }
       prev = __shfl(m, 63, 64) > prev ? __shfl(m, 63, 64) : prev;
       first = false;
-      q0 += 64;
+      q0 = qend;
       continue;
     }
     if (lane < sidx && (f0 || (isnew && (fq & F_B)))) {
@@ -598,7 +762,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
     }
     prev = __shfl(m, 63, 64) > prev ? __shfl(m, 63, 64) : prev;
     first = false;
-    q0 += 64;
+    q0 = qend;
   }
   if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
   if (lane == 0) {
@@ -1327,6 +1491,7 @@ struct PatternEngine : Engine {
   uint32_t bpos_mask = 0;    // e2-side attributes read by the operand filters (ExtRows::bpos)
   uint32_t apos_mask = 0;    // e1-side attributes read by the operand filters (ExtRows::apos_mask)
   DevBuf d_bpos[kMaxCols], d_bpos_nul[kMaxCols];
+  DevBuf d_bsum;   // k_block_sum output (long walks)
   int s_first = 1, s_second = -1;
   int64_t W = INT64_MAX;
   bool partitioned = false;
@@ -1828,7 +1993,21 @@ struct PatternEngine : Engine {
       hipLaunchKernelGGL(k_gather_bpos, dim3(grid_for(n_ext, 1, 4096)), dim3(kBlock), 0, s, dev_args(sa.x), spv, n_ext);
       SHD_CHECK_LAUNCH();
     }
+    // long dense walks (a partial expects >= 64 events of its key inside
+    // `within`) skip whole 64-position blocks that cannot end them
+    sa.bsum = nullptr;
+    const bool skip_ok = grouped && !hash_mask && !sorted64 && !ts64 && isB && logical == 0 && rmode != 0 &&
+                         sa.f2.fp.ok && !getenv("SHD_NO_BLOCK_SKIP") && (e_key >= 64.0 || getenv("SHD_BLOCK_SKIP"));
+    if (skip_ok && block_skip_term(sa.f2.fp, s_first, sa.bs_ci, sa.bs_side, sa.bs_op, sa.bs_attr)) {
+      d_bsum.reserve(ceil_div(n_ext, 64) * (int64_t)sizeof(BlockSum));
+      sa.bsum = d_bsum.as<BlockSum>();
+    }
     const ScanArgs* d_sa = dev_args(sa);
+    if (sa.bsum) {
+      hipLaunchKernelGGL(k_block_sum, dim3(grid_for(ceil_div(n_ext, 64) * 64, 1, 4096)), dim3(kBlock), 0, s, d_sa,
+                         n_ext, skey32, spv, sts32, d_bsum.as<BlockSum>());
+      SHD_CHECK_LAUNCH();
+    }
     // hot walk without f2 (deferrals), then the deferred walks with f2
 #define SHD_LAUNCH_SCAN(K64, TS64, H)                                                                           \
   hipLaunchKernelGGL((k_forward_scan<K64, TS64, H>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32,    \

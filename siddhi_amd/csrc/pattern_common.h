@@ -112,6 +112,19 @@ struct PairCtx {
   }
 };
 
+// Summary of 64 sorted positions [64b, 64b + 64) for walks that skip whole
+// blocks (k_block_sum): the key all non-skip positions share (flag 1; flag 4:
+// no non-skip position), whether the F_NEW times are nondecreasing (flag 2),
+// the first / last F_NEW time, the F_NEW count, and the max (ops > >=) or min
+// (< <=) of the e2 attribute the f2 comparison reads over the F_NEW B events.
+struct BlockSum {
+  uint32_t key;
+  uint16_t cnt;
+  uint8_t flags, pad;
+  int64_t tfirst, tlast;
+  double v;
+};
+
 struct ScanArgs {
   ExtRows x;
   DExprSet es;
@@ -131,6 +144,11 @@ struct ScanArgs {
   // interleaved in input order.  Only set when the batch rows are globally
   // time-ordered, carried partials precede them in time, and prune is on.
   uint32_t hash_mask;
+  // block skip (long walks): f2's comparison bs_ci reads the e2 attribute
+  // bs_attr, normalised as `e2.attr bs_op threshold` with the threshold on the
+  // e1 side (bs_side 0: its right term, 1: its left); bsum null: no skipping
+  const BlockSum* bsum;
+  int bs_ci, bs_side, bs_op, bs_attr;
 };
 
 struct ScanOut {
