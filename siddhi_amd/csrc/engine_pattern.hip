@@ -197,6 +197,8 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
   Val thr;
   thr.b = 0;
   thr.null = 1;
+  int64_t tried = -1;      // block whose skip was last tried
+  int64_t last_new = q;    // position of the walk's last F_NEW step (the resume point's time is prev)
   while (!stop && q < n_ext) {
     if constexpr (CAP > 0) {
       // CAP positions walked: yield before position q (nothing of it processed)
@@ -207,17 +209,31 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       it += WIN;
     }
     if constexpr (!DEFER) {
-      // long walks: whole 64-position blocks without an outcome are skipped
-      if (a.bsum && !first && !f2_now && (q & 63) == 0 && q + 64 <= n_ext) {
+      // long walks skip the rest of a 64-position block when none of it can
+      // end them: from a block boundary (block_skippable), or from inside the
+      // block once per block -- then the whole block's summary must allow it
+      // and, for the times, the walk's last step lies in this block (the
+      // block's times are nondecreasing, so the rest is no earlier than it)
+      const int64_t blk = q >> 6;
+      if (a.bsum && !first && !f2_now && blk != tried && (blk << 6) + 64 <= n_ext) {
+        tried = blk;
         if (!thr_ok) {
           thr = skip_threshold(a, r, q1);
           thr_ok = true;
         }
-        const BlockSum bs = a.bsum[q >> 6];
-        if (block_skippable(a, bs, k, tsi, prev, thr)) {
-          steps += bs.cnt;
-          if (bs.cnt) prev = bs.tlast;
-          q += 64;
+        const BlockSum bs = a.bsum[blk];
+        const int off = (int)(q & 63);
+        // the last step inside this block: the block's nondecreasing times
+        // after it are >= prev (block_skippable then only checks monotonicity)
+        const int64_t after = (off != 0 && last_new >= (blk << 6)) ? INT64_MIN : prev;
+        if (block_skippable(a, bs, k, tsi, after, thr)) {
+          const uint32_t c = (uint32_t)__popcll(bs.newmask >> off);
+          steps += c;
+          if (c) {
+            prev = bs.tlast;
+            last_new = (blk << 6) + 63;
+          }
+          q = (blk << 6) + 64;
           continue;
         }
       }
@@ -269,6 +285,7 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
             break;
           }
           prev = tq;
+          last_new = q;
           steps++;
           // stabilizeStates -> expireEvents: |ts_i - t| > within
           if (tq - tsi > a.within) {
@@ -555,6 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_block_sum(const ScanArgs* __restrict
       o.tfirst = tfirst;
       o.tlast = tlast;
       o.v = dv;
+      o.newmask = nm;
       out[b] = o;
     }
   }

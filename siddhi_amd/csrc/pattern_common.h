@@ -115,14 +115,16 @@ struct PairCtx {
 // Summary of 64 sorted positions [64b, 64b + 64) for walks that skip whole
 // blocks (k_block_sum): the key all non-skip positions share (flag 1; flag 4:
 // no non-skip position), whether the F_NEW times are nondecreasing (flag 2),
-// the first / last F_NEW time, the F_NEW count, and the max (ops > >=) or min
-// (< <=) of the e2 attribute the f2 comparison reads over the F_NEW B events.
+// the first / last F_NEW time, the F_NEW count and positions, and the max (ops
+// > >=) or min (< <=) of the e2 attribute the f2 comparison reads over the
+// F_NEW B events.
 struct BlockSum {
   uint32_t key;
   uint16_t cnt;
   uint8_t flags, pad;
   int64_t tfirst, tlast;
   double v;
+  uint64_t newmask;   // bit i: position 64b + i is an F_NEW non-skip event
 };
 
 struct ScanArgs {
