@@ -184,7 +184,7 @@ __device__ __forceinline__ bool block_skippable(const ScanArgs& a, const BlockSu
 // WIN: positions are loaded WIN at a time (one round trip for WIN steps);
 // walks over hashed buckets step over a few other keys, and a wave waits for
 // its longest walk, so they fetch ahead.
-template <bool DEFER, bool FAST, int WIN, class Ld, int CAP = 0>
+template <bool DEFER, bool FAST, int WIN, class Ld, int CAP = 0, bool SKIP = false>
 __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
                                                 int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
                                                 int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
@@ -208,14 +208,14 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
       }
       it += WIN;
     }
-    if constexpr (!DEFER) {
+    if constexpr (!DEFER && SKIP) {
       // long walks skip the rest of a 64-position block when none of it can
       // end them: from a block boundary (block_skippable), or from inside the
       // block once per block -- then the whole block's summary must allow it
       // and, for the times, the walk's last step lies in this block (the
       // block's times are nondecreasing, so the rest is no earlier than it)
       const int64_t blk = q >> 6;
-      if (a.bsum && !first && !f2_now && blk != tried && (blk << 6) + 64 <= n_ext) {
+      if (!first && !f2_now && blk != tried && (blk << 6) + 64 <= n_ext) {
         tried = blk;
         if (!thr_ok) {
           thr = skip_threshold(a, r, q1);
@@ -618,7 +618,7 @@ static bool block_skip_term(const FPred& fp, int s2, int& ci, int& side, int& op
 // its longest walk; here a partial that completes early costs one round and
 // one that never matches ceil(window / 64) rounds.  Plain and OR forms only
 // (an AND partial's operand state is sequential).
-template <bool FAST, class Ld>
+template <bool FAST, bool SKIP, class Ld>
 __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
                                             int64_t p, bool cont, int32_t* __restrict__ match_row,
                                             int32_t* __restrict__ match_other, uint8_t* __restrict__ pst,
@@ -653,7 +653,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
   thr.b = 0;
   thr.null = 1;
   while (q0 < n_ext) {
-    if (a.bsum && !first && (q0 & 63) == 0 && q0 + 64 <= n_ext) {
+    if (SKIP && !first && (q0 & 63) == 0 && q0 + 64 <= n_ext) {
       // a whole 64-position block without an outcome is skipped (block_skippable)
       if (!thr_ok) {
         thr = skip_threshold(a, r, p);
@@ -668,7 +668,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       }
     }
     // with block skipping, rounds end on 64-position block boundaries
-    const int64_t qend = a.bsum ? ((q0 | 63) + 1) : q0 + 64;
+    const int64_t qend = SKIP ? ((q0 | 63) + 1) : q0 + 64;
     const int64_t q = q0 + lane;
     const bool act = q < qend;
     const bool inb = act && q < n_ext;
@@ -808,7 +808,7 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
 // continue.  Same tiles as k_forward_scan.  MODE 2: one wave per deferred
 // partial (coop_resume); MODE 1: one position per lane per round; MODE 0: each
 // thread scans 16 outcome bytes and resumes its hits in turn.
-template <bool K64, bool FAST, bool TS64, int MODE>
+template <bool K64, bool FAST, bool TS64, int MODE, bool SKIP = false>
 __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __restrict__ ap, int64_t n_ext,
                                                            int64_t tile, const uint32_t* __restrict__ skey32,
                                                            const uint64_t* __restrict__ skey64,
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       uint32_t fm = 0;
       int64_t ra = -1, rb = -1;
       if (a.logical == 2) and_carried(a, pv_row(pvp), fm, ra, rb);
-      const uint8_t st = walk_partial<false, FAST, 1>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true,
+      const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 0, SKIP>(a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true,
                                                       j, steps, viol, fm, ra, rb, p);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       while (dm) {
         const int b = __ffsll((unsigned long long)dm) - 1;
         dm &= dm - 1;
-        coop_resume<FAST>(a, es, n_ext, ld, base + b, (cm >> b) & 1ull, match_row, match_other, pst, steps, pruned,
+        coop_resume<FAST, SKIP>(a, es, n_ext, ld, base + b, (cm >> b) & 1ull, match_row, match_other, pst, steps, pruned,
                           viol, nm, no);
       }
     }
@@ -884,7 +884,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
       int32_t j = -1;
       uint32_t fm = 0;
       int64_t ra = -1, rb = -1;
-      const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 64>(
+      const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 64, SKIP>(
           a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j, steps, viol, fm, ra, rb, p);
       uint8_t out = PS_NONE;
       if (st == ST_MATCH) {
@@ -2047,6 +2047,11 @@ struct PatternEngine : Engine {
   } while (0)
 #define SHD_LAUNCH_RESUME2(K64, FAST) \
   if (ts64) SHD_LAUNCH_RESUME(K64, FAST, true); else SHD_LAUNCH_RESUME(K64, FAST, false)
+    // block skipping (sa.bsum: 32-bit keys and times, fast f2): its own instantiations
+#define SHD_LAUNCH_SKIP(D, SLOT)                                                                                 \
+  hipLaunchKernelGGL((k_forward_resume<false, true, false, D, true>), dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, \
+                     tile, skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_mother.as<int32_t>(),      \
+                     d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>(), SLOT)
     if (sorted64) {
       if (ts64) SHD_LAUNCH_SCAN(true, true, false); else SHD_LAUNCH_SCAN(true, false, false);
       SHD_CHECK_LAUNCH();
@@ -2059,10 +2064,18 @@ struct PatternEngine : Engine {
         if (ts64) SHD_LAUNCH_SCAN(false, true, false); else SHD_LAUNCH_SCAN(false, false, false);
       }
       SHD_CHECK_LAUNCH();
-      if (fast2) { SHD_LAUNCH_RESUME2(false, true); }
+      if (sa.bsum) {
+        if (rmode == 3) {
+          SHD_LAUNCH_SKIP(3, ntile);
+          SHD_CHECK_LAUNCH();
+          SHD_LAUNCH_SKIP(2, 2 * ntile);
+        } else if (rmode == 2) SHD_LAUNCH_SKIP(2, ntile);
+        else SHD_LAUNCH_SKIP(1, ntile);
+      } else if (fast2) { SHD_LAUNCH_RESUME2(false, true); }
       else { SHD_LAUNCH_RESUME2(false, false); }
     }
 #undef SHD_LAUNCH_RESUME2
+#undef SHD_LAUNCH_SKIP
 #undef SHD_LAUNCH_RESUME_D
 #undef SHD_LAUNCH_RESUME
 #undef SHD_LAUNCH_SCAN
