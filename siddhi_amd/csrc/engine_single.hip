@@ -1802,11 +1802,10 @@ __global__ __launch_bounds__(kBlock) void k_cw_count(const CwArgs* __restrict__ 
 }
 
 template <int NC, int RC, int CALLCAP, int GCAP, bool LEN>
-__global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__ ap, int ncalls,
-                                                      const uint32_t* __restrict__ rbase) {
+__device__ __forceinline__ void cw_direct_call(const CwArgs& a, const int c, int ncalls,
+                                               const uint32_t* __restrict__ rbase) {
   constexpr bool kStage = RC <= 2048;
   constexpr int kExpN = (kStage && !LEN) ? RC : 1;
-  const CwArgs& a = *ap;
   __shared__ uint32_t sfirst[GCAP], slast[GCAP], scnt[GCAP];
   __shared__ uint16_t qslot[RC];
   // staged group ids; after the region pass, the window lists (u16)
@@ -1816,7 +1815,6 @@ __global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__
   __shared__ uint32_t wsum[kBlock / 64];
   uint16_t* list = reinterpret_cast<uint16_t*>(rkey);
   uint32_t* soff = scnt;                // list offsets, in place of the counts (kept in registers below)
-  const int c = blockIdx.x;
   if (c >= ncalls) return;
   const uint32_t s = a.citem[c], t = a.citem[c + 1];
   if (s == t) return;
@@ -1890,6 +1888,26 @@ __global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__
     // soff[g] now ends the group's list
     cw_fold_emit<NC>(a, c, lb, list, soff[g] - my_n[k], my_n[k], slast[g], base + srank[r - rs]);
   }
+}
+
+template <int NC, int RC, int CALLCAP, int GCAP, bool LEN>
+__global__ __launch_bounds__(kBlock) void k_cw_direct(const CwArgs* __restrict__ ap, int ncalls,
+                                                      const uint32_t* __restrict__ rbase) {
+  cw_direct_call<NC, RC, CALLCAP, GCAP, LEN>(*ap, blockIdx.x, ncalls, rbase);
+}
+
+// Every member of a window group in one launch (the members' CwArgs `stride`
+// bytes apart): the workgroups of one call -- one per member, its region a
+// suffix of the longest member's -- are dealt to the same XCD back to back
+// (workgroups go round-robin over the 8 XCDs), so the call's items are read
+// from HBM about once and from that XCD's L2 by the other members.
+template <int NC, int RC, int CALLCAP, int GCAP, bool LEN>
+__global__ __launch_bounds__(kBlock) void k_cw_direct_multi(const char* __restrict__ aps, int64_t stride, int nmem,
+                                                            int ncalls, const uint32_t* __restrict__ rbase) {
+  const int b = blockIdx.x, x = b & 7, i = b >> 3;
+  const int m = i % nmem, c = (i / nmem) * 8 + x;
+  cw_direct_call<NC, RC, CALLCAP, GCAP, LEN>(*reinterpret_cast<const CwArgs*>(aps + (int64_t)m * stride), c, ncalls,
+                                             rbase);
 }
 
 // The call's rows are written here, in first-seen order, at row0 + the rows
@@ -3280,8 +3298,12 @@ struct SingleEngine : Engine {
   // buffer and ids.  rows_known: k_cw_count's scan of the rows per call is
   // still current (a group's members share it: the calls' distinct groups do
   // not depend on the window).
+  // defer (window groups): the direct-mapped rows kernel is not launched here;
+  // the member's device arguments are appended for one k_cw_direct_multi, and
+  // the row count is left for the caller (the same for every member)
   void callwin_rows(SingleEngine& q, const Staged& b, int64_t total, int64_t cap, int64_t ncalls, int64_t X,
-                    uint32_t call, uint32_t region, uint64_t kmax, bool count_rows) {
+                    uint32_t call, uint32_t region, uint64_t kmax, bool count_rows,
+                    std::vector<const CwArgs*>* defer = nullptr) {
     hipStream_t s = stream;
     const int64_t m = total - C;
     q.ensure_groups((int64_t)kmax + 1);
@@ -3356,11 +3378,15 @@ struct SingleEngine : Engine {
                            (uint32_t*)(d_tot.as<uint64_t>() + 9), d_scan, s);
         SHD_HIP(hipMemsetAsync(d_tot.as<uint32_t>() + 19, 0, 4, s));   // (the row count's high word)
       }
-      switch (ca.nch) {
-        case 1: callwin_direct<1>(d_ca, ncalls, call, region); break;
-        case 2: callwin_direct<2>(d_ca, ncalls, call, region); break;
-        case 3: callwin_direct<3>(d_ca, ncalls, call, region); break;
-        default: callwin_direct<4>(d_ca, ncalls, call, region); break;
+      if (defer) {
+        defer->push_back(d_ca);
+      } else {
+        switch (ca.nch) {
+          case 1: callwin_direct<1>(d_ca, ncalls, call, region); break;
+          case 2: callwin_direct<2>(d_ca, ncalls, call, region); break;
+          case 3: callwin_direct<3>(d_ca, ncalls, call, region); break;
+          default: callwin_direct<4>(d_ca, ncalls, call, region); break;
+        }
       }
     } else {
       switch (ca.nch) {
@@ -3388,10 +3414,44 @@ struct SingleEngine : Engine {
       SHD_CHECK_LAUNCH();
     }
     mark("group_tables");
+    if (defer && !defer->empty() && defer->back() == d_ca) return;
     SHD_HIP(hipStreamSynchronize(s));
     const int64_t nrows = m > 0 ? (int64_t)h_tot.as<uint64_t>()[9] : 0;
     q.out.count += nrows;
     q.counters.matches += nrows;
+  }
+
+  // One launch of the direct-mapped rows kernel for a window group's members
+  // (callwin_rows with `defer`): their arguments must lie at a fixed stride in
+  // the argument arena (consecutive dev_args of one type).
+  void callwin_direct_multi(const std::vector<const CwArgs*>& args, int nch, int64_t ncalls, uint32_t call,
+                            uint32_t region) {
+    const int nm = (int)args.size();
+    const int64_t stride = nm > 1 ? (const char*)args[1] - (const char*)args[0] : 0;
+    for (int k = 1; k < nm; k++)
+      if ((const char*)args[k] - (const char*)args[0] != k * stride)
+        throw Error(SHD_E_DEVICE, "window group: member arguments not at a fixed stride");
+    const dim3 g((unsigned)(ceil_div(ncalls, 8) * 8 * nm)), bl(kBlock);
+    const uint32_t* base = d_cw_base.as<uint32_t>();
+    const char* a0 = (const char*)args[0];
+#define SHD_CW_MULTI(NC, RC, CC)                                                                                    \
+  hipLaunchKernelGGL((k_cw_direct_multi<NC, RC, CC, kCwDirectG, true>), g, bl, 0, stream, a0, stride, nm, (int)ncalls, \
+                     base)
+#define SHD_CW_MULTI_NC(NC)                                                   \
+  do {                                                                        \
+    if (region <= 2048 && call <= 512) SHD_CW_MULTI(NC, 2048, 512);           \
+    else if (region <= 2048) SHD_CW_MULTI(NC, 2048, kCwCall);                 \
+    else SHD_CW_MULTI(NC, kCwRegionMax, kCwCall);                             \
+  } while (0)
+    switch (nch) {
+      case 1: SHD_CW_MULTI_NC(1); break;
+      case 2: SHD_CW_MULTI_NC(2); break;
+      case 3: SHD_CW_MULTI_NC(3); break;
+      default: SHD_CW_MULTI_NC(4); break;
+    }
+#undef SHD_CW_MULTI_NC
+#undef SHD_CW_MULTI
+    SHD_CHECK_LAUNCH();
   }
 
   void agg_segscan(int64_t total, uint64_t kmax, int64_t cap) {
@@ -3695,14 +3755,30 @@ struct SingleEngine : Engine {
       if (!(cw_cand && cw_call <= (uint32_t)kCwCall && cw_region <= (uint32_t)kCwRegionMax))
         throw Error(SHD_E_UNSUPPORTED, "query group: a call above 1024 events or a window beyond the call-window "
                                        "path: run these queries alone");
+      // direct-mapped group ids: one rows kernel for all members (they share
+      // the calls' row counts); hashed ids: a launch per member
+      const bool multi = kmax < (uint64_t)kCwDirectG && !getenv("SHD_CW_HASH") && !getenv("SHD_CW_NO_MULTI") &&
+                         wkind == SHD_W_LENGTH;
+      std::vector<const CwArgs*> margs;
+      int mnch = 1;
       for (size_t k = 0; k < wmembers.size(); k++) {
         SingleEngine& q = *wmembers[k];
         const int64_t Xq = std::max<int64_t>(0, total - q.wparam);
-        callwin_rows(q, b, total, cap, ncalls, Xq, cw_call, cw_region, kmax, k == 0);
+        callwin_rows(q, b, total, cap, ncalls, Xq, cw_call, cw_region, kmax, k == 0, multi ? &margs : nullptr);
+        mnch = std::max(mnch, std::max(q.nch, 1));
         q.counters.events += n;
         q.counters.carry = total - Xq;
         q.chunk_seq += ncalls;
         q.seq += n;
+      }
+      if (multi && !margs.empty()) {
+        callwin_direct_multi(margs, mnch, ncalls, cw_call, cw_region);
+        SHD_HIP(hipStreamSynchronize(stream));
+        const int64_t nrows = m > 0 ? (int64_t)h_tot.as<uint64_t>()[9] : 0;
+        for (auto* qp : wmembers) {
+          qp->out.count += nrows;
+          qp->counters.matches += nrows;
+        }
       }
       mark("members");
       commit_carry(total, X, nops, ncalls);
