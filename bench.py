@@ -403,6 +403,7 @@ def run_multi(args, torch, dist, rank, world, local, dev):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded SplitMix64 StockStream, BASELINE.md)",
+            "build": __import__("siddhi_amd.buildinfo", fromlist=["source_hash"]).source_hash(),
             "config": {"workload": "M5", "queries": len(plans), "events": n, "keys": keys, "delta_ms": delta,
                        "micro_batch": batch, "call_size": 1024,
                        "parallelism": "query-parallel x%d (broadcast input)" % world,
