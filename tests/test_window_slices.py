@@ -126,3 +126,35 @@ def test_window_of_reads_the_plan():
     assert ex.window_of(compile_single_query(APPS["length"])[0]) == ("length", 3000)
     assert ex.window_of(compile_single_query(APPS["time"])[0]) == ("time", 200)
     assert ex.window_of(compile_single_query(wl.P3_APP)[0]) is None
+
+
+def _rank_too_long(rank, world, path, outdir):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="file://" + path, rank=rank, world_size=world)
+    n = 500
+    cols = [torch.arange(n, dtype=torch.int64) + rank * n]
+    # a length window of 2000 filter-passing items cannot be covered by a 500-event slice
+    try:
+        ex.halo_take(("length", 2000), n, lambda k: ex.exchange_tail(cols, k, rank, world),
+                     lambda halo: halo[0].numel() >= 2000)
+        ok = "returned"
+    except ValueError:
+        ok = "raised"
+    with open(os.path.join(outdir, "too_long_r%d.txt" % rank), "w") as f:
+        f.write(ok)
+    dist.destroy_process_group()
+
+
+def test_halo_take_raises_past_a_whole_slice(tmp_path):
+    """Every rank learns the same outcome: a window reaching past the whole
+    previous slice raises on all ranks (the flag is all-reduced)."""
+    path = tempfile.mktemp(dir=str(tmp_path))
+    mp.spawn(_rank_too_long, args=(2, path, str(tmp_path)), nprocs=2)
+    for r in range(2):
+        assert open(os.path.join(str(tmp_path), "too_long_r%d.txt" % r)).read() == "raised"
+
+
+def test_exchange_tail_is_a_no_op_alone():
+    cols = [torch.arange(10)]
+    assert ex.exchange_tail(cols, 4, 0, 1) is None
+    assert ex.exchange_tail(cols, 0, 0, 2) is None
