@@ -108,6 +108,15 @@ typedef struct shd_out {
                                    state of a pattern / sequence match, the
                                    absent state of a timer row); 0 for
                                    single-stream (filter / window) queries   */
+  /* list arena of SHD_T_OBJECT columns (multi-value selection of a count
+     state without an index, `select e1.price` over `e1=S[..]<m:n>`: the
+     reference's MultiValueVariableFunctionExecutor returns a java.util.List,
+     C/executor/MultiValueVariableFunctionExecutor.java:64-72).  An OBJECT
+     cell's payload is offset | count << 40 into these arrays
+     (SHD_LIST_OFFSET / SHD_LIST_COUNT, siddhi_ir.h).                        */
+  int64_t n_list;
+  const uint64_t* list_values;  /* [n_list] element payloads (element type of the column) */
+  const uint8_t* list_nulls;    /* [n_list] element null flags                   */
 } shd_out;
 
 typedef struct shd_counters {

@@ -14,6 +14,21 @@
  *   SINGLE: stream, n_handlers, { FILTER expr | WINDOW kind p_lo p_hi } * n_handlers
  *   selector: current_on, expired_on, n_aggs { kind, arg_expr, arg_type } ,
  *             n_group { expr }, having_expr, n_out { type, expr }
+ *   optional trailing words:
+ *     null_lo, null_hi       dictionary id of the string "null" (string group keys)
+ *     POST section (STATE plans whose selector aggregates or has `having`):
+ *       SHD_IR_POST_MAGIC, n_base, { type, expr } * n_base, n_words, <SINGLE plan words>
+ *     The selector runs on one StateEvent per chunk
+ *     (StateMultiProcessStreamReceiver.processAndClear, C/query/input/
+ *     StateMultiProcessStreamReceiver.java:47-68; SingleProcessStreamReceiver
+ *     :48-72), so over a state query's output rows it is a sequential fold in
+ *     emission order: the base expressions are the state variables the
+ *     selector reads, projected per match; the nested SINGLE plan is the same
+ *     selector restated over a stream whose attributes are those base values
+ *     (attribute k = base k).  The oracle evaluates the selector fields above
+ *     directly on StateEvents and ignores this section; libsiddhi_hip runs
+ *     the state plan with the base expressions as outputs, then the nested
+ *     plan over its rows with one InputHandler call per row.
  *
  * Node tree (StateInputStreamParser.parse, C/util/parser/StateInputStreamParser.java:148-408):
  *   NODE_STREAM  state_id stream absent waiting_lo waiting_hi n_filters expr*
@@ -27,6 +42,7 @@
 
 #define SHD_IR_MAGIC 0x50444853 /* 'SHDP' */
 #define SHD_IR_VERSION 1
+#define SHD_IR_POST_MAGIC 0x54534F50 /* 'POST' */
 
 enum shd_kind { SHD_KIND_STATE = 1, SHD_KIND_SINGLE = 2 };
 
@@ -38,8 +54,15 @@ enum shd_type {
   SHD_T_LONG = 2,
   SHD_T_FLOAT = 3,
   SHD_T_DOUBLE = 4,
-  SHD_T_BOOL = 5
+  SHD_T_BOOL = 5,
+  /* output only: a list (java.util.List) of values of one attribute over a
+   * count state's event chain (MultiValueVariableFunctionExecutor); the
+   * 64-bit payload is a handle into shd_out's list arena:
+   * offset | count << 40 (SHD_LIST_*) */
+  SHD_T_OBJECT = 6
 };
+#define SHD_LIST_OFFSET(h) ((h) & 0xFFFFFFFFFFull)
+#define SHD_LIST_COUNT(h) ((h) >> 40)
 
 /* Expression bytecode: fixed 4-word instructions {op, a, b, c} over a value
  * stack of (64-bit payload, null flag). Semantics follow
@@ -67,7 +90,13 @@ enum shd_op {
   SHD_OP_NOT = 19,    /* NOT(null) -> true                                 */
   SHD_OP_ISNULL = 20,
   SHD_OP_AGG = 21,    /* a = aggregator index (selector only)              */
-  SHD_OP_TS = 22      /* a = state, b = chain index : event timestamp      */
+  SHD_OP_TS = 22,     /* a = state, b = chain index : event timestamp      */
+  SHD_OP_IFELSE = 23, /* a = result type; pops else, then, cond: cond true -> then, else (null cond too)
+                         (C/executor/function/IfThenElseFunctionExecutor.java) */
+  SHD_OP_MULTI = 24   /* a = state, c = attr | elem type << 16: the attribute over the state's
+                         whole event chain, first to last, as a list (SHD_T_OBJECT); only as a
+                         whole selector output (C/executor/MultiValueVariableFunctionExecutor.java,
+                         wired at C/util/parser/ExpressionParser.java:1386-1437) */
 };
 
 /* Chain indices (SiddhiConstants.CURRENT / LAST, C/util/SiddhiConstants.java:89-92). */

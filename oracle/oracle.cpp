@@ -493,6 +493,12 @@ Val eval(const Plan& p, int expr, const EvalCtx& cx) {
       case SHD_OP_AGG:
         st[sp++] = (*cx.aggs)[in.a];
         break;
+      case SHD_OP_IFELSE: {
+        // IfThenElseFunctionExecutor.execute(Object[]): Boolean.TRUE.equals(data[0]) ? data[1] : data[2]
+        Val e = st[--sp], t = st[--sp], c = st[--sp];
+        st[sp++] = (!c.null && c.b) ? t : e;
+        break;
+      }
       default:
         throw std::runtime_error("bad opcode");
     }
@@ -606,6 +612,9 @@ struct Engine {
   Plan p;
   std::string err;
   std::vector<OutRow> rows;
+  // list arena of SHD_T_OBJECT outputs (handles: offset | count << 40)
+  std::vector<uint64_t> lists;
+  std::vector<uint8_t> list_nul;
   int64_t chunk_counter = 0;
   int64_t now = 0;            // TimestampGeneratorImpl.lastEventTimestamp (playback)
   int64_t seq = 0;
@@ -1660,7 +1669,10 @@ struct Engine {
           // StateMultiProcessStreamReceiver.processAndClear: the selector runs
           // now (output data is populated at match time), the callback later.
           std::vector<OutRow> h;
-          for (SE* s : r) if (selectorAccepts(s)) h.push_back(make_row(s));
+          for (SE* s : r) {
+            OutRow row;
+            if (select_row(s, row)) h.push_back(std::move(row));
+          }
           if (!h.empty()) holders.push_back(std::move(h));
         }
       }
@@ -1680,50 +1692,78 @@ struct Engine {
         std::vector<SE*> r = processAndReturn(procs[0], ce);
         ret.insert(ret.end(), r.begin(), r.end());
       }
-      for (SE* s : ret) {
-        if (selectorAccepts(s)) emitChunk({s});
-      }
+      for (SE* s : ret) emitChunk({s});
     }
-  }
-
-  bool selectorAccepts(SE* s) {
-    // QuerySelector.processNoGroupBy: keep CURRENT if currentOn / EXPIRED if expiredOn
-    if (s->type == CURRENT) return p.current_on;
-    if (s->type == EXPIRED) return p.expired_on;
-    return false;
   }
 
   int64_t cur_seq = 0;   // the event being processed (timers: the next event's index)
 
-  OutRow make_row(SE* s) {
-    OutRow r;
+  // QuerySelector.process over a chunk of ONE StateEvent: the receivers hand
+  // every returned StateEvent to the selector on its own
+  // (StateMultiProcessStreamReceiver.processAndClear, C/query/input/
+  // StateMultiProcessStreamReceiver.java:47-68; SingleProcessStreamReceiver
+  // .java:48-72; AbsentStreamPreStateProcessor.java:240).  isBatch() is always
+  // true (C/event/ComplexEventChunk.java:265-270), so: group by ->
+  // processInBatchGroupBy, aggregators -> processInBatchNoGroupBy, else
+  // processNoGroupBy (QuerySelector.java:76-99).  For one event all three keep
+  // it iff, after the aggregators folded it in (CURRENT adds, EXPIRED
+  // removes), `having` holds and its type is selected (:161-205, :271-373).
+  bool select_row(SE* s, OutRow& r) {
+    if (s->type != CURRENT && s->type != EXPIRED) return false;   // TIMER / RESET
+    EvalCtx cx;
+    cx.se = s;
+    if (!p.aggs.empty()) {
+      run_aggs_ctx(state_aggs, cx, s->type);
+      cx.aggs = &agg_vals;
+    }
+    r = OutRow();
     r.seq = cur_seq;
     r.chunk = -1;
     r.type = s->type;
     r.ts = s->ts;
-    EvalCtx cx;
-    cx.se = s;
     for (auto& o : p.outputs) {
+      const auto& code = p.exprs[o.second];
+      if (code.size() == 1 && code[0].op == SHD_OP_MULTI) {
+        // MultiValueVariableFunctionExecutor.execute (C/executor/
+        // MultiValueVariableFunctionExecutor.java:64-72): getStreamEvent(position)
+        // (index 0: the chain head), then every getNext(), into a List
+        const uint64_t off = lists.size();
+        uint64_t cnt = 0;
+        for (Ev* x = s->ev[code[0].a]; x; x = x->next, cnt++) {
+          Val v = load_attr(x, code[0].c & 0xFFFF);
+          lists.push_back(v.b);
+          list_nul.push_back(v.null);
+        }
+        r.vals.push_back(cnt ? (off | (cnt << 40)) : 0);
+        r.nul.push_back(0);
+        continue;
+      }
       Val v = eval(p, o.second, cx);
       r.vals.push_back(v.b);
       r.nul.push_back(v.null);
     }
-    return r;
+    if (p.having >= 0 && !eval_bool(p, p.having, cx)) return false;
+    if (s->type == CURRENT) return p.current_on;
+    return p.expired_on;
   }
 
+  // one callback chunk of the selected rows (none: no callback)
   void emitChunk(const std::vector<SE*>& ss) {
-    int64_t cid = chunk_counter++;
+    std::vector<OutRow> sel;
     for (SE* s : ss) {
-      OutRow r = make_row(s);
+      OutRow r;
+      if (select_row(s, r)) sel.push_back(std::move(r));
+    }
+    if (sel.empty()) return;
+    int64_t cid = chunk_counter++;
+    for (auto& r : sel) {
       r.chunk = cid;
       rows.push_back(std::move(r));
       counters[3]++;
     }
   }
 
-  void selectorEmitImmediate(SE* s) {
-    if (selectorAccepts(s)) emitChunk({s});
-  }
+  void selectorEmitImmediate(SE* s) { emitChunk({s}); }
 
   // ---------------- scheduler (playback) ----------------
   void notifyAt(int sched, int64_t t) {
@@ -1790,6 +1830,11 @@ struct Engine {
   };
   std::map<Key, std::unique_ptr<KeySingle>> single_keys;
   std::unique_ptr<KeySingle> single_global;
+  // Aggregator states of a state query's selector: one group table per
+  // partition key (PartitionStateHolder, C/util/snapshot/state/
+  // PartitionStateHolder.java:43-69; the planner refuses aggregation inside a
+  // partition, so only the unpartitioned table is used).
+  KeySingle state_aggs;
   int window_kind = 0;
   int64_t window_param = 0;
   int window_pos = -1;
@@ -1844,10 +1889,19 @@ struct Engine {
 
   // AttributeAggregatorExecutor.execute for each aggregator (plan order)
   void run_aggs(KeySingle* ks, Ev* e) {
-    agg_vals.assign(p.aggs.size(), Val{});
-    if (p.aggs.empty()) return;
     EvalCtx cx;
     cx.ev = e;
+    run_aggs_ctx(*ks, cx, e->type);
+  }
+
+  // the aggregators of the event in cx (a StreamEvent of a single-stream
+  // query or a StateEvent) under its group key; agg_vals = their results
+  void run_aggs_ctx(KeySingle& kst, const EvalCtx& cx, int etype) {
+    KeySingle* ks = &kst;
+    agg_vals.assign(p.aggs.size(), Val{});
+    if (p.aggs.empty()) return;
+    struct { int type; } ev_t{etype};
+    auto* e = &ev_t;
     std::vector<std::pair<uint64_t, uint8_t>> gk = group_key(cx);
     GroupAgg& ga = ks->groups[gk];
     if (ga.a.size() != p.aggs.size()) ga.a.resize(p.aggs.size());
@@ -2189,6 +2243,8 @@ int expr_type(const Plan& p, int expr) {
         st.pop_back(); st.back() = SHD_T_BOOL; break;
       case SHD_OP_NOT: case SHD_OP_ISNULL: st.back() = SHD_T_BOOL; break;
       case SHD_OP_AGG: st.push_back(SHD_T_DOUBLE); break;
+      case SHD_OP_MULTI: st.push_back(SHD_T_OBJECT); break;
+      case SHD_OP_IFELSE: { int t = st[st.size() - 2]; st.pop_back(); st.pop_back(); st.back() = t; break; }
     }
   }
   return st.empty() ? SHD_T_LONG : st.back();
@@ -2257,6 +2313,16 @@ int64_t orc_num_rows(void* h) { return (int64_t)((Engine*)h)->rows.size(); }
 
 int32_t orc_num_outputs(void* h) { return (int32_t)((Engine*)h)->p.outputs.size(); }
 
+int64_t orc_num_list(void* h) { return (int64_t)((Engine*)h)->lists.size(); }
+
+void orc_get_list(void* h, uint64_t* vals, uint8_t* nulls) {
+  Engine* e = (Engine*)h;
+  for (size_t i = 0; i < e->lists.size(); i++) {
+    vals[i] = e->lists[i];
+    nulls[i] = e->list_nul[i];
+  }
+}
+
 void orc_get_rows(void* h, int64_t* chunk, int32_t* type, int64_t* ts, uint64_t* vals, uint8_t* nulls) {
   Engine* e = (Engine*)h;
   size_t no = e->p.outputs.size();
@@ -2277,7 +2343,12 @@ void orc_get_rows_seq(void* h, int64_t* seq) {
   for (size_t i = 0; i < e->rows.size(); i++) seq[i] = e->rows[i].seq;
 }
 
-void orc_clear_rows(void* h) { ((Engine*)h)->rows.clear(); }
+void orc_clear_rows(void* h) {
+  Engine* e = (Engine*)h;
+  e->rows.clear();
+  e->lists.clear();
+  e->list_nul.clear();
+}
 
 void orc_counters(void* h, int64_t* out) {
   for (int i = 0; i < 8; i++) out[i] = ((Engine*)h)->counters[i];

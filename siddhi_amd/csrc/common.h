@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -133,6 +134,11 @@ struct Plan {
   int64_t null_str_id = -1;   // dictionary id of "null" (string group keys, GroupByKeyGenerator)
   int having = -1;
   std::vector<std::pair<int, int>> outputs;  // (type, expr)
+  // IR POST section (an aggregating / `having` selector of a STATE plan):
+  // base outputs (type, expr) the state engine projects per match, and the
+  // selector restated as a SINGLE plan over a stream of those values
+  std::vector<std::pair<int, int>> post_base;
+  std::shared_ptr<Plan> post;
 };
 
 Plan decode_plan(const int32_t* w, int64_t n);

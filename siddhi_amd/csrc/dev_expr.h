@@ -299,6 +299,14 @@ __device__ inline Val eval_expr(const int4* code, int len, const uint64_t* const
         st.set(sp++, v.b, v.null);
         break;
       }
+      case SHD_OP_IFELSE: {   // IfThenElseFunctionExecutor: Boolean.TRUE.equals(cond) ? then : else
+        if (sp < 3) break;
+        const Val e = st.val(sp - 1), t = st.val(sp - 2), c = st.val(sp - 3);
+        const Val o = (!c.null && c.b) ? t : e;
+        sp -= 3;
+        st.set(sp++, o.b, o.null);
+        break;
+      }
       default:
         break;
     }

@@ -27,6 +27,11 @@ struct OutputBuffer {
   uint8_t* d_nulls() { return nulls.as<uint8_t>(); }
   int64_t* d_seq() { return seq.as<int64_t>(); }   // shd_out.in_seq
   int32_t* d_sidx() { return sidx.as<int32_t>(); }  // shd_out.state_idx
+  // list arena of SHD_T_OBJECT outputs (multi-value selections): values and
+  // null flags; a row's list handle = offset | count << 40
+  DevBuf lvals, lnul;
+  int64_t lcount = 0, lcap = 0;
+  void ensure_list(int64_t extra, hipStream_t s);
 };
 
 // A batch staged on the device (columns either borrowed device pointers or

@@ -53,7 +53,8 @@ constexpr int kLaneBlock = 64;
 enum : int { PK_STREAM = 0, PK_COUNT = 1, PK_LOGICAL = 2, PK_ABSENT = 3, PK_ABSENT_LOGICAL = 4 };
 enum : uint8_t { FL_CHANGED = 1, FL_INIT = 2, FL_STARTED = 4, FL_SUCCESS = 8, FL_SSRESET = 16, FL_INACTIVE = 32 };
 enum : uint32_t {
-  OV_LIST = 1, OV_SE = 2, OV_EV = 4, OV_REC = 8, OV_SCHED = 16, OV_RET = 32, OV_WORK = 64, OV_ROWS = 128
+  OV_LIST = 1, OV_SE = 2, OV_EV = 4, OV_REC = 8, OV_SCHED = 16, OV_RET = 32, OV_WORK = 64, OV_ROWS = 128,
+  OV_MULTI = 256   // list arena of multi-value outputs
 };
 enum : int {
   MISC_SEEDED = 0, MISC_EVRET = 1, MISC_WKN = 2, MISC_RETN = 3, MISC_TMPN = 4,
@@ -74,6 +75,7 @@ struct DPost {
 // The processor graph of one plan (StateInputStreamParser output), uniform over keys.
 struct NfaProg {
   int npre, nstates, nsched, seq, nstart, nout, current_on, expired_on;
+  uint32_t multi_mask;            // outputs that are SHD_OP_MULTI lists
   int64_t within;                 // -1: no `within`
   int startIds[kNP];
   DPre pre[kNP];
@@ -128,6 +130,7 @@ struct NfaCtl {
   unsigned long long kmax;
   unsigned int overflow;
   unsigned int count;   // scan totals / slot counter
+  unsigned long long lrows;   // list arena entries written (multi-value outputs)
 };
 
 struct NfaRunArgs {
@@ -171,6 +174,9 @@ struct NfaRunArgs {
   int32_t* st_type;
   uint64_t* st_vals;
   uint8_t* st_nul;
+  int64_t LR;          // list arena capacity (entries)
+  uint64_t* st_lv;     // list arena values
+  uint8_t* st_ln;      // list arena null flags
   NfaCtl* ctl;
 };
 
@@ -1200,6 +1206,29 @@ struct Lane {
     if (t == SHD_EV_EXPIRED) return P.expired_on;
     return false;
   }
+  // one list per multi-value output: the attribute of every event of state
+  // st's chain, in chain order, into the list arena; returns the handle
+  // (offset | count << 40, offsets relative to this push's arena)
+  __device__ uint64_t emit_list(uint16_t s, int4 in) {
+    const uint16_t head = sev(s, in.y);
+    const int attr = in.w & 0xFFFF;
+    int len = 0;
+    for (uint16_t x = head; x != NIL; x = enext(x)) len++;
+    if (len == 0) return 0;
+    const unsigned long long base = atomicAdd(&A.ctl->lrows, (unsigned long long)len);
+    if ((int64_t)(base + len) > A.LR) {
+      ovf |= OV_MULTI;
+      return 0;
+    }
+    int i = 0;
+    for (uint16_t x = head; x != NIL; x = enext(x), i++) {
+      const uint16_t r = erec(x);
+      const bool z = (rnul(r) >> attr) & 1u;
+      A.st_lv[base + i] = z ? 0 : rval(r, attr);
+      A.st_ln[base + i] = z ? 1 : 0;
+    }
+    return (uint64_t)base | ((uint64_t)len << 40);
+  }
   __device__ uint64_t new_tag() { return ((uint64_t)slot << 24) | (uint64_t)(tagc++ & 0xFFFFFF); }
   __device__ void emit(uint16_t s, uint64_t tag) {
     if (quiet) return;   // warm-up event of a window lane
@@ -1211,6 +1240,11 @@ struct Lane {
     }
     SECtx cx{this, s};
     for (int c = 0; c < P.nout; c++) {
+      if ((P.multi_mask >> c) & 1u) {   // MultiValueVariableFunctionExecutor.execute: the chain from its head
+        A.st_vals[idx * P.nout + c] = emit_list(s, es.ins[P.outs[c].off]);
+        A.st_nul[idx * P.nout + c] = 0;
+        continue;
+      }
       Val v = eval_expr(es.ins + P.outs[c].off, P.outs[c].len, es.consts, cx);
       A.st_vals[idx * P.nout + c] = v.b;
       A.st_nul[idx * P.nout + c] = (uint8_t)v.null;
@@ -1886,7 +1920,8 @@ __global__ void k_out_rows(const uint32_t* perm, const uint32_t* hpos, const uin
                            int64_t chunk0, int64_t row0, const int64_t* sts, const int32_t* stype,
                            const uint64_t* svals, const uint8_t* snul, const uint64_t* sprim,
                            const int32_t* ssidx, int64_t* o_chunk, int32_t* o_type, int64_t* o_ts,
-                           uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq, int32_t* o_sidx) {
+                           uint64_t* o_vals, uint8_t* o_nul, int64_t* o_seq, int32_t* o_sidx, uint32_t multi_mask,
+                           int64_t lbase) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = perm[i];
     const int64_t r = row0 + i;
@@ -1897,7 +1932,9 @@ __global__ void k_out_rows(const uint32_t* perm, const uint32_t* hpos, const uin
     o_seq[r] = (int64_t)(sprim[j] >> 1);
     o_sidx[r] = ssidx[j];
     for (int c = 0; c < nout; c++) {
-      o_vals[r * nout + c] = svals[j * nout + c];
+      const uint64_t v = svals[j * nout + c];
+      // list handles: this push's arena lands at lbase of the output arena
+      o_vals[r * nout + c] = (((multi_mask >> c) & 1u) && (v >> 40) != 0) ? v + (uint64_t)lbase : v;
       o_nul[r * nout + c] = snul[j * nout + c];
     }
   }
@@ -2143,8 +2180,9 @@ void layout_offsets(NfaLayout& Y);
 // the engine grows its layout from the pre-push state and runs the push again.
 struct NfaOverflow : Error {
   unsigned flags;
-  int64_t rows;
-  NfaOverflow(unsigned f, int64_t r, const std::string& m) : Error(SHD_E_CAPACITY, m), flags(f), rows(r) {}
+  int64_t rows, lrows;
+  NfaOverflow(unsigned f, int64_t r, const std::string& m, int64_t lr = 0)
+      : Error(SHD_E_CAPACITY, m), flags(f), rows(r), lrows(lr) {}
 };
 
 struct NfaEngine : Engine {
@@ -2357,6 +2395,16 @@ struct NfaEngine : Engine {
     R = rows;
   }
 
+  // list arena of multi-value outputs (entries)
+  DevBuf st_lv, st_ln;
+  int64_t LR = 0;
+  void ensure_lists(int64_t n) {
+    if (n <= LR) return;
+    st_lv.reserve(n * 8);
+    st_ln.reserve(n);
+    LR = n;
+  }
+
   void push(const Staged& b) override { run_push(&b, 0); }
 
   // Key-sort the keyed events of a partitioned push, map keys to slots.
@@ -2525,15 +2573,16 @@ struct NfaEngine : Engine {
         run_push_once(b, t_only);
         return;
       } catch (NfaOverflow& o) {
-        grow(o.flags, o.rows, o.what());
+        if (o.flags & OV_MULTI) ensure_lists(2 * std::max(LR, o.lrows));
+        grow(o.flags & ~(unsigned)OV_MULTI, o.rows, o.what(), (o.flags & OV_MULTI) != 0);
       }
     }
   }
 
-  void grow(unsigned ovf, int64_t rows, const char* msg) {
+  void grow(unsigned ovf, int64_t rows, const char* msg, bool lists_grown = false) {
     args_begin();   // the failed attempt's argument blocks are no longer read
     NfaLayout ny = lay;
-    bool changed = false;
+    bool changed = lists_grown;
     auto dbl = [&](int& v, int mx) {
       const int nv = std::min(2 * v, mx);
       if (nv > v) {
@@ -2763,6 +2812,10 @@ struct NfaEngine : Engine {
     ra.st_type = st_type.as<int32_t>();
     ra.st_vals = st_vals.as<uint64_t>();
     ra.st_nul = st_nul.as<uint8_t>();
+    if (prog.multi_mask) ensure_lists(1 << 16);
+    ra.LR = LR;
+    ra.st_lv = st_lv.as<uint64_t>();
+    ra.st_ln = st_ln.as<uint8_t>();
     ra.ctl = d_ctl.as<NfaCtl>();
     NfaCtl hc{};
     const NfaProg* dp = dev_args(prog);
@@ -2844,10 +2897,10 @@ struct NfaEngine : Engine {
                     "timers %d, returned %d, rows %lld/%lld); raise SHD_NFA_LIST / SHD_NFA_PARTIALS / "
                     "SHD_NFA_EVENTS / SHD_NFA_RECORDS / SHD_NFA_TIMERS and reset the query",
                     hc.overflow, lay.L, lay.SC, lay.EC, lay.RC, lay.QC, lay.RETC, (long long)hc.rows, (long long)R);
-      throw NfaOverflow(hc.overflow, (int64_t)hc.rows, msg);
+      throw NfaOverflow(hc.overflow, (int64_t)hc.rows, msg, (int64_t)hc.lrows);
     }
     const int64_t m = (int64_t)hc.rows;
-    if (m > 0) order_rows(m, partitioned || (win && !win_one), timers, n);   // window lanes: merge by event order
+    if (m > 0) order_rows(m, partitioned || (win && !win_one), timers, n, (int64_t)hc.lrows);   // window lanes: merge by event order
     SHD_HIP(hipEventRecord(ev1, s));
     stage_end();
     SHD_HIP(hipEventSynchronize(ev1));
@@ -2871,7 +2924,7 @@ struct NfaEngine : Engine {
   }
 
   // staged rows -> reference order -> output arena
-  void order_rows(int64_t m, bool sort, bool timers, int64_t n) {
+  void order_rows(int64_t m, bool sort, bool timers, int64_t n, int64_t nlist = 0) {
     hipStream_t s = stream;
     d_perm.reserve(m * 4);
     d_perm_alt.reserve(m * 4);
@@ -2913,13 +2966,20 @@ struct NfaEngine : Engine {
     SHD_CHECK_LAUNCH();
     scan_exclusive_u32(d_thead.as<uint32_t>(), d_thpos.as<uint32_t>(), m, nullptr, d_scan, s);
     out.ensure(m, s);
+    const int64_t lbase = out.lcount;
+    if (nlist > 0) {   // this push's list arena after the unpolled rows' lists
+      out.ensure_list(nlist, s);
+      SHD_HIP(hipMemcpyAsync(out.lvals.as<uint64_t>() + lbase, st_lv.p, (size_t)nlist * 8, hipMemcpyDeviceToDevice, s));
+      SHD_HIP(hipMemcpyAsync(out.lnul.as<uint8_t>() + lbase, st_ln.p, (size_t)nlist, hipMemcpyDeviceToDevice, s));
+      out.lcount += nlist;
+    }
     hipLaunchKernelGGL(k_out_rows, dim3(grid_for(m)), dim3(kBlock), 0, s, (const uint32_t*)perm,
                        (const uint32_t*)d_thpos.as<uint32_t>(), (const uint32_t*)d_thead.as<uint32_t>(), m, prog.nout,
                        chunk_seq, out.count, (const int64_t*)st_ts.as<int64_t>(),
                        (const int32_t*)st_type.as<int32_t>(), (const uint64_t*)st_vals.as<uint64_t>(),
                        (const uint8_t*)st_nul.as<uint8_t>(), (const uint64_t*)st_p.as<uint64_t>(),
                        (const int32_t*)st_sidx.as<int32_t>(), out.d_chunk(), out.d_type(), out.d_ts(), out.d_vals(),
-                       out.d_nulls(), out.d_seq(), out.d_sidx());
+                       out.d_nulls(), out.d_seq(), out.d_sidx(), prog.multi_mask, lbase);
     SHD_CHECK_LAUNCH();
     // chunk ids consumed = number of distinct tags
     SHD_HIP(hipMemcpyAsync(h_ctl.as<char>() + 64, d_thpos.as<uint32_t>() + (m - 1), 4, hipMemcpyDeviceToHost, s));
@@ -3111,6 +3171,11 @@ std::unique_ptr<Engine> make_nfa_engine(const Plan& p, std::string& why, int64_t
   P.current_on = p.current_on;
   P.expired_on = p.expired_on;
   P.nout = (int)p.outputs.size();
+  P.multi_mask = 0;
+  for (int c = 0; c < P.nout && c < 32; c++) {
+    const auto& code = p.exprs[p.outputs[c].second];
+    if (code.size() == 1 && code[0].op == SHD_OP_MULTI) P.multi_mask |= 1u << c;
+  }
 
   // partition keys (ValuePartitionExecutor: one key class per query)
   e->partitioned = !p.part_keys.empty();

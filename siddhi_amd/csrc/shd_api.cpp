@@ -155,8 +155,30 @@ Plan decode_plan(const int32_t* w, int64_t n) {
     int e = r.next();
     p.outputs.push_back({t, e});
   }
-  // optional trailing section: dictionary id of the string "null" (group keys)
+  // optional trailing sections: dictionary id of the string "null" (group
+  // keys), then the POST section of a state plan's selector (siddhi_ir.h)
   if (r.i + 2 <= r.n) p.null_str_id = r.next64();
+  if (r.i < r.n) {
+    if (p.kind != SHD_KIND_STATE || r.next() != (int32_t)SHD_IR_POST_MAGIC)
+      throw Error(SHD_E_INVALID_PLAN, "unknown trailing plan section");
+    const int nb = r.next();
+    if (nb < 0 || nb > kMaxCols) throw Error(SHD_E_UNSUPPORTED, "too many selector base values");
+    for (int i = 0; i < nb; i++) {
+      const int t = r.next();
+      const int e = r.next();
+      p.post_base.push_back({t, e});
+    }
+    const int nw = r.next();
+    if (nw < 0 || r.i + nw > r.n) throw Error(SHD_E_INVALID_PLAN, "POST section truncated");
+    p.post = std::make_shared<Plan>(decode_plan(r.w + r.i, nw));
+    r.i += nw;
+    if (p.post->kind != SHD_KIND_SINGLE || p.post->stream_types.size() != 1 ||
+        p.post->stream_types[0].size() != (size_t)nb)
+      throw Error(SHD_E_INVALID_PLAN, "POST selector plan does not match its base values");
+    for (int i = 0; i < nb; i++)
+      if (p.post->stream_types[0][i] != p.post_base[i].first) throw Error(SHD_E_INVALID_PLAN, "POST base type");
+    if (r.i != r.n) throw Error(SHD_E_INVALID_PLAN, "trailing words after the POST section");
+  }
   // validation: expression ids, stack depth, constants
   auto check_expr = [&](int e) {
     if (e < 0 || e >= (int)p.exprs.size()) throw Error(SHD_E_INVALID_PLAN, "bad expression id");
@@ -167,6 +189,7 @@ Plan decode_plan(const int32_t* w, int64_t n) {
   };
   for (size_t e = 0; e < p.exprs.size(); e++) check_expr((int)e);
   for (auto& o : p.outputs) check_expr(o.second);
+  for (auto& o : p.post_base) check_expr(o.second);
   return p;
 }
 
@@ -175,12 +198,16 @@ int expr_max_depth(const Plan& p, int expr) {
   for (auto& in : p.exprs[expr]) {
     switch (in.op) {
       case SHD_OP_CONST: case SHD_OP_NULL: case SHD_OP_LOAD: case SHD_OP_EVNULL: case SHD_OP_TS: case SHD_OP_AGG:
+      case SHD_OP_MULTI:
         sp++;
         break;
       case SHD_OP_ADD: case SHD_OP_SUB: case SHD_OP_MUL: case SHD_OP_DIV: case SHD_OP_MOD: case SHD_OP_EQ:
       case SHD_OP_NE: case SHD_OP_GT: case SHD_OP_GE: case SHD_OP_LT: case SHD_OP_LE: case SHD_OP_AND:
       case SHD_OP_OR:
         sp--;
+        break;
+      case SHD_OP_IFELSE:
+        sp -= 2;
         break;
       default:
         break;
@@ -209,6 +236,10 @@ int expr_result_type(const Plan& p, int expr, const std::vector<int>&) {
         break;
       case SHD_OP_NOT: case SHD_OP_ISNULL: if (!st.empty()) st.back() = SHD_T_BOOL; break;
       case SHD_OP_AGG: st.push_back(SHD_T_DOUBLE); break;
+      case SHD_OP_MULTI: st.push_back(SHD_T_OBJECT); break;
+      case SHD_OP_IFELSE:
+        if (st.size() >= 3) { const int t = st[st.size() - 2]; st.pop_back(); st.pop_back(); st.back() = t; }
+        break;
     }
   }
   return st.empty() ? SHD_T_LONG : st.back();
@@ -268,6 +299,23 @@ void OutputBuffer::ensure(int64_t extra, hipStream_t s) {
   std::swap(sidx.p, x2.p); std::swap(sidx.cap, x2.cap);
   std::swap(seq.p, q2.p); std::swap(seq.cap, q2.cap);
   cap = nc;
+}
+
+void OutputBuffer::ensure_list(int64_t extra, hipStream_t s) {
+  const int64_t need = lcount + extra;
+  if (need <= lcap) return;
+  const int64_t nc = std::max<int64_t>(need, std::max<int64_t>(lcap * 2, 4096));
+  DevBuf v2, n2;
+  v2.reserve(nc * 8);
+  n2.reserve(nc);
+  if (lcount > 0) {
+    SHD_HIP(hipMemcpyAsync(v2.p, lvals.p, lcount * 8, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(n2.p, lnul.p, lcount, hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipStreamSynchronize(s));
+  }
+  std::swap(lvals.p, v2.p); std::swap(lvals.cap, v2.cap);
+  std::swap(lnul.p, n2.p); std::swap(lnul.cap, n2.cap);
+  lcap = nc;
 }
 
 void Engine::mark(const char* name) {
@@ -456,6 +504,12 @@ struct shd_ctx {
 struct shd_query {
   shd_ctx* ctx = nullptr;
   std::unique_ptr<Engine> eng;
+  // state plans with an aggregating / `having` selector (IR POST section):
+  // eng projects the selector's base values per match, post runs the
+  // selector over those rows (one call per row) and holds the query's output
+  std::unique_ptr<Engine> post;
+  DevBuf post_col[kMaxCols], post_nul[kMaxCols];
+  Engine& out_eng() { return post ? *post : *eng; }
   // host staging for SHD_MEM_HOST batches
   DevBuf stage_ts, stage_col[kMaxCols], stage_nul[kMaxCols];
   PinnedBuf pin;   // host staging for SHD_MEM_HOST batches
@@ -463,8 +517,8 @@ struct shd_query {
   std::vector<int64_t> h_chunk, h_ts, h_seq;
   std::vector<int32_t> h_sidx;
   std::vector<int32_t> h_type;
-  std::vector<uint64_t> h_vals;
-  std::vector<uint8_t> h_nulls;
+  std::vector<uint64_t> h_vals, h_lvals;
+  std::vector<uint8_t> h_nulls, h_lnul;
   uint64_t plan_hash = 0;         // FNV-1a of the plan IR (snapshot compatibility)
   std::vector<uint8_t> snap;      // last shd_snapshot image (library-owned)
 };
@@ -520,6 +574,104 @@ void stage_host(hipStream_t s, PinnedBuf& pin, DevBuf& dts, DevBuf* dcol, DevBuf
     st.cs.type[c] = (int8_t)types[c];
     st.cs.nul[c] = (b->nulls && b->nulls[c]) ? (const uint8_t*)stage(dnul[c], b->nulls[c], (size_t)b->n) : nullptr;
   }
+}
+
+// ---- selector over a state query's rows (IR POST section)
+struct PostXArgs {
+  int nc;
+  int32_t type[kMaxCols];
+  void* col[kMaxCols];
+  uint8_t* nul[kMaxCols];
+};
+
+// row-major 64-bit payloads of the state engine's rows -> typed columns of
+// the selector stream (one thread per row)
+__global__ __launch_bounds__(kBlock) void k_post_cols(const PostXArgs* __restrict__ ap, const uint64_t* vals,
+                                                      const uint8_t* nulls, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int nc = ap->nc;
+  for (int c = 0; c < nc; c++) {
+    const uint64_t b = vals[i * nc + c];
+    const uint8_t z = nulls[i * nc + c];
+    ap->nul[c][i] = z;
+    switch (ap->type[c]) {
+      case SHD_T_BOOL: ((uint8_t*)ap->col[c])[i] = (uint8_t)b; break;
+      case SHD_T_STRING: case SHD_T_INT: case SHD_T_FLOAT: ((uint32_t*)ap->col[c])[i] = (uint32_t)b; break;
+      default: ((uint64_t*)ap->col[c])[i] = b; break;
+    }
+  }
+}
+
+// selector rows [r0, r0 + m): back to the state rows that emitted them (the
+// selector stream's arrival index - seq0 = the state row): callback chunk,
+// in_seq and state index of that row
+__global__ __launch_bounds__(kBlock) void k_post_remap(int64_t* chunk, int64_t* seq, int32_t* sidx, int64_t r0,
+                                                       int64_t m, int64_t seq0, const int64_t* a_chunk,
+                                                       const int64_t* a_seq, const int32_t* a_sidx) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= m) return;
+  const int64_t a = seq[r0 + i] - seq0;
+  chunk[r0 + i] = a_chunk[a];
+  seq[r0 + i] = a_seq[a];
+  sidx[r0 + i] = a_sidx[a];
+}
+
+// The reference's selector sees one StateEvent per chunk
+// (StateMultiProcessStreamReceiver.processAndClear, C/query/input/
+// StateMultiProcessStreamReceiver.java:47-68), so the state rows pushed since
+// the last call are fed to the selector engine in emission order, one
+// InputHandler call per row; its rows then take the callback chunks, in_seq
+// and state indices of the state rows they came from.
+void run_post(shd_query* q) {
+  if (!q->post) return;
+  Engine& a = *q->eng;
+  Engine& b = *q->post;
+  const int64_t n = a.out.count;
+  if (n <= 0) return;
+  SHD_HIP(hipStreamSynchronize(a.stream));
+  hipStream_t s = b.stream;
+  const auto& types = b.plan.stream_types[0];
+  const int nc = (int)types.size();
+  if (nc != a.out.ncols) throw Error(SHD_E_DEVICE, "internal: selector base columns");
+  b.args_begin();
+  PostXArgs xa{};
+  xa.nc = nc;
+  Staged st;
+  st.stream = 0;
+  st.n = n;
+  st.advance_time = false;
+  st.cs.ncols = nc;
+  st.cs.n = n;
+  st.cs.ts = a.out.d_ts();
+  for (int c = 0; c < nc; c++) {
+    q->post_col[c].reserve((size_t)n * type_size(types[c]));
+    q->post_nul[c].reserve((size_t)n);
+    xa.type[c] = types[c];
+    xa.col[c] = q->post_col[c].p;
+    xa.nul[c] = q->post_nul[c].as<uint8_t>();
+    st.cs.col[c] = q->post_col[c].p;
+    st.cs.nul[c] = q->post_nul[c].as<uint8_t>();
+    st.cs.type[c] = (int8_t)types[c];
+  }
+  if (nc > 0) {
+    hipLaunchKernelGGL(k_post_cols, dim3(grid_cover(n)), dim3(kBlock), 0, s, b.dev_args(xa), a.out.d_vals(),
+                       a.out.d_nulls(), n);
+    SHD_CHECK_LAUNCH();
+  }
+  st.call_offsets.resize((size_t)n + 1);
+  for (int64_t i = 0; i <= n; i++) st.call_offsets[(size_t)i] = i;
+  const int64_t seq0 = b.seq, r0 = b.out.count;
+  b.push(st);
+  const int64_t m = b.out.count - r0;
+  if (m > 0) {
+    hipLaunchKernelGGL(k_post_remap, dim3(grid_cover(m)), dim3(kBlock), 0, s, b.out.d_chunk(), b.out.d_seq(),
+                       b.out.d_sidx(), r0, m, seq0, (const int64_t*)a.out.d_chunk(), (const int64_t*)a.out.d_seq(),
+                       (const int32_t*)a.out.d_sidx());
+    SHD_CHECK_LAUNCH();
+  }
+  SHD_HIP(hipStreamSynchronize(s));
+  a.out.count = 0;
 }
 
 // The running engine hit a valid input its formulation cannot process
@@ -699,7 +851,17 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
   return guarded([&]() -> int {
     if (!ctx || !ir || !out || (len % 4) != 0) return fail(SHD_E_ARG, "bad arguments");
     SHD_HIP(hipSetDevice(ctx->device));
-    Plan p = decode_plan((const int32_t*)ir, (int64_t)(len / 4));
+    Plan full = decode_plan((const int32_t*)ir, (int64_t)(len / 4));
+    // a POST selector: the state engine projects the base values instead
+    Plan p = full;
+    if (full.post) {
+      p.outputs = full.post_base;
+      p.aggs.clear();
+      p.group_by.clear();
+      p.having = -1;
+      p.post.reset();
+      p.post_base.clear();
+    }
     std::string why1, why2;
     std::unique_ptr<Engine> e;
     if (p.kind == SHD_KIND_STATE) {
@@ -717,10 +879,18 @@ int shd_plan_load(shd_ctx* ctx, const void* ir, size_t len, shd_query** out) {
       e = make_single_engine(p, why2);
     }
     if (!e) return fail(SHD_E_UNSUPPORTED, "plan outside the device path: " + why1 + why2);
+    std::unique_ptr<Engine> post;
+    if (full.post) {
+      std::string why3;
+      post = make_window_x_engine(*full.post, why3);
+      if (!post) return fail(SHD_E_UNSUPPORTED, "selector over state output: " + why3);
+      init_engine(*post, *full.post);
+    }
     init_engine(*e, p);
     auto* q = new shd_query();
     q->ctx = ctx;
     q->eng = std::move(e);
+    q->post = std::move(post);
     uint64_t h = 1469598103934665603ull;
     for (size_t i = 0; i < len; i++) h = (h ^ ((const uint8_t*)ir)[i]) * 1099511628211ull;
     q->plan_hash = h;
@@ -755,6 +925,7 @@ int shd_set_time(shd_query* q, int64_t ts) {
     if (!q) return fail(SHD_E_ARG, "null query");
     q->eng->args_begin();
     q->eng->set_time(ts);
+    run_post(q);
     return SHD_OK;
   });
 }
@@ -825,9 +996,11 @@ int shd_push(shd_query* q, const shd_batch* b) {
   return guarded([&]() -> int {
     if (!q || !b) return fail(SHD_E_ARG, "null argument");
     if (q->eng->grouped) return fail(SHD_E_ARG, "query belongs to a group: push through shd_group_push");
-    return push_batch(q, b, [&](const Staged& st, const shd_counters& before, const NeedNfa& nf) {
+    const int rc = push_batch(q, b, [&](const Staged& st, const shd_counters& before, const NeedNfa& nf) {
       switch_to_nfa(q, st, before, nf.what());
     });
+    if (rc == SHD_OK) run_post(q);
+    return rc;
   });
 }
 
@@ -851,7 +1024,7 @@ int shd_flush(shd_query* q) {
 int shd_poll(shd_query* q, shd_out* out) {
   return guarded([&]() -> int {
     if (!q || !out) return fail(SHD_E_ARG, "null argument");
-    Engine& e = *q->eng;
+    Engine& e = q->out_eng();
     hipStream_t s = e.stream;
     int64_t n = e.out.count;
     int nc = e.out.ncols;
@@ -873,8 +1046,19 @@ int shd_poll(shd_query* q, shd_out* out) {
         SHD_HIP(hipMemcpyAsync(q->h_nulls.data(), e.out.nulls.p, n * nc, hipMemcpyDeviceToHost, s));
       }
     }
+    const int64_t nl = e.out.lcount;
+    q->h_lvals.resize(std::max<int64_t>(nl, 1));
+    q->h_lnul.resize(std::max<int64_t>(nl, 1));
+    if (nl > 0) {
+      SHD_HIP(hipMemcpyAsync(q->h_lvals.data(), e.out.lvals.p, nl * 8, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(q->h_lnul.data(), e.out.lnul.p, nl, hipMemcpyDeviceToHost, s));
+    }
     SHD_HIP(hipStreamSynchronize(s));
     e.out.count = 0;
+    e.out.lcount = 0;
+    out->n_list = nl;
+    out->list_values = q->h_lvals.data();
+    out->list_nulls = q->h_lnul.data();
     out->n_rows = n;
     out->n_cols = nc;
     out->chunk = q->h_chunk.data();
@@ -891,6 +1075,8 @@ int shd_poll(shd_query* q, shd_out* out) {
 int shd_discard_output(shd_query* q) {
   if (!q) return fail(SHD_E_ARG, "null query");
   q->eng->out.count = 0;
+  q->eng->out.lcount = 0;
+  if (q->post) q->post->out.count = 0;
   return SHD_OK;
 }
 
@@ -900,6 +1086,10 @@ int shd_reset(shd_query* q) {
     if (q->eng->grouped) return fail(SHD_E_ARG, "query belongs to a group: reset through shd_group_reset");
     SHD_HIP(hipStreamSynchronize(q->eng->stream));
     q->eng->reset();
+    if (q->post) {
+      SHD_HIP(hipStreamSynchronize(q->post->stream));
+      q->post->reset();
+    }
     return SHD_OK;
   });
 }
@@ -920,6 +1110,7 @@ int shd_stage_times(shd_query* q, int64_t* ns, const char** names, int max, int*
 // fields (arrival seq, playback time, next chunk id, counters), then the
 // engine's own section (Engine::save_state).  Pending output rows must have
 // been polled (the runtime drains after every push).
+static void save_post(Engine& b, SnapW& w);
 static constexpr uint32_t kSnapMagic = 0x53444853u;   // "SHDS"
 static constexpr uint32_t kSnapVersion = 2;   // 2: + layout hint and start time
 
@@ -929,7 +1120,7 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
     Engine& e = *q->eng;
     if (e.grouped) return fail(SHD_E_UNSUPPORTED, "a grouped query has no state of its own to snapshot");
     SHD_HIP(hipStreamSynchronize(e.stream));
-    if (e.out.count > 0) return fail(SHD_E_ARG, "snapshot with unpolled output rows");
+    if (e.out.count > 0 || q->out_eng().out.count > 0) return fail(SHD_E_ARG, "snapshot with unpolled output rows");
     SnapW w;
     w.s = e.stream;
     w.put<uint32_t>(kSnapMagic);
@@ -943,6 +1134,7 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
     w.put<int64_t>(e.chunk_seq);
     w.put<shd_counters>(e.counters);
     e.save_state(w);
+    if (q->post) save_post(*q->post, w);
     q->snap.swap(w.b);
     *data = q->snap.data();
     *len = q->snap.size();
@@ -950,12 +1142,36 @@ int shd_snapshot(shd_query* q, const void** data, size_t* len) {
   });
 }
 
-// Common fields + engine section of an image, from after the header.
-static void load_image(Engine& e, SnapR& r) {
+// The selector engine of a POST plan (its aggregator tables): common fields
+// + its own section, after the state engine's.
+static void save_post(Engine& b, SnapW& w) {
+  SHD_HIP(hipStreamSynchronize(b.stream));
+  w.s = b.stream;
+  w.put<int64_t>(b.seq);
+  w.put<int64_t>(b.now);
+  w.put<int64_t>(b.chunk_seq);
+  b.save_state(w);
+}
+
+static void load_post(Engine& b, SnapR& r) {
+  b.reset();
+  const int64_t seq = r.get<int64_t>(), now = r.get<int64_t>(), chunk = r.get<int64_t>();
+  r.s = b.stream;
+  b.load_state(r);
+  b.seq = seq;
+  b.now = now;
+  b.chunk_seq = chunk;
+  b.out.count = 0;
+}
+
+// Common fields + engine section of an image, from after the header
+// (post: the query's selector engine, whose section follows).
+static void load_image(Engine& e, SnapR& r, Engine* post = nullptr) {
   e.reset();
   const int64_t seq = r.get<int64_t>(), now = r.get<int64_t>(), chunk = r.get<int64_t>();
   const shd_counters c = r.get<shd_counters>();
   e.load_state(r);
+  if (post) load_post(*post, r);
   if (r.at != r.n) throw Error(SHD_E_ARG, "trailing bytes in snapshot");
   e.seq = seq;
   e.now = now;
@@ -998,7 +1214,7 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
       init_engine(*fresh, cur.plan);
       fresh->start_time = start;
       r.s = fresh->stream;
-      load_image(*fresh, r);
+      load_image(*fresh, r, q->post.get());
       q->eng = std::move(fresh);
       return SHD_OK;
     }
@@ -1011,15 +1227,16 @@ int shd_restore(shd_query* q, const void* data, size_t len) {
     bk.put<int64_t>(cur.chunk_seq);
     bk.put<shd_counters>(cur.counters);
     cur.save_state(bk);
+    if (q->post) save_post(*q->post, bk);
     try {
-      load_image(cur, r);
+      load_image(cur, r, q->post.get());
       cur.start_time = start;
     } catch (...) {
       SnapR br;
       br.p = bk.b.data();
       br.n = bk.b.size();
       br.s = cur.stream;
-      load_image(cur, br);
+      load_image(cur, br, q->post.get());
       throw;
     }
     return SHD_OK;
@@ -1048,8 +1265,10 @@ int shd_group_create(shd_ctx* ctx, const void* leader_ir, size_t len, shd_query*
     if (rc != SHD_OK) return rc;
     std::unique_ptr<shd_query> own(lq);
     std::vector<Engine*> es;
+    if (lq->post) return fail(SHD_E_UNSUPPORTED, "a query with an aggregating / having selector cannot lead a group");
     for (int i = 0; i < n; i++) {
       if (!members[i]) return fail(SHD_E_ARG, "null member");
+      if (members[i]->post) return fail(SHD_E_UNSUPPORTED, "group member with an aggregating / having selector");
       if (members[i]->ctx->device != ctx->device) return fail(SHD_E_ARG, "group member on another device");
       SHD_HIP(hipStreamSynchronize(members[i]->eng->stream));
       es.push_back(members[i]->eng.get());

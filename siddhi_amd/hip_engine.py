@@ -14,7 +14,7 @@ from typing import List
 import numpy as np
 
 from . import planner as pl
-from .runtime import OutputChunk, split_chunks
+from .runtime import OutputChunk, decode_lists, list_columns, split_chunks
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SHD_LIB") or os.path.join(_HERE, "libsiddhi_hip.so")
@@ -48,7 +48,8 @@ class ShdBatch(ctypes.Structure):
 class ShdOut(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int64), ("n_cols", ctypes.c_int32), ("chunk", ctypes.c_void_p),
                 ("type", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("values", ctypes.c_void_p),
-                ("nulls", ctypes.c_void_p), ("in_seq", ctypes.c_void_p), ("state_idx", ctypes.c_void_p)]
+                ("nulls", ctypes.c_void_p), ("in_seq", ctypes.c_void_p), ("state_idx", ctypes.c_void_p),
+                ("n_list", ctypes.c_int64), ("list_values", ctypes.c_void_p), ("list_nulls", ctypes.c_void_p)]
 
 
 class ShdCounters(ctypes.Structure):
@@ -221,6 +222,14 @@ class DeviceQuery:
         # shd_out.state_idx: state id of the emitting processor, per row
         self.last_state_idx = np.ctypeslib.as_array(ctypes.cast(o.state_idx, ctypes.POINTER(ctypes.c_int32)),
                                                     (n,)).copy()
+        nl = o.n_list
+        # list arena of OBJECT columns (shd_out.list_values / list_nulls)
+        if nl > 0:
+            self.last_lists = (
+                np.ctypeslib.as_array(ctypes.cast(o.list_values, ctypes.POINTER(ctypes.c_uint64)), (nl,)).copy(),
+                np.ctypeslib.as_array(ctypes.cast(o.list_nulls, ctypes.POINTER(ctypes.c_uint8)), (nl,)).copy())
+        else:
+            self.last_lists = (np.zeros(0, np.uint64), np.zeros(0, np.uint8))
         typ = np.ctypeslib.as_array(ctypes.cast(o.type, ctypes.POINTER(ctypes.c_int32)), (n,)).copy()
         ts = np.ctypeslib.as_array(ctypes.cast(o.ts, ctypes.POINTER(ctypes.c_int64)), (n,)).copy()
         if nc > 0:
@@ -347,7 +356,9 @@ class HipQueryEngine:
         r = self.dq.poll()
         if r is None:
             return []
-        return split_chunks(*r)
+        lcols = list_columns(self.qp)
+        objs = decode_lists(r[3], lcols, *self.dq.last_lists) if lcols else None
+        return split_chunks(*r, objs)
 
     def start(self, t):
         """SiddhiAppRuntime.start() at app time t (shd_set_option "start_time")."""

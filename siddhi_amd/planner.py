@@ -26,14 +26,17 @@ from . import query_compiler as qc
 
 # ---- IR constants (mirror include/siddhi_ir.h) -----------------------------
 MAGIC, VERSION = 0x50444853, 1
+POST_MAGIC = 0x54534F50
 KIND_STATE, KIND_SINGLE = 1, 2
 T_STRING, T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL = 0, 1, 2, 3, 4, 5
+T_OBJECT = 6   # output only: a list over a count state's chain (include/siddhi_ir.h SHD_T_OBJECT)
 TYPE_CODE = {"string": T_STRING, "int": T_INT, "long": T_LONG, "float": T_FLOAT,
              "double": T_DOUBLE, "bool": T_BOOL}
 TYPE_NAME = {v: k for k, v in TYPE_CODE.items()}
+TYPE_NAME[T_OBJECT] = "object"
 (OP_END, OP_CONST, OP_NULL, OP_LOAD, OP_EVNULL, OP_CVT, OP_ADD, OP_SUB, OP_MUL,
  OP_DIV, OP_MOD, OP_EQ, OP_NE, OP_GT, OP_GE, OP_LT, OP_LE, OP_AND, OP_OR, OP_NOT,
- OP_ISNULL, OP_AGG, OP_TS) = range(23)
+ OP_ISNULL, OP_AGG, OP_TS, OP_IFELSE, OP_MULTI) = range(25)
 IDX_CURRENT, IDX_LAST = -1, -2
 NODE_STREAM, NODE_NEXT, NODE_EVERY, NODE_LOGICAL, NODE_COUNT = 1, 2, 3, 4, 5
 H_FILTER, H_WINDOW = 1, 2
@@ -122,6 +125,9 @@ class Plan:
     # String.valueOf(null), C/query/selector/GroupByKeyGenerator.java:63-73);
     # -1 when no group-by attribute is a string.  Optional trailing IR words.
     null_str_id: int = -1
+    # STATE plans with an aggregating / `having` selector: (base outputs
+    # [(type, expr)], nested SINGLE plan) -- the IR's POST section
+    post: Optional[Tuple[List[Tuple[int, int]], "Plan"]] = None
     target: str = ""
     # descriptive (host/runtime only)
     states: List[Meta] = field(default_factory=list)
@@ -166,6 +172,14 @@ class Plan:
         for _, t, e in self.outputs:
             w.extend([t, e])
         w.extend(_split64(self.null_str_id))
+        if self.post is not None:
+            base, sub = self.post
+            sw = sub.to_words()
+            w.extend([POST_MAGIC, len(base)])
+            for t, e in base:
+                w.extend([t, e])
+            w.append(len(sw))
+            w.extend(sw)
         return w
 
     def to_bytes(self) -> bytes:
@@ -207,12 +221,15 @@ class ExprCompiler:
         self.metas = metas
         self.state_query = state_query
         self.agg_allowed = False
+        self.multi_top = None
 
     def compile(self, expr, current_state: int, default_index: int, want_bool=False,
-                allow_agg=False) -> Tuple[int, int]:
-        """Returns (expr id, result type)."""
+                allow_agg=False, allow_multi=False) -> Tuple[int, int]:
+        """Returns (expr id, result type).  allow_multi: a selector output that
+        is one variable may be a multi-value selection (SHD_OP_MULTI)."""
         code: List[Tuple[int, int, int, int]] = []
         self.agg_allowed = allow_agg
+        self.multi_top = expr if allow_multi and isinstance(expr, qc.Var) else None
         t = self._emit(expr, code, current_state, default_index)
         if want_bool and t != T_BOOL:
             raise SiddhiAppValidationException("condition must be of type BOOL but found %s" % TYPE_NAME.get(t))
@@ -328,6 +345,39 @@ class ExprCompiler:
             if e.namespace is None and name == "eventtimestamp" and not e.args:
                 code.append((OP_TS, 0, IDX_CURRENT, 0))
                 return T_LONG
+            if e.namespace is None and name == "ifthenelse":
+                # IfThenElseFunctionExecutor (C/executor/function/IfThenElseFunctionExecutor.java):
+                # all three arguments are evaluated, a true condition picks the
+                # second, anything else (false, null) the third
+                if len(e.args) != 3:
+                    raise SiddhiAppValidationException("Invalid no of arguments passed to ifThenElse() function, "
+                                                       "required only 3, but found %d" % len(e.args))
+                if self._emit(e.args[0], code, cs, di) != T_BOOL:
+                    raise SiddhiAppValidationException("Input type of if in ifThenElse function should be of "
+                                                       "type BOOL")
+                t1 = self._emit(e.args[1], code, cs, di)
+                t2 = self._emit(e.args[2], code, cs, di)
+                if t1 != t2:
+                    raise SiddhiAppValidationException("Input type of then in ifThenElse function and else in "
+                                                       "ifThenElse function should be of equivalent type")
+                code.append((OP_IFELSE, t1, 0, 0))
+                return t1
+            if e.namespace is None and name in _INSTANCE_OF:
+                # InstanceOf*FunctionExecutor (C/executor/function/InstanceOf*.java):
+                # `data instanceof X`; an attribute's value is boxed as its
+                # declared type, so the test is "non-null" for that type and
+                # false for every other
+                if len(e.args) != 1:
+                    raise SiddhiAppValidationException("Invalid no of arguments passed to %s() function" % e.name)
+                scratch: List[Tuple[int, int, int, int]] = []
+                t = self._emit(e.args[0], scratch, cs, di)
+                if t == _INSTANCE_OF[name]:
+                    code.extend(scratch)
+                    code.append((OP_ISNULL, 0, 0, 0))
+                    code.append((OP_NOT, 0, 0, 0))
+                else:
+                    code.append((OP_CONST, self._const(T_BOOL, False), T_BOOL, 0))
+                return T_BOOL
             raise UnsupportedPlanException("function %s is outside the hot path" % e.name)
         raise SiddhiAppValidationException("unsupported expression %r" % (e,))
 
@@ -393,8 +443,15 @@ class ExprCompiler:
                             and v.index <= qc.LAST and v.stream == self.metas[cs].ref:
                         ci = v.index
                     elif cs == UNKNOWN_STATE and v.index is None and m.multi:
-                        raise UnsupportedPlanException(
-                            "multi-value selection of count state '%s' without index" % v.stream)
+                        # ExpressionParser.parseVariable (:1386-1388, :1430-1437): a count
+                        # state's attribute without an index in the selector is the
+                        # MultiValueVariableFunctionExecutor -- a List of the attribute
+                        # over the whole chain (type OBJECT)
+                        if self.multi_top is not v:
+                            raise UnsupportedPlanException(
+                                "multi-value selection of count state '%s' inside an expression" % v.stream)
+                        code.append((OP_MULTI, i, 0, f[0] | (f[1] << 16)))
+                        return T_OBJECT
                     break
         if state is None:
             if v.stream is None:
@@ -490,7 +547,7 @@ def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta],
         attrs = sel.attrs
     cs = UNKNOWN_STATE if state_query else 0
     for oa in attrs:
-        eid, t = ec.compile(oa.expr, cs, 0, allow_agg=True)
+        eid, t = ec.compile(oa.expr, cs, 0, allow_agg=True, allow_multi=state_query)
         plan.outputs.append((oa.name, t, eid))
         names.append(oa.name)
         types.append(t)
@@ -500,8 +557,6 @@ def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta],
         if gt == T_STRING:
             plan.null_str_id = ec.dict.id("null")
     if sel.having is not None:
-        if state_query:
-            raise UnsupportedPlanException("having over pattern / sequence output is outside the hot path")
         # QuerySelector's having condition is parsed against the selector's
         # output event (SelectorParser.parse, C/util/parser/SelectorParser.java:
         # havingConditionExecutor over the output attributes): an attribute name
@@ -513,6 +568,93 @@ def _plan_selector(plan: Plan, q: qc.Query, ec: ExprCompiler, metas: List[Meta],
             raise SiddhiAppValidationException("having condition must be of type BOOL")
         plan.having = eid
     return names, types
+
+
+_AGG_FUNCS = ("sum", "avg", "count")
+_INSTANCE_OF = {"instanceofboolean": T_BOOL, "instanceofdouble": T_DOUBLE, "instanceoffloat": T_FLOAT,
+                "instanceofinteger": T_INT, "instanceoflong": T_LONG, "instanceofstring": T_STRING}
+
+
+def _has_agg(e) -> bool:
+    if isinstance(e, qc.Func):
+        if e.namespace is None and e.name.lower() in _AGG_FUNCS:
+            return True
+        return any(_has_agg(a) for a in e.args)
+    if isinstance(e, qc.BinOp):
+        return _has_agg(e.left) or _has_agg(e.right)
+    if isinstance(e, (qc.Not, qc.IsNull)):
+        return _has_agg(e.expr)
+    return False
+
+
+def _reads_event(e) -> bool:
+    """Whether an expression reads the StateEvent (a variable, a stream
+    reference or eventTimestamp())."""
+    if isinstance(e, (qc.Var, qc.StreamRef)):
+        return True
+    if isinstance(e, qc.Func):
+        if e.namespace is None and e.name.lower() == "eventtimestamp":
+            return True
+        return any(_reads_event(a) for a in e.args)
+    if isinstance(e, qc.BinOp):
+        return _reads_event(e.left) or _reads_event(e.right)
+    if isinstance(e, (qc.Not, qc.IsNull)):
+        return _reads_event(e.expr)
+    return False
+
+
+def _lift_bases(e, bases: Dict[str, Tuple[int, object]]):
+    """The selector AST with every maximal aggregator-free subtree that reads
+    the StateEvent replaced by a base attribute `_b<k>` (bases: repr -> (k, subtree))."""
+    if not _has_agg(e):
+        if not _reads_event(e):
+            return e
+        k = bases.setdefault(repr(e), (len(bases), e))[0]
+        return qc.Var("_b%d" % k)
+    if isinstance(e, qc.Func):
+        return qc.Func(e.name, [_lift_bases(a, bases) for a in e.args], e.namespace)
+    if isinstance(e, qc.BinOp):
+        return qc.BinOp(e.op, _lift_bases(e.left, bases), _lift_bases(e.right, bases))
+    if isinstance(e, qc.Not):
+        return qc.Not(_lift_bases(e.expr, bases))
+    if isinstance(e, qc.IsNull):
+        return qc.IsNull(_lift_bases(e.expr, bases))
+    return e
+
+
+def _plan_post_selector(app, q: qc.Query, ec: ExprCompiler, metas: List[Meta], dictionary):
+    """Device decomposition of a state query's aggregating / `having`
+    selector (include/siddhi_ir.h POST section).  The reference runs
+    QuerySelector on a chunk of ONE StateEvent (StateMultiProcessStreamReceiver.
+    processAndClear, C/query/input/StateMultiProcessStreamReceiver.java:47-68;
+    SingleProcessStreamReceiver.java:48-72), so processInBatchNoGroupBy /
+    processInBatchGroupBy (QuerySelector.java:271-373) emit that event whenever
+    `having` passes, with the aggregators folded over every earlier match in
+    emission order.  The state variables the selector reads become base
+    outputs of the state plan; the same selector over a stream of those base
+    values is a SINGLE plan (one InputHandler call per match row)."""
+    sel = q.selector
+    if sel.select_all:
+        attrs = [qc.OutAttr(qc.Var(n, m.ref or m.stream, None), n) for m in metas for (n, _) in m.attrs]
+    else:
+        attrs = sel.attrs
+    bases: Dict[str, Tuple[int, object]] = {}
+    new_attrs = [qc.OutAttr(_lift_bases(oa.expr, bases), oa.name) for oa in attrs]
+    new_group = [_lift_bases(g, bases) for g in sel.group_by]
+    new_having = None
+    if sel.having is not None:
+        new_having = _lift_bases(_subst_outputs(sel.having, {oa.name: oa.expr for oa in attrs}), bases)
+    base_out: List[Tuple[int, int]] = []
+    base_attrs = []
+    for key, (k, node) in sorted(bases.items(), key=lambda kv: kv[1][0]):
+        eid, t = ec.compile(node, UNKNOWN_STATE, 0)
+        base_out.append((t, eid))
+        base_attrs.append(("_b%d" % k, TYPE_NAME[t]))
+    sd = qc.StreamDef("_post", base_attrs)
+    q2 = qc.Query(q.name, qc.SingleInput("_post", []),
+                  qc.Selector(False, new_attrs, new_group, new_having), q.target, q.event_type)
+    sub = _plan_single(app, q2, dictionary, None, {"_post": sd})
+    return base_out, sub.plan
 
 
 def _subst_outputs(e, outs):
@@ -581,8 +723,11 @@ def _plan_state(app, q, dictionary, partition, extra_streams) -> QueryPlan:
     plan.n_states = len(metas)
     plan.states = metas
     names, types = _plan_selector(plan, q, ec, metas, True)
-    if plan.aggs or plan.group_by:
-        raise UnsupportedPlanException("aggregation over pattern output is outside the round-1 hot path")
+    if plan.aggs or plan.group_by or plan.having >= 0:
+        if partition is not None and (plan.aggs or plan.group_by):
+            raise UnsupportedPlanException("aggregation over partitioned pattern / sequence output "
+                                           "(aggregator state per partition key) is outside the hot path")
+        plan.post = _plan_post_selector(app, q, ec, metas, dictionary)
     _plan_partition(plan, None, partition, streams, app, dictionary, extra_streams)
     plan.target = q.target
     plan.shape = classify_state_shape(plan, si)
@@ -678,6 +823,9 @@ def share_signature(q: qc.Query) -> Optional[str]:
     query name, annotations and the insert target."""
     if q.output_rate is not None:
         return None
+    sel = q.selector
+    if sel.group_by or sel.having is not None or any(_has_agg(oa.expr) for oa in sel.attrs):
+        return None   # aggregating / having selectors run per query (IR POST section)
     import copy
     if _e1_site(q) is not None:
         q2 = copy.deepcopy(q)

@@ -153,16 +153,43 @@ def decode_value(bits: int, t: int, dictionary):
 class OutputChunk:
     """One callback invocation worth of output rows (ComplexEventChunk)."""
 
-    __slots__ = ("types", "ts", "values", "nulls")
+    __slots__ = ("types", "ts", "values", "nulls", "objects")
 
-    def __init__(self, types, ts, values, nulls):
+    def __init__(self, types, ts, values, nulls, objects=None):
         self.types = types      # np.int32 [n] CURRENT / EXPIRED
         self.ts = ts            # np.int64 [n]
         self.values = values    # np.uint64 [n, n_out] bit patterns
         self.nulls = nulls      # np.uint8 [n, n_out]
+        # OBJECT columns (multi-value selections): col -> per row a list of
+        # (bits, null) element payloads
+        self.objects = objects or {}
 
 
-def split_chunks(chunk_ids, types, ts, vals, nulls) -> List[OutputChunk]:
+def list_columns(qp) -> Dict[int, int]:
+    """Output columns of type OBJECT (multi-value selections of a count
+    state, include/siddhi_ir.h SHD_OP_MULTI) -> their element type."""
+    out = {}
+    for k, (_, t, e) in enumerate(qp.plan.outputs):
+        if t == pl.T_OBJECT:
+            out[k] = qp.plan.exprs[e][0][3] >> 16
+    return out
+
+
+def decode_lists(vals, cols, lvals, lnul) -> Dict[int, list]:
+    """Per OBJECT column, per row: the list its handle (offset | count << 40)
+    addresses in the list arena, as (bits, null) pairs."""
+    out = {}
+    for k in cols:
+        rows = []
+        for h in vals[:, k]:
+            h = int(h)
+            off, cnt = h & ((1 << 40) - 1), h >> 40
+            rows.append([(int(lvals[off + j]), bool(lnul[off + j])) for j in range(cnt)])
+        out[k] = rows
+    return out
+
+
+def split_chunks(chunk_ids, types, ts, vals, nulls, objects=None) -> List[OutputChunk]:
     out = []
     n = len(chunk_ids)
     if n == 0:
@@ -170,7 +197,8 @@ def split_chunks(chunk_ids, types, ts, vals, nulls) -> List[OutputChunk]:
     starts = np.flatnonzero(np.r_[True, chunk_ids[1:] != chunk_ids[:-1]])
     ends = np.r_[starts[1:], n]
     for s, e in zip(starts, ends):
-        out.append(OutputChunk(types[s:e], ts[s:e], vals[s:e], nulls[s:e]))
+        obj = {k: v[s:e] for k, v in objects.items()} if objects else None
+        out.append(OutputChunk(types[s:e], ts[s:e], vals[s:e], nulls[s:e], obj))
     return out
 
 
@@ -475,18 +503,24 @@ class SiddhiAppRuntime:
                 else:
                     v = batch.cols[a][i]
                     data.append(self.dictionary.lookup(int(v)) if t == pl.T_STRING else
-                                bool(v) if t == pl.T_BOOL else v.item())
+                                bool(v) if t == pl.T_BOOL else v if t == pl.T_OBJECT else v.item())
             evs.append(Event(int(batch.ts[i]), data))
         return evs
+
+    def _list_value(self, elems, et):
+        """A multi-value cell: the List MultiValueVariableFunctionExecutor returns."""
+        return [None if z else decode_value(b, et, self.dictionary) for b, z in elems]
 
     def _deliver(self, q: _QueryRuntime, chunks: List[OutputChunk]):
         if not chunks:
             return
         types = q.qp.output_types
+        lcols = list_columns(q.qp) if pl.T_OBJECT in types else {}
         for ch in chunks:
             evs = []
             for i in range(len(ch.ts)):
-                data = [None if ch.nulls[i, k] else decode_value(ch.values[i, k], t, self.dictionary)
+                data = [self._list_value(ch.objects[k][i], lcols[k]) if t == pl.T_OBJECT else
+                        None if ch.nulls[i, k] else decode_value(ch.values[i, k], t, self.dictionary)
                         for k, t in enumerate(types)]
                 evs.append(Event(int(ch.ts[i]), data, int(ch.types[i]) == EXPIRED))
             # QueryCallback.receiveStreamEvent (QueryCallback.java:61-91)
@@ -501,6 +535,12 @@ class SiddhiAppRuntime:
             if target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target)):
                 cols, nulls = [], []
                 for k, t in enumerate(types):
+                    if t == pl.T_OBJECT:   # java.util.List values travel as objects
+                        col = np.empty(len(ch.ts), object)
+                        col[:] = [self._list_value(ch.objects[k][i], lcols[k]) for i in range(len(ch.ts))]
+                        cols.append(col)
+                        nulls.append(None)
+                        continue
                     col = np.array([ch.values[i, k] for i in range(len(ch.ts))], np.uint64)
                     cols.append(_bits_to_col(col, t))
                     nm = ch.nulls[:, k].astype(np.uint8)

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 from siddhi_amd import planner as pl
-from siddhi_amd.runtime import OutputChunk, split_chunks
+from siddhi_amd.runtime import OutputChunk, decode_lists, list_columns, split_chunks
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "liboracle.so")
@@ -43,6 +43,9 @@ def load_oracle():
     lib.orc_get_rows.argtypes = [P, P, P, P, P, P]
     lib.orc_clear_rows.argtypes = [P]
     lib.orc_get_rows_seq.argtypes = [P, P]
+    lib.orc_num_list.restype = ctypes.c_int64
+    lib.orc_num_list.argtypes = [P]
+    lib.orc_get_list.argtypes = [P, P, P]
     lib.orc_counters.argtypes = [P, P]
     lib.orc_last_error.restype = ctypes.c_char_p
     _lib = lib
@@ -100,8 +103,16 @@ class OracleQueryEngine:
         sq = np.empty(n, np.int64)
         self.lib.orc_get_rows_seq(self.h, sq.ctypes.data)
         self.drained_seq.append(sq)   # shd_out.in_seq of the drained rows
+        nl = self.lib.orc_num_list(self.h)
+        lv = np.zeros(max(nl, 1), np.uint64)
+        ln = np.zeros(max(nl, 1), np.uint8)
+        if nl:
+            self.lib.orc_get_list(self.h, lv.ctypes.data, ln.ctypes.data)
+        self.last_lists = (lv, ln)
         self.lib.orc_clear_rows(self.h)
-        return split_chunks(chunk, typ, ts, vals[:, :self.n_out], nul[:, :self.n_out])
+        lcols = list_columns(self.qp)
+        objs = decode_lists(vals, lcols, lv, ln) if lcols else None
+        return split_chunks(chunk, typ, ts, vals[:, :self.n_out], nul[:, :self.n_out], objs)
 
     # snapshot / restore for the checker: the oracle's state is a function of
     # its input history, so its "snapshot" is that history (replayed into a
