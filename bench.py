@@ -256,8 +256,9 @@ def parity_prefix(torch, he, qp, cols, ts, offs_all, prefix, ora_rows, window, b
             assert_rows_agg(dev, ora_rows, qp, exact=False)
         else:
             assert_same_rows(dev, ora_rows)
-        return "equal (%d events, %d rows%s)" % (prefix, len(dev[2]), ", doubles within 1e-9" if window else ""), \
-            dq.counters()
+        pushes = -(-prefix // batch)
+        return "equal (%d events in %d pushes of %d, %d rows%s)" % (
+            prefix, pushes, batch, len(dev[2]), ", doubles within 1e-9" if window else ""), dq.counters()
     except AssertionError as e:
         return "DIFFERENT: %s" % str(e).splitlines()[0], dq.counters()
     finally:
@@ -736,18 +737,9 @@ def main():
                       file=sys.stderr, flush=True)
 
         # SURVEY.md §8d algorithmic bytes need the reference's pending-scan counts
-        # (P-bar: (partial, event) pairs its pending lists visit).  The sort path's
-        # walks count exactly those; the bucketed walk skips expiry visits beyond its
-        # `within` lookahead, so the counts come from one untimed step on the sort path.
-        calib = None
-        if pattern:
-            prev = os.environ.get("SHD_NO_BUCKET")
-            os.environ["SHD_NO_BUCKET"] = "1"
-            calib = run_step()
-            if prev is None:
-                del os.environ["SHD_NO_BUCKET"]
-            else:
-                os.environ["SHD_NO_BUCKET"] = prev
+        # (P-bar: (partial, event) pairs its pending lists visit): the walks count
+        # exactly those, taken from one untimed calibration step.
+        calib = run_step() if pattern else None
         for _ in range(args.warmup):
             run_step()
         torch.cuda.synchronize()
@@ -831,12 +823,15 @@ def main():
     prefix = None
     derived_check = None
     if rank == 0 and world == 1 and args.cpu_sample != 0:
-        sample = args.cpu_sample if args.cpu_sample > 0 else (2_000_000 if pattern else 1_000_000)
+        sample = args.cpu_sample if args.cpu_sample > 0 else (4_000_000 if pattern else 2_000_000)
         sample = min(sample, n)
         cpu, ora_rows, _, oc = cpu_baseline(args.config, app, keys, delta, sample)
         if mode == "prepartitioned" and kb == 0:
+            # at least two pushes: the prefix cut like the timed stream is, in
+            # micro-batches, so the state carried between pushes is compared
+            # (at most half the prefix per push)
             prefix, pc = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, sample, ora_rows,
-                                       not pattern, min(batch, sample))
+                                       not pattern, max(1, min(batch, sample // 2)))
             if args.config in ("P1", "P3", "P3-dense"):
                 # the §8d counts two ways on the same prefix: the device's walks
                 # ((partial, event) pairs visited, the expiring visit included) and

@@ -131,7 +131,6 @@ typedef struct shd_counters {
                                    grouping (hashed buckets when below the key
                                    width), 0 when not partitioned              */
   int64_t kernel_ns_total;      /* device time of every push since load / reset  */
-  int64_t dormant;              /* reserved (0): every open partial is carried   */
 } shd_counters;
 
 int shd_device_count(int* n);

@@ -121,6 +121,13 @@ struct NeedNfa : Error {
   explicit NeedNfa(const std::string& m) : Error(SHD_E_UNSUPPORTED, m) {}
 };
 
+// Thrown by a query group's leader whose shared pass cannot take a push (a
+// window group's operand range or call shape): shd_group_push dissolves the
+// group (Engine::group_dissolve) and each member takes the push alone.
+struct NeedDissolve : NeedNfa {
+  explicit NeedDissolve(const std::string& m) : NeedNfa(m) {}
+};
+
 // Host image of a query's open partial matches as the events whose replay
 // rebuilds them, in arrival order: one part per run of same-stream events
 // (typed columns as in shd_batch).  skip_start[i] = 1: event i is replayed
@@ -208,6 +215,8 @@ struct Engine {
     throw Error(SHD_E_UNSUPPORTED, "this query's engine cannot lead a query group");
   }
   virtual void group_detach() {}
+  // leader: hand each member the state it would hold running alone, detach
+  virtual void group_dissolve() { throw Error(SHD_E_UNSUPPORTED, "this group cannot dissolve"); }
 
   // Kernel argument blocks (column tables, expression handles) are placed in
   // device memory and kernels receive a pointer: the kernels index column

@@ -38,6 +38,31 @@ constexpr int64_t kMaxDenseKey = (int64_t)1 << 26;
 // segmented scans only while every operand seen so far is finite and the
 // non-zero magnitudes span at most 2^kSegMaxExpSpan (k_operand_stats)
 constexpr uint32_t kSegMaxExpSpan = 30;
+// ... and all of one sign: a window of mixed signs can cancel to far below its
+// operands, where the reference's running sum keeps its rounding history
+// (a difference of prefix sums does not bound that within 1e-9)
+constexpr uint32_t kOpNeg = 2u, kOpPos = 4u;
+
+// One aggregated operand into the range guard's statistics: flags (1 non-
+// finite, kOpNeg, kOpPos) and the binary exponent range of the non-zero
+// magnitudes.  int operands are skipped: their double running sums are exact
+// (every partial sum is an integer below 2^53) in the reference and in the scans.
+__device__ __forceinline__ void guard_operand(uint64_t b, int type, uint32_t& nf, uint32_t& emax, uint32_t& emin) {
+  double d;
+  if (type == SHD_T_INT) return;
+  if (type == SHD_T_FLOAT) d = (double)__uint_as_float((uint32_t)b);
+  else if (type == SHD_T_LONG) d = (double)(int64_t)b;
+  else d = __longlong_as_double((long long)b);
+  if (!(d - d == 0.0)) {   // Inf or NaN
+    nf |= 1u;
+    return;
+  }
+  if (d == 0.0) return;
+  nf |= d < 0.0 ? kOpNeg : kOpPos;
+  const uint32_t e = (uint32_t)((__double_as_longlong(d) >> 52) & 0x7FF);
+  emax = e > emax ? e : emax;
+  emin = e < emin ? e : emin;
+}
 constexpr int kMaxChan = 4;                   // distinct aggregated expressions (segmented scans)
 
 struct RowCtx {
@@ -323,8 +348,8 @@ struct FusedArgs {
   unsigned long long* kmax_out;
   int nch;              // range guard channels (0: none)
   int ch_agg[kMaxChan];
-  int ch_f32[kMaxChan];
-  uint32_t* opstats;    // [3]: non-finite flag, max / min binary exponent
+  int ch_t[kMaxChan];   // operand type of each channel
+  uint32_t* opstats;    // [3]: flags (1 non-finite, kOpNeg, kOpPos), max / min binary exponent
   int probe;            // timing experiments (SHD_FI_PROBE): 1 = no look-back wait, 2 = no item writes
 };
 
@@ -408,16 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __rest
         for (int ch = 0; ch < a.nch; ch++) {
           const int g = a.ch_agg[ch];
           if (a.iargn[(int64_t)g * a.cap + t]) continue;
-          const uint64_t b = a.iargv[(int64_t)g * a.cap + t];
-          const double d = a.ch_f32[ch] ? (double)__uint_as_float((uint32_t)b) : __longlong_as_double((long long)b);
-          if (!(d - d == 0.0)) {   // Inf or NaN
-            nf = 1;
-            continue;
-          }
-          if (d == 0.0) continue;
-          const uint32_t e = (uint32_t)((__double_as_longlong(d) >> 52) & 0x7FF);
-          emax = e > emax ? e : emax;
-          emin = e < emin ? e : emin;
+          guard_operand(a.iargv[(int64_t)g * a.cap + t], a.ch_t[ch], nf, emax, emin);
         }
       }
     }
@@ -436,8 +452,8 @@ __global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __rest
   if (lane == 0) {
     if (kmax > cw_status_load((const uint64_t*)a.kmax_out)) atomicMax(a.kmax_out, (unsigned long long)kmax);
     if (a.nch) {
-      if (nf && !__hip_atomic_load(&a.opstats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicOr(&a.opstats[0], 1u);
+      if (nf & ~__hip_atomic_load(&a.opstats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(&a.opstats[0], nf);
       if (emax > __hip_atomic_load(&a.opstats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicMax(&a.opstats[1], emax);
       if (emin < __hip_atomic_load(&a.opstats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
@@ -458,20 +474,11 @@ __global__ __launch_bounds__(kBlock) void k_operand_stats(const uint64_t* argv, 
   uint32_t nf = 0, emax = 0, emin = 0xFFFFFFFFu;
   for (int c = 0; c < nch; c++) {
     const int g = ch_agg[c];
-    const bool f32 = ch_type[c] == SHD_T_FLOAT;
+    const int type = ch_type[c];
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
       const int64_t t = C + i;
       if (argn[(int64_t)g * cap + t]) continue;
-      const uint64_t b = argv[(int64_t)g * cap + t];
-      const double d = f32 ? (double)__uint_as_float((uint32_t)b) : __longlong_as_double((long long)b);
-      if (!(d - d == 0.0)) {   // Inf or NaN
-        nf = 1;
-        continue;
-      }
-      if (d == 0.0) continue;
-      const uint32_t e = (uint32_t)((__double_as_longlong(d) >> 52) & 0x7FF);
-      emax = e > emax ? e : emax;
-      emin = e < emin ? e : emin;
+      guard_operand(argv[(int64_t)g * cap + t], type, nf, emax, emin);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -494,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_operand_stats(const uint64_t* argv, 
       emax = sh[1][k] > emax ? sh[1][k] : emax;
       emin = sh[2][k] < emin ? sh[2][k] : emin;
     }
-    if (nf) atomicOr(&flags[0], 1u);
+    if (nf) atomicOr(&flags[0], nf);
     atomicMax(&flags[1], emax);
     atomicMin(&flags[2], emin);
   }
@@ -2625,6 +2632,7 @@ struct SingleEngine : Engine {
   // running operand statistics of every push since reset (k_operand_stats):
   // the window can hold items of earlier pushes, so the span covers them all
   uint32_t op_emax = 0, op_emin = 0xFFFFFFFFu;
+  uint32_t op_signs = 0;     // kOpNeg / kOpPos of every operand since reset
   bool seg_pref = true;      // the mode asked for (option / default), restored by reset()
   DevBuf d_chmeta;
   PinnedBuf h_chmeta;
@@ -2666,6 +2674,7 @@ struct SingleEngine : Engine {
     seg_unsafe = false;
     op_emax = 0;
     op_emin = 0xFFFFFFFFu;
+    op_signs = 0;
     seg_mode = seg_ok && seg_pref;
   }
 
@@ -2698,6 +2707,7 @@ struct SingleEngine : Engine {
     w.put<int32_t>(seg_unsafe ? 1 : 0);
     w.put<uint32_t>(op_emax);
     w.put<uint32_t>(op_emin);
+    w.put<uint32_t>(op_signs);
     // group dictionary (dictionary-mode group keys)
     gd.save(w);
   }
@@ -2733,6 +2743,7 @@ struct SingleEngine : Engine {
     seg_unsafe = r.get<int32_t>() != 0;
     op_emax = r.get<uint32_t>();
     op_emin = r.get<uint32_t>();
+    op_signs = r.get<uint32_t>();
     seg_mode = seg_ok && seg_pref && !seg_unsafe;
     gd.nk = std::max(ngk, 1);
     gd.load(r, stream);
@@ -2795,6 +2806,57 @@ struct SingleEngine : Engine {
     for (SingleEngine* m : wmembers) m->grouped = false;
     wmembers.clear();
     grouped = false;
+  }
+
+  // The leader hands its window over: every member's state becomes the one it
+  // would hold running alone -- its length window is the last `wparam` of the
+  // leader's carried items (filter passed, same group ids and operands), its
+  // group tables are already current (k_cw_gtables after every push), the
+  // group dictionary is the leader's, and the operand statistics carry the
+  // range guard over.  The members leave the group.
+  void group_dissolve() override {
+    SHD_HIP(hipStreamSynchronize(stream));
+    for (SingleEngine* m : wmembers) m->adopt_window(*this);
+    group_detach();
+  }
+
+  void adopt_window(SingleEngine& L) {
+    SHD_HIP(hipStreamSynchronize(stream));
+    hipStream_t s = stream;
+    const int64_t k = std::min<int64_t>(L.C, wparam);
+    const int64_t from = L.C - k;
+    cur = 0;
+    if (k > 0) {
+      ensure_items(0, k);
+      SHD_HIP(hipMemcpyAsync(ikey[0].p, L.ikey[L.cur].as<uint64_t>() + from, k * 8, hipMemcpyDeviceToDevice, s));
+      SHD_HIP(hipMemcpyAsync(its[0].p, L.its[L.cur].as<int64_t>() + from, k * 8, hipMemcpyDeviceToDevice, s));
+      for (int g = 0; g < nagg; g++) {
+        SHD_HIP(hipMemcpyAsync(iargv[0].as<uint64_t>() + g * icap[0], L.iargv[L.cur].as<uint64_t>() + g * L.icap[L.cur] +
+                               from, k * 8, hipMemcpyDeviceToDevice, s));
+        SHD_HIP(hipMemcpyAsync(iargn[0].as<uint8_t>() + g * icap[0], L.iargn[L.cur].as<uint8_t>() + g * L.icap[L.cur] +
+                               from, k, hipMemcpyDeviceToDevice, s));
+      }
+    }
+    C = k;
+    if (!gdense) {   // hashed group ids: the leader's dictionary assigned them
+      SnapW w;
+      w.s = L.stream;
+      L.gd.save(w);
+      SnapR r;
+      r.p = w.b.data();
+      r.n = w.b.size();
+      r.s = s;
+      gd.nk = std::max(ngk, 1);
+      gd.load(r, s);
+    }
+    op_emax = L.op_emax;
+    op_emin = L.op_emin;
+    op_signs = L.op_signs;
+    seg_unsafe = L.seg_unsafe;
+    seg_mode = seg_ok && seg_pref && !seg_unsafe;
+    kmax_known = false;
+    counters.carry = C;
+    SHD_HIP(hipStreamSynchronize(s));
   }
 
   std::vector<int64_t> h_offs;   // lives until the next push (async H2D source)
@@ -3618,7 +3680,7 @@ struct SingleEngine : Engine {
     fu.nch = seg_mode ? nch : 0;
     for (int c = 0; c < nch; c++) {
       fu.ch_agg[c] = ch_agg[c];
-      fu.ch_f32[c] = ch_type[c] == SHD_T_FLOAT;
+      fu.ch_t[c] = ch_type[c];
     }
     fu.opstats = (uint32_t*)(d_tot.as<uint64_t>() + 5);
     fu.probe = getenv("SHD_FI_PROBE") ? atoi(getenv("SHD_FI_PROBE")) : 0;
@@ -3731,15 +3793,18 @@ struct SingleEngine : Engine {
       // (SumAttributeAggregatorExecutor.java:184-198).  With a non-finite
       // operand the reference's sum stays Inf / NaN for good (Inf - Inf), and
       // over a wide magnitude range its rounding history shows in the result
-      // (1e20 + 1 - 1e20 = 0): from the first such push on, this query keeps the
+      // (1e20 + 1 - 1e20 = 0), as it does when operands of both signs cancel
+      // (1e6 + 1e-3 - 1e6): from the first such push on, this query keeps the
       // bit-exact sequential fold (the group tables carry over).
-      // the span is over every operand since reset (window items of earlier
-      // pushes included), not just this push's
+      // the span and the signs are over every operand since reset (window
+      // items of earlier pushes included), not just this push's
       const uint32_t* fl = h_tot.as<uint32_t>() + 10;
       op_emax = std::max(op_emax, fl[1]);
       op_emin = std::min(op_emin, fl[2]);
+      op_signs |= fl[0] & (kOpNeg | kOpPos);
       const bool wide = op_emin != 0xFFFFFFFFu && op_emax > op_emin + kSegMaxExpSpan;
-      if (fl[0] || wide) {
+      const bool mixed = (op_signs & (kOpNeg | kOpPos)) == (kOpNeg | kOpPos);
+      if ((fl[0] & 1u) || wide || mixed) {
         seg_mode = false;
         seg_unsafe = true;
       }
@@ -3749,12 +3814,16 @@ struct SingleEngine : Engine {
     ensure_groups((int64_t)kmax + 1);
     const int64_t nops = m + X;
     if (!wmembers.empty()) {   // a window group's leader: its members' rows from these items, no rows of its own
+      // the shared call-window pass needs the segmented scans' operand range
+      // and the call-window shape; otherwise the group dissolves before this
+      // push changes anything the members read: each member takes its window
+      // (a suffix of the carried items) and runs this push and every later
+      // one alone (shd_group_push, group_dissolve)
       if (!seg_mode)
-        throw Error(SHD_E_UNSUPPORTED, "query group: an operand outside the segmented scans' range (non-finite, "
-                                       "or magnitudes spanning more than 2^30): run these queries alone");
+        throw NeedDissolve("query group: an operand outside the segmented scans' range (non-finite, magnitudes "
+                           "spanning more than 2^30, or of both signs)");
       if (!(cw_cand && cw_call <= (uint32_t)kCwCall && cw_region <= (uint32_t)kCwRegionMax))
-        throw Error(SHD_E_UNSUPPORTED, "query group: a call above 1024 events or a window beyond the call-window "
-                                       "path: run these queries alone");
+        throw NeedDissolve("query group: a call above 1024 events or a window beyond the call-window path");
       // direct-mapped group ids: one rows kernel for all members (they share
       // the calls' row counts); hashed ids: a launch per member
       const bool multi = kmax < (uint64_t)kCwDirectG && !getenv("SHD_CW_HASH") && !getenv("SHD_CW_NO_MULTI") &&

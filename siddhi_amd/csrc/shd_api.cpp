@@ -1285,17 +1285,31 @@ int shd_group_create(shd_ctx* ctx, const void* leader_ir, size_t len, shd_query*
 int shd_group_push(shd_group* g, const shd_batch* b) {
   return guarded([&]() -> int {
     if (!g || !b) return fail(SHD_E_ARG, "null argument");
-    if (g->dissolved) {
+    // dissolved: every member alone; members stay marked grouped (shd_push /
+    // shd_plan_free refuse them) until shd_group_free
+    auto push_members = [&]() -> int {
       for (shd_query* q : g->members) {
         int rc = push_batch(q, b, [&](const Staged& st, const shd_counters& before, const NeedNfa& nf) {
           switch_to_nfa(q, st, before, nf.what());
         });
+        q->eng->grouped = true;
         if (rc != SHD_OK) return rc;
       }
       return SHD_OK;
-    }
+    };
+    if (g->dissolved) return push_members();
     shd_query* lq = g->leader;
     return push_batch(lq, b, [&](const Staged& st, const shd_counters&, const NeedNfa& nf) {
+      if (dynamic_cast<const NeedDissolve*>(&nf)) {
+        // window group: members adopt the leader's window, then take this
+        // push (and all later ones) alone
+        lq->eng->group_dissolve();
+        g->dissolved = true;
+        for (shd_query* q : g->members) q->eng->grouped = true;
+        const int rc = push_members();
+        if (rc != SHD_OK) throw Error(rc, g_err);
+        return;
+      }
       // the leader's open partials, replayed into each member's generic NFA
       // engine, rebuild exactly that member's (its f1 re-selects them); each
       // member then takes this batch on its own and the group runs dissolved
@@ -1310,6 +1324,7 @@ int shd_group_push(shd_group* g, const shd_batch* b) {
         const shd_counters before = q->eng->counters;
         switch_to_nfa(q, st, before, nf.what(), &parts);
         q->eng->counters.kernel_ns_total += q->eng->counters.kernel_ns;
+        q->eng->grouped = true;   // the new engine stays in the (dissolved) group
       }
     });
   });
@@ -1338,7 +1353,10 @@ int shd_group_free(shd_group* g) {
   if (!g) return SHD_OK;
   (void)hipStreamSynchronize(g->leader->eng->stream);
   g->leader->eng->group_detach();
-  for (shd_query* q : g->members) q->eng->reset();
+  for (shd_query* q : g->members) {
+    q->eng->grouped = false;
+    q->eng->reset();
+  }
   delete g->leader;
   delete g;
   return SHD_OK;

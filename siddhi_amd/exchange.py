@@ -323,20 +323,44 @@ def window_of(qp) -> Optional[Tuple[str, int]]:
     return None
 
 
+def _peer(rank: int, group: Optional[dist.ProcessGroup]) -> int:
+    """Global rank of group rank `rank` (P2POp addresses global ranks)."""
+    return rank if group is None else dist.get_global_rank(group, rank)
+
+
 def exchange_tail(cols: List[torch.Tensor], take: int, rank: int, world: int,
-                  group: Optional[dist.ProcessGroup] = None) -> Optional[List[torch.Tensor]]:
-    """Rank r sends the last `take` rows of its slice to rank r+1 and receives
-    rank r-1's (None on rank 0).  `take` must be the same on every rank and at
-    most every rank's slice length; columns travel packed (pack())."""
+                  group: Optional[dist.ProcessGroup] = None,
+                  nulls: Optional[List[Optional[torch.Tensor]]] = None):
+    """Rank r (its rank in `group`) sends the last `take` rows of its slice to
+    rank r+1 and receives rank r-1's (None on rank 0).  `take` must be the
+    same on every rank and at most every rank's slice length (halo_take
+    returns such a size); columns travel packed (pack()).  nulls: per-column
+    null masks (None = no nulls); they travel as one extra bit-mask column
+    (as in route()) and the call returns (columns, masks): a halo row whose
+    value is null must prime the query as null, not as its placeholder value."""
+    if nulls is not None:
+        if len(nulls) != len(cols) or len(cols) > 62:
+            raise ValueError("one null mask (or None) per column, at most 62 columns")
+        bits = torch.zeros(cols[0].numel(), dtype=torch.int64, device=cols[0].device)
+        for j, m in enumerate(nulls):
+            if m is not None:
+                bits |= m.to(torch.int64) << j
+        got = exchange_tail(list(cols) + [bits], take, rank, world, group)
+        if got is None:
+            return None
+        rb = got.pop()
+        return got, [((rb >> j) & 1).to(torch.uint8) for j in range(len(cols))]
     dtypes = [c.dtype for c in cols]
     if take <= 0 or world == 1:
         return None
+    if take > cols[0].numel():
+        raise ValueError("halo of %d rows from a slice of %d" % (take, cols[0].numel()))
     ops, recv = [], None
     if rank + 1 < world:
-        ops.append(dist.P2POp(dist.isend, pack([c[-take:] for c in cols]), rank + 1, group))
+        ops.append(dist.P2POp(dist.isend, pack([c[-take:] for c in cols]), _peer(rank + 1, group), group))
     if rank > 0:
         recv = torch.empty((take, len(cols)), dtype=torch.int64, device=cols[0].device)
-        ops.append(dist.P2POp(dist.irecv, recv, rank - 1, group))
+        ops.append(dist.P2POp(dist.irecv, recv, _peer(rank - 1, group), group))
     for w in dist.batch_isend_irecv(ops):
         w.wait()
     return None if recv is None else unpack(recv, dtypes)
@@ -366,7 +390,14 @@ def halo_take(window: Tuple[str, int], n: int, exchange, prime, device=None,
     at which every rank's halo covers its window.  exchange(take) -> the
     received halo columns (None on rank 0); prime(halo) -> bool, the
     halo_covers() verdict after pushing `halo` into a fresh query.  Raises when
-    a whole previous slice is not enough (the window reaches back past it)."""
+    a whole previous slice is not enough (the window reaches back past it).
+    Slices may differ in length (a stream that does not divide evenly): every
+    rank works with the shortest slice length, so every rank computes the same
+    sizes, sends as many rows as its successor expects and takes the raise
+    branch together."""
+    nt = torch.tensor([int(n)], dtype=torch.int64, device=device)
+    dist.all_reduce(nt, op=dist.ReduceOp.MIN, group=group)
+    n = int(nt.item())
     take = min(n, start or (2 * window[1] if window[0] == "length" else 4096))
     while True:
         halo = exchange(take)

@@ -54,8 +54,7 @@ class ShdOut(ctypes.Structure):
 
 class ShdCounters(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("events", "matches", "partials", "partial_scans", "bytes_touched",
-                                               "kernel_ns", "carry", "group_bits", "kernel_ns_total",
-                                               "dormant")]
+                                               "kernel_ns", "carry", "group_bits", "kernel_ns_total")]
 
 
 _lib = None

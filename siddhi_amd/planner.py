@@ -824,8 +824,9 @@ def share_signature(q: qc.Query) -> Optional[str]:
     if q.output_rate is not None:
         return None
     sel = q.selector
-    if sel.group_by or sel.having is not None or any(_has_agg(oa.expr) for oa in sel.attrs):
-        return None   # aggregating / having selectors run per query (IR POST section)
+    if isinstance(q.input, qc.StateInput) and (sel.group_by or sel.having is not None or
+                                               any(_has_agg(oa.expr) for oa in sel.attrs)):
+        return None   # aggregating / having selectors over state output run per query (IR POST section)
     import copy
     if _e1_site(q) is not None:
         q2 = copy.deepcopy(q)

@@ -323,7 +323,7 @@ def test_sparse_keys_carry_and_go_back(hip_available, back):
     assert_same_rows(dev, ora)
     assert kind == (4 if back else 1)
     if not back:
-        assert counters["carry"] > 0 and counters["dormant"] == 0
+        assert counters["carry"] > 0
 
 
 @pytest.mark.parametrize("shape", ["sparse", "dense"])

@@ -211,3 +211,30 @@ def test_chunked_window_walk(hip_available, monkeypatch, name, app, keys, call):
     monkeypatch.setenv("SHD_NO_WCHUNK", "1")
     seg, _, _ = run_device(qp, batches)
     assert_rows_agg(dev, seg, qp, exact=False)
+
+
+@pytest.mark.parametrize("late", [False, True])
+def test_range_guard_sign_channel(hip_available, late):
+    """a window whose operands have both signs can cancel to
+    far below them (+-1e8 pairs whose windows sum to a few units), where the
+    reference's running `sum += v; sum -= v` keeps the rounding history of the
+    big operands (SumAttributeAggregatorExecutor.java:184-198) and a
+    difference of prefix sums cannot agree within 1e-9.  The guard's sign
+    channel sees both signs and keeps the exact fold from that push on (late:
+    the first pushes are one-signed and run on the scans)."""
+    qp, _ = compile_single_query("@app:playback " + SCHEMA +
+                                 "from S#window.length(64) select k, sum(d) as s, avg(d) as a, count() as c "
+                                 "group by k insert into O;")
+    batches = make_batches(5, 4, 8_000, 2, nulls=False)
+    rng = np.random.default_rng(9)
+    for j, (_, b) in enumerate(batches):
+        d = b.cols[4]
+        if late and j < 2:
+            continue
+        sign = np.where(np.arange(len(d)) % 2 == 0, 1.0, -1.0)
+        d[:] = sign * 1e8 + rng.random(len(d))
+    ora = run_oracle(qp, batches)
+    dev, _, _ = run_device(qp, batches)
+    s = ora[3][:, 1].view(np.float64)
+    assert np.median(np.abs(s[len(s) // 2:])) < 1e3   # the windows do cancel
+    assert_rows_agg(dev, ora, qp, exact=False)

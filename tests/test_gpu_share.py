@@ -212,3 +212,34 @@ def test_window_group_refusals(hip_available):
     finally:
         for dq in dqs:
             dq.close()
+
+
+@pytest.mark.parametrize("trip", ["nan", "inf", "mixed-sign", "big-call"])
+def test_window_group_dissolves_into_members(hip_available, trip):
+    """An operand the shared segmented pass cannot take (NaN / Inf, both
+    signs) or a call beyond the call-window shape: the group dissolves before
+    that push -- each member adopts its window (a suffix of the leader's
+    carried items) and takes that push and every later one alone (exact fold
+    from the guard's trip on); every member still equals its own oracle run."""
+    from parity import assert_rows_agg
+    plans, leader = member_plans(window_app(WINDOW_LENGTHS))
+    batches = make_batches(91, 4, 6_000, 9)
+    si, b = batches[2]
+    p = b.cols[1].copy()
+    if trip == "nan":
+        p[100] = np.nan
+    elif trip == "inf":
+        p[100] = np.inf
+    elif trip == "mixed-sign":
+        p[100:3000:7] = -p[100:3000:7]
+    offs = b.call_offsets
+    if trip == "big-call":
+        offs = np.array([0, 2000, b.n], np.int64)   # calls above 1024 events
+    batches[2] = (si, ColumnBatch(b.ts, [b.cols[0], p, b.cols[2]], b.nulls, offs))
+    dev, kinds, counters, _ = run_group(plans, leader, batches)
+    assert all(k == 2 for k in kinds)
+    for qp, d, c in zip(plans, dev, counters):
+        ora = run_oracle(qp, batches)
+        assert len(ora[2]) > 0
+        assert_rows_agg(d, ora, qp, exact=False)
+        assert c["matches"] == len(ora[2])

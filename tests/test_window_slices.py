@@ -158,3 +158,101 @@ def test_exchange_tail_is_a_no_op_alone():
     cols = [torch.arange(10)]
     assert ex.exchange_tail(cols, 4, 0, 1) is None
     assert ex.exchange_tail(cols, 0, 0, 2) is None
+
+
+SLICE_LENS = [8192, 5120, 6144]   # a stream that does not divide evenly over 3 ranks
+
+
+def slice_columns_nulls(rank):
+    """Slice `rank` of one global stream with ~5% null prices; slices of
+    unequal length (SLICE_LENS), cut on calls."""
+    n = SLICE_LENS[rank]
+    start = sum(SLICE_LENS[:rank])
+    s, p, v, t = wl.stock_stream(sum(SLICE_LENS), KEYS, DELTA, seed_offset=6)
+    s, p, v, t = s[start:start + n], p[start:start + n], v[start:start + n], t[start:start + n]
+    rng = np.random.default_rng(1000 + rank)
+    null = (rng.random(n) < 0.05).astype(np.uint8)
+    return s, p, v, t, null
+
+
+def oracle_after_halo_nulls(qp, halo, own):
+    from oracle_engine import OracleQueryEngine
+    from parity import concat_rows
+    from siddhi_amd.runtime import ColumnBatch
+    eng = OracleQueryEngine(qp, None)
+    parts, cid = [], 0
+    for keep, cols in ((False, halo), (True, own)):
+        if cols is None:
+            continue
+        s, p, v, t, nl = cols
+        for a in range(0, len(t), CALL):
+            b = min(len(t), a + CALL)
+            sub = ColumnBatch(t[a:b], [s[a:b], p[a:b], v[a:b]], [None, nl[a:b], None])
+            for ch in eng.set_time(int(t[b - 1])) + eng.push(0, sub):
+                if keep:
+                    parts.append((np.full(len(ch.ts), cid, np.int64), ch.types, ch.ts, ch.values, ch.nulls))
+                    cid += 1
+    eng.close()
+    return concat_rows(parts)
+
+
+def _rank_nulls(rank, world, path, outdir, kind):
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from parity import compile_single_query
+    dist.init_process_group("gloo", init_method="file://" + path, rank=rank, world_size=world)
+    qp, _ = compile_single_query(APPS[kind])
+    window = ex.window_of(qp)
+    s, p, v, t, nl = slice_columns_nulls(rank)
+    cols = [torch.from_numpy(s.astype(np.int32)), torch.from_numpy(p), torch.from_numpy(v), torch.from_numpy(t)]
+    nulls = [None, torch.from_numpy(nl), None, None]
+
+    def prime(halo):
+        (hs, hp, hv, ht), hn = halo
+        passing = (hp.numpy() > 60.0) & (hn[1].numpy() == 0)   # a null price fails `price > 60`
+        carry = min(window[1], int(passing.sum())) if window[0] == "length" else 0
+        return ex.halo_covers(window, carry, ht, int(t[0]))
+
+    take = ex.halo_take(window, len(t), lambda k: ex.exchange_tail(cols, k, rank, world, nulls=nulls), prime)
+    halo = ex.exchange_tail(cols, take, rank, world, nulls=nulls)
+    hc = None
+    if halo is not None:
+        (hs, hp, hv, ht), hn = halo
+        hc = (hs.numpy().astype(np.uint32), hp.numpy(), hv.numpy(), ht.numpy(), hn[1].numpy())
+    rows = oracle_after_halo_nulls(qp, hc, (s, p, v, t, nl))
+    np.savez(os.path.join(outdir, "n%s_w%d_r%d.npz" % (kind, world, rank)), take=take,
+             **{"x%d" % i: a for i, a in enumerate(rows)})
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["length", "time"])
+def test_sliced_window_nulls_unequal_slices(tmp_path, kind):
+    """the halo carries the null masks (a null price primes the
+    query as null), and slices of unequal length agree on one halo size (the
+    shortest slice bounds it on every rank); world 3, rows == one query."""
+    from parity import assert_rows_agg, compile_single_query, run_oracle
+    from siddhi_amd.runtime import ColumnBatch
+    world = 3
+    path = tempfile.mktemp(dir=str(tmp_path))
+    mp.spawn(_rank_nulls, args=(world, path, str(tmp_path), kind), nprocs=world)
+    qp, _ = compile_single_query(APPS[kind])
+    batches = []
+    for r in range(world):
+        s, p, v, t, nl = slice_columns_nulls(r)
+        offs = np.append(np.arange(0, len(t), CALL, dtype=np.int64), np.int64(len(t)))
+        batches.append((0, ColumnBatch(t, [s, p, v], [None, nl, None], offs)))
+    whole = run_oracle(qp, batches)
+    parts, base = [], 0
+    for r in range(world):
+        z = np.load(os.path.join(str(tmp_path), "n%s_w%d_r%d.npz" % (kind, world, r)))
+        x = [z["x%d" % i] for i in range(5)]
+        x[0] = x[0] + base
+        base = int(x[0].max()) + 1 if len(x[0]) else base
+        parts.append(tuple(x))
+    merged = tuple(np.concatenate([q[i] for q in parts]) for i in range(5))
+    assert len(whole[2]) > 0
+    assert_rows_agg(merged, whole, qp, exact=False)
