@@ -335,5 +335,20 @@ __device__ __forceinline__ void prep_block_reduce(PrepAcc acc, PrepAgg* blk, int
   }
 }
 
+// Bucket walk (engine_bucket.hip): sort width of its hashed buckets, and the
+// launch of bucket bounds + walk over a sort of that width; returns the
+// number of ScanOut partials written to blk.
+constexpr uint32_t kBwMask = 0xFFFFu;   // 16 hashed bits = two radix passes
+// workgroups of the bucket walk's deferred-walk kernel (16 positions per thread)
+inline int bucket_resume_blocks(int64_t n_ext) {
+  const int64_t b = (n_ext + 256 * 16 - 1) / (256 * 16);
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+// perm: n_ext u16 (the buckets' key-grouped orders); blk: nbw + bucket_resume_blocks(n_ext)
+// ScanOut partials, the count returned
+int bucket_walk_launch(hipStream_t s, const ScanArgs* d_sa, int64_t n_ext, const uint32_t* skey, const uint32_t* spv,
+                       const int32_t* sts, uint32_t* bnd, uint16_t* perm, int nblk, int32_t* match_row, uint8_t* pst,
+                       ScanOut* blk, uint32_t* ovf, int per_wg);
+
 }  // namespace pat
 }  // namespace shd

@@ -1,0 +1,247 @@
+// pattern_walk.h -- the per-partial walk of the pattern engine (the
+// StreamPreStateProcessor step for `every e1=A[f1] -> e2=B[f2] within W`),
+// shared by the sort-path kernels (engine_pattern.hip) and the bucket walk
+// (engine_bucket.hip).  Included inside namespace shd::(anonymous) with
+// shd::pat in scope.
+#pragma once
+
+// Walk of one candidate partial P (row r, key k, timestamp tsi) over the
+// later events of its key, starting at position q whose pv / ts / key are
+// already loaded (pq, tq, kq).  StreamPreStateProcessor.processAndReturn for
+// this plan shape: expire when ts - tsi > within, complete at the first
+// B event with f2(P, event).
+//   DEFER: f2 is not evaluated here; the walk stops at the first B event
+//          inside `within` and returns ST_DEFER with q at that event (the
+//          step is already counted).  Keeps the hot kernel free of the f2
+//          code (its registers and instruction footprint).
+//   f2_first: resume at a deferred event: evaluate f2 at q first.
+// Position loads (flags/row, timestamp, key at sorted position q) from global memory.
+template <bool K64, bool TS64>
+struct GlobalPos {
+  const uint32_t* __restrict__ skey32;
+  const uint64_t* __restrict__ skey64;
+  const uint32_t* __restrict__ spv;
+  const int32_t* __restrict__ sts32;
+  const int64_t* __restrict__ sts64;
+  int64_t tbase;
+  int partitioned;
+  __device__ __forceinline__ void operator()(int64_t q, uint32_t& pq, int64_t& tq, uint64_t& kq) const {
+    pq = spv[q];
+    tq = TS64 ? sts64[q] : tbase + (int64_t)sts32[q];
+    if (partitioned) kq = K64 ? skey64[q] : skey32[q];
+  }
+};
+
+// Block skip: f2's threshold for partial (row r, sorted position q1) -- the
+// e1 side of comparison bs_ci (null: f2 can never pass).
+__device__ __forceinline__ Val skip_threshold(const ScanArgs& a, int64_t r, int64_t q1) {
+  const FCmp& c = a.f2.fp.c[a.bs_ci];
+  PairCtx cx{&a.x, r, -1, a.s_first};
+  cx.q1 = q1;
+  return fp_term(a.bs_side == 0 ? c.r : c.l, cx);
+}
+
+// True when a walk of key k (created at tsi, last step at prev) passes the
+// whole block without an outcome: every non-skip position is of key k, no
+// F_NEW event expires it or goes back in time, and no B event can pass f2.
+__device__ __forceinline__ bool block_skippable(const ScanArgs& a, const BlockSum& b, uint64_t k, int64_t tsi,
+                                                int64_t prev, Val thr) {
+  if (a.partitioned && !(b.flags & 4u) && (!(b.flags & 1u) || b.key != (uint32_t)k)) return false;
+  if (b.cnt && a.within != INT64_MAX) {
+    if (!(b.flags & 2u) || b.tfirst < prev || b.tlast - tsi > a.within) return false;
+  }
+  if (thr.null) return true;
+  const double t = v_f64(thr.b), v = b.v;
+  switch (a.bs_op) {
+    case SHD_OP_GT: return v <= t;
+    case SHD_OP_GE: return v < t;
+    case SHD_OP_LT: return v >= t;
+    case SHD_OP_LE: return v > t;
+  }
+  return false;
+}
+
+// WIN: positions are loaded WIN at a time (one round trip for WIN steps);
+// walks over hashed buckets step over a few other keys, and a wave waits for
+// its longest walk, so they fetch ahead.
+template <bool DEFER, bool FAST, int WIN, class Ld, int CAP = 0, bool SKIP = false>
+__device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSet& es, int64_t n_ext, const Ld& ld,
+                                                int64_t r, uint64_t k, int64_t tsi, int64_t& q, uint32_t pq,
+                                                int64_t tq, uint64_t kq, int64_t prev, bool f2_now, int32_t& j,
+                                                uint64_t& steps, uint32_t& viol, uint32_t& fm, int64_t& ra,
+                                                int64_t& rb, int64_t q1 = -1) {
+  uint8_t st = ST_OPEN;
+  bool stop = false, first = true;
+  int it = 0;
+  bool thr_ok = false;
+  Val thr;
+  thr.b = 0;
+  thr.null = 1;
+  int64_t tried = -1;      // block whose skip was last tried
+  int64_t last_new = q;    // position of the walk's last F_NEW step (the resume point's time is prev)
+  while (!stop && q < n_ext) {
+    if constexpr (CAP > 0) {
+      // CAP positions walked: yield before position q (nothing of it processed)
+      if (!f2_now && it >= CAP) {
+        st = ST_YIELD;
+        break;
+      }
+      it += WIN;
+    }
+    if constexpr (!DEFER && SKIP) {
+      // long walks skip the rest of a 64-position block when none of it can
+      // end them: from a block boundary (block_skippable), or from inside the
+      // block once per block -- then the whole block's summary must allow it
+      // and, for the times, the walk's last step lies in this block (the
+      // block's times are nondecreasing, so the rest is no earlier than it)
+      const int64_t blk = q >> 6;
+      if (!first && !f2_now && blk != tried && (blk << 6) + 64 <= n_ext) {
+        tried = blk;
+        if (!thr_ok) {
+          thr = skip_threshold(a, r, q1);
+          thr_ok = true;
+        }
+        const BlockSum bs = a.bsum[blk];
+        const int off = (int)(q & 63);
+        // the last step inside this block: the block's nondecreasing times
+        // after it are >= prev (block_skippable then only checks monotonicity)
+        const int64_t after = (off != 0 && last_new >= (blk << 6)) ? INT64_MIN : prev;
+        if (block_skippable(a, bs, k, tsi, after, thr)) {
+          const uint32_t c = (uint32_t)__popcll(bs.newmask >> off);
+          steps += c;
+          if (c) {
+            prev = bs.tlast;
+            last_new = (blk << 6) + 63;
+          }
+          q = (blk << 6) + 64;
+          continue;
+        }
+      }
+    }
+    uint32_t wp[WIN];
+    int64_t wt[WIN];
+    uint64_t wk[WIN];
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+      wk[i] = 0;
+      if (i == 0 && first) {
+        wp[0] = pq;
+        wt[0] = tq;
+        wk[0] = kq;
+      } else {
+        const int64_t qi = q + i < n_ext ? q + i : n_ext - 1;
+        ld(qi, wp[i], wt[i], wk[i]);
+      }
+    }
+    first = false;
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+      if (q >= n_ext) {
+        stop = true;
+        break;
+      }
+      pq = wp[i];
+      tq = wt[i];
+      kq = wk[i];
+      // rows of dropped (null-key) events carry no usable key: passed over
+    if (!f2_now && a.partitioned && kq != k && !(pv_flags(pq) & F_SKIP)) {
+        stop = true;
+        if (!a.hash_mask) break;   // end of the key's run
+        if ((key_bucket_mix((uint32_t)kq) ^ key_bucket_mix((uint32_t)k)) & a.hash_mask) break;   // end of the bucket
+        // another key of the bucket: pushed rows are time-ordered, so once one is
+        // beyond `within` every later event of this key is too -- the partial
+        // can no longer match (OPEN here; the horizon rule below retires it,
+        // t_end >= tq > tsi + within)
+        if (pv_row(pq) >= (uint32_t)a.x.C && tq - tsi > a.within) break;
+        stop = false;
+      } else if (!f2_now) {
+        const uint32_t fq = pv_flags(pq);
+        if ((fq & F_NEW) && !(fq & F_SKIP)) {
+          // a per-key time regression only matters under `within` (expiry);
+          // without it the outcome of every partial is time-independent
+          if (a.within != INT64_MAX && tq < prev) {
+            viol = 1;
+            stop = true;
+            break;
+          }
+          prev = tq;
+          last_new = q;
+          steps++;
+          // stabilizeStates -> expireEvents: |ts_i - t| > within
+          if (tq - tsi > a.within) {
+            st = ST_DEAD;
+            stop = true;
+            break;
+          }
+          if (fq & F_B) {
+            if (DEFER) {
+              st = ST_DEFER;
+              stop = true;
+              break;
+            }
+            f2_now = true;
+          }
+        }
+      }
+      if constexpr (!DEFER) {
+        if (f2_now) {
+          f2_now = false;
+          const int64_t r2 = pv_row(pq);
+          if (a.logical == 2) {
+            // LogicalPre/PostStateProcessor (AND): an operand that passes fills
+            // its slot and leaves its processor's pending list; the partial
+            // completes when the partner slot is filled too -- possibly by the
+            // partner processor on this same event (LogicalPostStateProcessor.java:59-86)
+            int32_t br = -1;
+            if (!(fm & 1u)) {
+              PairCtx cx{&a.x, r, r2, a.s_first, false, (fm & 2u) ? rb : -1, a.s_second, q, q1};
+              if (FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx)) {
+                fm |= 1u;
+                ra = r2;
+                if (fm == 3u) br = 0;
+              }
+            }
+            if (br < 0 && !(fm & 2u)) {
+              PairCtx cx{&a.x, r, r2, a.s_second, false, (fm & 1u) ? ra : -1, a.s_first, q, q1};
+              if (FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx)) {
+                fm |= 2u;
+                rb = r2;
+                if (fm == 3u) br = 1;
+              }
+            }
+            if (br >= 0) {
+              st = ST_MATCH;
+              j = (int32_t)r2 | (br << kRowBits);
+              stop = true;
+              break;
+            }
+            q++;
+            continue;
+          }
+          PairCtx cx{&a.x, r, r2, a.s_first};
+          cx.q2 = q;
+          cx.q1 = q1;
+          bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+          int32_t br = 0;
+          if (!hit && a.logical) {
+            // LogicalPreStateProcessor (OR): the partner processor sees the
+            // same event next (LogicalPreStateProcessor.java:113-154)
+            cx.s2 = a.s_second;
+            hit = FAST ? eval_fpred(a.f3.fp, cx) : eval_filters(es, a.f3, cx);
+            br = 1;
+          }
+          if (hit) {
+            st = ST_MATCH;
+            j = (int32_t)r2 | (br << kRowBits);   // matched branch above the row bits
+            stop = true;
+            break;
+          }
+        }
+      }
+      q++;
+    }
+  }
+  if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+  return st;
+}
+

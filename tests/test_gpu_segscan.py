@@ -225,7 +225,7 @@ def test_range_guard_sign_channel(hip_available, late):
     qp, _ = compile_single_query("@app:playback " + SCHEMA +
                                  "from S#window.length(64) select k, sum(d) as s, avg(d) as a, count() as c "
                                  "group by k insert into O;")
-    batches = make_batches(5, 4, 8_000, 2, nulls=False)
+    batches = make_batches(5, 4, 8_000, 1, nulls=False)   # one group: its window alternates signs
     rng = np.random.default_rng(9)
     for j, (_, b) in enumerate(batches):
         d = b.cols[4]
