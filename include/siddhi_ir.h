@@ -11,7 +11,8 @@
  *   n_exprs,   { n_instr, { op, a, b, c } * n_instr } * n_exprs
  *   partition: n_keys, { stream, expr } * n_keys             (n_keys = 0: unpartitioned)
  *   STATE:  state_type, within_lo, within_hi, n_states, node tree (prefix order)
- *   SINGLE: stream, n_handlers, { FILTER expr | WINDOW kind p_lo p_hi } * n_handlers
+ *   SINGLE: stream, n_handlers, { FILTER expr | WINDOW kind p_lo p_hi q_lo q_hi } * n_handlers
+ *     (p = the window's first parameter, q = its second: see shd_window)
  *   selector: current_on, expired_on, n_aggs { kind, arg_expr, arg_type } ,
  *             n_group { expr }, having_expr, n_out { type, expr }
  *   optional trailing words:
@@ -107,7 +108,13 @@ enum shd_node { SHD_NODE_STREAM = 1, SHD_NODE_NEXT = 2, SHD_NODE_EVERY = 3,
                 SHD_NODE_LOGICAL = 4, SHD_NODE_COUNT = 5 };
 
 enum shd_handler { SHD_H_FILTER = 1, SHD_H_WINDOW = 2 };
-enum shd_window { SHD_W_LENGTH = 1, SHD_W_TIME = 2 };
+/* Windows (C/query/processor/stream/window/): p = length or time (ms); q:
+ *   LENGTH_BATCH  q = 0 (LengthBatchWindowProcessor.java:153-243, full-batch mode)
+ *   TIME_BATCH    q = start.time, or INT64_MIN when absent (TimeBatchWindowProcessor.java:279-366)
+ *   TIME_LENGTH   q = window.length (TimeLengthWindowProcessor.java:139-188)
+ *   LENGTH / TIME q = 0 */
+enum shd_window { SHD_W_LENGTH = 1, SHD_W_TIME = 2, SHD_W_LENGTH_BATCH = 3, SHD_W_TIME_BATCH = 4,
+                  SHD_W_TIME_LENGTH = 5 };
 enum shd_agg { SHD_AGG_SUM = 1, SHD_AGG_AVG = 2, SHD_AGG_COUNT = 3 };
 
 /* Output / input event types (ComplexEvent.Type). */

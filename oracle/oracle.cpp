@@ -74,7 +74,7 @@ struct Plan {
   std::unique_ptr<Node> root;
   // single
   int single_stream = 0;
-  struct Handler { int kind; int expr; int wkind; int64_t param; };
+  struct Handler { int kind; int expr; int wkind; int64_t param, param2; };
   std::vector<Handler> handlers;
   // selector
   bool current_on = true, expired_on = false;
@@ -183,6 +183,7 @@ Plan decode(const int32_t* w, int64_t n) {
       } else {
         h.wkind = r.next();
         h.param = r.next64();
+        h.param2 = r.next64();
       }
       p.handlers.push_back(h);
     }
@@ -1825,6 +1826,10 @@ struct Engine {
     // Scheduler.SchedulerState.toNotifyQueue: a FIFO (LinkedBlockingQueue),
     // peeked / polled at its head (C/util/Scheduler.java:113-209,330-332)
     std::deque<int64_t> notify;
+    // LengthBatch / TimeBatch WindowProcessor.WindowState (full-batch mode):
+    // currentEventQueue, expiredEventQueue, resetEvent != null
+    std::deque<Ev*> cur_q, exp_q;
+    bool reset_pending = false;
     // aggregator states per group key
     std::map<std::vector<std::pair<uint64_t, uint8_t>>, GroupAgg> groups;
   };
@@ -1836,14 +1841,23 @@ struct Engine {
   // partition, so only the unpartitioned table is used).
   KeySingle state_aggs;
   int window_kind = 0;
-  int64_t window_param = 0;
+  int64_t window_param = 0, window_param2 = 0;
   int window_pos = -1;
+  // TimeBatchWindowProcessor.nextEmitTime: a field of the processor, not of a
+  // partition's state (:136, :283-300)
+  int64_t next_emit = -1;
+  // in_seq of the rows of a batch window's flush chunk (the emitting event)
+  int64_t flush_seq = -1;
+  bool batch_window() const {
+    return window_kind == SHD_W_LENGTH_BATCH || window_kind == SHD_W_TIME_BATCH;
+  }
 
   void build_single() {
     for (int i = 0; i < (int)p.handlers.size(); i++) {
       if (p.handlers[i].kind == SHD_H_WINDOW) {
         window_kind = p.handlers[i].wkind;
         window_param = p.handlers[i].param;
+        window_param2 = p.handlers[i].param2;
         window_pos = i;
       }
     }
@@ -1996,11 +2010,109 @@ struct Engine {
           if (eval_bool(p, h.expr, cx)) out.push_back(e);
         }
         chunk.swap(out);
+      } else if (batch_window()) {
+        // one output chunk per flush (LengthBatchWindowProcessor.process :154-187:
+        // each flush's chunk goes to the next processor on its own)
+        std::vector<std::pair<std::vector<Ev*>, int64_t>> flushes = batch_process(ks, chunk);
+        for (auto& f : flushes) {
+          flush_seq = f.second;
+          single_chunk(ks, f.first, hi + 1);
+          flush_seq = -1;
+        }
+        return;
       } else {
         chunk = window_process(ks, chunk);
       }
     }
     selector_process(ks, chunk);
+  }
+
+  Ev* reset_event() {
+    Ev* r = ev_arena.get();
+    *r = Ev();
+    r->type = RESET;
+    return r;
+  }
+
+  // A flush of a batch window's WindowState: [expired events of the previous
+  // batch, timestamp currentTime] + RESET + [the batch's current events] (the
+  // current events become the next flush's expired events when the query
+  // outputs expired events: outputExpectsExpiredEvents).
+  std::vector<Ev*> batch_flush(KeySingle* ks, int64_t currentTime) {
+    std::vector<Ev*> out;
+    if (p.expired_on && !ks->exp_q.empty()) {
+      for (Ev* x : ks->exp_q) {
+        x->ts = currentTime;
+        out.push_back(x);
+      }
+      ks->exp_q.clear();
+    }
+    if (ks->reset_pending) {
+      out.push_back(reset_event());
+      ks->reset_pending = false;
+    }
+    if (!ks->cur_q.empty()) {
+      for (Ev* c : ks->cur_q) {
+        if (p.expired_on) {
+          Ev* x = clone_ev(c);
+          x->type = EXPIRED;
+          ks->exp_q.push_back(x);
+        }
+        out.push_back(c);
+      }
+      ks->cur_q.clear();
+    }
+    return out;
+  }
+
+  // Batch windows over one input chunk: the flush chunks, each with the
+  // in_seq of its emitting event.
+  std::vector<std::pair<std::vector<Ev*>, int64_t>> batch_process(KeySingle* ks, const std::vector<Ev*>& in) {
+    std::vector<std::pair<std::vector<Ev*>, int64_t>> res;
+    const int64_t currentTime = now;
+    if (window_kind == SHD_W_LENGTH_BATCH) {
+      // LengthBatchWindowProcessor.processFullBatchEvents (:206-243), length >= 1
+      for (Ev* e : in) {
+        ks->reset_pending = true;   // resetEvent: a copy of the first event after a flush
+        ks->cur_q.push_back(clone_ev(e));
+        ks->count++;
+        if (ks->count == window_param) {
+          std::vector<Ev*> out = batch_flush(ks, currentTime);
+          ks->count = 0;
+          if (!out.empty()) res.push_back({out, e->seq});
+        }
+      }
+      return res;
+    }
+    // TimeBatchWindowProcessor.process (:279-366), full-batch mode
+    if (next_emit == -1) {
+      if (window_param2 != INT64_MIN) {
+        // getNextEmitTime (:368-373): aligned to start.time
+        const int64_t elapsed = (currentTime - window_param2) % window_param;
+        next_emit = currentTime + (window_param - elapsed);
+      } else {
+        next_emit = currentTime + window_param;
+      }
+      ks->notify.push_back(next_emit);
+    }
+    bool send = false;
+    if (currentTime >= next_emit) {
+      next_emit += window_param;
+      ks->notify.push_back(next_emit);
+      send = true;
+    }
+    int64_t last_seq = cur_seq;
+    for (Ev* e : in) {
+      if (e->type != CURRENT) continue;
+      ks->reset_pending = true;
+      ks->cur_q.push_back(clone_ev(e));
+      last_seq = e->seq;
+    }
+    if (send) {
+      std::vector<Ev*> out = batch_flush(ks, currentTime);
+      if (!out.empty()) res.push_back({out, last_seq});
+    }
+    return res;
   }
 
   std::vector<Ev*> window_process(KeySingle* ks, const std::vector<Ev*>& in) {
@@ -2028,6 +2140,40 @@ struct Engine {
             throw std::runtime_error("length(0) window (RESET path) outside the hot path");
           }
         }
+      }
+    } else if (window_kind == SHD_W_TIME_LENGTH) {
+      // TimeLengthWindowProcessor.process (:139-188): time expiry before each
+      // event (TIMER events only expire), then the length bound; every added
+      // event schedules ts + time
+      const int64_t T = window_param, L = window_param2;
+      const int64_t currentTime = now;
+      for (Ev* e : in) {
+        while (!ks->q.empty()) {
+          Ev* x = ks->q.front();
+          if (x->ts - currentTime + T <= 0) {
+            ks->q.pop_front();
+            ks->count--;
+            x->ts = currentTime;
+            out.push_back(x);
+          } else {
+            break;
+          }
+        }
+        if (e->type != CURRENT) continue;
+        Ev* c = clone_ev(e);
+        c->type = EXPIRED;
+        if (ks->count < L) {
+          ks->count++;
+          ks->q.push_back(c);
+        } else if (!ks->q.empty()) {
+          Ev* f = ks->q.front();
+          ks->q.pop_front();
+          f->ts = currentTime;
+          out.push_back(f);
+          ks->q.push_back(c);
+        }
+        ks->notify.push_back(c->ts + T);
+        out.push_back(e);
       }
     } else {
       // TimeWindowProcessor.process (:132-169)
@@ -2072,12 +2218,19 @@ struct Engine {
     OutRow last;
     bool have_last = false;
     for (Ev* e : chunk) {
-      if (e->type != CURRENT && e->type != EXPIRED) continue;   // TIMER / RESET
+      // RESET: every aggregator's cleanGroupByStates -- all group states of
+      // this partition (AttributeAggregatorExecutor.processReset :144-150,
+      // PartitionStateHolder.cleanGroupByStates :92-99)
+      if (e->type == RESET) {
+        ks->groups.clear();
+        continue;
+      }
+      if (e->type != CURRENT && e->type != EXPIRED) continue;   // TIMER
       run_aggs(ks, e);
       OutRow r;
       r.type = e->type;
       r.ts = e->ts;
-      r.seq = e->seq;
+      r.seq = flush_seq >= 0 ? flush_seq : e->seq;
       EvalCtx cx;
       cx.ev = e;
       cx.aggs = &agg_vals;
@@ -2121,7 +2274,7 @@ struct Engine {
   }
 
   void single_on_time_change(int64_t t) {
-    if (window_kind != SHD_W_TIME) return;
+    if (window_kind != SHD_W_TIME && window_kind != SHD_W_TIME_BATCH && window_kind != SHD_W_TIME_LENGTH) return;
     // Scheduler.onTimeChange: states with head notify <= t, sorted by time.
     std::vector<std::pair<int64_t, KeySingle*>> due;
     if (partitioned) {

@@ -125,7 +125,7 @@ struct Plan {
   int n_states = 0;
   PNode root;
   int single_stream = 0;
-  struct Handler { int kind; int expr; int wkind; int64_t param; };
+  struct Handler { int kind; int expr; int wkind; int64_t param, param2; };
   std::vector<Handler> handlers;
   bool current_on = true, expired_on = false;
   struct Agg { int kind, expr, type; };

@@ -130,6 +130,7 @@ Plan decode_plan(const int32_t* w, int64_t n) {
       else {
         h.wkind = r.next();
         h.param = r.next64();
+        h.param2 = r.next64();
       }
       p.handlers.push_back(h);
     }

@@ -40,7 +40,8 @@ TYPE_NAME[T_OBJECT] = "object"
 IDX_CURRENT, IDX_LAST = -1, -2
 NODE_STREAM, NODE_NEXT, NODE_EVERY, NODE_LOGICAL, NODE_COUNT = 1, 2, 3, 4, 5
 H_FILTER, H_WINDOW = 1, 2
-W_LENGTH, W_TIME = 1, 2
+W_LENGTH, W_TIME, W_LENGTH_BATCH, W_TIME_BATCH, W_TIME_LENGTH = 1, 2, 3, 4, 5
+INT64_MIN = -(1 << 63)
 AGG_SUM, AGG_AVG, AGG_COUNT = 1, 2, 3
 UNKNOWN_STATE = -1
 NUMERIC_RANK = {T_INT: 0, T_LONG: 1, T_FLOAT: 2, T_DOUBLE: 3}
@@ -161,7 +162,7 @@ class Plan:
                 if h[0] == H_FILTER:
                     w.extend([H_FILTER, h[1]])
                 else:
-                    w.extend([H_WINDOW, h[1], *_split64(h[2])])
+                    w.extend([H_WINDOW, h[1], *_split64(h[2]), *_split64(h[3] if len(h) > 3 else 0)])
         w.extend([int(self.current_on), int(self.expired_on), len(self.aggs)])
         for a in self.aggs:
             w.extend(a)
@@ -744,25 +745,75 @@ def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
     n_windows = 0
     for h in si.handlers:
         if isinstance(h, qc.Filter):
+            if any(x[0] == H_WINDOW and x[1] in (W_LENGTH_BATCH, W_TIME_BATCH) for x in plan.handlers):
+                raise UnsupportedPlanException("a filter after a batch window is outside the hot path")
             eid, _ = ec.compile(h.expr, 0, IDX_CURRENT, want_bool=True)
             plan.handlers.append((H_FILTER, eid))
         else:
             n_windows += 1
             if n_windows > 1:
                 raise SiddhiAppValidationException("only one window per stream")
-            if h.name not in ("length", "time"):
-                raise UnsupportedPlanException("window %s is outside the round-1 hot path" % h.name)
-            if len(h.params) != 1 or not isinstance(h.params[0], qc.Const) or \
-                    h.params[0].type not in ("int", "long"):
-                raise SiddhiAppValidationException("%s window needs one constant int/long parameter" % h.name)
-            plan.handlers.append((H_WINDOW, W_LENGTH if h.name == "length" else W_TIME,
-                                  int(h.params[0].value)))
+            plan.handlers.append(_window_handler(h, partition is not None))
     names, types = _plan_selector(plan, q, ec, [m], False)
     _plan_partition(plan, None, partition, [si.stream], app, dictionary, extra_streams)
     plan.target = q.target
     plan.shape = {"kind": "single", "window": next((h[1] for h in plan.handlers if h[0] == H_WINDOW), 0)}
     return QueryPlan(plan, plan.to_bytes(), [si.stream], names, types, q.target, q.name,
                      partition is not None, {si.stream: "single"})
+
+
+def _window_handler(h, partitioned: bool):
+    """(H_WINDOW, kind, p, q) of a `#window.<name>(...)` handler (include/siddhi_ir.h
+    shd_window).  Batch windows in full-batch mode only: `stream.current.event`
+    true (ProcessingMode.RESET) is refused, and so is `timeBatch` inside a
+    partition (its nextEmitTime is a field of the processor shared by every
+    partition key, TimeBatchWindowProcessor.java:136,283-300)."""
+    ps = h.params
+
+    def const(i, types, what):
+        if i >= len(ps) or not isinstance(ps[i], qc.Const) or ps[i].type not in types:
+            raise SiddhiAppValidationException("%s window's %s should be a constant %s" %
+                                               (h.name, what, "/".join(types)))
+        return ps[i].value
+
+    if h.name in ("length", "time"):
+        if len(ps) != 1:
+            raise SiddhiAppValidationException("%s window needs one constant int/long parameter" % h.name)
+        return (H_WINDOW, W_LENGTH if h.name == "length" else W_TIME, int(const(0, ("int", "long"), "parameter")), 0)
+    if h.name == "lengthbatch":
+        if not 1 <= len(ps) <= 2:
+            raise SiddhiAppValidationException("LengthBatch window should have one or two parameters")
+        n = int(const(0, ("int",), "window.length"))
+        if len(ps) == 2 and bool(const(1, ("bool",), "stream.current.event")):
+            raise UnsupportedPlanException("lengthBatch with stream.current.event is outside the hot path")
+        if n <= 0:
+            raise UnsupportedPlanException("lengthBatch(0) (RESET path) is outside the hot path")
+        return (H_WINDOW, W_LENGTH_BATCH, n, 0)
+    if h.name == "timebatch":
+        if not 1 <= len(ps) <= 3:
+            raise SiddhiAppValidationException("TimeBatch window should have one to three parameters")
+        t = int(const(0, ("int", "long"), "window.time"))
+        start = INT64_MIN
+        if len(ps) >= 2:
+            if ps[1].type == "bool" and len(ps) == 2:
+                if bool(ps[1].value):
+                    raise UnsupportedPlanException("timeBatch with stream.current.event is outside the hot path")
+            else:
+                start = int(const(1, ("int", "long"), "start.time"))
+                if len(ps) == 3 and bool(const(2, ("bool",), "stream.current.event")):
+                    raise UnsupportedPlanException("timeBatch with stream.current.event is outside the hot path")
+        if partitioned:
+            raise UnsupportedPlanException("timeBatch inside a partition is outside the hot path")
+        if t <= 0:
+            raise SiddhiAppValidationException("TimeBatch window's window.time should be positive")
+        return (H_WINDOW, W_TIME_BATCH, t, start)
+    if h.name == "timelength":
+        if len(ps) != 2:
+            raise SiddhiAppValidationException("TimeLength window should only have two parameters")
+        t = int(const(0, ("int", "long"), "window.time"))
+        n = int(const(1, ("int",), "window.length"))
+        return (H_WINDOW, W_TIME_LENGTH, t, n)
+    raise UnsupportedPlanException("window %s is outside the hot path" % h.name)
 
 
 def _uses_inner_stream(inp) -> bool:

@@ -374,6 +374,8 @@ def extract(name, body, line, fname):
     events_ok = True
     stmt_re = re.compile(
         r"(?P<wait>TestUtil\.waitForInEvents\((?P<wms>\d+),\s*\w+,\s*(?P<wn>\d+)\))"
+        r"|(?P<swait>SiddhiTestHelper\.waitForEvents\((?P<sms>\d+),\s*(?P<sn>\d+),\s*\w+(?:\.get\(\))?,\s*"
+        r"(?P<sto>\d+)\))"
         r"|(?P<sleep>Thread\.sleep\((?P<ms>\d+)\))"
         r"|(?P<nowdecl>long (?P<nv>\w+) = (?P<nval>System\.currentTimeMillis\(\)|\d+L?);)"
         r"|(?P<nowadd>(?P<nv2>\w+) \+= (?P<addexpr>[\d *]+);)"
@@ -405,6 +407,14 @@ def extract(name, body, line, fname):
             if not playback:
                 sends.append({"wait": int(sm.group("wms")), "retry": int(sm.group("wn"))})
             clock += int(sm.group("wms"))
+        elif sm.group("swait"):
+            # SiddhiTestHelper.waitForEvents(sleep, n, counter, timeout)
+            # (C/util/SiddhiTestHelper.java:49-57): sleep until the counter
+            # reaches n or the timeout passed; wall-clock timers fire meanwhile
+            if not playback:
+                ms_ = int(sm.group("sms"))
+                sends.append({"wait": ms_, "retry": int(sm.group("sto")) // ms_ + 1, "until": int(sm.group("sn"))})
+            clock += int(sm.group("sms"))
         elif sm.group("sleep"):
             clock += int(sm.group("ms"))
             if playback and "idle.time" in app:

@@ -97,10 +97,14 @@ def run_case(case, engine_factory):
         if "idle" in s:          # Thread.sleep on a playback app with idle.time (heartbeat)
             app.idle(s["idle"])
             continue
-        if "wait" in s:          # TestUtil.waitForInEvents(sleep, cb, retry) (T/TestUtil.java:69-79)
+        if "wait" in s:          # TestUtil.waitForInEvents(sleep, cb, retry) (T/TestUtil.java:69-79),
+            # SiddhiTestHelper.waitForEvents(sleep, until, counter, timeout) (C/util/SiddhiTestHelper.java:49-57)
+            until = s.get("until")
             for _ in range(s["retry"]):
+                if until is not None and len(col.in_events) >= until:
+                    break
                 tick_to(clock + s["wait"])
-                if len(col.in_events) == 1:
+                if until is None and len(col.in_events) == 1:
                     break
             continue
         clock = max(clock, s["ts"])

@@ -28,7 +28,7 @@ def test_window_leader_holds_the_longest_window():
     d = pl.StringDictionary()
     wl.register_symbols(d, 10)
     lead = pl.plan_shared_leader(app, qs[50:], d)
-    assert lead.plan.handlers[-1][-1] == 5000   # (kind, window kind, length)
+    assert lead.plan.handlers[-1][2] == 5000   # (kind, window kind, length, second parameter)
     # a different filter (or aggregate, or group-by) is another group
     other = qc.parse(wl.M5_APP.replace("from StockStream[price>60]#window.length(400)",
                                        "from StockStream[price>61]#window.length(400)"))
