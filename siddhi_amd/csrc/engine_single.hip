@@ -4010,6 +4010,9 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
   if (e->nagg > kMaxAggs) { why = "too many aggregators"; return nullptr; }
   e->partitioned = !p.part_keys.empty();
   bool needs_agg = e->nagg > 0 || !p.group_by.empty();
+  // batch windows (flush chunks with RESET) and timeLength: the window-x engine
+  if (e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH || e->wkind == SHD_W_TIME_LENGTH)
+    return make_window_x_engine(p, why);
   // EXPIRED output, `having`, no CURRENT output, aggregation inside a
   // partition: the keyed exact window engine (engine_window.hip)
   if ((p.expired_on && (needs_agg || e->wkind != 0)) || p.having >= 0 || !p.current_on ||

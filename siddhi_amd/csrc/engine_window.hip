@@ -40,6 +40,8 @@
 // the push's clock moves (k_xw_time_lane); everything else is data-parallel.
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
+#include <deque>
 #include <cstdlib>
 
 #include "engine.h"
@@ -625,6 +627,10 @@ struct FoldArgsX {
   double* dsum;
   int64_t* lsum;
   int64_t* cnt;
+  // batch windows: the chunk of a state's last RESET-started add (RESET clears
+  // every group state of the partition; applied when the state is next added to)
+  int64_t* epoch;     // [nstates], null: no batch window
+  int64_t chunk0;
   uint64_t* resv;     // [nagg][nops]
   uint8_t* resn;
   uint8_t* rowflag;   // [nops]
@@ -656,12 +662,22 @@ __global__ __launch_bounds__(kBlock) void k_xw_fold(const FoldArgsX* __restrict_
       l[g] = a.lsum[(int64_t)g * a.nstates + sid];
       c[g] = a.cnt[(int64_t)g * a.nstates + sid];
     }
+    int64_t ep = a.epoch ? a.epoch[sid] : 0;
     uint32_t cur = 0xFFFFFFFFu;
     int64_t first = -1, last = -1;
     for (int64_t p = q0; p < q1; p++) {
       const uint32_t q = sq[p];
       const uint32_t it = a.op_item[q];
       const bool add = a.op_add[q];
+      if (a.epoch && add && ep != a.chunk0 + (int64_t)a.op_chunk[q]) {
+        // the flush's RESET came after this state's last operation
+        ep = a.chunk0 + (int64_t)a.op_chunk[q];
+        for (int g = 0; g < a.nagg; g++) {
+          d[g] = 0.0;
+          l[g] = 0;
+          c[g] = 0;
+        }
+      }
       uint64_t vv[kMaxAggs];
       uint8_t vn[kMaxAggs];
       for (int g = 0; g < a.nagg; g++) {
@@ -703,6 +719,7 @@ __global__ __launch_bounds__(kBlock) void k_xw_fold(const FoldArgsX* __restrict_
       a.lsum[(int64_t)g * a.nstates + sid] = l[g];
       a.cnt[(int64_t)g * a.nstates + sid] = c[g];
     }
+    if (a.epoch) a.epoch[sid] = ep;
   }
 }
 
@@ -793,6 +810,7 @@ struct CarryArgs {
   const uint32_t* koff;
   const uint32_t* segid;
   const int64_t* last_out;   // per segment (time windows), may be null
+  const uint8_t* added_j;    // batch windows: per sorted position, carried as ilast (0 / 1)
   const uint64_t* pk; const int64_t* ts; const int64_t* seq; const uint64_t* sid;
   const uint64_t* attr; const uint8_t* nul; const uint64_t* argv; const uint8_t* argn;
   uint64_t* d_pk; int64_t* d_ts; int64_t* d_seq; uint64_t* d_sid; int64_t* d_last; int32_t* d_call; int32_t* d_row;
@@ -810,7 +828,7 @@ __global__ __launch_bounds__(kBlock) void k_xw_carry(const CarryArgs* __restrict
     a.d_ts[t] = a.ts[it];
     a.d_seq[t] = a.seq[it];
     a.d_sid[t] = a.sid[it];
-    a.d_last[t] = a.last_out ? a.last_out[a.segid[j]] : INT64_MIN;
+    a.d_last[t] = a.added_j ? (int64_t)a.added_j[j] : (a.last_out ? a.last_out[a.segid[j]] : INT64_MIN);
     a.d_call[t] = -1;
     a.d_row[t] = -1;
     for (int c = 0; c < a.ncols; c++) {
@@ -882,6 +900,215 @@ __global__ __launch_bounds__(kBlock) void k_xw_fill_u64(uint64_t* p, int64_t n, 
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i = n) p[i] = v;
 }
 
+// ---------------------------------------------------------------- batch windows
+// lengthBatch / timeBatch in full-batch mode (LengthBatchWindowProcessor.java:
+// 206-243, TimeBatchWindowProcessor.java:279-366).  A flush F of a key emits
+// one chunk: the previous batch's items as EXPIRED (when the query outputs
+// expired events), RESET, the batch's items as CURRENT.  Items of a key
+// segment in FIFO order: [a carried items already added, awaiting expiry]
+// [carried items of the open batch] [new items]; each item's add and expiry
+// opportunities are flushes (2F + 1, expiry before add at one flush), both
+// non-decreasing along the segment, so the operations of a key keep
+// k_xw_ops' closed-form positions.  RESET (every group state of the partition
+// cleared, PartitionStateHolder.cleanGroupByStates) is applied lazily by the
+// fold: a state's first add of a flush starts it from zero (k_xw_fold epochs).
+
+// added_j[j]: the item at sorted position j was added at an earlier flush
+__global__ __launch_bounds__(kBlock) void k_xb_added(int64_t total, int64_t C, const uint32_t* sp, const int64_t* ilast,
+                                                     uint8_t* added_j) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j = total) {
+    const uint32_t it = sp[j];
+    added_j[j] = (it < (uint32_t)C && ilast[it] == 1) ? 1 : 0;
+  }
+}
+
+// carried items of the segment [s, s + ck) already added: a prefix (FIFO)
+__device__ __forceinline__ int64_t xb_added_count(const uint8_t* added_j, int64_t s, int64_t ck) {
+  int64_t lo = s, hi = s + ck;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (added_j[mid]) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - s;
+}
+
+struct XbArgs {
+  int64_t total, C, L;
+  int expired_on;
+  const uint32_t* sp;
+  const uint32_t* segid;
+  const int64_t* segS;
+  const int64_t* segCk;
+  const uint8_t* added_j;
+  const int32_t* irow;
+  const int32_t* icall;
+  const uint32_t* fr;        // lengthBatch: flush rank of each batch row (exclusive scan of the triggers)
+  const int32_t* bflush;     // timeBatch: per call, the flush its events join (-1: none in this push)
+  int64_t nf;                // timeBatch: flushes of this push
+  uint64_t* aopp;
+  uint64_t* eopp;
+};
+
+// lengthBatch triggers: the new item whose open-batch ordinal completes a batch
+__global__ __launch_bounds__(kBlock) void k_xb_len_trig(const XbArgs* __restrict__ ap, uint32_t* trig) {
+  const XbArgs& a = *ap;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < a.total; j = a.total) {
+    const uint32_t k = a.segid[j];
+    const int64_t s = a.segS[k], ck = a.segCk[k];
+    const int64_t na = xb_added_count(a.added_j, s, ck);
+    const int64_t o = j - s - na;
+    const uint32_t it = a.sp[j];
+    if (o >= 0 && (o + 1) % a.L == 0 && it >= (uint32_t)a.C) trig[a.irow[it]] = 1u;
+  }
+}
+
+// per flush (lengthBatch): its clock and in_seq, from the trigger row
+__global__ __launch_bounds__(kBlock) void k_xb_len_flushes(int64_t n, const uint32_t* trig, const uint32_t* fr,
+                                                           const int32_t* call_of, const int64_t* call_now, int64_t seq0,
+                                                           int64_t* fnow, int64_t* fseq) {
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r = n) {
+    if (!trig[r]) continue;
+    fnow[fr[r]] = call_now[call_of[r]];
+    fseq[fr[r]] = seq0 + r;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_xb_opp(const XbArgs* __restrict__ ap, int time_batch) {
+  const XbArgs& a = *ap;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < a.total; j = a.total) {
+    const uint32_t k = a.segid[j];
+    const int64_t s = a.segS[k], e = a.segS[k + 1], ck = a.segCk[k];
+    const int64_t na = xb_added_count(a.added_j, s, ck);
+    const uint32_t it = a.sp[j];
+    uint64_t ao = kNoOpp, eo = kNoOpp;
+    if (!time_batch) {
+      const int64_t tot = e - s - na;             // open batch + new items
+      const int64_t nb = tot / a.L;               // batches completed in this push
+      // flush of batch b: the trigger at ordinal (b + 1) L - 1
+      auto flush_of = [&](int64_t b) -> uint64_t {
+        return (uint64_t)a.fr[a.irow[a.sp[s + na + (b + 1) * a.L - 1]]];
+      };
+      if (j - s < na) {
+        if (a.expired_on && nb >= 1) eo = 2 * flush_of(0) + 1;
+      } else {
+        const int64_t b = (j - s - na) / a.L;
+        if (b < nb) ao = 2 * flush_of(b) + 1;
+        if (a.expired_on && b + 1 < nb) eo = 2 * flush_of(b + 1) + 1;
+      }
+    } else {
+      if (j - s < na) {
+        if (a.expired_on && a.nf >= 1) eo = 1;
+      } else {
+        const int64_t f = it < (uint32_t)a.C ? (a.nf >= 1 ? 0 : -1) : (int64_t)a.bflush[a.icall[it]];
+        if (f >= 0) {
+          ao = 2 * (uint64_t)f + 1;
+          if (a.expired_on && f + 1 < a.nf) eo = 2 * (uint64_t)(f + 1) + 1;
+        }
+      }
+    }
+    a.aopp[j] = ao;
+    a.eopp[j] = eo;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_xb_nops(int64_t total, const uint64_t* aopp, const uint64_t* eopp,
+                                                    uint32_t* nops) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j = total)
+    nops[j] = (aopp[j] != kNoOpp ? 1u : 0u) + (eopp[j] != kNoOpp ? 1u : 0u);
+}
+
+struct XbOpArgs {
+  int64_t total;
+  const uint32_t* sp;
+  const uint32_t* segid;
+  const int64_t* segS;
+  const int64_t* segCk;
+  const uint8_t* added_j;
+  const uint64_t* aopp;
+  const uint64_t* eopp;
+  const uint32_t* opscan;
+  const int64_t* fnow;
+  const int64_t* fseq;
+  int current_on, expired_on;
+  uint32_t* op_item;
+  uint8_t* op_add;
+  uint8_t* op_on;
+  uint32_t* op_chunk;
+  int64_t* op_now;
+  int64_t* op_seq;
+};
+
+// Operations of a key in the reference's order: per flush its expirations
+// (FIFO), then its adds (FIFO).  Adds occupy the contiguous positions
+// [s + a, ...), expirations a prefix [s, ...) of the segment.
+__global__ __launch_bounds__(kBlock) void k_xb_ops(const XbOpArgs* __restrict__ ap) {
+  const XbOpArgs& a = *ap;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < a.total; j = a.total) {
+    const uint32_t k = a.segid[j];
+    const int64_t s = a.segS[k], e = a.segS[k + 1], ck = a.segCk[k];
+    const int64_t base = a.opscan[s];
+    const int64_t na = xb_added_count(a.added_j, s, ck);
+    const uint32_t it = a.sp[j];
+    const uint64_t ao = a.aopp[j], eo = a.eopp[j];
+    if (ao != kNoOpp) {
+      int64_t lo = s, hi = e;   // expirations at or before this flush
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.eopp[mid] <= ao) lo = mid + 1;
+        else hi = mid;
+      }
+      const int64_t q = base + (j - s - na) + (lo - s);
+      const uint32_t f = (uint32_t)(ao >> 1);
+      a.op_item[q] = it;
+      a.op_add[q] = 1;
+      a.op_on[q] = (uint8_t)a.current_on;
+      a.op_chunk[q] = f;
+      a.op_now[q] = a.fnow[f];
+      a.op_seq[q] = a.fseq[f];
+    }
+    if (eo != kNoOpp) {
+      int64_t lo = s + na, hi = e;   // adds at earlier flushes
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.aopp[mid] < eo) lo = mid + 1;
+        else hi = mid;
+      }
+      const int64_t q = base + (j - s) + (lo - s - na);
+      const uint32_t f = (uint32_t)(eo >> 1);
+      a.op_item[q] = it;
+      a.op_add[q] = 0;
+      a.op_on[q] = (uint8_t)a.expired_on;
+      a.op_chunk[q] = f;
+      a.op_now[q] = a.fnow[f];
+      a.op_seq[q] = a.fseq[f];
+    }
+  }
+}
+
+// kept: the open batch, and (expired output) the last added batch awaiting
+// its expiry; added_out = the item has been added (carried as ilast = 1)
+__global__ __launch_bounds__(kBlock) void k_xb_keep(int64_t total, const uint8_t* added_j, const uint64_t* aopp,
+                                                    const uint64_t* eopp, int expired_on, uint32_t* keep,
+                                                    uint8_t* added_out) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j = total) {
+    const bool added = added_j[j] || aopp[j] != kNoOpp;
+    keep[j] = (!added || (expired_on && eopp[j] == kNoOpp)) ? 1u : 0u;
+    added_out[j] = added ? 1 : 0;
+  }
+}
+
+// timeBatch: per call its passing items and the in_seq of its last one
+__global__ __launch_bounds__(kBlock) void k_xb_call_items(int64_t C, int64_t m, const int32_t* icall,
+                                                          const int32_t* irow, int64_t seq0, uint32_t* ccount,
+                                                          int64_t* clast_seq) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j = m) {
+    const int32_t c = icall[C + j];
+    atomicAdd(ccount + c, 1u);
+    if (j + 1 == m || icall[C + j + 1] != c) clast_seq[c] = seq0 + irow[C + j];
+  }
+}
+
 int bits_for(uint64_t v) {
   int b = 0;
   while (b < 64 && (v >> b)) b++;
@@ -915,6 +1142,14 @@ struct WindowXEngine : Engine {
   // aggregator states [nagg][nstates]
   DevBuf g_dsum, g_lsum, g_cnt;
   int64_t nstates = 0;
+  // batch windows: per state its RESET epoch (k_xw_fold); timeBatch's
+  // processor-level nextEmitTime and the Scheduler's notify queue (FIFO)
+  bool batch = false;
+  int64_t wparam2 = 0;
+  DevBuf g_epoch;
+  int64_t tb_next = -1;
+  std::deque<int64_t> tb_notify;
+  DevBuf xb_added, xb_aopp, xb_trig, xb_fr, xb_fnow, xb_fseq, xb_bflush, xb_ccount, xb_clast, xb_added_out;
   // per-push scratch
   DevBuf d_offs, d_call_of, d_last, d_call_now, d_F, d_fnow, d_flags, d_cnt, d_off, d_pkey, d_start,
       d_run, d_runs_before, d_tot, d_scan, d_sort, kw, kn, kh, spk, spk2, sp, sp2, head, hscan, segS, segid, segCk,
@@ -944,11 +1179,14 @@ struct WindowXEngine : Engine {
     out.count = 0;
     counters = shd_counters{};
     last_global = INT64_MIN;
+    tb_next = -1;
+    tb_notify.clear();
     gd.reset(stream);
     if (nstates) {
       SHD_HIP(hipMemsetAsync(g_dsum.p, 0, g_dsum.cap, stream));
       SHD_HIP(hipMemsetAsync(g_lsum.p, 0, g_lsum.cap, stream));
       SHD_HIP(hipMemsetAsync(g_cnt.p, 0, g_cnt.cap, stream));
+      if (g_epoch.p) SHD_HIP(hipMemsetAsync(g_epoch.p, 0xFF, g_epoch.cap, stream));
     }
   }
 
@@ -1020,6 +1258,14 @@ struct WindowXEngine : Engine {
                              hipMemcpyDeviceToDevice, stream));
     }
     SHD_HIP(hipStreamSynchronize(stream));
+    if (batch) {
+      DevBuf ep;
+      ep.reserve((size_t)ns * 8);
+      SHD_HIP(hipMemsetAsync(ep.p, 0xFF, (size_t)ns * 8, stream));
+      if (nstates) SHD_HIP(hipMemcpyAsync(ep.p, g_epoch.p, nstates * 8, hipMemcpyDeviceToDevice, stream));
+      SHD_HIP(hipStreamSynchronize(stream));
+      std::swap(g_epoch.p, ep.p); std::swap(g_epoch.cap, ep.cap);
+    }
     std::swap(g_dsum.p, a.p); std::swap(g_dsum.cap, a.cap);
     std::swap(g_lsum.p, l.p); std::swap(g_lsum.cap, l.cap);
     std::swap(g_cnt.p, c.p); std::swap(g_cnt.cap, c.cap);
@@ -1056,7 +1302,8 @@ struct WindowXEngine : Engine {
 
   void set_time(int64_t t) override {
     if (t < now) return;
-    if (wkind == SHD_W_TIME && plan.expired_on) {
+    if ((wkind == SHD_W_TIME && plan.expired_on) ||
+        (wkind == SHD_W_TIME_BATCH && !tb_notify.empty() && tb_notify.front() <= t)) {
       Staged z;
       z.n = 0;
       z.call_offsets = {0, 0};
@@ -1095,6 +1342,7 @@ struct WindowXEngine : Engine {
     h_F.clear();
     h_fnow.clear();
     int64_t clk = now;
+    std::vector<char> moved(ncalls, 0);
     for (int c = 0; c < ncalls; c++) {
       int64_t t = INT64_MIN;
       bool move = false;
@@ -1109,6 +1357,7 @@ struct WindowXEngine : Engine {
         clk = t;
         h_F.push_back(c);
         h_fnow.push_back(t);
+        moved[c] = 1;
       }
       h_now[c] = clk;
     }
@@ -1254,11 +1503,16 @@ struct WindowXEngine : Engine {
       SHD_CHECK_LAUNCH();
     }
     mark("segments");
+    int64_t nt = 0, nflush = 0, nops = 0;
+    bool lane_ran = false;
+    if (batch) {
+      // ---- batch windows: flushes, opportunities, operations
+      nops = batch_operations(n, m, total, ncalls, moved, SP, nflush);
+      mark("operations");
+    } else {
     // ---- expiry opportunities
     eopp.reserve(std::max<int64_t>(total, 1) * 8);
     etid.reserve(std::max<int64_t>(total, 1) * 4);
-    int64_t nt = 0;
-    bool lane_ran = false;
     if (total > 0 && wkind == SHD_W_LENGTH) {
       hipLaunchKernelGGL(k_xw_len_expiry, dim3(grid_cover(total)), dim3(kBlock), 0, s, total, wparam,
                          (const int64_t*)segS.as<int64_t>(), (const uint32_t*)segid.as<uint32_t>(), SP,
@@ -1369,7 +1623,6 @@ struct WindowXEngine : Engine {
       SHD_HIP(hipMemsetAsync(d_runs_before.p, 0, (size_t)ncalls * 8, s));
     }
     // ---- operations in key-major order
-    int64_t nops = 0;
     nops_b.reserve(std::max<int64_t>(total, 1) * 4);
     opscan.reserve(std::max<int64_t>(total, 1) * 4);
     if (total > 0) {
@@ -1383,13 +1636,7 @@ struct WindowXEngine : Engine {
       d_start.reserve(n * 4);
       run_ids(n);
     }
-    const int64_t nop_alloc = std::max<int64_t>(nops, 1);
-    op_item.reserve(nop_alloc * 4);
-    op_add.reserve(nop_alloc);
-    op_on.reserve(nop_alloc);
-    op_chunk.reserve(nop_alloc * 4);
-    op_now.reserve(nop_alloc * 8);
-    op_seq.reserve(nop_alloc * 8);
+    reserve_ops(nops);
     if (nops > 0) {
       OpArgs oa{};
       oa.total = total;
@@ -1426,6 +1673,8 @@ struct WindowXEngine : Engine {
       SHD_CHECK_LAUNCH();
     }
     mark("operations");
+    }
+    const int64_t nop_alloc = std::max<int64_t>(nops, 1);
     // ---- selector: aggregator folds and the rows each chunk emits
     const int na = std::max(nagg, 1);
     rowflag.reserve(nop_alloc);
@@ -1459,6 +1708,8 @@ struct WindowXEngine : Engine {
     fa.dsum = g_dsum.as<double>();
     fa.lsum = g_lsum.as<int64_t>();
     fa.cnt = g_cnt.as<int64_t>();
+    fa.epoch = (batch && nagg > 0) ? g_epoch.as<int64_t>() : nullptr;
+    fa.chunk0 = chunk_seq;
     fa.resv = resv.as<uint64_t>();
     fa.resn = resn.as<uint8_t>();
     fa.rowflag = rowflag.as<uint8_t>();
@@ -1513,7 +1764,7 @@ struct WindowXEngine : Engine {
                          (const uint8_t*)rowflag.as<uint8_t>(), (const uint32_t*)roff.as<uint32_t>(),
                          (const uint32_t*)op_chunk.as<uint32_t>(), rkey.as<uint64_t>(), rq.as<uint32_t>());
       SHD_CHECK_LAUNCH();
-      const int64_t nchunks = nt + (partitioned ? (int64_t)nruns : (int64_t)ncalls);
+      const int64_t nchunks = batch ? nflush : nt + (partitioned ? (int64_t)nruns : (int64_t)ncalls);
       bool alt = false;
       radix_sort_pairs_u64(rkey.as<uint64_t>(), rq.as<uint32_t>(), rkey2.as<uint64_t>(), rq2.as<uint32_t>(), nrows,
                            32 + bits_for((uint64_t)nchunks), d_sort, s, alt);
@@ -1552,8 +1803,16 @@ struct WindowXEngine : Engine {
     if (total > 0) {
       keep.reserve(total * 4);
       koff.reserve(total * 4);
-      hipLaunchKernelGGL(k_xw_keep, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
-                         (const uint64_t*)eopp.as<uint64_t>(), wkind != 0 ? 1 : 0, keep.as<uint32_t>());
+      if (batch) {
+        xb_added_out.reserve(total);
+        hipLaunchKernelGGL(k_xb_keep, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
+                           (const uint8_t*)xb_added.as<uint8_t>(), (const uint64_t*)xb_aopp.as<uint64_t>(),
+                           (const uint64_t*)eopp.as<uint64_t>(), (int)plan.expired_on, keep.as<uint32_t>(),
+                           xb_added_out.as<uint8_t>());
+      } else {
+        hipLaunchKernelGGL(k_xw_keep, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
+                           (const uint64_t*)eopp.as<uint64_t>(), wkind != 0 ? 1 : 0, keep.as<uint32_t>());
+      }
       SHD_CHECK_LAUNCH();
       kept = scan(keep.as<uint32_t>(), koff.as<uint32_t>(), total);
     }
@@ -1570,6 +1829,7 @@ struct WindowXEngine : Engine {
       ca.koff = koff.as<uint32_t>();
       ca.segid = segid.as<uint32_t>();
       ca.last_out = lane_ran ? last_out.as<int64_t>() : nullptr;
+      ca.added_j = batch ? xb_added_out.as<uint8_t>() : nullptr;
       ca.pk = ipk[cur].as<uint64_t>(); ca.ts = its[cur].as<int64_t>(); ca.seq = iseq[cur].as<int64_t>();
       ca.sid = isid[cur].as<uint64_t>();
       ca.attr = iattr[cur].as<uint64_t>(); ca.nul = inul[cur].as<uint8_t>();
@@ -1604,9 +1864,186 @@ struct WindowXEngine : Engine {
     counters.matches += nrows;
     counters.carry = C;
     counters.partial_scans += nops;
-    chunk_seq += nt + (partitioned ? (int64_t)nruns : (int64_t)ncalls);
+    chunk_seq += batch ? nflush : nt + (partitioned ? (int64_t)nruns : (int64_t)ncalls);
     now = clk;
     seq += n;
+  }
+
+  void reserve_ops(int64_t nops) {
+    const int64_t nop_alloc = std::max<int64_t>(nops, 1);
+    op_item.reserve(nop_alloc * 4);
+    op_add.reserve(nop_alloc);
+    op_on.reserve(nop_alloc);
+    op_chunk.reserve(nop_alloc * 4);
+    op_now.reserve(nop_alloc * 8);
+    op_seq.reserve(nop_alloc * 8);
+  }
+
+  // TimeBatchWindowProcessor.process (:279-366) for one chunk at clock t:
+  // nextEmitTime set up by the first chunk; a flush when t reached it
+  bool tb_process(int64_t t) {
+    const int64_t T = wparam;
+    if (tb_next == -1) {
+      if (wparam2 != INT64_MIN) tb_next = t + (T - (t - wparam2) % T);   // getNextEmitTime (:368-373)
+      else tb_next = t + T;
+      tb_notify.push_back(tb_next);
+    }
+    if (t >= tb_next) {
+      tb_next += T;
+      tb_notify.push_back(tb_next);
+      return true;
+    }
+    return false;
+  }
+
+  // Batch windows: the push's flushes (chunk ordinals 0..nflush-1 in output
+  // order), each item's add / expiry flush, the operations in key-major
+  // order (k_xb_ops).  Returns the operation count.
+  int64_t batch_operations(int64_t n, int64_t m, int64_t total, int ncalls, const std::vector<char>& moved,
+                           const uint32_t* SP, int64_t& nflush) {
+    hipStream_t s = stream;
+    const int64_t ta = std::max<int64_t>(total, 1);
+    xb_added.reserve(ta);
+    xb_aopp.reserve(ta * 8);
+    eopp.reserve(ta * 8);
+    if (total > 0) {
+      hipLaunchKernelGGL(k_xb_added, dim3(grid_cover(total)), dim3(kBlock), 0, s, total, C, SP,
+                         (const int64_t*)ilast[cur].as<int64_t>(), xb_added.as<uint8_t>());
+      SHD_CHECK_LAUNCH();
+    }
+    XbArgs xb{};
+    xb.total = total;
+    xb.C = C;
+    xb.L = wparam;
+    xb.expired_on = plan.expired_on;
+    xb.sp = SP;
+    xb.segid = segid.as<uint32_t>();
+    xb.segS = segS.as<int64_t>();
+    xb.segCk = segCk.as<int64_t>();
+    xb.added_j = xb_added.as<uint8_t>();
+    xb.irow = irow[cur].as<int32_t>();
+    xb.icall = icall[cur].as<int32_t>();
+    xb.aopp = xb_aopp.as<uint64_t>();
+    xb.eopp = eopp.as<uint64_t>();
+    nflush = 0;
+    const bool tb = wkind == SHD_W_TIME_BATCH;
+    if (!tb) {
+      // lengthBatch: a flush per completed batch, ranked by its trigger row
+      xb_trig.reserve(std::max<int64_t>(n, 1) * 4);
+      xb_fr.reserve(std::max<int64_t>(n, 1) * 4);
+      if (n > 0) SHD_HIP(hipMemsetAsync(xb_trig.p, 0, n * 4, s));
+      if (total > 0) {
+        hipLaunchKernelGGL(k_xb_len_trig, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(xb),
+                           xb_trig.as<uint32_t>());
+        SHD_CHECK_LAUNCH();
+      }
+      nflush = n > 0 ? scan(xb_trig.as<uint32_t>(), xb_fr.as<uint32_t>(), n) : 0;
+      xb_fnow.reserve(std::max<int64_t>(nflush, 1) * 8);
+      xb_fseq.reserve(std::max<int64_t>(nflush, 1) * 8);
+      if (nflush > 0) {
+        hipLaunchKernelGGL(k_xb_len_flushes, dim3(grid_cover(n)), dim3(kBlock), 0, s, n,
+                           (const uint32_t*)xb_trig.as<uint32_t>(), (const uint32_t*)xb_fr.as<uint32_t>(),
+                           (const int32_t*)d_call_of.as<int32_t>(), (const int64_t*)d_call_now.as<int64_t>(), seq,
+                           xb_fnow.as<int64_t>(), xb_fseq.as<int64_t>());
+        SHD_CHECK_LAUNCH();
+      }
+      xb.fr = xb_fr.as<uint32_t>();
+    } else {
+      // timeBatch: the flush schedule is sequential in the chunks (calls and
+      // TIMER chunks), not in the events: run it on the host per call
+      xb_ccount.reserve((size_t)ncalls * 4);
+      xb_clast.reserve((size_t)ncalls * 8);
+      SHD_HIP(hipMemsetAsync(xb_ccount.p, 0, (size_t)ncalls * 4, s));
+      if (m > 0) {
+        hipLaunchKernelGGL(k_xb_call_items, dim3(grid_cover(m)), dim3(kBlock), 0, s, C, m,
+                           (const int32_t*)icall[cur].as<int32_t>(), (const int32_t*)irow[cur].as<int32_t>(), seq,
+                           xb_ccount.as<uint32_t>(), xb_clast.as<int64_t>());
+        SHD_CHECK_LAUNCH();
+      }
+      std::vector<uint32_t> cc(ncalls);
+      std::vector<int64_t> cl(ncalls);
+      h_pin.reserve((size_t)ncalls * 12);
+      SHD_HIP(hipMemcpyAsync(h_pin.p, xb_ccount.p, (size_t)ncalls * 4, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipMemcpyAsync(h_pin.as<char>() + (size_t)ncalls * 4, xb_clast.p, (size_t)ncalls * 8,
+                             hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipStreamSynchronize(s));
+      std::memcpy(cc.data(), h_pin.p, (size_t)ncalls * 4);
+      std::memcpy(cl.data(), h_pin.as<char>() + (size_t)ncalls * 4, (size_t)ncalls * 8);
+      std::vector<int32_t> bfl(ncalls, -1);
+      std::vector<int64_t> fn, fs;
+      std::vector<int> pending;
+      for (int c = 0; c < ncalls; c++) {
+        if (moved[c]) {
+          // Scheduler.sendTimerEvents (C/util/Scheduler.java:190-220): TIMER
+          // chunks while the queue head is due, each through the window
+          const int64_t t = h_now[c];
+          while (!tb_notify.empty() && tb_notify.front() <= t) {
+            tb_notify.pop_front();
+            if (tb_process(t)) {
+              for (int pc : pending) bfl[pc] = (int32_t)fn.size();
+              pending.clear();
+              fn.push_back(t);
+              fs.push_back(seq + h_offs[c]);
+            }
+          }
+        }
+        if (cc[c] > 0) {   // a chunk of events reaches the window
+          pending.push_back(c);
+          if (tb_process(h_now[c])) {
+            for (int pc : pending) bfl[pc] = (int32_t)fn.size();
+            pending.clear();
+            fn.push_back(h_now[c]);
+            fs.push_back(cl[c]);
+          }
+        }
+      }
+      nflush = (int64_t)fn.size();
+      upload(xb_bflush, bfl);
+      upload(xb_fnow, fn);
+      upload(xb_fseq, fs);
+      xb.bflush = xb_bflush.as<int32_t>();
+      xb.nf = nflush;
+    }
+    if (total > 0) {
+      hipLaunchKernelGGL(k_xb_opp, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(xb), tb ? 1 : 0);
+      SHD_CHECK_LAUNCH();
+    }
+    int64_t nops = 0;
+    nops_b.reserve(ta * 4);
+    opscan.reserve(ta * 4);
+    if (total > 0) {
+      hipLaunchKernelGGL(k_xb_nops, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
+                         (const uint64_t*)xb_aopp.as<uint64_t>(), (const uint64_t*)eopp.as<uint64_t>(),
+                         nops_b.as<uint32_t>());
+      SHD_CHECK_LAUNCH();
+      nops = scan(nops_b.as<uint32_t>(), opscan.as<uint32_t>(), total);
+    }
+    reserve_ops(nops);
+    if (nops > 0) {
+      XbOpArgs oa{};
+      oa.total = total;
+      oa.sp = SP;
+      oa.segid = segid.as<uint32_t>();
+      oa.segS = segS.as<int64_t>();
+      oa.segCk = segCk.as<int64_t>();
+      oa.added_j = xb_added.as<uint8_t>();
+      oa.aopp = xb_aopp.as<uint64_t>();
+      oa.eopp = eopp.as<uint64_t>();
+      oa.opscan = opscan.as<uint32_t>();
+      oa.fnow = xb_fnow.as<int64_t>();
+      oa.fseq = xb_fseq.as<int64_t>();
+      oa.current_on = plan.current_on;
+      oa.expired_on = plan.expired_on;
+      oa.op_item = op_item.as<uint32_t>();
+      oa.op_add = op_add.as<uint8_t>();
+      oa.op_on = op_on.as<uint8_t>();
+      oa.op_chunk = op_chunk.as<uint32_t>();
+      oa.op_now = op_now.as<int64_t>();
+      oa.op_seq = op_seq.as<int64_t>();
+      hipLaunchKernelGGL(k_xb_ops, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(oa));
+      SHD_CHECK_LAUNCH();
+    }
+    return nops;
   }
 
   // inclusive run id of each keyed event into d_start (k_xw_ops' run_of)
@@ -1722,6 +2159,11 @@ struct WindowXEngine : Engine {
       w.dev(g_cnt.p, (size_t)nagg * nstates * 8);
     }
     gd.save(w);
+    // batch windows: RESET epochs, timeBatch's nextEmitTime and notify queue
+    w.put<int64_t>(tb_next);
+    w.put<int64_t>((int64_t)tb_notify.size());
+    for (int64_t t : tb_notify) w.put<int64_t>(t);
+    if (batch && nagg > 0 && nstates > 0) w.dev(g_epoch.p, (size_t)nstates * 8);
   }
   void load_state(SnapR& r) override {
     const int64_t c0 = r.get<int64_t>();
@@ -1766,6 +2208,10 @@ struct WindowXEngine : Engine {
         g_dsum.reserve((size_t)nagg * ns * 8);
         g_lsum.reserve((size_t)nagg * ns * 8);
         g_cnt.reserve((size_t)nagg * ns * 8);
+        if (batch) {
+          g_epoch.release();
+          g_epoch.reserve((size_t)ns * 8);
+        }
         nstates = ns;
       }
       r.dev_into(g_dsum.p, (size_t)nagg * ns * 8);
@@ -1776,6 +2222,11 @@ struct WindowXEngine : Engine {
     }
     gd.nk = std::max(nw, 1);
     gd.load(r, stream);
+    tb_next = r.get<int64_t>();
+    tb_notify.clear();
+    const int64_t nn = r.get<int64_t>();
+    for (int64_t i = 0; i < nn; i++) tb_notify.push_back(r.get<int64_t>());
+    if (batch && nagg > 0 && nstates > 0) r.dev_into(g_epoch.p, (size_t)nstates * 8);
     counters.carry = C;
   }
 };
@@ -1795,10 +2246,14 @@ std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why) {
       seen_window = true;
       e->wkind = h.wkind;
       e->wparam = h.param;
+      e->wparam2 = h.param2;
     }
   }
   if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
   if (e->wkind == SHD_W_LENGTH && e->wparam <= 0) { why = "length(0) window"; return nullptr; }
+  e->batch = e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH;
+  if (e->wkind == SHD_W_TIME_LENGTH) { why = "timeLength window"; return nullptr; }
+  if (e->batch && e->wparam <= 0) { why = "batch window of size 0"; return nullptr; }
   if (e->wkind == SHD_W_TIME && e->wparam < 0) { why = "negative time window"; return nullptr; }
   if (p.outputs.size() > (size_t)kMaxCols) { why = "too many outputs"; return nullptr; }
   e->nagg = (int)p.aggs.size();

@@ -319,6 +319,8 @@ def window_of(qp) -> Optional[Tuple[str, int]]:
     from . import planner as pl
     for h in qp.plan.handlers:
         if h[0] == pl.H_WINDOW:
+            if h[1] not in (pl.W_LENGTH, pl.W_TIME):
+                raise pl.UnsupportedPlanException("slices with a halo need a sliding length / time window")
             return ("length" if h[1] == pl.W_LENGTH else "time", int(h[2]))
     return None
 
