@@ -328,6 +328,7 @@ struct LaneArgs {
   const int64_t* fnow;
   int nf;
   int64_t T;
+  int64_t L;                   // timeLength: the length bound (0: time window)
   int partitioned;
   int64_t last_global;         // unpartitioned: the window's lastTimestamp
   const int64_t* pv;           // pending notify values (sorted by key, then value)
@@ -425,8 +426,17 @@ __global__ __launch_bounds__(kBlock) void k_xw_time_lane(const LaneArgs* __restr
         a.etid[h] = kNoTimer;
         h++;
       }
+      // timeLength (TimeLengthWindowProcessor.java:160-178): a full window
+      // gives up its head to the add
+      if (a.L > 0 && y - h >= a.L) {
+        a.eopp[h] = oy;
+        a.etid[h] = kNoTimer;
+        h++;
+      }
       const int64_t tsy = a.its[a.sp[y]];
-      if (lastTs < tsy) {   // scheduler.notifyAt(ts + T) (:156-159)
+      // scheduler.notifyAt(ts + T): the time window when its lastTimestamp
+      // rises (TimeWindowProcessor :156-159), timeLength for every add (:177)
+      if (a.L > 0 || lastTs < tsy) {
         a.rec[y] = 1;
         lastTs = tsy;
         if (rnext < 0) rnext = y;
@@ -1163,6 +1173,8 @@ struct WindowXEngine : Engine {
   std::vector<int64_t> h_fnow;
 
   int kind() const override { return ENG_WINDOW; }
+  // sliding windows with timers: time, timeLength
+  bool time_like() const { return wkind == SHD_W_TIME || wkind == SHD_W_TIME_LENGTH; }
 
   // aggregates here always fold sequentially (bit-exact): the option is a no-op
   void set_option(const std::string& key, int64_t v) override {
@@ -1302,7 +1314,7 @@ struct WindowXEngine : Engine {
 
   void set_time(int64_t t) override {
     if (t < now) return;
-    if ((wkind == SHD_W_TIME && plan.expired_on) ||
+    if ((time_like() && plan.expired_on) ||
         (wkind == SHD_W_TIME_BATCH && !tb_notify.empty() && tb_notify.front() <= t)) {
       Staged z;
       z.n = 0;
@@ -1361,7 +1373,7 @@ struct WindowXEngine : Engine {
       }
       h_now[c] = clk;
     }
-    const bool timers = wkind == SHD_W_TIME && plan.expired_on;
+    const bool timers = time_like() && plan.expired_on;
     if (!timers) {   // clock moves only matter to the TIMER chunks
       h_F.clear();
       h_fnow.clear();
@@ -1518,7 +1530,7 @@ struct WindowXEngine : Engine {
                          (const int64_t*)segS.as<int64_t>(), (const uint32_t*)segid.as<uint32_t>(), SP,
                          (const int32_t*)irow[cur].as<int32_t>(), eopp.as<uint64_t>(), etid.as<uint32_t>());
       SHD_CHECK_LAUNCH();
-    } else if (total > 0 && wkind == SHD_W_TIME) {
+    } else if (total > 0 && time_like()) {
       const uint32_t room = nseg > 0 ? scan(proom.as<uint32_t>(), proom_off.as<uint32_t>(), nseg) : 0;
       rec.reserve(total);
       tF.reserve((np + m + 1) * 4);
@@ -1550,6 +1562,7 @@ struct WindowXEngine : Engine {
       la.fnow = d_fnow.as<int64_t>();
       la.nf = nf;
       la.T = wparam;
+      la.L = wkind == SHD_W_TIME_LENGTH ? wparam2 : 0;
       la.partitioned = partitioned;
       la.last_global = last_global;
       la.pv = pv.as<int64_t>();
@@ -1843,8 +1856,8 @@ struct WindowXEngine : Engine {
       SHD_CHECK_LAUNCH();
     }
     // time windows: notify entries still queued, the window's last time
-    if (wkind == SHD_W_TIME && timers) update_pending(nseg, nf, lane_ran);
-    if (wkind == SHD_W_TIME && !partitioned && lane_ran && nseg > 0) {
+    if (time_like() && timers) update_pending(nseg, nf, lane_ran);
+    if (time_like() && !partitioned && lane_ran && nseg > 0) {
       h_tot.reserve(64);
       SHD_HIP(hipMemcpyAsync(h_tot.p, last_out.p, 8, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipStreamSynchronize(s));
@@ -2252,7 +2265,10 @@ std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why) {
   if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
   if (e->wkind == SHD_W_LENGTH && e->wparam <= 0) { why = "length(0) window"; return nullptr; }
   e->batch = e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH;
-  if (e->wkind == SHD_W_TIME_LENGTH) { why = "timeLength window"; return nullptr; }
+  if (e->wkind == SHD_W_TIME_LENGTH && (e->wparam2 <= 0 || e->wparam < 0)) {
+    why = "timeLength window of length 0";
+    return nullptr;
+  }
   if (e->batch && e->wparam <= 0) { why = "batch window of size 0"; return nullptr; }
   if (e->wkind == SHD_W_TIME && e->wparam < 0) { why = "negative time window"; return nullptr; }
   if (p.outputs.size() > (size_t)kMaxCols) { why = "too many outputs"; return nullptr; }

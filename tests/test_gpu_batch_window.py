@@ -1,5 +1,6 @@
 """Batch windows on the device (window-x engine, engine_window.hip k_xb_*):
-lengthBatch and timeBatch in full-batch mode against the oracle's restatement
+lengthBatch and timeBatch in full-batch mode, and the timeLength sliding
+window (k_xw_time_lane with a length bound), against the oracle's restatement
 of the processors, row for row (values, timestamps, types, callback chunks),
 over several pushes: per-flush chunks of [expired previous batch] + RESET +
 [current batch], the selector's batch picks (last per group, first-seen
@@ -8,7 +9,8 @@ TIMER flushes (empty ones included) and start.time alignment, partitioned
 lengthBatch, and the state through snapshot / restore.
 
 Reference: C/query/processor/stream/window/LengthBatchWindowProcessor.java:153-243,
-TimeBatchWindowProcessor.java:279-373, C/util/Scheduler.java:71-220,
+TimeBatchWindowProcessor.java:279-373, TimeLengthWindowProcessor.java:139-188,
+C/util/Scheduler.java:71-220,
 C/query/selector/QuerySelector.java:271-373,
 C/query/selector/attribute/aggregator/AttributeAggregatorExecutor.java:144-150."""
 import numpy as np
@@ -44,6 +46,15 @@ APPS = [
      "count() as c insert all events into O;"),
     ("time-current", S + "@info(name = 'q') from S[price > 40]#window.timeBatch(500) select symbol, "
      "sum(price) as m insert into O;"),
+    # timeLength: a sliding window bounded by time and length (TIMER expiries too)
+    ("timelen-group", S + "@info(name = 'q') from S#window.timeLength(2 sec, 5) select symbol, sum(price) as s "
+     "group by symbol insert all events into O;"),
+    ("timelen-time", S + "@info(name = 'q') from S#window.timeLength(3, 1000) select symbol, price, count() as c "
+     "insert all events into O;"),
+    ("timelen-part", S + "partition with (symbol of S) begin @info(name = 'q') from S#window.timeLength(1 sec, 3) "
+     "select symbol, price, count() as c insert all events into O; end;"),
+    ("timelen-plain", S + "@info(name = 'q') from S#window.timeLength(40, 60) select symbol, price "
+     "insert expired events into O;"),
 ]
 
 
