@@ -2141,6 +2141,31 @@ struct Engine {
           }
         }
       }
+    } else if (window_kind == SHD_W_EXTERNAL_TIME) {
+      // ExternalTimeWindowProcessor.process (:124-158): the clock is each
+      // event's own LONG timestamp attribute; no scheduler
+      const int col = (int)window_param2;
+      const int64_t T = window_param;
+      for (Ev* e : in) {
+        if (e->type == TIMER) continue;
+        const int64_t currentTime = (int64_t)e->data[col];
+        while (!ks->q.empty()) {
+          Ev* x = ks->q.front();
+          if ((int64_t)x->data[col] - currentTime + T <= 0) {
+            ks->q.pop_front();
+            x->ts = currentTime;
+            out.push_back(x);
+          } else {
+            break;
+          }
+        }
+        if (e->type == CURRENT) {
+          Ev* c = clone_ev(e);
+          c->type = EXPIRED;
+          ks->q.push_back(c);
+        }
+        out.push_back(e);
+      }
     } else if (window_kind == SHD_W_TIME_LENGTH) {
       // TimeLengthWindowProcessor.process (:139-188): time expiry before each
       // event (TIMER events only expire), then the length bound; every added

@@ -4011,7 +4011,8 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
   e->partitioned = !p.part_keys.empty();
   bool needs_agg = e->nagg > 0 || !p.group_by.empty();
   // batch windows (flush chunks with RESET) and timeLength: the window-x engine
-  if (e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH || e->wkind == SHD_W_TIME_LENGTH)
+  if (e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH || e->wkind == SHD_W_TIME_LENGTH ||
+      e->wkind == SHD_W_EXTERNAL_TIME)
     return make_window_x_engine(p, why);
   // EXPIRED output, `having`, no CURRENT output, aggregation inside a
   // partition: the keyed exact window engine (engine_window.hip)

@@ -329,6 +329,9 @@ struct LaneArgs {
   int nf;
   int64_t T;
   int64_t L;                   // timeLength: the length bound (0: time window)
+  int ext_col;                 // externalTime: the item attribute holding its time (-1: the clock)
+  const uint64_t* iattr;       // [ncols][cap]
+  int64_t cap;
   int partitioned;
   int64_t last_global;         // unpartitioned: the window's lastTimestamp
   const int64_t* pv;           // pending notify values (sorted by key, then value)
@@ -419,9 +422,12 @@ __global__ __launch_bounds__(kBlock) void k_xw_time_lane(const LaneArgs* __restr
         fi = lo + 1;
       }
       if (y >= e) break;
-      const int64_t nowy = a.call_now[cy];
+      // externalTime (ExternalTimeWindowProcessor.java:128-149): each event's
+      // own time attribute is the clock, items expire by theirs
+      const int64_t nowy = a.ext_col >= 0 ? (int64_t)a.iattr[(int64_t)a.ext_col * a.cap + a.sp[y]] : a.call_now[cy];
       const uint64_t oy = 2ull * (uint64_t)a.irow[a.sp[y]] + 1ull;
-      while (h < y && a.its[a.sp[h]] + a.T <= nowy) {
+      while (h < y && (a.ext_col >= 0 ? (int64_t)a.iattr[(int64_t)a.ext_col * a.cap + a.sp[h]] : a.its[a.sp[h]]) + a.T <=
+                          nowy) {
         a.eopp[h] = oy;
         a.etid[h] = kNoTimer;
         h++;
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(kBlock) void k_xw_time_lane(const LaneArgs* __restr
       const int64_t tsy = a.its[a.sp[y]];
       // scheduler.notifyAt(ts + T): the time window when its lastTimestamp
       // rises (TimeWindowProcessor :156-159), timeLength for every add (:177)
-      if (a.L > 0 || lastTs < tsy) {
+      if (a.ext_col < 0 && (a.L > 0 || lastTs < tsy)) {
         a.rec[y] = 1;
         lastTs = tsy;
         if (rnext < 0) rnext = y;
@@ -520,6 +526,7 @@ struct OpArgs {
   const int32_t* sF;          // sorted timers' calls
   int64_t nt;
   const uint64_t* runs_before;   // per call: partition runs in earlier calls
+  const int64_t* row_now;     // externalTime: per batch row its time attribute (null: the call's clock)
   int partitioned;
   int current_on, expired_on;
   int64_t seq0;
@@ -589,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void k_xw_ops(const OpArgs* __restrict__ ap
       if (tid == kNoTimer) {
         const int64_t r = (int64_t)((o - 1) >> 1);
         a.op_chunk[q] = event_ordinal(a, r);
-        a.op_now[q] = a.call_now[a.call_of[r]];
+        a.op_now[q] = a.row_now ? a.row_now[r] : a.call_now[a.call_of[r]];
         a.op_seq[q] = a.seq0 + r;
       } else {
         const uint32_t t = a.trank[tid];
@@ -1174,7 +1181,9 @@ struct WindowXEngine : Engine {
 
   int kind() const override { return ENG_WINDOW; }
   // sliding windows with timers: time, timeLength
-  bool time_like() const { return wkind == SHD_W_TIME || wkind == SHD_W_TIME_LENGTH; }
+  bool time_like() const { return timed() || wkind == SHD_W_EXTERNAL_TIME; }
+  // with Scheduler TIMER chunks
+  bool timed() const { return wkind == SHD_W_TIME || wkind == SHD_W_TIME_LENGTH; }
 
   // aggregates here always fold sequentially (bit-exact): the option is a no-op
   void set_option(const std::string& key, int64_t v) override {
@@ -1314,7 +1323,7 @@ struct WindowXEngine : Engine {
 
   void set_time(int64_t t) override {
     if (t < now) return;
-    if ((time_like() && plan.expired_on) ||
+    if ((timed() && plan.expired_on) ||
         (wkind == SHD_W_TIME_BATCH && !tb_notify.empty() && tb_notify.front() <= t)) {
       Staged z;
       z.n = 0;
@@ -1373,7 +1382,7 @@ struct WindowXEngine : Engine {
       }
       h_now[c] = clk;
     }
-    const bool timers = time_like() && plan.expired_on;
+    const bool timers = timed() && plan.expired_on;
     if (!timers) {   // clock moves only matter to the TIMER chunks
       h_F.clear();
       h_fnow.clear();
@@ -1563,6 +1572,9 @@ struct WindowXEngine : Engine {
       la.nf = nf;
       la.T = wparam;
       la.L = wkind == SHD_W_TIME_LENGTH ? wparam2 : 0;
+      la.ext_col = wkind == SHD_W_EXTERNAL_TIME ? (int)wparam2 : -1;
+      la.iattr = iattr[cur].as<uint64_t>();
+      la.cap = cap;
       la.partitioned = partitioned;
       la.last_global = last_global;
       la.pv = pv.as<int64_t>();
@@ -1673,6 +1685,7 @@ struct WindowXEngine : Engine {
       oa.nt = nt;
       oa.runs_before = d_runs_before.as<uint64_t>();
       oa.partitioned = partitioned;
+      oa.row_now = wkind == SHD_W_EXTERNAL_TIME ? reinterpret_cast<const int64_t*>(b.cs.col[wparam2]) : nullptr;
       oa.current_on = plan.current_on;
       oa.expired_on = plan.expired_on;
       oa.seq0 = seq;
@@ -2265,6 +2278,10 @@ std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why) {
   if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
   if (e->wkind == SHD_W_LENGTH && e->wparam <= 0) { why = "length(0) window"; return nullptr; }
   e->batch = e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH;
+  if (e->wkind == SHD_W_EXTERNAL_TIME && (e->wparam2 < 0 || e->wparam2 >= e->ncols)) {
+    why = "externalTime attribute";
+    return nullptr;
+  }
   if (e->wkind == SHD_W_TIME_LENGTH && (e->wparam2 <= 0 || e->wparam < 0)) {
     why = "timeLength window of length 0";
     return nullptr;

@@ -40,7 +40,7 @@ TYPE_NAME[T_OBJECT] = "object"
 IDX_CURRENT, IDX_LAST = -1, -2
 NODE_STREAM, NODE_NEXT, NODE_EVERY, NODE_LOGICAL, NODE_COUNT = 1, 2, 3, 4, 5
 H_FILTER, H_WINDOW = 1, 2
-W_LENGTH, W_TIME, W_LENGTH_BATCH, W_TIME_BATCH, W_TIME_LENGTH = 1, 2, 3, 4, 5
+W_LENGTH, W_TIME, W_LENGTH_BATCH, W_TIME_BATCH, W_TIME_LENGTH, W_EXTERNAL_TIME = 1, 2, 3, 4, 5, 6
 INT64_MIN = -(1 << 63)
 AGG_SUM, AGG_AVG, AGG_COUNT = 1, 2, 3
 UNKNOWN_STATE = -1
@@ -753,7 +753,7 @@ def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
             n_windows += 1
             if n_windows > 1:
                 raise SiddhiAppValidationException("only one window per stream")
-            plan.handlers.append(_window_handler(h, partition is not None))
+            plan.handlers.append(_window_handler(h, partition is not None, m, si.stream))
     names, types = _plan_selector(plan, q, ec, [m], False)
     _plan_partition(plan, None, partition, [si.stream], app, dictionary, extra_streams)
     plan.target = q.target
@@ -762,7 +762,7 @@ def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
                      partition is not None, {si.stream: "single"})
 
 
-def _window_handler(h, partitioned: bool):
+def _window_handler(h, partitioned: bool, meta=None, stream=None):
     """(H_WINDOW, kind, p, q) of a `#window.<name>(...)` handler (include/siddhi_ir.h
     shd_window).  Batch windows in full-batch mode only: `stream.current.event`
     true (ProcessingMode.RESET) is refused, and so is `timeBatch` inside a
@@ -813,6 +813,17 @@ def _window_handler(h, partitioned: bool):
         t = int(const(0, ("int", "long"), "window.time"))
         n = int(const(1, ("int",), "window.length"))
         return (H_WINDOW, W_TIME_LENGTH, t, n)
+    if h.name == "externaltime":
+        if len(ps) != 2:
+            raise SiddhiAppValidationException("ExternalTime window should only have two parameters")
+        v = ps[0]
+        if not isinstance(v, qc.Var) or v.index is not None or v.stream not in (None, stream, meta.ref):
+            raise SiddhiAppValidationException("ExternalTime window's timeStamp should be a stream attribute")
+        names = [a for a, _ in meta.attrs]
+        if v.attr not in names or dict(meta.attrs)[v.attr] != T_LONG:
+            raise SiddhiAppValidationException("ExternalTime window's timeStamp should be type long")
+        t = int(const(1, ("int", "long"), "window.time"))
+        return (H_WINDOW, W_EXTERNAL_TIME, t, names.index(v.attr))
     raise UnsupportedPlanException("window %s is outside the hot path" % h.name)
 
 

@@ -485,6 +485,8 @@ class Parser:
                 saw_not = True
             elif depth == 0 and t.text == "=" and self.toks[j - 1].kind == "id":
                 saw_eq = True
+            elif depth == 0 and t.kind == "id" and t.low in ("join", "unidirectional"):
+                raise OutOfScopeSyntax("joins are outside the hot path")
             j += 1
         if saw_arrow or (saw_every and not saw_comma) or (saw_not and not saw_comma) or (saw_eq and not saw_comma):
             el = self.pattern_chain()

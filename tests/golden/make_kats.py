@@ -36,6 +36,10 @@ FILES = [
     "query/partition/WindowPartitionTestCase.java",
     "query/window/LengthWindowTestCase.java",
     "query/window/TimeWindowTestCase.java",
+    "query/window/LengthBatchWindowTestCase.java",
+    "query/window/TimeBatchWindowTestCase.java",
+    "query/window/TimeLengthWindowTestCase.java",
+    "query/window/ExternalTimeWindowTestCase.java",
     "query/GroupByTestCase.java",
     "query/FilterTestCase1.java",
     "query/FilterTestCase2.java",
@@ -472,10 +476,20 @@ def extract(name, body, line, fname):
     expected = list(tu_expected)
     cells = []
     # per-callback cell checks: "X".equals(inEvents[0].getData(k)) / assertEquals("X", inEvents[0].getData(k).toString())
+    def _conditional(at):
+        # inside `if (<condition on the event>) { ... }`: not a check of every chunk
+        pre = cbody[:at].rstrip()
+        if pre.endswith("AssertJUnit."):
+            pre = pre[:-len("AssertJUnit.")].rstrip()
+        k = pre.rfind("if (")
+        return pre.endswith("{") and k >= 0 and ";" not in pre[k:]
+
     for cm_ in re.finditer(r'assertTrue\("([^"]*)"\.equals\(inEvents\[0\]\.getData\((\d+)\)\)\)', cbody):
-        cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
+        if not _conditional(cm_.start()):
+            cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
     for cm_ in re.finditer(r'assertEquals\("([^"]*)",\s*inEvents\[0\]\.getData\((\d+)\)\.toString\(\)\)', cbody):
-        cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
+        if not _conditional(cm_.start()):
+            cells.append({"which": "first_of_each", "col": int(cm_.group(2)), "value": cm_.group(1)})
     cases = re.split(r"case (\d+):", cbody)
     if len(cases) > 1:
         for k in range(1, len(cases), 2):

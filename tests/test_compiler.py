@@ -56,7 +56,7 @@ def test_last_index_inside_own_filter_stays_previous():
 
 def test_unsupported_reports_reason():
     with pytest.raises(pl.UnsupportedPlanException):
-        plan_of("define stream A (x int); from A#window.externalTime(x, 1 sec) select x insert into O;")
+        plan_of("define stream A (x int); from A#window.frequent(2) select x insert into O;")
     with pytest.raises(pl.UnsupportedPlanException):   # full-batch mode only
         plan_of("define stream A (x int); from A#window.lengthBatch(4, true) select x insert into O;")
 

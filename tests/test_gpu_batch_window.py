@@ -120,3 +120,32 @@ def test_batch_window_snapshot_restore(hip_available, idx):
     dq2.close()
     dev = concat_rows([p for p in parts if p is not None])
     assert_same_rows(dev, ora)
+
+
+SE = "@app:playback define stream S (symbol string, price float, volume int, et long); "
+EXT_APPS = [
+    ("ext-group", SE + "@info(name = 'q') from S#window.externalTime(et, 30) select symbol, sum(price) as s "
+     "group by symbol insert all events into O;"),
+    ("ext-part", SE + "partition with (symbol of S) begin @info(name = 'q') from S#window.externalTime(et, 1 sec) "
+     "select symbol, et, price insert all events into O; end;"),
+    ("ext-plain", SE + "@info(name = 'q') from S[volume > 100]#window.externalTime(et, 7) select symbol, et "
+     "insert expired events into O;"),
+]
+
+
+@pytest.mark.parametrize("name,app", EXT_APPS, ids=[a[0] for a in EXT_APPS])
+def test_external_time_window_equals_oracle(hip_available, name, app):
+    """externalTime: the window's clock is each event's own LONG attribute
+    (here the arrival time plus a jitter of up to 6 ms, so it steps back now
+    and then), no scheduler (ExternalTimeWindowProcessor.java:124-158)."""
+    from siddhi_amd.runtime import ColumnBatch
+    qp, d = compile_single_query(app)
+    wl.register_symbols(d, 12)
+    out = []
+    for _, b in gapped_batches(12000, 12, seed=9):
+        et = (b.ts + (b.cols[2] % 7)).astype(np.int64)
+        out.append((0, ColumnBatch(b.ts, b.cols + [et], [None] * 4, b.call_offsets)))
+    ora = run_oracle(qp, out)
+    dev, _, _ = run_device(qp, out)
+    assert len(ora[2]) > 0 and (ora[1] == 1).any()
+    assert_same_rows(dev, ora)
