@@ -109,13 +109,15 @@ enum shd_node { SHD_NODE_STREAM = 1, SHD_NODE_NEXT = 2, SHD_NODE_EVERY = 3,
 
 enum shd_handler { SHD_H_FILTER = 1, SHD_H_WINDOW = 2 };
 /* Windows (C/query/processor/stream/window/): p = length or time (ms); q:
- *   LENGTH_BATCH  q = 0 (LengthBatchWindowProcessor.java:153-243, full-batch mode)
+ *   LENGTH_BATCH  q = 1: stream.current.event, else 0 (LengthBatchWindowProcessor.java:153-274;
+ *                 p = 0: processLengthZeroBatch)
  *   TIME_BATCH    q = start.time, or INT64_MIN when absent (TimeBatchWindowProcessor.java:279-366)
+ *   TIME_BATCH_STREAM  the same with stream.current.event
  *   TIME_LENGTH   q = window.length (TimeLengthWindowProcessor.java:139-188)
  *   EXTERNAL_TIME q = the LONG attribute holding the event time (ExternalTimeWindowProcessor.java:124-158)
  *   LENGTH / TIME q = 0 */
 enum shd_window { SHD_W_LENGTH = 1, SHD_W_TIME = 2, SHD_W_LENGTH_BATCH = 3, SHD_W_TIME_BATCH = 4,
-                  SHD_W_TIME_LENGTH = 5, SHD_W_EXTERNAL_TIME = 6 };
+                  SHD_W_TIME_LENGTH = 5, SHD_W_EXTERNAL_TIME = 6, SHD_W_TIME_BATCH_STREAM = 7 };
 enum shd_agg { SHD_AGG_SUM = 1, SHD_AGG_AVG = 2, SHD_AGG_COUNT = 3 };
 
 /* Output / input event types (ComplexEvent.Type). */

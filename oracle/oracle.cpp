@@ -1849,7 +1849,8 @@ struct Engine {
   // in_seq of the rows of a batch window's flush chunk (the emitting event)
   int64_t flush_seq = -1;
   bool batch_window() const {
-    return window_kind == SHD_W_LENGTH_BATCH || window_kind == SHD_W_TIME_BATCH;
+    return window_kind == SHD_W_LENGTH_BATCH || window_kind == SHD_W_TIME_BATCH ||
+           window_kind == SHD_W_TIME_BATCH_STREAM;
   }
 
   void build_single() {
@@ -2070,6 +2071,53 @@ struct Engine {
   std::vector<std::pair<std::vector<Ev*>, int64_t>> batch_process(KeySingle* ks, const std::vector<Ev*>& in) {
     std::vector<std::pair<std::vector<Ev*>, int64_t>> res;
     const int64_t currentTime = now;
+    if (window_kind == SHD_W_LENGTH_BATCH && window_param == 0) {
+      // processLengthZeroBatch (:189-204): every event its own chunk -- the
+      // event, its EXPIRED copy, RESET
+      for (Ev* e : in) {
+        std::vector<Ev*> out{e};
+        if (p.expired_on) {
+          Ev* x = clone_ev(e);
+          x->type = EXPIRED;
+          x->ts = currentTime;
+          out.push_back(x);
+        }
+        out.push_back(reset_event());
+        res.push_back({out, e->seq});
+      }
+      return res;
+    }
+    if (window_kind == SHD_W_LENGTH_BATCH && (window_param2 & 1)) {
+      // processStreamCurrentEvents (:245-274): each event passes at once (its
+      // own chunk); the (length+1)-th expires the previous batch and RESETs first
+      for (Ev* e : in) {
+        ks->reset_pending = true;
+        ks->count++;
+        std::vector<Ev*> out;
+        if (ks->count == window_param + 1) {
+          if (p.expired_on && !ks->exp_q.empty()) {
+            for (Ev* x : ks->exp_q) {
+              x->ts = currentTime;
+              out.push_back(x);
+            }
+            ks->exp_q.clear();
+          }
+          if (ks->reset_pending) {
+            out.push_back(reset_event());
+            ks->reset_pending = false;
+          }
+          ks->count = 1;
+        }
+        out.push_back(e);
+        if (p.expired_on) {
+          Ev* x = clone_ev(e);
+          x->type = EXPIRED;
+          ks->exp_q.push_back(x);
+        }
+        res.push_back({out, e->seq});
+      }
+      return res;
+    }
     if (window_kind == SHD_W_LENGTH_BATCH) {
       // LengthBatchWindowProcessor.processFullBatchEvents (:206-243), length >= 1
       for (Ev* e : in) {
@@ -2102,6 +2150,37 @@ struct Engine {
       send = true;
     }
     int64_t last_seq = cur_seq;
+    if (window_kind == SHD_W_TIME_BATCH_STREAM) {
+      // stream.current.event: the chunk's events stay in it (CURRENT); a flush
+      // appends every event since the last one as EXPIRED, then RESET
+      std::vector<Ev*> out;
+      for (Ev* e : in) {
+        if (e->type != CURRENT) continue;
+        ks->reset_pending = true;
+        if (p.expired_on) {
+          Ev* x = clone_ev(e);
+          x->type = EXPIRED;
+          ks->exp_q.push_back(x);
+        }
+        out.push_back(e);
+        last_seq = e->seq;
+      }
+      if (send) {
+        if (p.expired_on && !ks->exp_q.empty()) {
+          for (Ev* x : ks->exp_q) {
+            x->ts = currentTime;
+            out.push_back(x);
+          }
+          ks->exp_q.clear();
+        }
+        if (ks->reset_pending) {
+          out.push_back(reset_event());
+          ks->reset_pending = false;
+        }
+      }
+      if (!out.empty()) res.push_back({out, last_seq});
+      return res;
+    }
     for (Ev* e : in) {
       if (e->type != CURRENT) continue;
       ks->reset_pending = true;
@@ -2299,7 +2378,9 @@ struct Engine {
   }
 
   void single_on_time_change(int64_t t) {
-    if (window_kind != SHD_W_TIME && window_kind != SHD_W_TIME_BATCH && window_kind != SHD_W_TIME_LENGTH) return;
+    if (window_kind != SHD_W_TIME && window_kind != SHD_W_TIME_BATCH && window_kind != SHD_W_TIME_LENGTH &&
+        window_kind != SHD_W_TIME_BATCH_STREAM)
+      return;
     // Scheduler.onTimeChange: states with head notify <= t, sorted by time.
     std::vector<std::pair<int64_t, KeySingle*>> due;
     if (partitioned) {

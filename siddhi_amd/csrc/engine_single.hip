@@ -4012,7 +4012,7 @@ std::unique_ptr<Engine> make_single_engine(const Plan& p, std::string& why) {
   bool needs_agg = e->nagg > 0 || !p.group_by.empty();
   // batch windows (flush chunks with RESET) and timeLength: the window-x engine
   if (e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH || e->wkind == SHD_W_TIME_LENGTH ||
-      e->wkind == SHD_W_EXTERNAL_TIME)
+      e->wkind == SHD_W_EXTERNAL_TIME || e->wkind == SHD_W_TIME_BATCH_STREAM)
     return make_window_x_engine(p, why);
   // EXPIRED output, `having`, no CURRENT output, aggregation inside a
   // partition: the keyed exact window engine (engine_window.hip)

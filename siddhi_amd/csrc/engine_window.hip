@@ -647,7 +647,7 @@ struct FoldArgsX {
   // batch windows: the chunk of a state's last RESET-started add (RESET clears
   // every group state of the partition; applied when the state is next added to)
   int64_t* epoch;     // [nstates], null: no batch window
-  int64_t chunk0;
+  const int64_t* op_epoch;   // per add: the RESET epoch it folds in
   uint64_t* resv;     // [nagg][nops]
   uint8_t* resn;
   uint8_t* rowflag;   // [nops]
@@ -686,9 +686,9 @@ __global__ __launch_bounds__(kBlock) void k_xw_fold(const FoldArgsX* __restrict_
       const uint32_t q = sq[p];
       const uint32_t it = a.op_item[q];
       const bool add = a.op_add[q];
-      if (a.epoch && add && ep != a.chunk0 + (int64_t)a.op_chunk[q]) {
-        // the flush's RESET came after this state's last operation
-        ep = a.chunk0 + (int64_t)a.op_chunk[q];
+      if (a.epoch && add && ep != a.op_epoch[q]) {
+        // a RESET came after this state's last operation
+        ep = a.op_epoch[q];
         for (int g = 0; g < a.nagg; g++) {
           d[g] = 0.0;
           l[g] = 0;
@@ -827,7 +827,7 @@ struct CarryArgs {
   const uint32_t* koff;
   const uint32_t* segid;
   const int64_t* last_out;   // per segment (time windows), may be null
-  const uint8_t* added_j;    // batch windows: per sorted position, carried as ilast (0 / 1)
+  const int64_t* last_j;     // batch windows: per sorted position, its ilast in the carry
   const uint64_t* pk; const int64_t* ts; const int64_t* seq; const uint64_t* sid;
   const uint64_t* attr; const uint8_t* nul; const uint64_t* argv; const uint8_t* argn;
   uint64_t* d_pk; int64_t* d_ts; int64_t* d_seq; uint64_t* d_sid; int64_t* d_last; int32_t* d_call; int32_t* d_row;
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void k_xw_carry(const CarryArgs* __restrict
     a.d_ts[t] = a.ts[it];
     a.d_seq[t] = a.seq[it];
     a.d_sid[t] = a.sid[it];
-    a.d_last[t] = a.added_j ? (int64_t)a.added_j[j] : (a.last_out ? a.last_out[a.segid[j]] : INT64_MIN);
+    a.d_last[t] = a.last_j ? a.last_j[j] : (a.last_out ? a.last_out[a.segid[j]] : INT64_MIN);
     a.d_call[t] = -1;
     a.d_row[t] = -1;
     for (int c = 0; c < a.ncols; c++) {
@@ -963,9 +963,23 @@ struct XbArgs {
   const uint32_t* fr;        // lengthBatch: flush rank of each batch row (exclusive scan of the triggers)
   const int32_t* bflush;     // timeBatch: per call, the flush its events join (-1: none in this push)
   int64_t nf;                // timeBatch: flushes of this push
+  // stream.current.event timeBatch: per call its chunk, the first flush at or
+  // after it and its RESET epoch; the push's first flush (carried items)
+  const int32_t* cchunk;
+  const int32_t* cflush;
+  const int64_t* cepoch;
+  int64_t first_flush;
+  const int64_t* ilast;      // carried items' ilast (lengthBatch stream mode: their batch epoch)
+  int64_t chunk0;            // global id of the push's first chunk
   uint64_t* aopp;
   uint64_t* eopp;
+  int64_t* epoch_j;          // per sorted position: the RESET epoch its add folds in
+  uint8_t* keep_j;           // carried to the next push
+  int64_t* last_j;           // its ilast there
 };
+
+// batch window modes (WindowXEngine::bmode)
+enum : int { XB_FULL_LEN = 0, XB_FULL_TIME = 1, XB_STREAM_LEN = 2, XB_ZERO_LEN = 3, XB_STREAM_TIME = 4 };
 
 // lengthBatch triggers: the new item whose open-batch ordinal completes a batch
 __global__ __launch_bounds__(kBlock) void k_xb_len_trig(const XbArgs* __restrict__ ap, uint32_t* trig) {
@@ -991,41 +1005,97 @@ __global__ __launch_bounds__(kBlock) void k_xb_len_flushes(int64_t n, const uint
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_xb_opp(const XbArgs* __restrict__ ap, int time_batch) {
+// Each item's add / expiry opportunities (op positions: 2 * chunk + 1 when
+// expirations come first in the chunk, 2 * chunk for an add before them),
+// the epoch of its add and what is carried.
+__global__ __launch_bounds__(kBlock) void k_xb_opp(const XbArgs* __restrict__ ap, int mode) {
   const XbArgs& a = *ap;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < a.total; j = a.total) {
     const uint32_t k = a.segid[j];
     const int64_t s = a.segS[k], e = a.segS[k + 1], ck = a.segCk[k];
-    const int64_t na = xb_added_count(a.added_j, s, ck);
     const uint32_t it = a.sp[j];
     uint64_t ao = kNoOpp, eo = kNoOpp;
-    if (!time_batch) {
-      const int64_t tot = e - s - na;             // open batch + new items
-      const int64_t nb = tot / a.L;               // batches completed in this push
-      // flush of batch b: the trigger at ordinal (b + 1) L - 1
-      auto flush_of = [&](int64_t b) -> uint64_t {
-        return (uint64_t)a.fr[a.irow[a.sp[s + na + (b + 1) * a.L - 1]]];
-      };
-      if (j - s < na) {
-        if (a.expired_on && nb >= 1) eo = 2 * flush_of(0) + 1;
+    int64_t ep = -1, last = 0;
+    bool keep = false;
+    if (mode == XB_FULL_LEN || mode == XB_FULL_TIME) {
+      // full batches: [expired previous batch] RESET [batch] at each flush
+      const int64_t na = xb_added_count(a.added_j, s, ck);
+      if (mode == XB_FULL_LEN) {
+        const int64_t tot = e - s - na;             // open batch + new items
+        const int64_t nb = tot / a.L;               // batches completed in this push
+        // flush of batch b: the trigger at ordinal (b + 1) L - 1
+        auto flush_of = [&](int64_t b) -> uint64_t {
+          return (uint64_t)a.fr[a.irow[a.sp[s + na + (b + 1) * a.L - 1]]];
+        };
+        if (j - s < na) {
+          if (a.expired_on && nb >= 1) eo = 2 * flush_of(0) + 1;
+        } else {
+          const int64_t b = (j - s - na) / a.L;
+          if (b < nb) ao = 2 * flush_of(b) + 1;
+          if (a.expired_on && b + 1 < nb) eo = 2 * flush_of(b + 1) + 1;
+        }
       } else {
-        const int64_t b = (j - s - na) / a.L;
-        if (b < nb) ao = 2 * flush_of(b) + 1;
-        if (a.expired_on && b + 1 < nb) eo = 2 * flush_of(b + 1) + 1;
-      }
-    } else {
-      if (j - s < na) {
-        if (a.expired_on && a.nf >= 1) eo = 1;
-      } else {
-        const int64_t f = it < (uint32_t)a.C ? (a.nf >= 1 ? 0 : -1) : (int64_t)a.bflush[a.icall[it]];
-        if (f >= 0) {
-          ao = 2 * (uint64_t)f + 1;
-          if (a.expired_on && f + 1 < a.nf) eo = 2 * (uint64_t)(f + 1) + 1;
+        if (j - s < na) {
+          if (a.expired_on && a.nf >= 1) eo = 1;
+        } else {
+          const int64_t f = it < (uint32_t)a.C ? (a.nf >= 1 ? 0 : -1) : (int64_t)a.bflush[a.icall[it]];
+          if (f >= 0) {
+            ao = 2 * (uint64_t)f + 1;
+            if (a.expired_on && f + 1 < a.nf) eo = 2 * (uint64_t)(f + 1) + 1;
+          }
         }
       }
+      if (ao != kNoOpp) ep = a.chunk0 + (int64_t)(ao >> 1);   // the flush's RESET precedes its adds
+      const bool added = a.added_j[j] || ao != kNoOpp;
+      keep = !added || (a.expired_on && eo == kNoOpp);
+      last = added ? 1 : 0;
+    } else if (mode == XB_STREAM_LEN) {
+      // processStreamCurrentEvents: every event its own chunk (a new item's
+      // rank); batch b of the key = ordinals [bL, (b+1)L) with the carried open
+      // batch first; the first item of batch b + 1 expires batch b and RESETs
+      // before its own add
+      const int64_t o = j - s, bl = (e - s - 1) / a.L, b = o / a.L;
+      if (o >= ck) ao = 2 * (uint64_t)(it - (uint32_t)a.C) + 1;
+      if (a.expired_on && b < bl) eo = 2 * (uint64_t)(a.sp[s + (b + 1) * a.L] - (uint32_t)a.C) + 1;
+      const int64_t f = s + b * a.L;   // the batch's first item
+      ep = f < s + ck ? a.ilast[a.sp[f]] : a.chunk0 + (int64_t)(a.sp[f] - (uint32_t)a.C);
+      keep = b == bl;
+      last = ep;
+    } else if (mode == XB_ZERO_LEN) {
+      // processLengthZeroBatch: the event, its EXPIRED copy, RESET -- one chunk
+      const uint64_t c = (uint64_t)(it - (uint32_t)a.C);
+      ao = 2 * c;
+      if (a.expired_on) eo = 2 * c + 1;
+      ep = a.chunk0 + (int64_t)c;
+    } else {
+      // stream.current.event timeBatch: a call's events in its chunk, then at a
+      // flush (that chunk or a later TIMER) every event since the last flush
+      // as EXPIRED, then RESET
+      if (it < (uint32_t)a.C) {
+        if (a.expired_on && a.first_flush >= 0) eo = 2 * (uint64_t)a.first_flush + 1;
+      } else {
+        const int32_t c = a.icall[it];
+        ao = 2 * (uint64_t)a.cchunk[c];
+        if (a.expired_on && a.cflush[c] >= 0) eo = 2 * (uint64_t)a.cflush[c] + 1;
+        ep = a.cepoch[c];
+      }
+      keep = a.expired_on && eo == kNoOpp;
     }
     a.aopp[j] = ao;
     a.eopp[j] = eo;
+    a.epoch_j[j] = ep;
+    a.keep_j[j] = keep ? 1 : 0;
+    a.last_j[j] = last;
+  }
+}
+
+// per chunk of a new item (lengthBatch stream / zero modes): its clock and in_seq
+__global__ __launch_bounds__(kBlock) void k_xb_item_chunks(int64_t C, int64_t m, const int32_t* icall,
+                                                           const int32_t* irow, const int64_t* call_now, int64_t seq0,
+                                                           int64_t* fnow, int64_t* fseq) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j = m) {
+    fnow[j] = call_now[icall[C + j]];
+    fseq[j] = seq0 + irow[C + j];
   }
 }
 
@@ -1044,10 +1114,13 @@ struct XbOpArgs {
   const uint8_t* added_j;
   const uint64_t* aopp;
   const uint64_t* eopp;
+  const int64_t* epoch_j;
+  int full;                   // full-batch modes: carried items awaiting expiry precede the adds
   const uint32_t* opscan;
   const int64_t* fnow;
   const int64_t* fseq;
   int current_on, expired_on;
+  int64_t* op_epoch;
   uint32_t* op_item;
   uint8_t* op_add;
   uint8_t* op_on;
@@ -1065,7 +1138,9 @@ __global__ __launch_bounds__(kBlock) void k_xb_ops(const XbOpArgs* __restrict__ 
     const uint32_t k = a.segid[j];
     const int64_t s = a.segS[k], e = a.segS[k + 1], ck = a.segCk[k];
     const int64_t base = a.opscan[s];
-    const int64_t na = xb_added_count(a.added_j, s, ck);
+    // adds occupy [s + na, ...): after the carried items awaiting expiry (full
+    // batches), after every carried item (stream modes: carried items were added)
+    const int64_t na = a.full ? xb_added_count(a.added_j, s, ck) : ck;
     const uint32_t it = a.sp[j];
     const uint64_t ao = a.aopp[j], eo = a.eopp[j];
     if (ao != kNoOpp) {
@@ -1083,6 +1158,7 @@ __global__ __launch_bounds__(kBlock) void k_xb_ops(const XbOpArgs* __restrict__ 
       a.op_chunk[q] = f;
       a.op_now[q] = a.fnow[f];
       a.op_seq[q] = a.fseq[f];
+      a.op_epoch[q] = a.epoch_j[j];
     }
     if (eo != kNoOpp) {
       int64_t lo = s + na, hi = e;   // adds at earlier flushes
@@ -1100,18 +1176,6 @@ __global__ __launch_bounds__(kBlock) void k_xb_ops(const XbOpArgs* __restrict__ 
       a.op_now[q] = a.fnow[f];
       a.op_seq[q] = a.fseq[f];
     }
-  }
-}
-
-// kept: the open batch, and (expired output) the last added batch awaiting
-// its expiry; added_out = the item has been added (carried as ilast = 1)
-__global__ __launch_bounds__(kBlock) void k_xb_keep(int64_t total, const uint8_t* added_j, const uint64_t* aopp,
-                                                    const uint64_t* eopp, int expired_on, uint32_t* keep,
-                                                    uint8_t* added_out) {
-  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j = total) {
-    const bool added = added_j[j] || aopp[j] != kNoOpp;
-    keep[j] = (!added || (expired_on && eopp[j] == kNoOpp)) ? 1u : 0u;
-    added_out[j] = added ? 1 : 0;
   }
 }
 
@@ -1166,7 +1230,10 @@ struct WindowXEngine : Engine {
   DevBuf g_epoch;
   int64_t tb_next = -1;
   std::deque<int64_t> tb_notify;
-  DevBuf xb_added, xb_aopp, xb_trig, xb_fr, xb_fnow, xb_fseq, xb_bflush, xb_ccount, xb_clast, xb_added_out;
+  int bmode = 0;   // XB_* (k_xb_opp)
+  DevBuf xb_added, xb_aopp, xb_trig, xb_fr, xb_fnow, xb_fseq, xb_bflush, xb_ccount, xb_clast, xb_epoch, xb_keep,
+      xb_last, xb_cchunk, xb_cflush, xb_cepoch, op_epoch;
+  int64_t tb_epoch = -1;   // stream.current.event timeBatch: global chunk id of the last flush
   // per-push scratch
   DevBuf d_offs, d_call_of, d_last, d_call_now, d_F, d_fnow, d_flags, d_cnt, d_off, d_pkey, d_start,
       d_run, d_runs_before, d_tot, d_scan, d_sort, kw, kn, kh, spk, spk2, sp, sp2, head, hscan, segS, segid, segCk,
@@ -1201,6 +1268,7 @@ struct WindowXEngine : Engine {
     counters = shd_counters{};
     last_global = INT64_MIN;
     tb_next = -1;
+    tb_epoch = -1;
     tb_notify.clear();
     gd.reset(stream);
     if (nstates) {
@@ -1324,7 +1392,8 @@ struct WindowXEngine : Engine {
   void set_time(int64_t t) override {
     if (t < now) return;
     if ((timed() && plan.expired_on) ||
-        (wkind == SHD_W_TIME_BATCH && !tb_notify.empty() && tb_notify.front() <= t)) {
+        ((wkind == SHD_W_TIME_BATCH || wkind == SHD_W_TIME_BATCH_STREAM) && !tb_notify.empty() &&
+         tb_notify.front() <= t)) {
       Staged z;
       z.n = 0;
       z.call_offsets = {0, 0};
@@ -1735,7 +1804,7 @@ struct WindowXEngine : Engine {
     fa.lsum = g_lsum.as<int64_t>();
     fa.cnt = g_cnt.as<int64_t>();
     fa.epoch = (batch && nagg > 0) ? g_epoch.as<int64_t>() : nullptr;
-    fa.chunk0 = chunk_seq;
+    fa.op_epoch = op_epoch.as<int64_t>();
     fa.resv = resv.as<uint64_t>();
     fa.resn = resn.as<uint8_t>();
     fa.rowflag = rowflag.as<uint8_t>();
@@ -1830,11 +1899,8 @@ struct WindowXEngine : Engine {
       keep.reserve(total * 4);
       koff.reserve(total * 4);
       if (batch) {
-        xb_added_out.reserve(total);
-        hipLaunchKernelGGL(k_xb_keep, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
-                           (const uint8_t*)xb_added.as<uint8_t>(), (const uint64_t*)xb_aopp.as<uint64_t>(),
-                           (const uint64_t*)eopp.as<uint64_t>(), (int)plan.expired_on, keep.as<uint32_t>(),
-                           xb_added_out.as<uint8_t>());
+        hipLaunchKernelGGL(k_xw_widen, dim3(grid_cover(total)), dim3(kBlock), 0, s,
+                           (const uint8_t*)xb_keep.as<uint8_t>(), total, keep.as<uint32_t>());
       } else {
         hipLaunchKernelGGL(k_xw_keep, dim3(grid_cover(total)), dim3(kBlock), 0, s, total,
                            (const uint64_t*)eopp.as<uint64_t>(), wkind != 0 ? 1 : 0, keep.as<uint32_t>());
@@ -1855,7 +1921,7 @@ struct WindowXEngine : Engine {
       ca.koff = koff.as<uint32_t>();
       ca.segid = segid.as<uint32_t>();
       ca.last_out = lane_ran ? last_out.as<int64_t>() : nullptr;
-      ca.added_j = batch ? xb_added_out.as<uint8_t>() : nullptr;
+      ca.last_j = batch ? xb_last.as<int64_t>() : nullptr;
       ca.pk = ipk[cur].as<uint64_t>(); ca.ts = its[cur].as<int64_t>(); ca.seq = iseq[cur].as<int64_t>();
       ca.sid = isid[cur].as<uint64_t>();
       ca.attr = iattr[cur].as<uint64_t>(); ca.nul = inul[cur].as<uint8_t>();
@@ -1922,9 +1988,10 @@ struct WindowXEngine : Engine {
     return false;
   }
 
-  // Batch windows: the push's flushes (chunk ordinals 0..nflush-1 in output
-  // order), each item's add / expiry flush, the operations in key-major
-  // order (k_xb_ops).  Returns the operation count.
+  // Batch windows: the push's output chunks (ordinals 0..nflush-1 in output
+  // order: flushes, or every event / call in the stream modes), each item's
+  // add / expiry chunk and RESET epoch, the operations in key-major order
+  // (k_xb_ops).  Returns the operation count.
   int64_t batch_operations(int64_t n, int64_t m, int64_t total, int ncalls, const std::vector<char>& moved,
                            const uint32_t* SP, int64_t& nflush) {
     hipStream_t s = stream;
@@ -1932,6 +1999,9 @@ struct WindowXEngine : Engine {
     xb_added.reserve(ta);
     xb_aopp.reserve(ta * 8);
     eopp.reserve(ta * 8);
+    xb_epoch.reserve(ta * 8);
+    xb_keep.reserve(ta);
+    xb_last.reserve(ta * 8);
     if (total > 0) {
       hipLaunchKernelGGL(k_xb_added, dim3(grid_cover(total)), dim3(kBlock), 0, s, total, C, SP,
                          (const int64_t*)ilast[cur].as<int64_t>(), xb_added.as<uint8_t>());
@@ -1940,7 +2010,7 @@ struct WindowXEngine : Engine {
     XbArgs xb{};
     xb.total = total;
     xb.C = C;
-    xb.L = wparam;
+    xb.L = std::max<int64_t>(wparam, 1);
     xb.expired_on = plan.expired_on;
     xb.sp = SP;
     xb.segid = segid.as<uint32_t>();
@@ -1949,11 +2019,16 @@ struct WindowXEngine : Engine {
     xb.added_j = xb_added.as<uint8_t>();
     xb.irow = irow[cur].as<int32_t>();
     xb.icall = icall[cur].as<int32_t>();
+    xb.ilast = ilast[cur].as<int64_t>();
+    xb.chunk0 = chunk_seq;
+    xb.first_flush = -1;
     xb.aopp = xb_aopp.as<uint64_t>();
     xb.eopp = eopp.as<uint64_t>();
+    xb.epoch_j = xb_epoch.as<int64_t>();
+    xb.keep_j = xb_keep.as<uint8_t>();
+    xb.last_j = xb_last.as<int64_t>();
     nflush = 0;
-    const bool tb = wkind == SHD_W_TIME_BATCH;
-    if (!tb) {
+    if (bmode == XB_FULL_LEN) {
       // lengthBatch: a flush per completed batch, ranked by its trigger row
       xb_trig.reserve(std::max<int64_t>(n, 1) * 4);
       xb_fr.reserve(std::max<int64_t>(n, 1) * 4);
@@ -1974,6 +2049,18 @@ struct WindowXEngine : Engine {
         SHD_CHECK_LAUNCH();
       }
       xb.fr = xb_fr.as<uint32_t>();
+    } else if (bmode == XB_STREAM_LEN || bmode == XB_ZERO_LEN) {
+      // an output chunk per event (its rank among the push's new items)
+      nflush = m;
+      xb_fnow.reserve(std::max<int64_t>(m, 1) * 8);
+      xb_fseq.reserve(std::max<int64_t>(m, 1) * 8);
+      if (m > 0) {
+        hipLaunchKernelGGL(k_xb_item_chunks, dim3(grid_cover(m)), dim3(kBlock), 0, s, C, m,
+                           (const int32_t*)icall[cur].as<int32_t>(), (const int32_t*)irow[cur].as<int32_t>(),
+                           (const int64_t*)d_call_now.as<int64_t>(), seq, xb_fnow.as<int64_t>(),
+                           xb_fseq.as<int64_t>());
+        SHD_CHECK_LAUNCH();
+      }
     } else {
       // timeBatch: the flush schedule is sequential in the chunks (calls and
       // TIMER chunks), not in the events: run it on the host per call
@@ -1995,9 +2082,20 @@ struct WindowXEngine : Engine {
       SHD_HIP(hipStreamSynchronize(s));
       std::memcpy(cc.data(), h_pin.p, (size_t)ncalls * 4);
       std::memcpy(cl.data(), h_pin.as<char>() + (size_t)ncalls * 4, (size_t)ncalls * 8);
-      std::vector<int32_t> bfl(ncalls, -1);
-      std::vector<int64_t> fn, fs;
+      const bool stream_cur = bmode == XB_STREAM_TIME;
+      // per call: full batches -- the flush its events join; stream mode -- its
+      // chunk, the first flush at or after it, its RESET epoch
+      std::vector<int32_t> bfl(ncalls, -1), cch(ncalls, -1), cfl(ncalls, -1);
+      std::vector<int64_t> cep(ncalls, -1), fn, fs;
       std::vector<int> pending;
+      auto flush_here = [&](int64_t t, int64_t sq) {   // a flush ends the current chunk list
+        const int32_t f = (int32_t)fn.size();
+        for (int pc : pending) (stream_cur ? cfl : bfl)[pc] = f;
+        pending.clear();
+        fn.push_back(t);
+        fs.push_back(sq);
+        if (stream_cur) tb_epoch = chunk_seq + f;   // RESET after this chunk's expirations
+      };
       for (int c = 0; c < ncalls; c++) {
         if (moved[c]) {
           // Scheduler.sendTimerEvents (C/util/Scheduler.java:190-220): TIMER
@@ -2006,32 +2104,48 @@ struct WindowXEngine : Engine {
           while (!tb_notify.empty() && tb_notify.front() <= t) {
             tb_notify.pop_front();
             if (tb_process(t)) {
-              for (int pc : pending) bfl[pc] = (int32_t)fn.size();
-              pending.clear();
-              fn.push_back(t);
-              fs.push_back(seq + h_offs[c]);
+              if (xb.first_flush < 0) xb.first_flush = (int64_t)fn.size();
+              flush_here(t, seq + h_offs[c]);
             }
           }
         }
         if (cc[c] > 0) {   // a chunk of events reaches the window
           pending.push_back(c);
-          if (tb_process(h_now[c])) {
-            for (int pc : pending) bfl[pc] = (int32_t)fn.size();
-            pending.clear();
+          const bool send = tb_process(h_now[c]);
+          if (stream_cur) {   // the call is a chunk of its own (its events stay in it)
+            cch[c] = (int32_t)fn.size();
+            cep[c] = tb_epoch;
             fn.push_back(h_now[c]);
             fs.push_back(cl[c]);
+            if (send) {   // expirations appended to the same chunk
+              for (int pc : pending) cfl[pc] = cch[c];
+              pending.clear();
+              if (xb.first_flush < 0) xb.first_flush = cch[c];
+              tb_epoch = chunk_seq + cch[c];
+            }
+          } else if (send) {
+            flush_here(h_now[c], cl[c]);
           }
         }
       }
       nflush = (int64_t)fn.size();
-      upload(xb_bflush, bfl);
       upload(xb_fnow, fn);
       upload(xb_fseq, fs);
-      xb.bflush = xb_bflush.as<int32_t>();
-      xb.nf = nflush;
+      if (stream_cur) {
+        upload(xb_cchunk, cch);
+        upload(xb_cflush, cfl);
+        upload(xb_cepoch, cep);
+        xb.cchunk = xb_cchunk.as<int32_t>();
+        xb.cflush = xb_cflush.as<int32_t>();
+        xb.cepoch = xb_cepoch.as<int64_t>();
+      } else {
+        upload(xb_bflush, bfl);
+        xb.bflush = xb_bflush.as<int32_t>();
+        xb.nf = nflush;
+      }
     }
     if (total > 0) {
-      hipLaunchKernelGGL(k_xb_opp, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(xb), tb ? 1 : 0);
+      hipLaunchKernelGGL(k_xb_opp, dim3(grid_cover(total)), dim3(kBlock), 0, s, dev_args(xb), bmode);
       SHD_CHECK_LAUNCH();
     }
     int64_t nops = 0;
@@ -2045,6 +2159,7 @@ struct WindowXEngine : Engine {
       nops = scan(nops_b.as<uint32_t>(), opscan.as<uint32_t>(), total);
     }
     reserve_ops(nops);
+    op_epoch.reserve(std::max<int64_t>(nops, 1) * 8);
     if (nops > 0) {
       XbOpArgs oa{};
       oa.total = total;
@@ -2055,11 +2170,14 @@ struct WindowXEngine : Engine {
       oa.added_j = xb_added.as<uint8_t>();
       oa.aopp = xb_aopp.as<uint64_t>();
       oa.eopp = eopp.as<uint64_t>();
+      oa.epoch_j = xb_epoch.as<int64_t>();
+      oa.full = bmode == XB_FULL_LEN || bmode == XB_FULL_TIME;
       oa.opscan = opscan.as<uint32_t>();
       oa.fnow = xb_fnow.as<int64_t>();
       oa.fseq = xb_fseq.as<int64_t>();
       oa.current_on = plan.current_on;
       oa.expired_on = plan.expired_on;
+      oa.op_epoch = op_epoch.as<int64_t>();
       oa.op_item = op_item.as<uint32_t>();
       oa.op_add = op_add.as<uint8_t>();
       oa.op_on = op_on.as<uint8_t>();
@@ -2187,6 +2305,7 @@ struct WindowXEngine : Engine {
     gd.save(w);
     // batch windows: RESET epochs, timeBatch's nextEmitTime and notify queue
     w.put<int64_t>(tb_next);
+    w.put<int64_t>(tb_epoch);
     w.put<int64_t>((int64_t)tb_notify.size());
     for (int64_t t : tb_notify) w.put<int64_t>(t);
     if (batch && nagg > 0 && nstates > 0) w.dev(g_epoch.p, (size_t)nstates * 8);
@@ -2249,6 +2368,7 @@ struct WindowXEngine : Engine {
     gd.nk = std::max(nw, 1);
     gd.load(r, stream);
     tb_next = r.get<int64_t>();
+    tb_epoch = r.get<int64_t>();
     tb_notify.clear();
     const int64_t nn = r.get<int64_t>();
     for (int64_t i = 0; i < nn; i++) tb_notify.push_back(r.get<int64_t>());
@@ -2277,7 +2397,13 @@ std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why) {
   }
   if (e->filters.size() > 4) { why = "too many filters"; return nullptr; }
   if (e->wkind == SHD_W_LENGTH && e->wparam <= 0) { why = "length(0) window"; return nullptr; }
-  e->batch = e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH;
+  e->batch = e->wkind == SHD_W_LENGTH_BATCH || e->wkind == SHD_W_TIME_BATCH || e->wkind == SHD_W_TIME_BATCH_STREAM;
+  if (e->wkind == SHD_W_LENGTH_BATCH)
+    e->bmode = e->wparam == 0 ? XB_ZERO_LEN : ((e->wparam2 & 1) ? XB_STREAM_LEN : XB_FULL_LEN);
+  else if (e->wkind == SHD_W_TIME_BATCH)
+    e->bmode = XB_FULL_TIME;
+  else if (e->wkind == SHD_W_TIME_BATCH_STREAM)
+    e->bmode = XB_STREAM_TIME;
   if (e->wkind == SHD_W_EXTERNAL_TIME && (e->wparam2 < 0 || e->wparam2 >= e->ncols)) {
     why = "externalTime attribute";
     return nullptr;
@@ -2286,7 +2412,7 @@ std::unique_ptr<Engine> make_window_x_engine(const Plan& p, std::string& why) {
     why = "timeLength window of length 0";
     return nullptr;
   }
-  if (e->batch && e->wparam <= 0) { why = "batch window of size 0"; return nullptr; }
+  if (e->batch && e->wparam <= 0 && e->bmode != XB_ZERO_LEN) { why = "batch window of time 0"; return nullptr; }
   if (e->wkind == SHD_W_TIME && e->wparam < 0) { why = "negative time window"; return nullptr; }
   if (p.outputs.size() > (size_t)kMaxCols) { why = "too many outputs"; return nullptr; }
   e->nagg = (int)p.aggs.size();

@@ -41,6 +41,7 @@ IDX_CURRENT, IDX_LAST = -1, -2
 NODE_STREAM, NODE_NEXT, NODE_EVERY, NODE_LOGICAL, NODE_COUNT = 1, 2, 3, 4, 5
 H_FILTER, H_WINDOW = 1, 2
 W_LENGTH, W_TIME, W_LENGTH_BATCH, W_TIME_BATCH, W_TIME_LENGTH, W_EXTERNAL_TIME = 1, 2, 3, 4, 5, 6
+W_TIME_BATCH_STREAM = 7
 INT64_MIN = -(1 << 63)
 AGG_SUM, AGG_AVG, AGG_COUNT = 1, 2, 3
 UNKNOWN_STATE = -1
@@ -745,7 +746,8 @@ def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
     n_windows = 0
     for h in si.handlers:
         if isinstance(h, qc.Filter):
-            if any(x[0] == H_WINDOW and x[1] in (W_LENGTH_BATCH, W_TIME_BATCH) for x in plan.handlers):
+            if any(x[0] == H_WINDOW and x[1] in (W_LENGTH_BATCH, W_TIME_BATCH, W_TIME_BATCH_STREAM)
+                   for x in plan.handlers):
                 raise UnsupportedPlanException("a filter after a batch window is outside the hot path")
             eid, _ = ec.compile(h.expr, 0, IDX_CURRENT, want_bool=True)
             plan.handlers.append((H_FILTER, eid))
@@ -784,29 +786,28 @@ def _window_handler(h, partitioned: bool, meta=None, stream=None):
         if not 1 <= len(ps) <= 2:
             raise SiddhiAppValidationException("LengthBatch window should have one or two parameters")
         n = int(const(0, ("int",), "window.length"))
-        if len(ps) == 2 and bool(const(1, ("bool",), "stream.current.event")):
-            raise UnsupportedPlanException("lengthBatch with stream.current.event is outside the hot path")
-        if n <= 0:
-            raise UnsupportedPlanException("lengthBatch(0) (RESET path) is outside the hot path")
-        return (H_WINDOW, W_LENGTH_BATCH, n, 0)
+        stream_cur = len(ps) == 2 and bool(const(1, ("bool",), "stream.current.event"))
+        if n < 0:
+            raise SiddhiAppValidationException("LengthBatch window's window.length should not be negative")
+        return (H_WINDOW, W_LENGTH_BATCH, n, 1 if stream_cur else 0)
     if h.name == "timebatch":
         if not 1 <= len(ps) <= 3:
             raise SiddhiAppValidationException("TimeBatch window should have one to three parameters")
         t = int(const(0, ("int", "long"), "window.time"))
         start = INT64_MIN
+        stream_cur = False
         if len(ps) >= 2:
             if ps[1].type == "bool" and len(ps) == 2:
-                if bool(ps[1].value):
-                    raise UnsupportedPlanException("timeBatch with stream.current.event is outside the hot path")
+                stream_cur = bool(ps[1].value)
             else:
                 start = int(const(1, ("int", "long"), "start.time"))
-                if len(ps) == 3 and bool(const(2, ("bool",), "stream.current.event")):
-                    raise UnsupportedPlanException("timeBatch with stream.current.event is outside the hot path")
+                if len(ps) == 3:
+                    stream_cur = bool(const(2, ("bool",), "stream.current.event"))
         if partitioned:
             raise UnsupportedPlanException("timeBatch inside a partition is outside the hot path")
         if t <= 0:
             raise SiddhiAppValidationException("TimeBatch window's window.time should be positive")
-        return (H_WINDOW, W_TIME_BATCH, t, start)
+        return (H_WINDOW, W_TIME_BATCH_STREAM if stream_cur else W_TIME_BATCH, t, start)
     if h.name == "timelength":
         if len(ps) != 2:
             raise SiddhiAppValidationException("TimeLength window should only have two parameters")

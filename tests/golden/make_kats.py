@@ -523,6 +523,7 @@ def extract(name, body, line, fname):
             except ValueError as e:
                 return None, str(e)
     count = None
+    sizes = {}
     if tu:
         # the first count assertion after the callback (later ones follow more sends)
         cm = re.search(r'assertEquals\("[^"]*",\s*(\d+),\s*\w+\.getInEventCount\(\)\)', body[tu[0].end():])
@@ -559,6 +560,19 @@ def extract(name, body, line, fname):
         if rm:
             removes = int(rm.group(1))
             break
+    if cb_kind == "StreamCallback" and re.search(r"\bevents\.length == \d+\)", cbody):
+        # counters bumped per callback by chunk size: the checkable number is the
+        # total the callback saw (`for (Event event : events) count++`)
+        tm = re.search(r'assertEquals\("Total events",\s*(\d+),\s*count\)', body)
+        if not tm or not re.search(r"for \(Event \w+ : events\)", cbody) or "count++" not in cbody:
+            return None, "per-chunk-size counters"
+        count, removes = int(tm.group(1)), None
+        # `if (events.length == k) { c++; }` checked by assertEquals(..., n, c):
+        # n callback chunks of k events
+        for km in re.finditer(r"events\.length == (\d+)\)\s*\{\s*(\w+)\+\+;", cbody):
+            am = re.search(r'assertEquals\((?:"[^"]*",\s*)?(\d+),\s*' + km.group(2) + r"\)", body)
+            if am:
+                sizes[int(km.group(1))] = int(am.group(1))
     if cb_kind == "StreamCallback" and count is None and removes is not None and "inEventCount++" not in cbody:
         # a StreamCallback counter named removeEventCount counts every event it sees
         count, removes = removes, None
@@ -573,6 +587,7 @@ def extract(name, body, line, fname):
         "expected_rows": expected,
         "expected_count": count,
         "expected_remove_count": removes,
+        "expected_chunk_sizes": {str(k): v for k, v in sorted(sizes.items())},
         "expected_cells": cells,
         "expected_nth": nth,
         "playback": "@app:playback" in app.replace(" ", "").lower() or "@app:playback" in app.lower(),

@@ -153,6 +153,11 @@ def check_case(case, col, rtol=0.0):
             errs.append("event #%d col %d: %r != expected %r" % (cell["n"], cell["col"], d[cell["col"]] if
                                                                   cell["col"] < len(d) else None,
                                                                   _py(cell["value"])[1]))
+    for k, n in case.get("expected_chunk_sizes", {}).items():
+        # callbacks that received exactly k events (T/query/window/LengthBatchWindowTestCase.java)
+        got = sum(1 for c in col.chunks if len(c[0]) + len(c[1]) == int(k))
+        if got != n:
+            errs.append("%d chunks of %s events, expected %d" % (got, k, n))
     for cell in case.get("expected_cells", []):
         targets = [c[0][0] for c in col.chunks if c[0]] if cell["which"] == "first_of_each" else col.in_events
         for ev in targets:

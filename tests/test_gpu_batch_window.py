@@ -46,6 +46,21 @@ APPS = [
      "count() as c insert all events into O;"),
     ("time-current", S + "@info(name = 'q') from S[price > 40]#window.timeBatch(500) select symbol, "
      "sum(price) as m insert into O;"),
+    # stream.current.event: events pass at once, the batch expires and RESETs later
+    ("len-stream", S + "@info(name = 'q') from S#window.lengthBatch(5, true) select symbol, sum(price) as s "
+     "group by symbol insert all events into O;"),
+    ("len-stream-part", S + "partition with (symbol of S) begin @info(name = 'q') from S#window.lengthBatch(3, true) "
+     "select symbol, price, count() as c insert all events into O; end;"),
+    ("len-stream-plain", S + "@info(name = 'q') from S#window.lengthBatch(4, true) select symbol, price "
+     "insert all events into O;"),
+    ("len-zero", S + "@info(name = 'q') from S#window.lengthBatch(0) select symbol, sum(price) as s, count() as c "
+     "group by symbol insert all events into O;"),
+    ("time-stream", S + "@info(name = 'q') from S#window.timeBatch(1 sec, true) select symbol, sum(price) as s "
+     "group by symbol insert all events into O;"),
+    ("time-stream-start", S + "@info(name = 'q') from S#window.timeBatch(700, 100, true) select symbol, price "
+     "insert all events into O;"),
+    ("time-stream-cur", S + "@info(name = 'q') from S#window.timeBatch(500, true) select sum(price) as s, "
+     "count() as c insert into O;"),
     # timeLength: a sliding window bounded by time and length (TIMER expiries too)
     ("timelen-group", S + "@info(name = 'q') from S#window.timeLength(2 sec, 5) select symbol, sum(price) as s "
      "group by symbol insert all events into O;"),
@@ -95,7 +110,7 @@ def test_batch_window_single_event_calls(hip_available):
         assert_same_rows(dev, ora)
 
 
-@pytest.mark.parametrize("idx", [1, 5, 7])
+@pytest.mark.parametrize("idx", [1, 5, 7, 11, 12, 15])
 def test_batch_window_snapshot_restore(hip_available, idx):
     from siddhi_amd.hip_engine import DeviceQuery, SHD_MEM_HOST
     qp, d = compile_single_query(APPS[idx][1])
