@@ -57,8 +57,9 @@ def test_last_index_inside_own_filter_stays_previous():
 def test_unsupported_reports_reason():
     with pytest.raises(pl.UnsupportedPlanException):
         plan_of("define stream A (x int); from A#window.frequent(2) select x insert into O;")
-    with pytest.raises(pl.UnsupportedPlanException):   # full-batch mode only
-        plan_of("define stream A (x int); from A#window.lengthBatch(4, true) select x insert into O;")
+    with pytest.raises(pl.UnsupportedPlanException):   # timeBatch's nextEmitTime is per processor
+        plan_of("define stream A (x int); partition with (x of A) begin "
+                "from A#window.timeBatch(1 sec) select x insert into O; end;")
 
 
 def test_time_units():
