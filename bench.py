@@ -650,6 +650,7 @@ def main():
 
         routed_total = [0]
         take = [0]
+        pipe = ex.RoutePipeline(local) if seqs is not None else None
         cols4 = [sym, price, vol, ts]
 
         def push_halo(halo):
@@ -678,8 +679,24 @@ def main():
                 halo = ex.exchange_tail(cols4, take[0], rank, world)
                 if halo is not None:
                     push_halo(halo)
+            routed_iter = None
+            if seqs is not None and not os.environ.get("SHD_ROUTE_TORCH") and not os.environ.get("SHD_ROUTE_SYNC"):
+                # micro-batch k+1 routed on a side stream while k is pushed (exchange.RoutePipeline)
+                def job(a, b):
+                    lo = (a * world) // 1024 * 1024
+                    nb = -(-(b * world - lo) // 1024)
+                    return lambda: ex.route_device([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b], seqs[a:b],
+                                                   world, lo, 1024, nb, device=local)
+                routed_iter = pipe.run([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])])
             for a, b in zip(cuts[:-1], cuts[1:]):
-                if seqs is None:
+                if routed_iter is not None:
+                    (rs, rp, rv, rt), rseq, co, _ = next(routed_iter)
+                    m = rs.numel()
+                    routed_total[0] += m
+                    if m > 0:
+                        dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
+                                    he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+                elif seqs is None:
                     # InputHandler calls of 1024 events inside the micro-batch
                     lo = np.searchsorted(offs_all, a)
                     hi = np.searchsorted(offs_all, b)

@@ -292,6 +292,44 @@ def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor,
     return outs, rseq, co, stats
 
 
+class RoutePipeline:
+    """Micro-batch k+1's route (HIP bucket -> all-to-alls -> HIP merge) runs on a
+    side stream in a worker thread while the caller pushes micro-batch k: the
+    exchange overlaps the engine push.  The route's host reads -- the per-owner
+    counts that size the all-to-all and the merged call offsets -- happen in
+    the worker, off the push's critical path; nothing between the caller's
+    previous push and its next one waits on a device-to-host copy.  The worker
+    issues the collectives in micro-batch order (one thread: the same order on
+    every rank).  Usage: ``for routed in pipe.run(jobs): push(routed)`` where a
+    job is a no-argument callable returning route_device()'s result."""
+
+    def __init__(self, device: int = 0):
+        from concurrent.futures import ThreadPoolExecutor
+        self.device = device
+        self.stream = torch.cuda.Stream(device=device)
+        self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def _route(self, job):
+        torch.cuda.set_device(self.device)
+        with torch.cuda.stream(self.stream):
+            r = job()
+        self.stream.synchronize()   # routed columns complete before another stream reads them
+        return r
+
+    def run(self, jobs):
+        pending = None
+        for job in jobs:
+            nxt = self.pool.submit(self._route, job)   # k+1 starts before k is handed out
+            if pending is not None:
+                yield pending.result()
+            pending = nxt
+        if pending is not None:
+            yield pending.result()
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
 # ---------------------------------------------------------------------------
 # Time slices with a halo: unpartitioned window aggregates (configs W2-*).
 #

@@ -1,5 +1,5 @@
 """Multi-rank key routing (siddhi_amd/exchange.py) on the CPU with gloo,
-world_size 2: round-robin input re-routed by key owner must give every rank
+world_size 2 and 4: round-robin input re-routed by key owner must give every rank
 exactly the events of its keys in global arrival order, and the partitioned
 pattern (config P3) evaluated per rank on the routed events must produce the
 same matches as one engine over the whole stream."""
@@ -45,17 +45,18 @@ def _rank_main(rank, world, path, outdir):
     dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def routed(tmp_path_factory):
+@pytest.fixture(scope="module", params=[2, 4], ids=["world2", "world4"])
+def routed(request, tmp_path_factory):
+    world = request.param
     d = tmp_path_factory.mktemp("route")
     path = tempfile.mktemp(dir=str(d))
-    mp.spawn(_rank_main, args=(2, path, str(d)), nprocs=2)
-    return [np.load(os.path.join(str(d), "r%d.npz" % r)) for r in range(2)]
+    mp.spawn(_rank_main, args=(world, path, str(d)), nprocs=world)
+    return [np.load(os.path.join(str(d), "r%d.npz" % r)) for r in range(world)]
 
 
 def test_route_delivers_own_keys_in_arrival_order(routed):
     s, p, v, t = wl.stock_stream(N, KEYS, DELTA, seed_offset=3)
-    owner = ex.owner_of(torch.from_numpy(s.astype(np.int64)), 2).numpy()
+    owner = ex.owner_of(torch.from_numpy(s.astype(np.int64)), len(routed)).numpy()
     for r, z in enumerate(routed):
         seq = np.concatenate([z["seq0"], z["seq1"]])
         want = np.nonzero(owner == r)[0]
@@ -102,7 +103,7 @@ def test_partitioned_pattern_over_routed_ranks_matches_single_engine(routed):
 
     def canon(r):
         return sorted(zip(r[2].tolist(), r[3][:, 0].tolist(), r[3][:, 1].tolist(), r[3][:, 2].tolist()))
-    merged = sorted(canon(rows[0]) + canon(rows[1]))
+    merged = sorted(sum((canon(r) for r in rows), []))
     assert merged == canon(whole)
 
 

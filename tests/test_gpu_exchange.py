@@ -112,13 +112,16 @@ def _rr_rank(rank, world, path, outdir):
     seq = torch.from_numpy(idx).to(dev)
     dq = he.DeviceQuery(qp.ir)
     parts, lseqs, routed = [], [], []
-    for a in range(0, len(idx), BATCH_RR):   # BATCH_RR * world: whole 1024-event calls
-        b = min(len(idx), a + BATCH_RR)
+
+    def job(a, b):
         lo = (a * world) // 1024 * 1024
         nb = -(-(b * world - lo) // 1024)
-        (rs, rp, rv, rt), rseq, co, _ = ex2.route_device([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo,
-                                                         1024, nb, stage_host=True)
-        torch.cuda.synchronize()
+        return lambda: ex2.route_device([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo, 1024, nb,
+                                        stage_host=True)
+
+    cuts = list(range(0, len(idx), BATCH_RR)) + [len(idx)]   # BATCH_RR * world: whole 1024-event calls
+    pipe = ex2.RoutePipeline(0)   # micro-batch k+1 routed while k is pushed (bench.py's N > 1 path)
+    for (rs, rp, rv, rt), rseq, co, _ in pipe.run([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])]):
         m = rs.numel()
         if m == 0:
             continue
@@ -129,6 +132,7 @@ def _rr_rank(rank, world, path, outdir):
         if r is not None:
             parts.append(r[:5])
             lseqs.append(r[5])
+    pipe.close()
     dq.close()
     gall = np.concatenate(routed) if routed else np.zeros(0, np.int64)
     rows = concat_rows(parts)
@@ -138,14 +142,16 @@ def _rr_rank(rank, world, path, outdir):
     dist.destroy_process_group()
 
 
-def test_roundrobin_route_device_world2_merges_to_single_engine(hip_available, tmp_path):
-    """The N > 1 bench path end to end (bench.py --input roundrobin): two ranks
-    on one GPU, HIP bucket -> all-to-all -> HIP merge -> P3 query per rank, rows
-    mapped to global sequence numbers and k-way merged (exchange.merge_outputs):
-    equal to one device query over the whole stream and to the CPU oracle."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_roundrobin_route_device_merges_to_single_engine(hip_available, tmp_path, world):
+    """The N > 1 bench path end to end (bench.py --input roundrobin): 2 or 4
+    ranks on one GPU, HIP bucket -> all-to-all -> HIP merge -> P3 query per rank,
+    the next micro-batch routed while the current one is pushed
+    (exchange.RoutePipeline), rows mapped to global sequence numbers and k-way
+    merged (exchange.merge_outputs): equal to one device query over the whole
+    stream and to the CPU oracle."""
     import tempfile
     import torch.multiprocessing as mp
-    world = 2
     mp.spawn(_rr_rank, args=(world, tempfile.mktemp(dir=str(tmp_path)), str(tmp_path)), nprocs=world)
     parts = []
     for r in range(world):
