@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--batch", type=int, default=50_000_000, help="micro-batch size (events)")
     ap.add_argument("--no-share", action="store_true", help="M5: every query scans alone (no shd_group)")
+    ap.add_argument("--m5-direct", action="store_true",
+                    help="M5 parity: every query against its own oracle run over the prefix (no leader lemma)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample size for cpu_baseline (0=skip)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads of the per-key parallel CPU baseline (partitioned configs; 0=skip)")
@@ -424,13 +426,13 @@ def run_multi(args, torch, dist, rank, world, local, dev):
     if rank == 0 and args.cpu_sample != 0:
         sample = min(n, args.cpu_sample if args.cpu_sample > 0 else 200_000)
         line["parity_prefix"], line["cpu_baseline"] = m5_parity_prefix(
-            he, qa, queries, plans, d, sym, price, vol, ts, sample, keys, delta, not args.no_share)
+            he, qa, queries, plans, d, sym, price, vol, ts, sample, keys, delta, not args.no_share, args.m5_direct)
         print(json.dumps(line))
     elif rank == 0:
         print(json.dumps(line))
 
 
-def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, keys, delta, share):
+def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, keys, delta, share, direct_all=False):
     """Every M5 query on the first `prefix` events of the benchmark stream, run
     the way the timed loop runs it (the shared scans of shd_group included, one
     push), against the CPU oracle on the same events: pattern rows bit-exact,
@@ -443,7 +445,8 @@ def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, key
     member's expected rows are the leader's whose e1 passes the member's
     threshold (planner.share_groups' lemma, pinned on the oracle itself by
     tests/test_share_plan.py), and the group's first, middle and last members
-    also run in the oracle directly.  Oracle runs go to a thread pool (ctypes
+    also run in the oracle directly.  direct_all (--m5-direct): every member
+    against its own oracle run instead.  Oracle runs go to a thread pool (ctypes
     drops the GIL in the C++ oracle).
 
     cpu_baseline: all queries of the app through the oracle, one after the
@@ -516,7 +519,7 @@ def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, key
     direct = set(range(len(plans)))
     leaders = []
     for g in groups:
-        if _e1_site(queries[g[0]]) is None:   # a window group: every member against its own oracle run
+        if direct_all or _e1_site(queries[g[0]]) is None:   # every member against its own oracle run
             continue
         lead = plan_shared_leader(qa, [queries[i] for i in g], d)
         spot = {g[0], g[len(g) // 2], g[-1]}
@@ -537,6 +540,9 @@ def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, key
                     assert_same_rows(dev, ora)
                 rows += len(dev[2])
                 checked_direct += 1
+                if checked_direct % 5 == 0:
+                    print("M5 parity: %d / %d direct checks" % (checked_direct, len(fut_direct)), file=sys.stderr,
+                          flush=True)
             print("M5 parity: %d queries checked directly" % checked_direct, file=sys.stderr, flush=True)
             for (g, lead, spot), f in zip(leaders, fut_lead):
                 lead_rows, _ = f.result()
