@@ -5,8 +5,11 @@
         --out profiles/rNN_pmc_<config>.json
 
 HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE
-are KiB; FETCH_SIZE counts half the bytes of a streaming read on gfx950, so it
-is doubled; WRITE_SIZE is exact.  Each counter comes from its own --pmc pass of
+are KiB; FETCH_SIZE counts half the bytes of a coalesced streaming read on
+gfx950, so it is doubled for streaming kernels, and one 64-B request per random
+access, which is what a gather moves, so gather kernels (GATHER below) take it
+as is -- both calibrated by scripts/calib_fetch.hip
+(profiles/r05_fetch_calibration.json); WRITE_SIZE is exact.  Each counter comes from its own --pmc pass of
 the same command (they do not fit one pass).  Output, per kernel: dispatches
 per push, average duration (kernel trace), HBM bytes per dispatch, bytes per
 event and the kernel's own HBM rate and fraction of the 8 TB/s peak; plus the
@@ -23,6 +26,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from siddhi_amd.buildinfo import source_hash  # noqa: E402
 
 PEAK_GBS = 8000.0
+# kernels whose reads are dominated by row gathers (FETCH_SIZE x1); every other
+# kernel streams (x2)
+GATHER = ("k_gather_list", "k_project", "k_emit_pairs", "k_gather_bpos", "k_xw_gather_u64", "k_xw_gather_u32",
+          "k_bucket_resume")
+
+
+def fetch_factor(kernel):
+    return 1.0 if kernel.startswith(GATHER) else 2.0
 
 
 def short(nm):
@@ -50,7 +61,7 @@ def main():
     a = ap.parse_args()
 
     dur = load(a.trace, lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    fetch = load(a.fetch, lambda r: float(r["Counter_Value"]) * 1024.0 * 2)   # gfx950 half-count
+    fetch = load(a.fetch, lambda r: float(r["Counter_Value"]) * 1024.0 * fetch_factor(short(r["Kernel_Name"])))
     write = load(a.write, lambda r: float(r["Counter_Value"]) * 1024.0)
     kernels, tot_b, tot_us = {}, 0.0, 0.0
     for k in sorted(dur, key=lambda x: -dur[x][1]):
@@ -75,7 +86,9 @@ def main():
         # uses the traffic only when its own tree hashes the same)
         "build": source_hash(),
         "source": {"trace": a.trace, "fetch": a.fetch, "write": a.write},
-        "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
+        "correction": ("FETCH_SIZE KiB x1024, x2 for streaming kernels (gfx950 half-count), x1 for the gather "
+                       "kernels %s (one 64-B request per access); WRITE_SIZE KiB x1024; calibration: "
+                       "profiles/r05_fetch_calibration.json" % (list(GATHER),)),
         "events_per_push": a.events,
         "pushes": a.pushes,
         "push": {"kernel_us": round(tot_us, 1), "hbm_bytes": round(tot_b),
