@@ -493,6 +493,11 @@ class QueryPlan:
     name: Optional[str]
     partitioned: bool
     receiver_kind: Dict[str, str]        # stream -> 'single' | 'multi' (state queries)
+    # `output ... every` (C/query/output/ratelimit/**): applied by the host runtime
+    # to the selector's output chunks; rate_group_cols: the output columns that
+    # hold the group-by values (GroupedComplexEvent keys)
+    output_rate: Optional[object] = None
+    rate_group_cols: Optional[List[int]] = None
 
 
 def _stream_meta(app: qc.SiddhiApp, sid: str, ref=None, extra_streams=None) -> Meta:
@@ -508,10 +513,45 @@ def plan_query(app: qc.SiddhiApp, q: qc.Query, dictionary: StringDictionary,
     if q.inner_target or getattr(inp, "inner", False) or _uses_inner_stream(inp):
         raise UnsupportedPlanException("partition-inner streams (#stream) are outside the hot path")
     if isinstance(inp, qc.StateInput):
-        return _plan_state(app, q, dictionary, partition, extra_streams)
-    if isinstance(inp, qc.SingleInput):
-        return _plan_single(app, q, dictionary, partition, extra_streams)
-    raise UnsupportedPlanException("input kind %s is outside the hot path" % type(inp).__name__)
+        qp = _plan_state(app, q, dictionary, partition, extra_streams)
+    elif isinstance(inp, qc.SingleInput):
+        qp = _plan_single(app, q, dictionary, partition, extra_streams)
+    else:
+        raise UnsupportedPlanException("input kind %s is outside the hot path" % type(inp).__name__)
+    if q.output_rate is not None:
+        _plan_output_rate(qp, q, partition)
+    return qp
+
+
+def _plan_output_rate(qp: QueryPlan, q: qc.Query, partition):
+    """Output rate limiting (OutputParser.constructOutputRateLimiter,
+    C/util/parser/OutputParser.java:282-331): event- and time-based, all / first
+    / last, per group when the query groups.  Its state is per partition key
+    inside a partition (refused here); a group's key is its group-by values,
+    which must be selected as they are."""
+    if partition is not None:
+        raise UnsupportedPlanException("output rate limiting inside a partition is outside the hot path")
+    rate = q.output_rate
+    if rate.value <= 0:
+        raise SiddhiAppValidationException("output rate should be positive")
+    qp.output_rate = rate
+    gb = q.selector.group_by if q.selector else []
+    if gb and rate.kind in ("first", "last"):
+        cols = []
+        for g in gb:
+            hit = None
+            for c, oa in enumerate(q.selector.attrs):
+                if isinstance(oa.expr, qc.Var) and oa.expr.attr == g.attr and oa.expr.index is None and \
+                        (g.stream is None or oa.expr.stream in (None, g.stream)):
+                    hit = c
+                    break
+            if hit is None and q.selector.select_all and g.attr in qp.output_names:
+                hit = qp.output_names.index(g.attr)
+            if hit is None:
+                raise UnsupportedPlanException("output %s every ... with group by needs the group-by attributes "
+                                               "selected as they are" % rate.kind)
+            cols.append(hit)
+        qp.rate_group_cols = cols
 
 
 def _plan_partition(plan: Plan, comp_factory, partition, streams: List[str], app, dictionary,

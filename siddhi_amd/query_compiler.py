@@ -170,6 +170,13 @@ class Selector:
 
 
 @dataclass
+class OutputRate:
+    unit: str       # events | time
+    kind: str       # all | first | last
+    value: int      # events, or ms
+
+
+@dataclass
 class Query:
     name: Optional[str]
     input: object
@@ -440,8 +447,18 @@ class Parser:
         else:
             sel = Selector(True, [])
         rate = None
-        if self.at_kw("output"):
-            raise OutOfScopeSyntax("output rate limiting is out of scope for the hot path")
+        if self.accept("output"):
+            # output_rate (SiddhiQL.g4): output [all|first|last] every <n> events | <time>
+            if self.at_kw("snapshot"):
+                raise OutOfScopeSyntax("output snapshot rate limiting is outside the hot path")
+            kind = self.name().lower() if self.at_kw("all", "first", "last") else "all"
+            self.expect("every")
+            if self.peek().kind == "num" and self.at_kw("events", "event", k=1):
+                n = int(self.next().text)
+                self.next()
+                rate = OutputRate("events", kind, n)
+            else:
+                rate = OutputRate("time", kind, self.time_value())
         self.expect("insert")
         et = "current"
         if self.at_kw("all", "expired", "current", "events"):

@@ -209,6 +209,8 @@ class _QueryRuntime:
         self.engine = engine
         self.name = name
         self.callbacks: List[QueryCallback] = []
+        rate = getattr(qp, "output_rate", None)
+        self.limiter = OutputRateLimiter(rate, qp.rate_group_cols is not None) if rate is not None else None
 
 
 class InputHandler:
@@ -343,6 +345,8 @@ class SiddhiAppRuntime:
             st = getattr(q.engine, "start", None)
             if st:
                 st(t0)
+            if q.limiter is not None:
+                q.limiter.start(self._wall_clock())
         self.started = True
 
     # -- state persistence (C/SiddhiAppRuntimeImpl.java:677-745)
@@ -439,6 +443,7 @@ class SiddhiAppRuntime:
             self._event_time = t
         for q in self.queries:
             self._deliver(q, q.engine.set_time(t))
+            self._limit_time(q, t)
 
     def idle(self, ms: int):
         """`ms` of wall-clock time pass with no events on a playback app: its
@@ -481,6 +486,7 @@ class SiddhiAppRuntime:
             self._event_time = t
         for q in self.queries:
             self._deliver(q, q.engine.set_time(t))
+            self._limit_time(q, t)
         self._junction(stream_id, batch)
 
     def _junction(self, stream_id, batch: ColumnBatch):
@@ -511,6 +517,17 @@ class SiddhiAppRuntime:
         """A multi-value cell: the List MultiValueVariableFunctionExecutor returns."""
         return [None if z else decode_value(b, et, self.dictionary) for b, z in elems]
 
+    def _limiter_now(self):
+        # TimestampGenerator.currentTime(): event time in playback, else the wall clock
+        if self.playback and self._event_time is not None:
+            return self._event_time
+        return self._wall_clock()
+
+    def _limit_time(self, q: _QueryRuntime, t: int):
+        if q.limiter is not None and q.limiter.timed():
+            for out in q.limiter.on_time(t):
+                self._emit(q, [r[0] for r in out], None)
+
     def _deliver(self, q: _QueryRuntime, chunks: List[OutputChunk]):
         if not chunks:
             return
@@ -523,6 +540,22 @@ class SiddhiAppRuntime:
                         None if ch.nulls[i, k] else decode_value(ch.values[i, k], t, self.dictionary)
                         for k, t in enumerate(types)]
                 evs.append(Event(int(ch.ts[i]), data, int(ch.types[i]) == EXPIRED))
+            if q.limiter is None:
+                self._emit(q, evs, ch)
+                continue
+            gc = q.qp.rate_group_cols
+            rows = [(e, tuple(repr(e.data[c]) for c in gc) if gc is not None else None) for e in evs]
+            out = q.limiter.process(rows, self._limiter_now())
+            if out:
+                self._emit(q, [r[0] for r in out], None)
+
+    def _emit(self, q: _QueryRuntime, evs, ch):
+        """One output chunk to the query's callbacks and its target stream
+        (OutputRateLimiter.sendToCallBacks); ch: the engine chunk the events
+        are, unchanged (None: rows picked by a rate limiter)."""
+        types = q.qp.output_types
+        lcols = list_columns(q.qp) if pl.T_OBJECT in types else {}
+        if True:
             # QueryCallback.receiveStreamEvent (QueryCallback.java:61-91)
             if q.callbacks:
                 cur = [e for e in evs if not e.is_expired] or None
@@ -532,7 +565,11 @@ class SiddhiAppRuntime:
                     cb.receive(ts, cur, rem)
             # InsertIntoStreamCallback: EXPIRED -> CURRENT, into the target junction
             target = q.qp.target
-            if target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target)):
+            if ch is None and target in self.stream_types and (self.stream_callbacks.get(target) or
+                                                                self.subscribers.get(target)):
+                self._junction(target, rows_to_batch(types, [Event(e.timestamp, e.data) for e in evs],
+                                                     self.dictionary))
+            elif target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target)):
                 cols, nulls = [], []
                 for k, t in enumerate(types):
                     if t == pl.T_OBJECT:   # java.util.List values travel as objects
@@ -637,3 +674,117 @@ class SiddhiManager:
         for r in self._runtimes:
             r.shutdown()
         self._runtimes = []
+
+
+# ---------------------------------------------------------------- output rate limiting
+class OutputRateLimiter:
+    """`output [all|first|last] every <n> events | <time>` on the selector's
+    output chunks (C/query/output/ratelimit/{event,time}/*.java), on the host:
+    it reorders and drops whole rows the engines already projected.  process()
+    takes one selector chunk (rows = (Event, key), key = the group-by values
+    for the per-group kinds) and returns the rows to send, as ONE chunk
+    (OutputRateLimiter.sendToCallBacks); on_timer() is the Scheduler's TIMER
+    (C/util/Scheduler.java:190-220) for the time-based kinds that flush."""
+
+    def __init__(self, rate, grouped: bool):
+        self.unit, self.kind, self.value = rate.unit, rate.kind, int(rate.value)
+        self.grouped = grouped
+        self.counter = 0
+        self.buf = []                    # all: the held rows
+        self.last = None                 # last (ungrouped, time)
+        self.groups = {}                 # first: group -> count / output time; last: group -> row (insertion order)
+        self.out_time = None             # first per time (ungrouped)
+        self.scheduled = None
+        self.notify = []                 # the Scheduler's toNotifyQueue (FIFO)
+
+    def timed(self):
+        return self.unit == "time" and self.kind in ("all", "last")
+
+    def start(self, wall_now: int):
+        # partitionCreated (e.g. AllPerTimeOutputRateLimiter.java:97-108):
+        # scheduledTime = System.currentTimeMillis() + value
+        if self.timed():
+            self.scheduled = wall_now + self.value
+            self.notify.append(self.scheduled)
+
+    def process(self, rows, now: int):
+        out = []
+        if self.unit == "events":
+            if self.kind == "all":                       # AllPerEventOutputRateLimiter.process
+                for r in rows:
+                    self.buf.append(r)
+                    self.counter += 1
+                    if self.counter == self.value:
+                        out += self.buf
+                        self.buf, self.counter = [], 0
+            elif self.kind == "first" and not self.grouped:   # FirstPerEventOutputRateLimiter
+                for r in rows:
+                    self.counter += 1
+                    if self.counter == 1:
+                        out.append(r)
+                    elif self.counter == self.value:
+                        self.counter = 0
+            elif self.kind == "first":                   # FirstGroupByPerEventOutputRateLimiter
+                for r in rows:
+                    c = self.groups.get(r[1])
+                    if c is None:
+                        self.groups[r[1]] = 1
+                        out.append(r)
+                    elif c == self.value - 1:
+                        del self.groups[r[1]]
+                    else:
+                        self.groups[r[1]] = c + 1
+            elif not self.grouped:                       # LastPerEventOutputRateLimiter
+                for r in rows:
+                    self.counter += 1
+                    if self.counter == self.value:
+                        out.append(r)
+                        self.counter = 0
+            else:                                        # LastGroupByPerEventOutputRateLimiter
+                for r in rows:
+                    self.groups[r[1]] = r   # LinkedHashMap.put: a known group keeps its place
+                    self.counter += 1
+                    if self.counter == self.value:
+                        self.counter = 0
+                        out += list(self.groups.values())
+                        self.groups = {}
+            return out
+        if self.kind == "all":                           # AllPerTimeOutputRateLimiter
+            self.buf += rows
+        elif self.kind == "last" and not self.grouped:   # LastPerTimeOutputRateLimiter
+            if rows:
+                self.last = rows[-1]
+        elif self.kind == "last":                        # LastGroupByPerTimeOutputRateLimiter
+            for r in rows:
+                self.groups[r[1]] = r
+        elif not self.grouped:                           # FirstPerTimeOutputRateLimiter: the chunk's first row
+            if rows and (self.out_time is None or self.out_time + self.value <= now):
+                self.out_time = now
+                out.append(rows[0])
+        else:                                            # FirstGroupByPerTimeOutputRateLimiter
+            for r in rows:
+                t0 = self.groups.get(r[1])
+                if t0 is None or t0 + self.value <= now:
+                    self.groups[r[1]] = now
+                    out.append(r)
+        return out
+
+    def on_time(self, t: int):
+        """Due TIMERs up to clock t: the flushed chunks, in order."""
+        chunks = []
+        while self.notify and self.notify[0] <= t:
+            ts = self.notify.pop(0)
+            if ts < self.scheduled:
+                continue
+            if self.kind == "all":
+                out, self.buf = self.buf, []
+            elif not self.grouped:
+                out = [self.last] if self.last is not None else []
+                self.last = None
+            else:
+                out, self.groups = list(self.groups.values()), {}
+            self.scheduled += self.value
+            self.notify.append(self.scheduled)
+            if out:
+                chunks.append(out)
+        return chunks

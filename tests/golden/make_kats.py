@@ -40,6 +40,8 @@ FILES = [
     "query/window/TimeBatchWindowTestCase.java",
     "query/window/TimeLengthWindowTestCase.java",
     "query/window/ExternalTimeWindowTestCase.java",
+    "query/ratelimit/EventOutputRateLimitTestCase.java",
+    "query/ratelimit/TimeOutputRateLimitTestCase.java",
     "query/GroupByTestCase.java",
     "query/FilterTestCase1.java",
     "query/FilterTestCase2.java",
@@ -319,7 +321,8 @@ def _callback_bodies(body):
 def _count_mult(cbody):
     """Events counted per in-event by a callback body (count.addAndGet(inEvents.length) k times)."""
     return (len(re.findall(r"count\.addAndGet\(inEvents\.length\)", cbody)) +
-            len(re.findall(r"count\s*=\s*count\s*\+\s*inEvents\.length", cbody)))
+            len(re.findall(r"count\s*=\s*count\s*\+\s*inEvents\.length", cbody)) +
+            len(re.findall(r"\bcount\s*\+=\s*inEvents\.length", cbody)))
 
 
 def extract(name, body, line, fname):
@@ -443,7 +446,8 @@ def extract(name, body, line, fname):
             if not am:
                 return None, "send form %r" % args[:40]
             try:
-                vals = parse_values(am.group("vals"))
+                # a wall-clock reading as an attribute value: the send's clock
+                vals = parse_values(am.group("vals").replace("System.currentTimeMillis()", "%dL" % clock))
             except ValueError as e:
                 return None, str(e)
             ts_expr = am.group("ts")
