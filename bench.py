@@ -96,6 +96,17 @@ def gen_roundrobin_columns(torch, n, keys_total, delta, rank, world, dev):
     return sym, price, vol, ts, seq
 
 
+def align_calls(batch, n, call=1024):
+    """Micro-batch size for n events in as many pushes as `batch` gives, each
+    push whole InputHandler calls of `call` events (a cut inside a call would
+    make two calls of it)."""
+    if n <= call or batch >= n:
+        return max(1, min(batch, n))
+    k = -(-n // max(1, batch))          # pushes
+    b = -(-n // k)
+    return min(n, -(-b // call) * call)
+
+
 def align_rr(batch, world, call=1024):
     """Largest micro-batch <= batch (at least one unit) whose cuts a * world are
     multiples of the call size: round-robin micro-batches then hold whole
@@ -304,7 +315,7 @@ def run_multi(args, torch, dist, rank, world, local, dev):
             grouped.update(idx)
     units += [(None, [i]) for i in mine if i not in grouped]
     # 100 queries each keep their own scratch: 10M-event micro-batches by default
-    batch = min(args.batch if args.batch != 50_000_000 else 10_000_000, n)
+    batch = align_calls(min(args.batch if args.batch != 50_000_000 else 10_000_000, n), n)
     cuts = list(range(0, n, batch)) + [n]
     offs_all = wl.call_offsets(n)
 
@@ -645,7 +656,7 @@ def main():
         from siddhi_amd import exchange as ex
         he.context(local)
         dq = he.DeviceQuery(qp.ir, device=local)
-        batch = min(args.batch, n)
+        batch = align_calls(min(args.batch, n), n)   # micro-batches of whole InputHandler calls
         if seqs is not None:
             # a micro-batch [a, b) of this rank's round-robin share spans global
             # seqs [a * world, b * world): cut on InputHandler call boundaries
@@ -853,8 +864,11 @@ def main():
             # at least two pushes: the prefix cut like the timed stream is, in
             # micro-batches, so the state carried between pushes is compared
             # (at most half the prefix per push)
+            # (at most half the prefix per push, whole InputHandler calls: a push
+            # cut inside a call would make two calls of it)
+            pb = align_calls(max(1, min(batch, sample // 2)), sample)
             prefix, pc = parity_prefix(torch, he, qp, [sym, price, vol], ts, offs_all, sample, ora_rows,
-                                       not pattern, max(1, min(batch, sample // 2)))
+                                       not pattern, pb)
             if args.config in ("P1", "P3", "P3-dense"):
                 # the §8d counts two ways on the same prefix: the device's walks
                 # ((partial, event) pairs visited, the expiring visit included) and
