@@ -66,6 +66,27 @@ __device__ __forceinline__ Val col_load(const ColSet& cs, int64_t row, int attr)
   return v;
 }
 
+// col_load of one column given by its pointers and type (pre-resolved
+// descriptors: no column-table lookups per call).
+__device__ __forceinline__ Val col_load_raw(const void* col, const uint8_t* nm, int type, int64_t row) {
+  Val v;
+  v.null = 0;
+  switch (type) {
+    case SHD_T_STRING: v.b = gld((const uint32_t*)col, row); break;
+    case SHD_T_INT: v.b = p_i32(gld((const int32_t*)col, row)); break;
+    case SHD_T_LONG: v.b = (uint64_t)gld((const int64_t*)col, row); break;
+    case SHD_T_FLOAT: v.b = (uint64_t)gld((const uint32_t*)col, row); break;
+    case SHD_T_DOUBLE: v.b = gld((const uint64_t*)col, row); break;
+    case SHD_T_BOOL: v.b = gld((const uint8_t*)col, row) ? 1 : 0; break;
+    default: v.b = 0; v.null = 1;
+  }
+  if (nm && gld(nm, row)) {
+    v.b = 0;
+    v.null = 1;
+  }
+  return v;
+}
+
 // Number.xValue() widening used by the planner's CVT ops.
 __device__ __forceinline__ uint64_t d_cvt(uint64_t b, int from, int to) {
   if (from == to) return b;

@@ -371,6 +371,43 @@ static bool block_skip_term(const FPred& fp, int s2, int& ci, int& side, int& op
   return false;
 }
 
+// Split f2 (F2Split) for the plain form: every comparison either reads no
+// e2 attribute (decided once per partial) or compares one plain e2 attribute
+// load (+ conversion) with a term free of e2.  False: eval_fpred per step.
+static bool split_f2(const FPred& fp, int s2, const ExtRows& x, F2Split& sp) {
+  sp = F2Split{};
+  if (!fp.ok || fp.n > kSplitMax) return false;
+  auto e2dep = [&](const FAtom& t) { return t.kind == FA_LOAD && t.st == s2; };
+  auto dep = [&](const FTerm& t) { return e2dep(t.a) || (t.aop != 0 && e2dep(t.b)); };
+  for (int i = 0; i < fp.n; i++) {
+    const FCmp& c = fp.c[i];
+    SplitCmp& o = sp.c[i];
+    o.op = c.op;
+    o.type = c.type;
+    const bool dl = dep(c.l), dr = dep(c.r);
+    if (!dl && !dr) {
+      o.konst = 1;
+      continue;
+    }
+    if (dl && dr) return false;
+    const FTerm& e = dl ? c.l : c.r;
+    if (e.aop != 0 || (e.a.idx != 0 && e.a.idx != SHD_IDX_CURRENT)) return false;
+    const int attr = e.a.attr;
+    if (attr < 0 || attr >= x.batch.ncols || attr >= kMaxCols) return false;
+    o.swap = dr ? 1 : 0;
+    o.pos = (x.bpos_mask >> attr) & 1u;
+    const ColSet& cs = o.pos ? x.bpos : x.batch;
+    o.col = cs.col[attr];
+    o.nul = cs.nul[attr];
+    o.ctype = cs.type[attr];
+    o.cvt_from = e.a.cvt_from;
+    o.cvt_to = e.a.cvt_to;
+  }
+  sp.n = fp.n;
+  sp.ok = 1;
+  return true;
+}
+
 // Cooperative walk (resume MODE 2): the 64 lanes of a wave scan ONE deferred
 // partial's later positions 64 at a time (coalesced loads, f2 evaluated for all
 // of them at once) and ballot the first terminating position -- the same
@@ -408,6 +445,9 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
   int64_t ra = -1, rb = -1;
   int32_t other = -1;
   if (a.logical == 2) and_carried(a, r, fm, ra, rb);
+  // split f2: the partial's side once (the same for every lane)
+  SplitThr sth;
+  if (FAST && a.sp.ok && !a.logical) sth = split_prep(a, r, p);
   uint64_t wsteps = 0;
   bool wviol = false;
   bool thr_ok = false;
@@ -515,7 +555,8 @@ __device__ __forceinline__ void coop_resume(const ScanArgs& a, const DExprSet& e
       PairCtx cx{&a.x, r, r2, a.s_first};
       cx.q2 = q;
       cx.q1 = p;
-      hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+      if (FAST && a.sp.ok && !a.logical) hit = split_eval(a.sp, sth, r2 - a.x.C, q);
+      else hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
       int32_t br = 0;
       if (!hit && a.logical) {
         cx.s2 = a.s_second;
@@ -689,6 +730,108 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
     }
   }
   scan_block_reduce(steps, pruned, viol, nm, no, blk, slot0 + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
+}
+
+// Lockstep walks (plain `e1 -> e2` form, full-key sort, pre-decoded f2): one
+// lane per position as in k_forward_scan, but f2 is evaluated in the walk
+// itself, so every candidate of a wave starts at its successor and all of
+// them advance one position per round -- at round d lane i reads position
+// base + i + d: the key / payload / time / e2-attribute loads of a wave are
+// one contiguous 64-position slice per round (coalesced, and each slice
+// overlaps the previous one by 63 positions in L1/L2), where the deferred
+// walks start at scattered B events.  Same steps and outcomes as
+// walk_partial; a walk that has met a B event and still runs after 64
+// positions is handed to the wave-cooperative pass (PS_CONT, resume position
+// in match_row).  Writes the per-tile counts like k_forward_scan.
+template <bool TS64>
+__global__ __launch_bounds__(kBlock) void k_lockstep_walk(const ScanArgs* __restrict__ ap, int64_t n_ext, int64_t tile,
+                                                          const uint32_t* __restrict__ skey32,
+                                                          const uint32_t* __restrict__ spv,
+                                                          const int32_t* __restrict__ sts32,
+                                                          const int64_t* __restrict__ sts64,
+                                                          int32_t* __restrict__ match_row, uint8_t* __restrict__ pst,
+                                                          uint32_t* __restrict__ bcnt, ScanOut* __restrict__ blk) {
+  const ScanArgs& a = *ap;
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0, nm = 0, no = 0;
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
+  const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
+  const GlobalPos<false, TS64> ld{skey32, nullptr, spv, sts32, sts64, tbase, a.partitioned};
+  for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) {
+    uint32_t pvp;
+    int64_t tsi;
+    uint64_t k = 0;
+    ld(p, pvp, tsi, k);
+    uint8_t out = PS_NONE;
+    if (pv_flags(pvp) & F_CAND) {
+      const int64_t r = pv_row(pvp);
+      uint8_t st = ST_OPEN;
+      bool metb = false;
+      SplitThr sth;   // split f2: prepared at the first B event
+      int32_t j = -1;
+      int64_t prev = tsi;
+      int64_t q = p + 1;
+      for (int d = 0; q < n_ext; q++, d++) {
+        if (d >= 64 && metb) {
+          st = ST_YIELD;
+          break;
+        }
+        uint32_t pq;
+        int64_t tq;
+        uint64_t kq = 0;
+        ld(q, pq, tq, kq);
+        const uint32_t fq = pv_flags(pq);
+        if (fq & F_SKIP) continue;   // dropped (null-key) rows: passed over
+        if (kq != k) break;          // end of the key's run
+        if (!(fq & F_NEW)) continue;
+        if (a.within != INT64_MAX && tq < prev) {
+          viol = 1;
+          break;
+        }
+        prev = tq;
+        steps++;
+        if (tq - tsi > a.within) {
+          st = ST_DEAD;
+          break;
+        }
+        if (fq & F_B) {
+          bool hit;
+          if (a.sp.ok) {
+            if (!metb) sth = split_prep(a, r, p);
+            hit = split_eval(a.sp, sth, (int64_t)pv_row(pq) - a.x.C, q);
+          } else {
+            PairCtx cx{&a.x, r, (int64_t)pv_row(pq), a.s_first};
+            cx.q2 = q;
+            cx.q1 = p;
+            hit = eval_fpred(a.f2.fp, cx);
+          }
+          metb = true;
+          if (hit) {
+            st = ST_MATCH;
+            j = (int32_t)pv_row(pq);
+            break;
+          }
+        }
+      }
+      if (st == ST_OPEN && a.prune && a.t_end - tsi > a.within) st = ST_PRUNED;
+      if (st == ST_MATCH) {
+        out = PS_MATCH;
+        match_row[p] = j;
+        nm++;
+      } else if (st == ST_OPEN) {
+        out = metb ? (uint8_t)(PS_OPEN | PS_PEND) : (uint8_t)PS_OPEN;
+        no++;
+      } else if (st == ST_PRUNED) {
+        pruned++;
+      } else if (st == ST_YIELD) {
+        out = PS_CONT;
+        match_row[p] = (int32_t)q;
+      }
+    }
+    pst[p] = out;
+  }
+  scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
 }
 
 // Per-tile match / open counts of the outcome bytes (the compaction tiles of
@@ -1775,11 +1918,17 @@ struct PatternEngine : Engine {
       const int m = atoi(f);
       if (m >= 0 && m <= 3 && !(m >= 2 && (hash_mask || (logical == 2 && (m == 3 || !and_indep))))) rmode = m;
     }
+    // plain form over the full-key sort with a pre-decoded f2 and walks shorter
+    // than the block-skip range: lockstep walks (k_lockstep_walk) instead of
+    // the hot walk + deferred walks (SHD_LOCKSTEP=0: off)
+    const char* ls_env = getenv("SHD_LOCKSTEP");
+    const bool lockstep = grouped && !hash_mask && !sorted64 && logical == 0 && isB && fast2 && e_key < 64.0 &&
+                          !(ls_env && atoi(ls_env) == 0) && !bw && ls_env;
     // dense grouped walks revisit each position once per partial of its key
     // inside `within`: the e2 attributes the filters read are copied into
     // position order once, so the walks load them coalesced; worth its pass
     // only when walks are long (SHD_NO_BPOS: off, SHD_BPOS: always when dense)
-    if (grouped && rmode != 0 && isB && bpos_mask && !getenv("SHD_NO_BPOS") && (e_key >= 8.0 || getenv("SHD_BPOS"))) {
+    if (grouped && (rmode != 0 || lockstep) && isB && bpos_mask && !getenv("SHD_NO_BPOS") && (e_key >= 8.0 || getenv("SHD_BPOS"))) {
       // e1 operands position-major too (same stream schema, columns the carry keeps)
       uint32_t apos = getenv("SHD_NO_APOS") ? 0u : (apos_mask & carry_mask);
       for (int c = 0; c < kMaxCols; c++)
@@ -1799,10 +1948,13 @@ struct PatternEngine : Engine {
       hipLaunchKernelGGL(k_gather_bpos, dim3(grid_for(n_ext, 1, 4096)), dim3(kBlock), 0, s, dev_args(sa.x), spv, n_ext);
       SHD_CHECK_LAUNCH();
     }
+    // plain form: f2 split per comparison (SHD_NO_SPLIT: eval_fpred per step)
+    sa.sp = F2Split{};
+    if (fast2 && logical == 0 && !getenv("SHD_NO_SPLIT")) split_f2(sa.f2.fp, s_first, sa.x, sa.sp);
     // long dense walks (a partial expects >= 64 events of its key inside
     // `within`) skip whole 64-position blocks that cannot end them
     sa.bsum = nullptr;
-    const bool skip_ok = grouped && !hash_mask && !sorted64 && !ts64 && isB && logical == 0 && rmode != 0 &&
+    const bool skip_ok = grouped && !hash_mask && !sorted64 && !ts64 && isB && logical == 0 && rmode != 0 && !lockstep &&
                          sa.f2.fp.ok && !getenv("SHD_NO_BLOCK_SKIP") && (e_key >= 64.0 || getenv("SHD_BLOCK_SKIP"));
     if (skip_ok && block_skip_term(sa.f2.fp, s_first, sa.bs_ci, sa.bs_side, sa.bs_op, sa.bs_attr)) {
       d_bsum.reserve(ceil_div(n_ext, 64) * (int64_t)sizeof(BlockSum));
@@ -1871,13 +2023,27 @@ struct PatternEngine : Engine {
       if (fast2) { SHD_LAUNCH_RESUME2(true, true); }
       else { SHD_LAUNCH_RESUME2(true, false); }
     } else {
-      if (hash_mask) {
+      if (lockstep) {
+        // lockstep walks with f2, then the wave-cooperative pass for the
+        // capped ones (PS_CONT)
+        if (ts64)
+          hipLaunchKernelGGL(k_lockstep_walk<true>, dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32, spv,
+                             sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(),
+                             d_blk.as<ScanOut>());
+        else
+          hipLaunchKernelGGL(k_lockstep_walk<false>, dim3(ntile), dim3(kBlock), 0, s, d_sa, n_ext, tile, skey32, spv,
+                             sts32, sts64, d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(),
+                             d_blk.as<ScanOut>());
+      } else if (hash_mask) {
         if (ts64) SHD_LAUNCH_SCAN(false, true, true); else SHD_LAUNCH_SCAN(false, false, true);
       } else {
         if (ts64) SHD_LAUNCH_SCAN(false, true, false); else SHD_LAUNCH_SCAN(false, false, false);
       }
       SHD_CHECK_LAUNCH();
-      if (sa.bsum) {
+      if (lockstep) {
+        if (ts64) SHD_LAUNCH_RESUME_D(false, true, true, 2, ntile);
+        else SHD_LAUNCH_RESUME_D(false, true, false, 2, ntile);
+      } else if (sa.bsum) {
         if (rmode == 3) {
           SHD_LAUNCH_SKIP(3, ntile);
           SHD_CHECK_LAUNCH();
@@ -1895,7 +2061,7 @@ struct PatternEngine : Engine {
     SHD_CHECK_LAUNCH();
     // partials: [0, ntile) hot walk, [ntile, 2 ntile) deferred walks, [2 ntile, 3 ntile) continued walks
     hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(),
-                       (rmode == 3 ? 3 : 2) * ntile,
+                       (rmode == 3 && !lockstep ? 3 : 2) * ntile,
                        d_so);
     SHD_CHECK_LAUNCH();
     }

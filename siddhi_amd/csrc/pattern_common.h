@@ -127,6 +127,25 @@ struct BlockSum {
   uint64_t newmask;   // bit i: position 64b + i is an F_NEW non-skip event
 };
 
+// f2 of the plain form split per comparison (split_f2, engine_pattern.hip):
+// the side free of e2 is evaluated once per partial (split_prep), the e2 side
+// is a plain attribute load (+ one conversion) per walk step (split_eval) --
+// the same operations as eval_fpred, without re-deciding the descriptor's
+// atoms, the e1 operand loads and the e1 arithmetic at every step.
+struct SplitCmp {
+  const void* col;          // the e2 attribute's column: position-major (bpos) when pos, else batch rows
+  const uint8_t* nul;
+  int32_t ctype, pos, cvt_from, cvt_to;
+  int32_t op, type;
+  int32_t swap;             // the e2 load is the right operand
+  int32_t konst;            // no e2 operand: decided once per partial
+};
+constexpr int kSplitMax = 3;
+struct F2Split {
+  int32_t ok, n;
+  SplitCmp c[kSplitMax];
+};
+
 struct ScanArgs {
   ExtRows x;
   DExprSet es;
@@ -151,6 +170,7 @@ struct ScanArgs {
   // e1 side (bs_side 0: its right term, 1: its left); bsum null: no skipping
   const BlockSum* bsum;
   int bs_ci, bs_side, bs_op, bs_attr;
+  F2Split sp;           // plain form: f2 split per comparison (sp.ok = 0: eval_fpred)
 };
 
 struct ScanOut {

@@ -32,6 +32,48 @@ struct GlobalPos {
   }
 };
 
+// Split f2 (F2Split): the per-partial side of every comparison, and the
+// step's evaluation against an e2 event (batch row r2b = ext row - C, sorted
+// position q2).  Same result as eval_fpred(a.f2.fp, PairCtx{r, r2}).
+struct SplitThr {
+  Val t[kSplitMax];
+  bool never;   // a comparison free of e2 fails: f2 never passes for this partial
+};
+__device__ __forceinline__ SplitThr split_prep(const ScanArgs& a, int64_t r, int64_t q1) {
+  SplitThr th;
+  th.never = false;
+  PairCtx cx{&a.x, r, -1, a.s_first};
+  cx.q1 = q1;
+#pragma unroll
+  for (int i = 0; i < kSplitMax; i++) {
+    th.t[i].b = 0;
+    th.t[i].null = 1;
+    if (i >= a.sp.n) continue;
+    const FCmp& c = a.f2.fp.c[i];
+    if (a.sp.c[i].konst) {
+      const Val l = fp_term(c.l, cx), rr = fp_term(c.r, cx);
+      if (l.null || rr.null || !d_compare(c.op, c.type, l.b, rr.b)) th.never = true;
+    } else {
+      th.t[i] = fp_term(a.sp.c[i].swap ? c.l : c.r, cx);
+    }
+  }
+  return th;
+}
+__device__ __forceinline__ bool split_eval(const F2Split& sp, const SplitThr& th, int64_t r2b, int64_t q2) {
+  if (th.never) return false;
+#pragma unroll
+  for (int i = 0; i < kSplitMax; i++) {
+    if (i >= sp.n) break;
+    const SplitCmp& c = sp.c[i];
+    if (c.konst) continue;
+    Val v = col_load_raw(c.col, c.nul, c.ctype, c.pos ? q2 : r2b);
+    if (c.cvt_to >= 0 && !v.null) v.b = d_cvt(v.b, c.cvt_from, c.cvt_to);
+    if (v.null || th.t[i].null) return false;
+    if (!d_compare(c.op, c.type, c.swap ? th.t[i].b : v.b, c.swap ? v.b : th.t[i].b)) return false;
+  }
+  return true;
+}
+
 // Block skip: f2's threshold for partial (row r, sorted position q1) -- the
 // e1 side of comparison bs_ci (null: f2 can never pass).
 __device__ __forceinline__ Val skip_threshold(const ScanArgs& a, int64_t r, int64_t q1) {
@@ -77,6 +119,8 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
   Val thr;
   thr.b = 0;
   thr.null = 1;
+  SplitThr sth;            // split f2: the partial's side, prepared at its first B event
+  bool th_ok = false;
   int64_t tried = -1;      // block whose skip was last tried
   int64_t last_new = q;    // position of the walk's last F_NEW step (the resume point's time is prev)
   while (!stop && q < n_ext) {
@@ -221,7 +265,16 @@ __device__ __forceinline__ uint8_t walk_partial(const ScanArgs& a, const DExprSe
           PairCtx cx{&a.x, r, r2, a.s_first};
           cx.q2 = q;
           cx.q1 = q1;
-          bool hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+          bool hit;
+          if (FAST && a.sp.ok && !a.logical) {
+            if (!th_ok) {
+              sth = split_prep(a, r, q1);
+              th_ok = true;
+            }
+            hit = split_eval(a.sp, sth, r2 - a.x.C, q);
+          } else {
+            hit = FAST ? eval_fpred(a.f2.fp, cx) : eval_filters(es, a.f2, cx);
+          }
           int32_t br = 0;
           if (!hit && a.logical) {
             // LogicalPreStateProcessor (OR): the partner processor sees the
