@@ -900,9 +900,16 @@ struct Lane {
     const DPre& pr = P.pre[p];
     fl(p) &= (uint8_t)~FL_CHANGED;
     SECtx cx{this, s};
-    for (int i = 0; i < pr.filters.n; i++) {
+    if (pr.filters.n == 1 && pr.filters.fp.ok) {
+      // one filter pre-decoded on the host (compile_fast_pred): straight-line
+      // comparisons, no bytecode fetched and dispatched per state event
       scans++;
-      if (!eval_bool(es.ins + pr.filters.f[i].off, pr.filters.f[i].len, es.consts, cx)) return false;
+      if (!eval_fpred(pr.filters.fp, cx)) return false;
+    } else {
+      for (int i = 0; i < pr.filters.n; i++) {
+        scans++;
+        if (!eval_bool(es.ins + pr.filters.f[i].off, pr.filters.f[i].len, es.consts, cx)) return false;
+      }
     }
     postProcess(pr.thisPost, s);
     return true;

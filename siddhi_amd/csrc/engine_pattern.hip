@@ -402,6 +402,28 @@ static bool split_f2(const FPred& fp, int s2, const ExtRows& x, F2Split& sp) {
     o.ctype = cs.type[attr];
     o.cvt_from = e.a.cvt_from;
     o.cvt_to = e.a.cvt_to;
+    // pre-resolved kinds (split_eval): the operator flipped so e2 is on the left
+    const bool cvt = o.cvt_to >= 0 && o.cvt_to != o.cvt_from;
+    const bool rel = c.op == SHD_OP_EQ || c.op == SHD_OP_NE || c.op == SHD_OP_GT || c.op == SHD_OP_GE ||
+                     c.op == SHD_OP_LT || c.op == SHD_OP_LE;
+    o.kind = SK_GENERIC;
+    if (rel && c.type == SHD_T_DOUBLE && o.ctype == SHD_T_FLOAT && cvt && o.cvt_from == SHD_T_FLOAT &&
+        o.cvt_to == SHD_T_DOUBLE)
+      o.kind = SK_F32_F64;
+    else if (rel && c.type == SHD_T_DOUBLE && o.ctype == SHD_T_DOUBLE && !cvt)
+      o.kind = SK_F64;
+    else if ((c.op == SHD_OP_EQ || c.op == SHD_OP_NE) && c.type == SHD_T_STRING && o.ctype == SHD_T_STRING && !cvt)
+      o.kind = SK_STR_EQ;
+    else if (rel && c.type == SHD_T_INT && o.ctype == SHD_T_INT && !cvt)
+      o.kind = SK_I32;
+    if (o.kind != SK_GENERIC && o.swap) {
+      switch (c.op) {
+        case SHD_OP_GT: o.op = SHD_OP_LT; break;
+        case SHD_OP_GE: o.op = SHD_OP_LE; break;
+        case SHD_OP_LT: o.op = SHD_OP_GT; break;
+        case SHD_OP_LE: o.op = SHD_OP_GE; break;
+      }
+    }
   }
   sp.n = fp.n;
   sp.ok = 1;
@@ -1920,10 +1942,11 @@ struct PatternEngine : Engine {
     }
     // plain form over the full-key sort with a pre-decoded f2 and walks shorter
     // than the block-skip range: lockstep walks (k_lockstep_walk) instead of
-    // the hot walk + deferred walks (SHD_LOCKSTEP=0: off)
+    // the hot walk + deferred walks -- by default where the capped lane walks
+    // would run (dense keys); SHD_LOCKSTEP=0 / 1 forces
     const char* ls_env = getenv("SHD_LOCKSTEP");
     const bool lockstep = grouped && !hash_mask && !sorted64 && logical == 0 && isB && fast2 && e_key < 64.0 &&
-                          !(ls_env && atoi(ls_env) == 0) && !bw && ls_env;
+                          !bw && (ls_env ? atoi(ls_env) != 0 : rmode == 3);
     // dense grouped walks revisit each position once per partial of its key
     // inside `within`: the e2 attributes the filters read are copied into
     // position order once, so the walks load them coalesced; worth its pass

@@ -139,7 +139,10 @@ struct SplitCmp {
   int32_t op, type;
   int32_t swap;             // the e2 load is the right operand
   int32_t konst;            // no e2 operand: decided once per partial
+  int32_t kind;             // SK_*: a pre-resolved load + conversion + comparison (op with e2 on the left)
 };
+// split comparison kinds (SK_GENERIC: col_load_raw + d_cvt + d_compare)
+enum : int32_t { SK_GENERIC = 0, SK_F32_F64 = 1, SK_F64 = 2, SK_STR_EQ = 3, SK_I32 = 4 };
 constexpr int kSplitMax = 3;
 struct F2Split {
   int32_t ok, n;

@@ -55,6 +55,7 @@ __device__ __forceinline__ SplitThr split_prep(const ScanArgs& a, int64_t r, int
       if (l.null || rr.null || !d_compare(c.op, c.type, l.b, rr.b)) th.never = true;
     } else {
       th.t[i] = fp_term(a.sp.c[i].swap ? c.l : c.r, cx);
+      if (th.t[i].null) th.never = true;   // a null operand fails the comparison at every step
     }
   }
   return th;
@@ -66,10 +67,50 @@ __device__ __forceinline__ bool split_eval(const F2Split& sp, const SplitThr& th
     if (i >= sp.n) break;
     const SplitCmp& c = sp.c[i];
     if (c.konst) continue;
-    Val v = col_load_raw(c.col, c.nul, c.ctype, c.pos ? q2 : r2b);
-    if (c.cvt_to >= 0 && !v.null) v.b = d_cvt(v.b, c.cvt_from, c.cvt_to);
-    if (v.null || th.t[i].null) return false;
-    if (!d_compare(c.op, c.type, c.swap ? th.t[i].b : v.b, c.swap ? v.b : th.t[i].b)) return false;
+    const int64_t row = c.pos ? q2 : r2b;
+    const uint64_t t = th.t[i].b;
+    // the common kinds: one typed load, the comparison with e2 on the left
+    // (the host flipped the operator of a swapped comparison)
+    int cc;
+    switch (c.kind) {
+      case SK_F32_F64: {
+        const double x = (double)gld((const float*)c.col, row), y = v_f64(t);
+        cc = (x < y) ? -1 : (x > y) ? 1 : (x == y) ? 0 : 2;
+        break;
+      }
+      case SK_F64: {
+        const double x = gld((const double*)c.col, row), y = v_f64(t);
+        cc = (x < y) ? -1 : (x > y) ? 1 : (x == y) ? 0 : 2;
+        break;
+      }
+      case SK_STR_EQ:
+        cc = ((uint64_t)gld((const uint32_t*)c.col, row) == t) ? 0 : 2;
+        break;
+      case SK_I32: {
+        const int32_t x = gld((const int32_t*)c.col, row), y = v_i32(t);
+        cc = x < y ? -1 : (x > y ? 1 : 0);
+        break;
+      }
+      default: {
+        Val v = col_load_raw(c.col, c.nul, c.ctype, row);
+        if (c.cvt_to >= 0 && !v.null) v.b = d_cvt(v.b, c.cvt_from, c.cvt_to);
+        if (v.null) return false;
+        if (!d_compare(c.op, c.type, c.swap ? t : v.b, c.swap ? v.b : t)) return false;
+        continue;
+      }
+    }
+    if (c.nul && gld(c.nul, row)) return false;
+    bool ok;
+    switch (c.op) {
+      case SHD_OP_EQ: ok = cc == 0; break;
+      case SHD_OP_NE: ok = cc != 0; break;
+      case SHD_OP_GT: ok = cc == 1; break;
+      case SHD_OP_GE: ok = cc == 1 || cc == 0; break;
+      case SHD_OP_LT: ok = cc == -1; break;
+      case SHD_OP_LE: ok = cc == -1 || cc == 0; break;
+      default: ok = false;
+    }
+    if (!ok) return false;
   }
   return true;
 }

@@ -1,9 +1,9 @@
 """Lockstep pattern walks and the split f2 (k_lockstep_walk, siddhi_amd/csrc/engine_pattern.hip,
-opt-in SHD_LOCKSTEP=1): f2 evaluated inside the one-lane-per-position walk,
+the default for dense keys; SHD_LOCKSTEP=1 / 0 forces it on / off): f2 evaluated inside the one-lane-per-position walk,
 every candidate of a wave advancing one sorted position per round, walks past
 64 positions continued by the wave-cooperative pass (PS_CONT).  Rows must
 equal the CPU oracle and the walk counters (partial_scans, matches) the
-default hot-walk + deferred-walk path's, for sparse keys, dense keys with
+hot-walk + deferred-walk path's, for sparse keys, dense keys with
 walks beyond the 64-position cap, null e2 attributes and a push going back
 in time inside a key.
 
@@ -24,10 +24,7 @@ CASES = {
 
 
 def run(qp, bs, monkeypatch, lockstep):
-    if lockstep:
-        monkeypatch.setenv("SHD_LOCKSTEP", "1")
-    else:
-        monkeypatch.delenv("SHD_LOCKSTEP", raising=False)
+    monkeypatch.setenv("SHD_LOCKSTEP", "1" if lockstep else "0")
     return run_device(qp, bs)
 
 
@@ -65,8 +62,10 @@ def test_lockstep_time_going_back(hip_available, monkeypatch):
 
 
 # f2 split per comparison (split_f2 / split_prep / split_eval): a comparison
-# free of e2 decided once per partial, the e2 load on either side, int / long
-# e2 attributes converted to the comparison's type, null e2 attributes
+# free of e2 decided once per partial, the e2 load on either side (swapped
+# operators flipped), int / long e2 attributes converted to the comparison's
+# type, the pre-resolved kinds (float column vs double: the StockStream
+# configs; string equality; double) and the generic one, null e2 attributes
 SPLIT_F2 = {
     "konst": "e1.volume > 20 and price > e1.price * 1.05",
     "konst-false": "e1.price < 0.0 and price > e1.price",
@@ -74,6 +73,7 @@ SPLIT_F2 = {
     "cvt-long": "volume > e1.volume",
     "cvt-mixed": "volume > e1.price",
     "two-e2": "price > e1.price and volume < e1.volume",
+    "ne": "price != e1.price and e1.price <= price",
 }
 
 
@@ -90,3 +90,31 @@ def test_split_f2_equals_oracle(hip_available, monkeypatch, name, lockstep):
     _, c_plain, _ = run(qp, bs, monkeypatch, lockstep)
     assert c_split["partial_scans"] == c_plain["partial_scans"]
     assert c_split["matches"] == c_plain["matches"] == len(ora[2])
+
+
+def test_split_f2_float_int_schema(hip_available, monkeypatch):
+    """The StockStream schema (float price, int volume): SK_F32_F64 (the
+    configs' `price > e1.price * 1.05`) and SK_I32, against the oracle and the
+    unsplit walk."""
+    import numpy as np
+    from siddhi_amd.runtime import ColumnBatch
+    schema = "@app:playback define stream S (symbol string, price float, volume int); "
+    q = (schema + "@info(name='q') from every e1=S[price > 60] -> e2=S[symbol == e1.symbol and "
+         "price > e1.price * 1.05 and volume >= e1.volume] within 1 sec "
+         "select e1.symbol as s, e1.price as p1, e2.price as p2, e2.volume as v insert into O;")
+    qp, _ = compile_single_query(q)
+    bs = []
+    for o, b in batches(nulls=True, seed=31, keys=2_000):
+        sym, price, vol = b.cols
+        bs.append((o, ColumnBatch(b.ts, [sym, price.astype(np.float32), (vol % 1000).astype(np.int32)],
+                                  b.nulls, b.call_offsets)))
+    ora = run_oracle(qp, bs)
+    for ls in (False, True):
+        monkeypatch.delenv("SHD_NO_SPLIT", raising=False)
+        dev, c_split, kind = run(qp, bs, monkeypatch, ls)
+        assert kind == 1 and len(ora[2]) > 0
+        assert_same_rows(dev, ora)
+        monkeypatch.setenv("SHD_NO_SPLIT", "1")
+        _, c_plain, _ = run(qp, bs, monkeypatch, ls)
+        assert c_split["partial_scans"] == c_plain["partial_scans"]
+        assert c_split["matches"] == c_plain["matches"] == len(ora[2])
