@@ -248,6 +248,9 @@ struct Engine {
   DExpr dexpr(int e) const { return DExpr{ex.off[e], ex.len[e]}; }
   DExprSet dset() const { return DExprSet{ex.ins.as<int4>(), ex.consts.as<uint64_t>(), ex.nins, ex.nconsts}; }
   DFilters dfilters(const std::vector<int>& ids) const;
+  // An output / operand expression that is one LOAD / CONST / NULL, optionally
+  // followed by one CVT, pre-decoded as an FAtom (fp_atom: no bytecode per row).
+  bool fast_atom(int expr_id, FAtom& out) const;
 };
 
 std::unique_ptr<Engine> make_pattern_engine(const Plan& p, std::string& why);

@@ -790,19 +790,30 @@ __global__ __launch_bounds__(kBlock) void k_lockstep_walk(const ScanArgs* __rest
       const int64_t r = pv_row(pvp);
       uint8_t st = ST_OPEN;
       bool metb = false;
-      SplitThr sth;   // split f2: prepared at the first B event
+      // split f2: the partial's side up front (its loads overlap the first
+      // position's)
+      SplitThr sth;
+      if (a.sp.ok) sth = split_prep(a, r, p);
       int32_t j = -1;
       int64_t prev = tsi;
       int64_t q = p + 1;
+      // software pipeline: position q + 1 is loaded while q's f2 operand
+      // load is in flight (one memory round trip per step, not two; two
+      // deep -- q + 1's operands too -- measured slower: 11.6 vs 10.1 ms per
+      // P3-dense step, the extra registers cost occupancy)
+      uint32_t pn = 0;
+      int64_t tn = 0;
+      uint64_t kn = 0;
+      if (q < n_ext) ld(q, pn, tn, kn);
       for (int d = 0; q < n_ext; q++, d++) {
         if (d >= 64 && metb) {
           st = ST_YIELD;
           break;
         }
-        uint32_t pq;
-        int64_t tq;
-        uint64_t kq = 0;
-        ld(q, pq, tq, kq);
+        const uint32_t pq = pn;
+        const int64_t tq = tn;
+        const uint64_t kq = kn;
+        if (q + 1 < n_ext) ld(q + 1, pn, tn, kn);
         const uint32_t fq = pv_flags(pq);
         if (fq & F_SKIP) continue;   // dropped (null-key) rows: passed over
         if (kq != k) break;          // end of the key's run
@@ -820,7 +831,6 @@ __global__ __launch_bounds__(kBlock) void k_lockstep_walk(const ScanArgs* __rest
         if (fq & F_B) {
           bool hit;
           if (a.sp.ok) {
-            if (!metb) sth = split_prep(a, r, p);
             hit = split_eval(a.sp, sth, (int64_t)pv_row(pq) - a.x.C, q);
           } else {
             PairCtx cx{&a.x, r, (int64_t)pv_row(pq), a.s_first};
@@ -1006,6 +1016,8 @@ struct ProjArgs {
   const int32_t* sot;
   int64_t chunk0;
   int64_t row0;         // output buffer offset
+  int fast;             // every output is a pre-decoded atom (oat): no bytecode per row
+  FAtom oat[kMaxCols];
 };
 
 __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__ ap, const uint32_t* pj,
@@ -1030,7 +1042,7 @@ __global__ __launch_bounds__(kBlock) void k_project(const ProjArgs* __restrict__
     PairCtx cx{&x, i, j, br ? a.s_second : a.s_first, true, other, br ? a.s_first : a.s_second};
     int64_t row = a.row0 + k;
     for (int c = 0; c < a.nout; c++) {
-      Val v = eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
+      const Val v = a.fast ? fp_atom(a.oat[c], cx) : eval_expr(es.ins + a.outs[c].off, a.outs[c].len, es.consts, cx);
       o_vals[row * a.nout + c] = v.b;
       o_nul[row * a.nout + c] = (uint8_t)v.null;
     }
@@ -2171,7 +2183,11 @@ struct PatternEngine : Engine {
         pr.x = x;
         pr.es = dset();
         pr.nout = (int)outs.size();
-        for (size_t c = 0; c < outs.size(); c++) pr.outs[c] = dexpr(outs[c]);
+        pr.fast = 1;
+        for (size_t c = 0; c < outs.size(); c++) {
+          pr.outs[c] = dexpr(outs[c]);
+          if (!fast_atom(outs[c], pr.oat[c])) pr.fast = 0;
+        }
         pr.multi = (sA == sB);
         pr.logical = logical;
         pr.s_first = s_first;
@@ -2390,7 +2406,11 @@ struct PatternEngine : Engine {
       pr.x = x;
       pr.es = e.dset();
       pr.nout = (int)e.outs.size();
-      for (size_t c = 0; c < e.outs.size(); c++) pr.outs[c] = e.dexpr(e.outs[c]);
+      pr.fast = 1;
+      for (size_t c = 0; c < e.outs.size(); c++) {
+        pr.outs[c] = e.dexpr(e.outs[c]);
+        if (!e.fast_atom(e.outs[c], pr.oat[c])) pr.fast = 0;
+      }
       pr.multi = (sA == sB);
       pr.logical = 0;
       pr.s_first = e.s_first;

@@ -60,46 +60,75 @@ __device__ __forceinline__ SplitThr split_prep(const ScanArgs& a, int64_t r, int
   }
   return th;
 }
-__device__ __forceinline__ bool split_eval(const F2Split& sp, const SplitThr& th, int64_t r2b, int64_t q2) {
+// The step in two halves, so a walk can issue the next event's operand
+// loads before it tests the current one: split_fetch loads the e2 operands
+// (one typed load per comparison, null bits), split_test compares them.
+struct SplitRaw {
+  uint64_t v[kSplitMax];
+  uint32_t nul;   // bit i: comparison i's e2 operand is null
+};
+__device__ __forceinline__ SplitRaw split_fetch(const F2Split& sp, int64_t r2b, int64_t q2) {
+  SplitRaw w;
+  w.nul = 0;
+#pragma unroll
+  for (int i = 0; i < kSplitMax; i++) {
+    w.v[i] = 0;
+    if (i >= sp.n) break;
+    const SplitCmp& c = sp.c[i];
+    if (c.konst) continue;
+    const int64_t row = c.pos ? q2 : r2b;
+    switch (c.kind) {
+      case SK_F32_F64: case SK_STR_EQ: case SK_I32: w.v[i] = gld((const uint32_t*)c.col, row); break;
+      case SK_F64: w.v[i] = gld((const uint64_t*)c.col, row); break;
+      default: {
+        const Val v = col_load_raw(c.col, c.nul, c.ctype, row);
+        w.v[i] = v.b;
+        if (v.null) w.nul |= 1u << i;
+        continue;
+      }
+    }
+    if (c.nul && gld(c.nul, row)) w.nul |= 1u << i;
+  }
+  return w;
+}
+__device__ __forceinline__ bool split_test(const F2Split& sp, const SplitThr& th, const SplitRaw& w) {
   if (th.never) return false;
 #pragma unroll
   for (int i = 0; i < kSplitMax; i++) {
     if (i >= sp.n) break;
     const SplitCmp& c = sp.c[i];
     if (c.konst) continue;
-    const int64_t row = c.pos ? q2 : r2b;
+    if ((w.nul >> i) & 1u) return false;
     const uint64_t t = th.t[i].b;
-    // the common kinds: one typed load, the comparison with e2 on the left
-    // (the host flipped the operator of a swapped comparison)
+    // the common kinds: the comparison with e2 on the left (the host flipped
+    // the operator of a swapped comparison)
     int cc;
     switch (c.kind) {
       case SK_F32_F64: {
-        const double x = (double)gld((const float*)c.col, row), y = v_f64(t);
+        const double x = (double)__uint_as_float((uint32_t)w.v[i]), y = v_f64(t);
         cc = (x < y) ? -1 : (x > y) ? 1 : (x == y) ? 0 : 2;
         break;
       }
       case SK_F64: {
-        const double x = gld((const double*)c.col, row), y = v_f64(t);
+        const double x = v_f64(w.v[i]), y = v_f64(t);
         cc = (x < y) ? -1 : (x > y) ? 1 : (x == y) ? 0 : 2;
         break;
       }
       case SK_STR_EQ:
-        cc = ((uint64_t)gld((const uint32_t*)c.col, row) == t) ? 0 : 2;
+        cc = (w.v[i] == t) ? 0 : 2;
         break;
       case SK_I32: {
-        const int32_t x = gld((const int32_t*)c.col, row), y = v_i32(t);
+        const int32_t x = v_i32(w.v[i]), y = v_i32(t);
         cc = x < y ? -1 : (x > y ? 1 : 0);
         break;
       }
       default: {
-        Val v = col_load_raw(c.col, c.nul, c.ctype, row);
-        if (c.cvt_to >= 0 && !v.null) v.b = d_cvt(v.b, c.cvt_from, c.cvt_to);
-        if (v.null) return false;
-        if (!d_compare(c.op, c.type, c.swap ? t : v.b, c.swap ? v.b : t)) return false;
+        uint64_t b = w.v[i];
+        if (c.cvt_to >= 0) b = d_cvt(b, c.cvt_from, c.cvt_to);
+        if (!d_compare(c.op, c.type, c.swap ? t : b, c.swap ? b : t)) return false;
         continue;
       }
     }
-    if (c.nul && gld(c.nul, row)) return false;
     bool ok;
     switch (c.op) {
       case SHD_OP_EQ: ok = cc == 0; break;
@@ -113,6 +142,10 @@ __device__ __forceinline__ bool split_eval(const F2Split& sp, const SplitThr& th
     if (!ok) return false;
   }
   return true;
+}
+__device__ __forceinline__ bool split_eval(const F2Split& sp, const SplitThr& th, int64_t r2b, int64_t q2) {
+  if (th.never) return false;
+  return split_test(sp, th, split_fetch(sp, r2b, q2));
 }
 
 // Block skip: f2's threshold for partial (row r, sorted position q1) -- the

@@ -493,6 +493,38 @@ DFilters Engine::dfilters(const std::vector<int>& ids) const {
   return f;
 }
 
+bool Engine::fast_atom(int expr_id, FAtom& out) const {
+  out = FAtom{};
+  out.kind = FA_NONE;
+  out.cvt_from = out.cvt_to = -1;
+  const char* nf = std::getenv("SHD_NO_FAST_PRED");
+  if ((nf && *nf && *nf != '0') || expr_id < 0 || expr_id >= (int)plan.exprs.size()) return false;
+  const std::vector<Instr>& code = plan.exprs[expr_id];
+  if (code.empty() || code.size() > 2) return false;
+  const Instr& in = code[0];
+  if (in.op == SHD_OP_LOAD) {
+    if (in.b < -2 || in.b > 127 || in.a < 0 || in.a > 127) return false;
+    out.kind = FA_LOAD;
+    out.st = in.a;
+    out.idx = in.b;
+    out.attr = in.c & 0xFFFF;
+  } else if (in.op == SHD_OP_CONST) {
+    if (in.a < 0 || in.a >= (int)plan.consts.size()) return false;
+    out.kind = FA_CONST;
+    out.cval = plan.consts[in.a];
+  } else if (in.op == SHD_OP_NULL) {
+    out.kind = FA_NULL;
+  } else {
+    return false;
+  }
+  if (code.size() == 2) {
+    if (code[1].op != SHD_OP_CVT) return false;
+    out.cvt_from = code[1].a;
+    out.cvt_to = code[1].b;
+  }
+  return true;
+}
+
 }  // namespace shd
 
 // ====================================================================== C-ABI
