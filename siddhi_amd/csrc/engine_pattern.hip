@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
 // positions is handed to the wave-cooperative pass (PS_CONT, resume position
 // in match_row).  Writes the per-tile counts like k_forward_scan.
 template <bool TS64>
-__global__ __launch_bounds__(kBlock) void k_lockstep_walk(const ScanArgs* __restrict__ ap, int64_t n_ext, int64_t tile,
+__global__ __launch_bounds__(kBlock, 8) void k_lockstep_walk(const ScanArgs* __restrict__ ap, int64_t n_ext, int64_t tile,
                                                           const uint32_t* __restrict__ skey32,
                                                           const uint32_t* __restrict__ spv,
                                                           const int32_t* __restrict__ sts32,
