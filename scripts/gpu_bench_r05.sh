@@ -8,3 +8,8 @@ for cfg in P3 P3-dense; do
   timeout -k 10 300 python bench.py --config $cfg > gpurun_out/r05b_bench_$cfg.json 2> gpurun_out/r05b_bench_$cfg.err
   echo $cfg; cut -c1-150 gpurun_out/r05b_bench_$cfg.json
 done
+# k_filter_items probes (timing only, results invalid): 1 = no look-back wait, 2 = no item writes
+for pr in 0 1 2; do
+  SHD_FI_PROBE=$pr timeout -k 10 300 python bench.py --config W2-length --cpu-sample 0 > gpurun_out/r05b_fi$pr.json 2> gpurun_out/r05b_fi$pr.err || true
+  echo probe $pr; cut -c1-120 gpurun_out/r05b_fi$pr.json
+done
