@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--key-base", type=int, default=-1,
                     help="first key id of this rank's slice (default rank * keys; diagnostics)")
     ap.add_argument("--sweep-batches", default="", help="comma list of micro-batch sizes to time first (stderr lines)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="end-to-end line instead: host columns -> SiddhiManager -> InputHandler.send_batch -> "
+                         "QueryCallback (SURVEY.md section 8d, reported separately from the engine number)")
+    ap.add_argument("--e2e-batch", type=int, default=5_000_000, help="events per send_batch call (--e2e)")
     ap.add_argument("--input", default="auto", choices=["auto", "prepartitioned", "roundrobin", "slices"],
                     help="roundrobin: every rank holds a round-robin share of the global stream and events are "
                          "re-routed to their key's owner with one RCCL all-to-all per micro-batch; slices "
@@ -585,8 +589,116 @@ def m5_parity_prefix(he, qa, queries, plans, d, sym, price, vol, ts, prefix, key
     return verdict, cpu
 
 
+def run_e2e(args):
+    """SURVEY.md section 8d "End-to-end InputHandler throughput is reported
+    separately": the config's app through the public API
+    (SiddhiManager.createSiddhiAppRuntime -> InputHandler.send_batch of host
+    SoA columns in InputHandler calls of 1024 events -> QueryCallback.receive
+    with decoded Event[] rows), timed from the first send to the last
+    callback; plus InputHandler.send(Event[]) per call on a sample (the
+    per-event API, rows converted on the host).  The rows the callbacks saw
+    are checked against a DeviceQuery fed the same events directly.
+    Reference: C/stream/input/InputHandler.java:85-95,
+    C/query/output/callback/QueryCallback.java:61-91."""
+    from siddhi_amd import workloads as wl
+    from siddhi_amd import hip_engine as he
+    from siddhi_amd.runtime import SiddhiManager, QueryCallback, ColumnBatch, Event
+    app, n_def, k_def, delta = wl.CONFIGS[args.config]
+    n = args.events or 10_000_000
+    keys = args.keys or k_def
+    sym, price, vol, ts = wl.stock_stream(n, keys, delta)
+
+    class Count(QueryCallback):
+        def __init__(self):
+            self.rows = 0
+            self.calls = 0
+            self.t_last = None
+
+        def receive(self, timestamp, inEvents, removeEvents):  # noqa: N802,N803
+            self.calls += 1
+            self.rows += (len(inEvents) if inEvents else 0) + (len(removeEvents) if removeEvents else 0)
+            self.t_last = time.perf_counter()
+
+    def run(n_ev, per_event=False):
+        sm = SiddhiManager()
+        rt = sm.createSiddhiAppRuntime(app)
+        # the first query of the config app (P3: the partitioned pattern, W2: the window)
+        cb = Count()
+        rt.addCallback(rt.queries[0].name, cb)
+        ih = rt.getInputHandler("StockStream")
+        rt.start()
+        # the symbol column as dictionary ids of "S%07d" strings
+        d = rt.dictionary
+        if per_event:
+            names = ["S%07d" % i for i in range(keys)]
+            calls = []
+            for a in range(0, n_ev, 1024):
+                b = min(a + 1024, n_ev)
+                calls.append([Event(int(ts[i]), [names[int(sym[i])], float(price[i]), int(vol[i])])
+                              for i in range(a, b)])
+            t0 = time.perf_counter()
+            for c in calls:
+                ih.send(c)
+        else:
+            for i in range(keys):
+                d.id("S%07d" % i)
+            t0 = time.perf_counter()
+            for a in range(0, n_ev, args.e2e_batch):
+                b = min(a + args.e2e_batch, n_ev)
+                offs = np.append(np.arange(0, b - a, 1024, dtype=np.int64), np.int64(b - a))
+                ih.send_batch(ColumnBatch(ts[a:b], [sym[a:b], price[a:b], vol[a:b]], [None, None, None], offs))
+        t1 = time.perf_counter()
+        eng = rt.queries[0].engine
+        rt.shutdown()
+        return (t1 - t0), cb, eng.engine_name
+    he.load_library()
+    run(min(n, 2_000_000))   # warm-up (library, device context, first allocations)
+    el, cb, engine = run(n)
+    sample = min(n, 200_000)
+    el_ev, cb_ev, _ = run(sample, per_event=True)
+    # the same events straight into the engine (no runtime): its row count
+    dq = he.DeviceQuery(__import__("siddhi_amd.planner", fromlist=["x"]).plan_query(
+        *_first_query(app)).ir)
+    rows = 0
+    for a in range(0, n, args.e2e_batch):
+        b = min(a + args.e2e_batch, n)
+        offs = np.append(np.arange(0, b - a, 1024, dtype=np.int64), np.int64(b - a))
+        dq.push_raw(0, b - a, ts[a:b].ctypes.data, [sym[a:b].ctypes.data, price[a:b].ctypes.data,
+                                                    vol[a:b].ctypes.data], [0, 0, 0], he.SHD_MEM_HOST, offs, True)
+        r = dq.poll()
+        rows += 0 if r is None else len(r[0])
+    dq.close()
+    from siddhi_amd.buildinfo import source_hash
+    print(json.dumps({
+        "metric": "end-to-end InputHandler events/s (host SoA columns -> SiddhiManager -> InputHandler.send_batch "
+                  "-> QueryCallback Event[])",
+        "value": round(n / el, 1), "unit": "events/s", "n_gpus": 1, "higher_is_better": True,
+        "build": source_hash(),
+        "config": {"workload": args.config, "events": n, "keys": keys, "delta_ms": delta,
+                   "send_batch_events": args.e2e_batch, "call_size": 1024, "engine": engine},
+        "seconds": round(el, 3), "callback_rows": cb.rows, "callback_invocations": cb.calls,
+        "rows_equal_engine_direct": cb.rows == rows,
+        "per_event_api": {"value": round(sample / el_ev, 1), "unit": "events/s", "events": sample,
+                          "note": "InputHandler.send(Event[]) of 1024-event calls (Python objects -> SoA on the "
+                                  "host, one push per call)", "callback_rows": cb_ev.rows},
+        "note": "PCIe-inclusive: columns pushed from host memory (SHD_MEM_HOST); never the engine `value`"}))
+
+
+def _first_query(app):
+    from siddhi_amd.planner import StringDictionary
+    from siddhi_amd import query_compiler as qc
+    qa = qc.parse(app)
+    item = qa.execution_order[0]
+    if isinstance(item, qc.Partition):
+        return qa, item.queries[0], StringDictionary(), item
+    return qa, item, StringDictionary(), None
+
+
 def main():
     args = parse()
+    if args.e2e:
+        run_e2e(args)
+        return
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -705,14 +817,17 @@ def main():
                     return lambda: ex.route_device([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b], seqs[a:b],
                                                    world, lo, 1024, nb, device=local)
                 routed_iter = pipe.run([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])])
+            held = None   # the previous micro-batch's routed tensors (RoutePipeline: lifetime)
             for a, b in zip(cuts[:-1], cuts[1:]):
                 if routed_iter is not None:
-                    (rs, rp, rv, rt), rseq, co, _ = next(routed_iter)
+                    routed = next(routed_iter)
+                    (rs, rp, rv, rt), rseq, co, _ = routed
                     m = rs.numel()
                     routed_total[0] += m
                     if m > 0:
                         dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
                                     he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+                    held = routed   # released after the next push has returned
                 elif seqs is None:
                     # InputHandler calls of 1024 events inside the micro-batch
                     lo = np.searchsorted(offs_all, a)

@@ -155,9 +155,12 @@ int shd_set_time(shd_query* q, int64_t ts);
  *     north_star) while the operands are finite and their non-zero
  *     magnitudes span at most 2^30; the first push that brings a non-finite
  *     or wider-ranged operand switches the query to the exact fold for good
- *     (the reference's running sum keeps Inf / NaN and its rounding history;
- *     a mixed-sign window that cancels to far below its operands is the case
- *     the 2^30 span does not bound -- use exact_aggregates there). */
+ *     (the reference's running sum keeps Inf / NaN and its rounding history).
+ *     A mixed-sign window -- operands of both signs since the aggregate's last
+ *     reset, which can cancel to far below its operands -- is caught by the
+ *     guard's sign channel and also takes the exact fold (int operands are
+ *     exempt: their sums are exact; long operands by value), so the default
+ *     needs no option for it. */
 int shd_set_option(shd_query* q, const char* key, int64_t value);
 int shd_push(shd_query* q, const shd_batch* batch);
 int shd_flush(shd_query* q);                  /* wait for queued device work      */

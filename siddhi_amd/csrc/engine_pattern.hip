@@ -1468,9 +1468,10 @@ struct PatternEngine : Engine {
   int64_t t_last = INT64_MIN;   // time of the last event (arrival order) of the committed pushes
   int64_t last_b_seq = -1;      // arrival index of the last B-stream event (export_replay placement)
   static constexpr int64_t kPruneMinRows = 1 << 16;
-  int64_t bw_fallbacks = 0;
-  DevBuf d_bwb;          // bucket bounds of the bucket walk
-  bool bw_off = false;   // this push re-runs on the full-key sort (a bucket overflowed the LDS stage)
+  // fused prepare + first key-sort pass (keyed_sort.hip): the host reads the
+  // push aggregates while the first pass runs
+  DevBuf d_kps;
+  hipEvent_t ev_pg = nullptr;
   // sorted times of this push's positions (finish: carried partials' times)
   const int32_t* fin_sts32 = nullptr;
   const int64_t* fin_sts64 = nullptr;
@@ -1707,6 +1708,10 @@ struct PatternEngine : Engine {
     return best_b;
   }
 
+  ~PatternEngine() override {
+    if (ev_pg) (void)hipEventDestroy(ev_pg);
+  }
+
   void push(const Staged& b) override {
     if (b.n <= 0) return;
     fin_sts32 = nullptr;
@@ -1781,7 +1786,25 @@ struct PatternEngine : Engine {
     d_blk.reserve((size_t)3 * nblk * std::max(sizeof(PrepAgg), sizeof(ScanOut)));   // per-block partials
     const PrepArgs* d_pa_args = dev_args(pa);
     const bool fast1 = (!isA || pa.f1.fp.ok) && (!keyed || pa.key_col >= 0);
-    if (fast1)
+    // fused prepare + first sort pass: partitioned on a 32-bit plain key
+    // attribute, f1 pre-decoded over at most one attribute, a push big enough
+    // to pay for the extra launches (SHD_FUSED_SORT=0 / 1: off / on at any size)
+    const char* fs_env = getenv("SHD_FUSED_SORT");
+    const int fattr = keyed_sort_f1_attr(pa.f1, isA);
+    const bool fused = partitioned && !key64 && pa.key_col >= 0 && fattr >= -1 &&
+                       (key_type[slot] == SHD_T_STRING || key_type[slot] == SHD_T_INT) && n_ext >= 2 &&
+                       (fs_env ? atoi(fs_env) != 0 : n_ext >= ((int64_t)1 << 20));
+    unsigned long long* d_ncand = reinterpret_cast<unsigned long long*>(d_agg.as<char>() + 224);
+    KsInfo* d_ksi = reinterpret_cast<KsInfo*>(d_agg.as<char>() + 232);
+    if (fused) {
+      if (!ev_pg) SHD_HIP(hipEventCreateWithFlags(&ev_pg, hipEventDisableTiming));
+      keyed_sort_front(s, d_pa_args, pa, n_ext, d_kps, d_pa, d_ksi, d_ncand);
+      SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipEventRecord(ev_pg, s));
+      keyed_sort_pass0(s, d_pa_args, pa, fattr, n_ext, d_kps, d_ksi, d_k32.as<uint32_t>(), d_pv.as<uint32_t>(),
+                       d_ts.as<uint32_t>(), d_ncand);
+      SHD_HIP(hipEventSynchronize(ev_pg));
+    } else if (fast1)
       hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
                          d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
                          d_blk.as<PrepAgg>());
@@ -1789,11 +1812,13 @@ struct PatternEngine : Engine {
       hipLaunchKernelGGL(k_prepare<false>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
                          d_k32.as<uint32_t>(), d_k64.as<uint64_t>(), d_pv.as<uint32_t>(), d_ts.as<int32_t>(),
                          d_blk.as<PrepAgg>());
-    SHD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
-    SHD_CHECK_LAUNCH();
-    SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
+    if (!fused) {
+      SHD_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_finish_prep, dim3(1), dim3(kBlock), 0, s, (const PrepAgg*)d_blk.as<PrepAgg>(), nblk, d_pa);
+      SHD_CHECK_LAUNCH();
+      SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipStreamSynchronize(s));
+    }
     PrepAgg pg;
     std::memcpy(&pg, h_agg.p, sizeof(pg));
     mark("prepare");
@@ -1825,21 +1850,6 @@ struct PatternEngine : Engine {
     const bool grouped = partitioned || (implicit_key && !pg.unmono && (C == 0 || pg.carry_tmax <= pg.ts_min));
     uint32_t hash_mask = 0;
     counters.group_bits = 0;
-    // sparse partitioned pushes (P3): two hashed radix passes + keys grouped in
-    // LDS per bucket (k_bucket_walk) instead of the full-key sort; E = expected
-    // events of a partial's key inside one `within` span (as for `dense` below).
-    // Opt-in (SHD_BUCKET_WALK=1): measured slower than the full-key sort on
-    // P3 (the per-bucket chain is latency-bound)
-    bool bw = false;
-    int full_bits = 0;
-    uint32_t full_kbase = 0;
-    if (grouped && partitioned && !key64 && logical == 0 && !pg.ovf && !getenv("SHD_TS64") &&
-        n_ext <= ((int64_t)1 << 26) && !bw_off && dfilters(f2).fp.ok && getenv("SHD_BUCKET_WALK")) {
-      const double span = (double)(pg.ts_max - pg.ts_min) + 1.0;
-      const double per_w = W == INT64_MAX ? (double)n_ext : std::min((double)n_ext, (double)n_ext * ((double)W + 1.0) / span);
-      const double nk = (double)(pg.kmax - std::min(pg.kmin, pg.kmax)) + 1.0;
-      bw = per_w / nk < 0.25 || atoi(getenv("SHD_BUCKET_WALK")) > 1;   // 2: also denser pushes (tests)
-    }
     if (grouped) {
       // keys of this push span [kmin, kmax]: sort the offsets from kmin (a
       // rank owning one key slice sorts as many bits as rank 0)
@@ -1871,19 +1881,15 @@ struct PatternEngine : Engine {
                            d_k32.as<uint32_t>(), n_ext);
         SHD_CHECK_LAUNCH();
       }
-      if (bw && bits <= 32 && hash_mask == 0 && (bits > 16 || atoi(getenv("SHD_BUCKET_WALK")) > 1)) {
-        full_bits = bits;
-        full_kbase = kbase;
-        bits = 16;
-        hash_mask = kBwMask;
-      } else {
-        bw = false;
-      }
+      if (fused && (hash_mask || bits > 32))
+        throw Error(SHD_E_DEVICE, "pattern engine: fused key sort on a hashed or wide key");
       if (bits <= 32) {
         d_k32_alt.reserve(n_ext * 4);
-        radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
-                               d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
-                               bits, d_sort, s, in_alt, hash_mask != 0, hash_mask ? 0u : kbase);
+        // fused: the first pass ran already (keyed_sort_pass0, same digits)
+        if (!fused || bits > 8)
+          radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
+                                 d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
+                                 bits, d_sort, s, in_alt, hash_mask != 0, hash_mask ? 0u : kbase, fused ? 8 : 0);
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);
@@ -1958,7 +1964,7 @@ struct PatternEngine : Engine {
     // would run (dense keys); SHD_LOCKSTEP=0 / 1 forces
     const char* ls_env = getenv("SHD_LOCKSTEP");
     const bool lockstep = grouped && !hash_mask && !sorted64 && logical == 0 && isB && fast2 && e_key < 64.0 &&
-                          !bw && (ls_env ? atoi(ls_env) != 0 : rmode == 3);
+                          (ls_env ? atoi(ls_env) != 0 : rmode == 3);
     // dense grouped walks revisit each position once per partial of its key
     // inside `within`: the e2 attributes the filters read are copied into
     // position order once, so the walks load them coalesced; worth its pass
@@ -1995,32 +2001,7 @@ struct PatternEngine : Engine {
       d_bsum.reserve(ceil_div(n_ext, 64) * (int64_t)sizeof(BlockSum));
       sa.bsum = d_bsum.as<BlockSum>();
     }
-    if (bw) {
-      sa.hash_mask = 0;   // the walks see whole keys (grouped in LDS)
-      sa.bsum = nullptr;
-    }
     const ScanArgs* d_sa = dev_args(sa);
-    uint32_t* d_bwovf = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 200);
-    if (bw) {
-      const int nbk = (int)kBwMask + 1;
-      // runs of consecutive buckets per workgroup: about 4 resident per CU
-      const int per_wg = (int)std::max<int64_t>(1, std::min<int64_t>(1024, getenv("SHD_BW_PER_WG") ?
-                                                    atoi(getenv("SHD_BW_PER_WG")) : 64));
-      d_blk.reserve((size_t)std::max<int64_t>(3 * nblk, ceil_div(nbk, per_wg) + bucket_resume_blocks(n_ext)) *
-                    std::max(sizeof(PrepAgg), sizeof(ScanOut)));
-      d_bwb.reserve((size_t)(nbk + 1) * 4);
-      SHD_HIP(hipMemsetAsync(d_bwovf, 0, 4, s));
-      // the key buffer the two radix passes left free holds the buckets' key-grouped orders
-      uint16_t* perm = reinterpret_cast<uint16_t*>(skey32 == d_k32.as<uint32_t>() ? d_k32_alt.p : d_k32.p);
-      const int nbw = bucket_walk_launch(s, d_sa, n_ext, skey32, spv, sts32, d_bwb.as<uint32_t>(), perm, nblk,
-                                         d_match.as<int32_t>(), d_pst.as<uint8_t>(), d_blk.as<ScanOut>(), d_bwovf,
-                                         per_wg);
-      hipLaunchKernelGGL(k_tile_count, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(), n_ext,
-                         tile, d_bcnt.as<uint32_t>());
-      SHD_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(), nbw, d_so);
-      SHD_CHECK_LAUNCH();
-    } else {
     if (sa.bsum) {
       hipLaunchKernelGGL(k_block_sum, dim3(grid_for(ceil_div(n_ext, 64) * 64, 1, 4096)), dim3(kBlock), 0, s, d_sa,
                          n_ext, skey32, spv, sts32, d_bsum.as<BlockSum>());
@@ -2099,7 +2080,6 @@ struct PatternEngine : Engine {
                        (rmode == 3 && !lockstep ? 3 : 2) * ntile,
                        d_so);
     SHD_CHECK_LAUNCH();
-    }
     mark("forward_scan");
 
     // ---- per-tile compaction offsets for matches and open partials (position order)
@@ -2110,22 +2090,9 @@ struct PatternEngine : Engine {
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     // time of the push's last event in arrival order (NeedNfa hand-over: global expiry of unpartitioned plans)
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    if (bw) SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 200, d_bwovf, 4, hipMemcpyDeviceToHost, s));
+    if (fused) SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 224, d_ncand, 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    if (bw && h_agg.as<uint32_t>()[50]) {
-      // a bucket beyond the LDS stage (skewed keys): this push again on the
-      // full-key sort (nothing of the engine's state changed yet)
-      bw_off = true;
-      try {
-        sort_push(b);
-      } catch (...) {
-        bw_off = false;
-        throw;
-      }
-      bw_off = false;
-      bw_fallbacks++;
-      return;
-    }
+    if (fused) pg.n_cand = *reinterpret_cast<const unsigned long long*>(h_agg.as<char>() + 224);
     ScanOut so;
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];

@@ -350,7 +350,6 @@ struct FusedArgs {
   int ch_agg[kMaxChan];
   int ch_t[kMaxChan];   // operand type of each channel
   uint32_t* opstats;    // [3]: flags (1 non-finite, kOpNeg, kOpPos), max / min binary exponent
-  int probe;            // timing experiments (SHD_FI_PROBE): 1 = no look-back wait, 2 = no item writes
 };
 
 __global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __restrict__ ap, int64_t n) {
@@ -382,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __rest
     if (lane == 0)
       atomicExch((unsigned long long*)&a.status[c], (unsigned long long)((c == 0 ? kInc : kAgg) | local));
     uint64_t tb = 0;
-    for (int top = (a.probe & 1) ? -1 : c - 1; top >= 0;) {
+    for (int top = c - 1; top >= 0;) {
       const int j = top - lane;
       const uint64_t st = j >= 0 ? cw_status_load(&a.status[j]) : kInc;
       if (__any((st >> 62) == 0)) {   // an earlier, running workgroup has not published yet
@@ -425,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_items(const FusedArgs* __rest
       const int32_t ci = a.call_of[i];
       const int32_t cp = i > 0 ? a.call_of[i - 1] : -1;
       for (int cc = cp + 1; cc <= ci; cc++) a.citem[cc] = (uint32_t)(a.it.C + pos);
-      if (((bal[j] >> lane) & 1ull) && !(a.probe & 2)) {
+      if ((bal[j] >> lane) & 1ull) {
         make_item(a.it, i, pos, a.call_of, a.call_now, a.ikey, a.its, a.iargv, a.iargn, a.ievrow, a.icall, a.inow,
                   a.cap);
         const int64_t t = a.it.C + pos;
@@ -1623,7 +1622,6 @@ struct CwArgs {
   int32_t* o_sidx;
   uint64_t* status;     // [ncalls] look-back words (zeroed before the launch)
   uint64_t* nrows;      // rows of the push (written by the last call)
-  int probe;            // timing experiments (SHD_CW_PROBE)
 };
 
 __device__ __forceinline__ double cw_operand(const CwArgs& a, int c, int64_t q, bool& nul) {
@@ -1711,7 +1709,7 @@ __device__ __forceinline__ void cw_fold_emit(const CwArgs& a, int c, uint32_t lb
     acc[ch] = DD{0.0, 0.0};
     nn[ch] = 0;
   }
-  for (uint32_t j = 0; j < ((a.probe & 2) ? 0u : n_in); j++) {
+  for (uint32_t j = 0; j < n_in; j++) {
     const int64_t q = (int64_t)lb + list[l0 + j];
 #pragma unroll
     for (int ch = 0; ch < NC; ch++) {
@@ -1890,7 +1888,7 @@ __device__ __forceinline__ void cw_direct_call(const CwArgs& a, const int c, int
   const int64_t base = a.row0 + (int64_t)rbase[c];
   for (int k = 0; k < CALLCAP / kBlock; k++) {
     const int r = rs + threadIdx.x + k * kBlock;
-    if (r >= nr || !my_n[k] || (a.probe & 4)) continue;
+    if (r >= nr || !my_n[k]) continue;
     const uint32_t g = my_g[k];
     // soff[g] now ends the group's list
     cw_fold_emit<NC>(a, c, lb, list, soff[g] - my_n[k], my_n[k], slast[g], base + srank[r - rs]);
@@ -1999,7 +1997,7 @@ __global__ __launch_bounds__(kBlock) void k_cw(const CwArgs* __restrict__ ap, in
     const int lane = threadIdx.x;
     const uint64_t local = nslots;
     uint64_t base = 0;
-    for (int top = (a.probe & 1) ? -1 : c - 1; top >= 0;) {
+    for (int top = c - 1; top >= 0;) {
       const int j = top - lane;
       uint64_t st = j >= 0 ? cw_status_load(&a.status[j]) : kInc;
       if (__any((st >> 62) == 0)) {   // an earlier, running workgroup has not published yet
@@ -2070,7 +2068,6 @@ __global__ __launch_bounds__(kBlock) void k_cw(const CwArgs* __restrict__ ap, in
   __syncthreads();
   // 3. one thread per group: fold the window, write the row
   for (int i = threadIdx.x; i < (int)nslots; i += kBlock) {
-    if (a.probe & 4) continue;
     const uint32_t xf = sfirst[i];
     cw_fold_emit<NC>(a, c, lb, list, soff[i] - scnt[i], scnt[i], slast[i],
                      a.row0 + (int64_t)sbase + srank[xf - s]);
@@ -3385,7 +3382,6 @@ struct SingleEngine : Engine {
     ca.C = C;
     ca.total = total;
     ca.wlen = wkind == SHD_W_LENGTH ? q.wparam : 0;
-    ca.probe = getenv("SHD_CW_PROBE") ? atoi(getenv("SHD_CW_PROBE")) : 0;
     ca.ikey = ikey[cur].as<uint64_t>();
     ca.e = e_exp.as<uint32_t>();
     ca.iargv = iargv[cur].as<uint64_t>();
@@ -3683,7 +3679,6 @@ struct SingleEngine : Engine {
       fu.ch_t[c] = ch_type[c];
     }
     fu.opstats = (uint32_t*)(d_tot.as<uint64_t>() + 5);
-    fu.probe = getenv("SHD_FI_PROBE") ? atoi(getenv("SHD_FI_PROBE")) : 0;
     hipLaunchKernelGGL(k_filter_items, dim3((unsigned)ntiles), dim3(kBlock), 0, s, dev_args(fu), n);
     SHD_CHECK_LAUNCH();
     SHD_HIP(hipMemcpyAsync(h_tot.p, d_tot.p, 24, hipMemcpyDeviceToHost, s));

@@ -358,20 +358,23 @@ __device__ __forceinline__ void prep_block_reduce(PrepAcc acc, PrepAgg* blk, int
   }
 }
 
-// Bucket walk (engine_bucket.hip): sort width of its hashed buckets, and the
-// launch of bucket bounds + walk over a sort of that width; returns the
-// number of ScanOut partials written to blk.
-constexpr uint32_t kBwMask = 0xFFFFu;   // 16 hashed bits = two radix passes
-// workgroups of the bucket walk's deferred-walk kernel (16 positions per thread)
-inline int bucket_resume_blocks(int64_t n_ext) {
-  const int64_t b = (n_ext + 256 * 16 - 1) / (256 * 16);
-  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
-}
-// perm: n_ext u16 (the buckets' key-grouped orders); blk: nbw + bucket_resume_blocks(n_ext)
-// ScanOut partials, the count returned
-int bucket_walk_launch(hipStream_t s, const ScanArgs* d_sa, int64_t n_ext, const uint32_t* skey, const uint32_t* spv,
-                       const int32_t* sts, uint32_t* bnd, uint16_t* perm, int nblk, int32_t* match_row, uint8_t* pst,
-                       ScanOut* blk, uint32_t* ovf, int per_wg);
+// Fused row preparation + first key-sort pass (keyed_sort.hip; partitioned
+// plans on a 32-bit plain key attribute).  KsInfo: the sort's key base and
+// width as sort_push derives them from the push's key range.
+struct KsInfo {
+  uint32_t kb;
+  int32_t bits;
+};
+// The one attribute f1's loads read (-1: none or the pushed stream is not A;
+// -2: f1 is not a pre-decoded chain over one attribute -- not fusable).
+int keyed_sort_f1_attr(const DFilters& f1, bool is_a);
+// hist + aggregates (d_pg: the push's PrepAgg with n_cand 0, d_info, *d_ncand = 0)
+void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int64_t n_ext, DevBuf& scratch,
+                      PrepAgg* d_pg, KsInfo* d_info, unsigned long long* d_ncand);
+// first pass: rows sorted by the first digit into (k32, pv, ts); *d_ncand += candidates created
+void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int fattr, int64_t n_ext,
+                      DevBuf& scratch, const KsInfo* d_info, uint32_t* k32, uint32_t* pv, uint32_t* ts,
+                      unsigned long long* d_ncand);
 
 }  // namespace pat
 }  // namespace shd

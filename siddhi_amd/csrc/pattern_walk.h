@@ -1,8 +1,7 @@
 // pattern_walk.h -- the per-partial walk of the pattern engine (the
 // StreamPreStateProcessor step for `every e1=A[f1] -> e2=B[f2] within W`),
-// shared by the sort-path kernels (engine_pattern.hip) and the bucket walk
-// (engine_bucket.hip).  Included inside namespace shd::(anonymous) with
-// shd::pat in scope.
+// used by the sort-path kernels of engine_pattern.hip.  Included inside
+// namespace shd::(anonymous) with shd::pat in scope.
 #pragma once
 
 // Walk of one candidate partial P (row r, key k, timestamp tsi) over the

@@ -55,12 +55,15 @@ __device__ __forceinline__ uint32_t rs_hdigit(K k, int shift, K kb) {
 // offset inside the digit (gr) and the digit's total (dt); wave w holds rows
 // [wb, wb + 64R) of the tile starting at t0, R per lane (k, v, x; rows >= n
 // are padding).
-template <class K, int R, bool P2, bool H>
-__device__ __forceinline__ void rs_scatter_tile(const K (&k)[R], const uint32_t (&v)[R],
-                                                const uint32_t (&x)[P2 ? R : 1], int64_t n, int64_t t0, int64_t wb,
-                                                int shift, uint32_t c, uint32_t gr, uint32_t dt, K kb,
-                                                K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                uint32_t* __restrict__ wout) {
+// dig(key) -> digit in [0, 256): rs_scatter_tile below takes the digits of
+// (key - kb) >> shift (or of the hashed key); the fused first pass of the
+// pattern engine's key sort (keyed_sort.hip) passes its own.
+template <class K, int R, bool P2, class Dig>
+__device__ __forceinline__ void rs_scatter_tile_fn(const K (&k)[R], const uint32_t (&v)[R],
+                                                   const uint32_t (&x)[P2 ? R : 1], int64_t n, int64_t t0,
+                                                   int64_t wb, const Dig& dig, uint32_t c, uint32_t gr, uint32_t dt,
+                                                   K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                   uint32_t* __restrict__ wout) {
   constexpr int T = rs_tile(R);
   __shared__ K sk[T];
   __shared__ uint32_t sv[T];
@@ -104,7 +107,7 @@ __device__ __forceinline__ void rs_scatter_tile(const K (&k)[R], const uint32_t 
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool ok = wb + r * 64 + lane < n;
-    const uint32_t d = rs_hdigit<H>(k[r], shift, kb);
+    const uint32_t d = dig(k[r]);
     uint64_t peers = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -133,7 +136,7 @@ __device__ __forceinline__ void rs_scatter_tile(const K (&k)[R], const uint32_t 
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (wb + r * 64 + lane < n) {
-      const uint32_t pos = wcnt[w][rs_hdigit<H>(k[r], shift, kb)] + lr[r];
+      const uint32_t pos = wcnt[w][dig(k[r])] + lr[r];
       sk[pos] = k[r];
       sv[pos] = v[r];
       if (P2) sw[pos] = x[r];
@@ -144,12 +147,22 @@ __device__ __forceinline__ void rs_scatter_tile(const K (&k)[R], const uint32_t 
 #pragma unroll 4
   for (int i = tid; i < tile_n; i += kRsBlock) {
     const K kk = sk[i];
-    const uint32_t d = rs_hdigit<H>(kk, shift, kb);
+    const uint32_t d = dig(kk);
     const uint32_t o = gbase[d] + (uint32_t)i - lpre[d];
     kout[o] = kk;
     vout[o] = sv[i];
     if (P2) wout[o] = sw[i];
   }
+}
+
+template <class K, int R, bool P2, bool H>
+__device__ __forceinline__ void rs_scatter_tile(const K (&k)[R], const uint32_t (&v)[R],
+                                                const uint32_t (&x)[P2 ? R : 1], int64_t n, int64_t t0, int64_t wb,
+                                                int shift, uint32_t c, uint32_t gr, uint32_t dt, K kb,
+                                                K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                uint32_t* __restrict__ wout) {
+  rs_scatter_tile_fn<K, R, P2>(k, v, x, n, t0, wb, [shift, kb](K kk) { return rs_hdigit<H>(kk, shift, kb); }, c, gr,
+                               dt, kout, vout, wout);
 }
 
 }  // namespace shd

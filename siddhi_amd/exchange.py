@@ -301,7 +301,13 @@ class RoutePipeline:
     previous push and its next one waits on a device-to-host copy.  The worker
     issues the collectives in micro-batch order (one thread: the same order on
     every rank).  Usage: ``for routed in pipe.run(jobs): push(routed)`` where a
-    job is a no-argument callable returning route_device()'s result."""
+    job is a no-argument callable returning route_device()'s result.
+    Lifetime: the routed tensors live on the side stream's pool; the engine
+    reads them on its own stream, so the caller keeps micro-batch k's result
+    referenced until its NEXT push has returned (every shd_push synchronises
+    the engine's stream at least once, so push k + 1 returning means push k's
+    kernels are done): only then may the allocator hand k's memory to the
+    route of a later micro-batch (bench.py run_step holds it that way)."""
 
     def __init__(self, device: int = 0):
         from concurrent.futures import ThreadPoolExecutor
@@ -435,6 +441,8 @@ def halo_take(window: Tuple[str, int], n: int, exchange, prime, device=None,
     rank works with the shortest slice length, so every rank computes the same
     sizes, sends as many rows as its successor expects and takes the raise
     branch together."""
+    if device is None and dist.get_backend(group) != "gloo":
+        device = torch.device("cuda", torch.cuda.current_device())   # RCCL reduces device tensors only
     nt = torch.tensor([int(n)], dtype=torch.int64, device=device)
     dist.all_reduce(nt, op=dist.ReduceOp.MIN, group=group)
     n = int(nt.item())

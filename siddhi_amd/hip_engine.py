@@ -332,6 +332,10 @@ class DeviceGroup:
 class HipQueryEngine:
     """Query engine of SiddhiAppRuntime backed by libsiddhi_hip (MI355X)."""
 
+    # a push may hold several InputHandler calls (shd_batch.call_offsets):
+    # the engine advances playback time per call (SiddhiAppRuntime._batch_push_ok)
+    batch_calls = True
+
     def __init__(self, qp: pl.QueryPlan, dictionary, exact_aggregates: bool = False):
         self.qp = qp
         try:

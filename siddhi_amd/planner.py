@@ -806,10 +806,12 @@ def _plan_single(app, q, dictionary, partition, extra_streams) -> QueryPlan:
 
 def _window_handler(h, partitioned: bool, meta=None, stream=None):
     """(H_WINDOW, kind, p, q) of a `#window.<name>(...)` handler (include/siddhi_ir.h
-    shd_window).  Batch windows in full-batch mode only: `stream.current.event`
-    true (ProcessingMode.RESET) is refused, and so is `timeBatch` inside a
-    partition (its nextEmitTime is a field of the processor shared by every
-    partition key, TimeBatchWindowProcessor.java:136,283-300)."""
+    shd_window).  Batch windows in both modes: full batch (expired + RESET +
+    current per flush) and `stream.current.event` true (W_TIME_BATCH_STREAM,
+    lengthBatch with q = 1: the current events go out as they arrive).
+    Refused: `timeBatch` inside a partition (its nextEmitTime is a field of
+    the processor shared by every partition key,
+    TimeBatchWindowProcessor.java:136,283-300)."""
     ps = h.params
 
     def const(i, types, what):

@@ -120,15 +120,25 @@ def _java_value(v, t, dictionary):
 
 
 def rows_to_batch(types: List[int], events: List[Event], dictionary) -> ColumnBatch:
+    """Event[] of one InputHandler call -> SoA batch (StreamEventConverter's
+    job, C/event/stream/converter/SimpleStreamEventConverter.java:36-42)."""
     n = len(events)
     ts = np.fromiter((e.timestamp for e in events), np.int64, n)
     cols, nulls = [], []
     for a, t in enumerate(types):
-        raw = [_java_value(e.data[a] if a < len(e.data) else None, t, dictionary) for e in events]
+        raw = [e.data[a] if a < len(e.data) else None for e in events]
         nm = np.fromiter((x is None for x in raw), np.uint8, n)
-        col = np.array([0 if x is None else x for x in raw], dtype=_NP[t])
+        has_null = bool(nm.any())
+        if t == pl.T_STRING:
+            ids = dictionary.ids
+            col = np.fromiter((0 if x is None else (ids.get(x) if type(x) is str and x in ids else
+                                                    dictionary.id(str(x))) for x in raw), np.uint32, n)
+        elif t == pl.T_DOUBLE and not has_null and all(type(x) is float for x in raw):
+            col = np.array(raw, np.float64)
+        else:
+            col = np.array([0 if x is None else _java_value(x, t, dictionary) for x in raw], dtype=_NP[t])
         cols.append(col)
-        nulls.append(nm if nm.any() else None)
+        nulls.append(nm if has_null else None)
     return ColumnBatch(ts, cols, nulls)
 
 
@@ -211,6 +221,7 @@ class _QueryRuntime:
         self.callbacks: List[QueryCallback] = []
         rate = getattr(qp, "output_rate", None)
         self.limiter = OutputRateLimiter(rate, qp.rate_group_cols is not None) if rate is not None else None
+        self.list_cols = list_columns(qp) if pl.T_OBJECT in qp.output_types else {}
 
 
 class InputHandler:
@@ -359,7 +370,9 @@ class SiddhiAppRuntime:
         blobs = [q.engine.snapshot() for q in self.queries]
         head = {"app": hashlib.sha256(self.app_text.encode()).hexdigest(),
                 "dictionary": self.dictionary.strings, "last_wall": self._last_wall,
-                "queries": [q.name for q in self.queries], "sizes": [len(b) for b in blobs]}
+                "queries": [q.name for q in self.queries], "sizes": [len(b) for b in blobs],
+                # host-side output rate limiters (their RateLimiterState maps)
+                "limiters": {q.name: q.limiter.state() for q in self.queries if q.limiter is not None}}
         hb = json.dumps(head).encode()
         return self._SNAP_MAGIC + struct.pack("<Q", len(hb)) + hb + b"".join(blobs)
 
@@ -392,6 +405,10 @@ class SiddhiAppRuntime:
         for q, n in zip(self.queries, sizes):
             q.engine.restore(snapshot[at:at + n])
             at += n
+        lim = head.get("limiters", {})
+        for q in self.queries:
+            if q.limiter is not None and q.name in lim:
+                q.limiter.load(lim[q.name])
 
     def persist(self) -> "PersistenceReference":
         """SiddhiAppRuntime.persist(): snapshot saved to the manager's persistence store."""
@@ -472,6 +489,29 @@ class SiddhiAppRuntime:
         if batch.n == 0:
             return
         offs = batch.call_offsets
+        if len(offs) > 2 and self._batch_push_ok(stream_id):
+            # several InputHandler calls, one push per query: each engine
+            # advances playback time per call itself (shd_batch.call_offsets +
+            # advance_time: setCurrentTimestamp before each call's events,
+            # InputHandler.java:85-95); with no query chained to another and
+            # no rate limiter, every query's chunks are the per-call path's
+            ends = np.asarray(offs[1:], np.int64) - 1
+            t = int(np.max(batch.ts[ends]))
+            if self._event_time is None or t > self._event_time:
+                self._event_time = t
+            subs = {id(q): si for q, si in self.subscribers.get(stream_id, [])}
+            for q in self.queries:
+                if q.limiter is not None:
+                    continue
+                si = subs.get(id(q))
+                if si is None:
+                    # not fed by this stream: its clock still moves call by call
+                    # (a TIMER's expired rows carry the time it fired at)
+                    for tc in batch.ts[ends].tolist():
+                        self._deliver(q, q.engine.set_time(tc))
+                else:
+                    self._deliver(q, q.engine.push(si, batch, advance_time=True))
+            return
         if len(offs) > 2:
             # several InputHandler calls in one batch: time advances per call
             for c in range(len(offs) - 1):
@@ -489,6 +529,24 @@ class SiddhiAppRuntime:
             self._limit_time(q, t)
         self._junction(stream_id, batch)
 
+    def _batch_push_ok(self, stream_id) -> bool:
+        """A multi-call batch may go to each engine as one push: no stream
+        callback on the stream (it receives one Event[] per call), no rate
+        limiter, no query feeding another query or a stream callback, and
+        every engine takes call boundaries itself (HipQueryEngine)."""
+        if self.stream_callbacks.get(stream_id):
+            return False
+        subs = [id(q) for q, _ in self.subscribers.get(stream_id, [])]
+        if len(subs) != len(set(subs)):
+            return False
+        for q in self.queries:
+            if q.limiter is not None or not getattr(q.engine, "batch_calls", False):
+                return False
+            tg = q.qp.target
+            if self.stream_callbacks.get(tg) or self.subscribers.get(tg):
+                return False
+        return True
+
     def _junction(self, stream_id, batch: ColumnBatch):
         cbs = self.stream_callbacks.get(stream_id)
         if cbs:
@@ -499,19 +557,24 @@ class SiddhiAppRuntime:
             self._deliver(q, q.engine.push(si, batch))
 
     def _batch_events(self, stream_id, batch):
+        """A batch as the Event[] a StreamCallback receives (column-wise decode)."""
         types = self.stream_types[stream_id]
-        evs = []
-        for i in range(batch.n):
-            data = []
-            for a, t in enumerate(types):
-                if batch.nulls[a] is not None and batch.nulls[a][i]:
-                    data.append(None)
-                else:
-                    v = batch.cols[a][i]
-                    data.append(self.dictionary.lookup(int(v)) if t == pl.T_STRING else
-                                bool(v) if t == pl.T_BOOL else v if t == pl.T_OBJECT else v.item())
-            evs.append(Event(int(batch.ts[i]), data))
-        return evs
+        cols = []
+        for a, t in enumerate(types):
+            c = batch.cols[a]
+            if t == pl.T_STRING:
+                strings = self.dictionary.strings
+                vals = [strings[i] for i in c.tolist()]
+            elif t == pl.T_BOOL:
+                vals = [bool(v) for v in c.tolist()]
+            else:
+                vals = list(c) if t == pl.T_OBJECT else c.tolist()
+            nm = batch.nulls[a]
+            if nm is not None and nm.any():
+                for i in np.flatnonzero(nm).tolist():
+                    vals[i] = None
+            cols.append(vals)
+        return [Event(t, list(d)) for t, d in zip(batch.ts.tolist(), zip(*cols))]
 
     def _list_value(self, elems, et):
         """A multi-value cell: the List MultiValueVariableFunctionExecutor returns."""
@@ -526,64 +589,68 @@ class SiddhiAppRuntime:
     def _limit_time(self, q: _QueryRuntime, t: int):
         if q.limiter is not None and q.limiter.timed():
             for out in q.limiter.on_time(t):
-                self._emit(q, [r[0] for r in out], None)
+                self._emit(q, [r[0] for r in out], None, q.list_cols)
 
     def _deliver(self, q: _QueryRuntime, chunks: List[OutputChunk]):
         if not chunks:
             return
         types = q.qp.output_types
-        lcols = list_columns(q.qp) if pl.T_OBJECT in types else {}
+        lcols = q.list_cols
+        target = q.qp.target
+        chained = target in self.stream_types and bool(self.stream_callbacks.get(target) or
+                                                       self.subscribers.get(target))
         for ch in chunks:
-            evs = []
-            for i in range(len(ch.ts)):
-                data = [self._list_value(ch.objects[k][i], lcols[k]) if t == pl.T_OBJECT else
-                        None if ch.nulls[i, k] else decode_value(ch.values[i, k], t, self.dictionary)
-                        for k, t in enumerate(types)]
-                evs.append(Event(int(ch.ts[i]), data, int(ch.types[i]) == EXPIRED))
+            if q.limiter is None and not q.callbacks:
+                if chained:
+                    self._emit(q, None, ch, lcols)
+                continue
+            # whole columns decoded at once (QueryCallback.receiveStreamEvent's Event[])
+            cols = decode_columns(ch.values, ch.nulls, types, self.dictionary, ch.objects,
+                                  lambda elems, k: self._list_value(elems, lcols[k]))
+            exp = (ch.types == EXPIRED).tolist()
+            evs = [Event(t, list(d), x) for t, d, x in zip(ch.ts.tolist(), zip(*cols), exp)] if cols else \
+                [Event(t, [], x) for t, x in zip(ch.ts.tolist(), exp)]
             if q.limiter is None:
-                self._emit(q, evs, ch)
+                self._emit(q, evs, ch, lcols)
                 continue
             gc = q.qp.rate_group_cols
             rows = [(e, tuple(repr(e.data[c]) for c in gc) if gc is not None else None) for e in evs]
             out = q.limiter.process(rows, self._limiter_now())
             if out:
-                self._emit(q, [r[0] for r in out], None)
+                self._emit(q, [r[0] for r in out], None, lcols)
 
-    def _emit(self, q: _QueryRuntime, evs, ch):
+    def _emit(self, q: _QueryRuntime, evs, ch, lcols):
         """One output chunk to the query's callbacks and its target stream
         (OutputRateLimiter.sendToCallBacks); ch: the engine chunk the events
-        are, unchanged (None: rows picked by a rate limiter)."""
+        are, unchanged (None: rows picked by a rate limiter; evs None: no
+        query callback, the chunk only feeds the target stream)."""
         types = q.qp.output_types
-        lcols = list_columns(q.qp) if pl.T_OBJECT in types else {}
-        if True:
-            # QueryCallback.receiveStreamEvent (QueryCallback.java:61-91)
-            if q.callbacks:
-                cur = [e for e in evs if not e.is_expired] or None
-                rem = [e for e in evs if e.is_expired] or None
-                ts = evs[-1].timestamp
-                for cb in q.callbacks:
-                    cb.receive(ts, cur, rem)
-            # InsertIntoStreamCallback: EXPIRED -> CURRENT, into the target junction
-            target = q.qp.target
-            if ch is None and target in self.stream_types and (self.stream_callbacks.get(target) or
-                                                                self.subscribers.get(target)):
-                self._junction(target, rows_to_batch(types, [Event(e.timestamp, e.data) for e in evs],
-                                                     self.dictionary))
-            elif target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target)):
-                cols, nulls = [], []
-                for k, t in enumerate(types):
-                    if t == pl.T_OBJECT:   # java.util.List values travel as objects
-                        col = np.empty(len(ch.ts), object)
-                        col[:] = [self._list_value(ch.objects[k][i], lcols[k]) for i in range(len(ch.ts))]
-                        cols.append(col)
-                        nulls.append(None)
-                        continue
-                    col = np.array([ch.values[i, k] for i in range(len(ch.ts))], np.uint64)
-                    cols.append(_bits_to_col(col, t))
-                    nm = ch.nulls[:, k].astype(np.uint8)
-                    nulls.append(nm if nm.any() else None)
-                out = ColumnBatch(np.asarray(ch.ts, np.int64), cols, nulls)
-                self._junction(target, out)
+        # QueryCallback.receiveStreamEvent (QueryCallback.java:61-91)
+        if q.callbacks and evs:
+            cur = [e for e in evs if not e.is_expired] or None
+            rem = [e for e in evs if e.is_expired] or None
+            ts = evs[-1].timestamp
+            for cb in q.callbacks:
+                cb.receive(ts, cur, rem)
+        # InsertIntoStreamCallback: EXPIRED -> CURRENT, into the target junction
+        target = q.qp.target
+        if not (target in self.stream_types and (self.stream_callbacks.get(target) or self.subscribers.get(target))):
+            return
+        if ch is None:
+            self._junction(target, rows_to_batch(types, [Event(e.timestamp, e.data) for e in evs], self.dictionary))
+            return
+        cols, nulls = [], []
+        for k, t in enumerate(types):
+            if t == pl.T_OBJECT:   # java.util.List values travel as objects
+                col = np.empty(len(ch.ts), object)
+                col[:] = [self._list_value(ch.objects[k][i], lcols[k]) for i in range(len(ch.ts))]
+                cols.append(col)
+                nulls.append(None)
+                continue
+            cols.append(_bits_to_col(np.ascontiguousarray(ch.values[:, k], np.uint64), t))
+            nm = ch.nulls[:, k].astype(np.uint8)
+            nulls.append(nm if nm.any() else None)
+        self._junction(target, ColumnBatch(np.asarray(ch.ts, np.int64), cols, nulls))
 
 
 def _bits_to_col(bits: np.ndarray, t: int) -> np.ndarray:
@@ -598,6 +665,31 @@ def _bits_to_col(bits: np.ndarray, t: int) -> np.ndarray:
     if t == pl.T_BOOL:
         return bits.astype(np.uint8)
     return bits.astype(np.uint32)
+
+
+def decode_columns(values: np.ndarray, nulls: np.ndarray, types: List[int], dictionary, objects=None,
+                   list_value=None) -> List[list]:
+    """Output bit patterns -> the Java values of whole columns (None for
+    nulls): decode_value applied per column with NumPy views instead of per
+    cell.  OBJECT columns (multi-value lists) go through list_value."""
+    n = values.shape[0]
+    out = []
+    for k, t in enumerate(types):
+        if t == pl.T_OBJECT:
+            out.append([list_value(objects[k][i], k) for i in range(n)])
+            continue
+        bits = values[:, k]
+        nm = nulls[:, k]
+        if t == pl.T_STRING:
+            strings = dictionary.strings
+            vals = [None if z else strings[i] for i, z in zip(bits.tolist(), nm.tolist())]
+        else:
+            vals = (bits != 0).tolist() if t == pl.T_BOOL else _bits_to_col(bits, t).tolist()
+            if nm.any():
+                for i in np.flatnonzero(nm).tolist():
+                    vals[i] = None
+        out.append(vals)
+    return out
 
 
 class CannotRestoreSiddhiAppStateException(Exception):
@@ -699,6 +791,42 @@ class OutputRateLimiter:
 
     def timed(self):
         return self.unit == "time" and self.kind in ("all", "last")
+
+    # -- snapshot / restore: the limiters' RateLimiterState maps
+    # (e.g. AllPerTimeOutputRateLimiter.RateLimiterState: the held chunk and
+    # scheduledTime; the per-event kinds: counter; the group-by kinds: the
+    # per-group maps), as JSON-able values in the runtime's snapshot head
+    @staticmethod
+    def _row_out(r):
+        e, key = r
+        return [e.timestamp, e.data, e.is_expired, list(key) if key is not None else None]
+
+    @staticmethod
+    def _row_in(x):
+        return (Event(x[0], x[1], x[2]), tuple(x[3]) if x[3] is not None else None)
+
+    def _group_vals(self):
+        # first: count (per event) / output time (per time); last: the row
+        return "row" if self.kind == "last" else "int"
+
+    def state(self) -> dict:
+        gv = self._group_vals()
+        return {"counter": self.counter, "buf": [self._row_out(r) for r in self.buf],
+                "last": self._row_out(self.last) if self.last is not None else None,
+                "groups": [[list(k) if isinstance(k, tuple) else k, self._row_out(v) if gv == "row" else v]
+                           for k, v in self.groups.items()],
+                "out_time": self.out_time, "scheduled": self.scheduled, "notify": list(self.notify)}
+
+    def load(self, st: dict):
+        gv = self._group_vals()
+        self.counter = int(st["counter"])
+        self.buf = [self._row_in(x) for x in st["buf"]]
+        self.last = self._row_in(st["last"]) if st["last"] is not None else None
+        self.groups = {(tuple(k) if isinstance(k, list) else k): (self._row_in(v) if gv == "row" else v)
+                       for k, v in st["groups"]}
+        self.out_time = st["out_time"]
+        self.scheduled = st["scheduled"]
+        self.notify = list(st["notify"])
 
     def start(self, wall_now: int):
         # partitionCreated (e.g. AllPerTimeOutputRateLimiter.java:97-108):
