@@ -14,6 +14,7 @@ if [ -n "${TESTS:-}" ]; then
   [ $rc -eq 0 ] || exit $rc
 fi
 for C in ${CONFIGS:-P3}; do
+  [ "$C" = none ] && continue
   timeout -k 10 300 python3 -u bench.py --config $C ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench_$C.json 2> gpurun_out/${TAG}_bench_$C.err
   rc=$?; echo "bench $C rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_bench_$C.err; exit $rc; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(round(d['value']/1e9,3), 'G ev/s', d['ms_per_step'], d.get('stage_ms_per_step'), d.get('parity_prefix'), (d.get('derived_check') or {}).get('equal'))" gpurun_out/${TAG}_bench_$C.json

@@ -1885,11 +1885,16 @@ struct PatternEngine : Engine {
         throw Error(SHD_E_DEVICE, "pattern engine: fused key sort on a hashed or wide key");
       if (bits <= 32) {
         d_k32_alt.reserve(n_ext * 4);
-        // fused: the first pass ran already (keyed_sort_pass0, same digits)
-        if (!fused || bits > 8)
+        // fused: the first pass ran already (keyed_sort_pass0, same digits);
+        // the rest on keyed_sort.hip's pipelined passes
+        if (fused)
+          keyed_sort_rest(s, n_ext, bits, kbase, d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
+                          d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), d_kps, d_sort,
+                          in_alt);
+        else
           radix_sort_triples_u32(d_k32.as<uint32_t>(), d_pv.as<uint32_t>(), d_ts.as<uint32_t>(),
                                  d_k32_alt.as<uint32_t>(), d_pv_alt.as<uint32_t>(), d_ts_alt.as<uint32_t>(), n_ext,
-                                 bits, d_sort, s, in_alt, hash_mask != 0, hash_mask ? 0u : kbase, fused ? 8 : 0);
+                                 bits, d_sort, s, in_alt, hash_mask != 0, hash_mask ? 0u : kbase);
         skey32 = in_alt ? d_k32_alt.as<uint32_t>() : d_k32.as<uint32_t>();
       } else {
         d_k64_alt.reserve(n_ext * 8);

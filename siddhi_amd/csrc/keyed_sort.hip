@@ -29,6 +29,8 @@
 // unchanged.  Reference semantics of the row flags: PartitionStreamReceiver
 // (null key -> dropped, C/partition/PartitionStreamReceiver.java:81-283),
 // FilterProcessor on the start state (StreamPreStateProcessor.java:364-403).
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "engine.h"
@@ -507,6 +509,7 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
   }
 }
 
+
 }  // namespace
 
 int keyed_sort_f1_attr(const DFilters& f1, bool is_a) {
@@ -656,6 +659,21 @@ void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, i
 #undef SHD_KS_LAUNCH_N
 #undef SHD_KS_LAUNCH
   SHD_CHECK_LAUNCH();
+}
+
+
+// The passes after the first (digits from shift 8 up to `bits`), on
+// (k32, pv, ts) -> alternate buffers and back; in_alt: the result is in the
+// alternate set.  These run on the library's radix passes: a persistent,
+// software-pipelined pass kernel with tile-major offsets (the next tile's
+// loads issued before the current tile's ranking) was built and measured
+// slower on P3 (447 vs 300 us per 56 M-row pass).
+void keyed_sort_rest(hipStream_t s, int64_t n_ext, int bits, uint32_t kb, uint32_t* k32, uint32_t* pv, uint32_t* ts,
+                     uint32_t* k32_alt, uint32_t* pv_alt, uint32_t* ts_alt, DevBuf&, DevBuf& sort_scratch,
+                     bool& in_alt) {
+  in_alt = false;
+  if (bits <= 8) return;
+  radix_sort_triples_u32(k32, pv, ts, k32_alt, pv_alt, ts_alt, n_ext, bits, sort_scratch, s, in_alt, false, kb, 8);
 }
 
 }  // namespace pat

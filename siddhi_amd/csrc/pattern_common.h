@@ -375,6 +375,10 @@ void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, i
 void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int fattr, int64_t n_ext,
                       DevBuf& scratch, const KsInfo* d_info, uint32_t* k32, uint32_t* pv, uint32_t* ts,
                       unsigned long long* d_ncand);
+// the remaining passes (digits from shift 8 to bits) of a fused sort
+void keyed_sort_rest(hipStream_t s, int64_t n_ext, int bits, uint32_t kb, uint32_t* k32, uint32_t* pv, uint32_t* ts,
+                     uint32_t* k32_alt, uint32_t* pv_alt, uint32_t* ts_alt, DevBuf& scratch, DevBuf& sort_scratch,
+                     bool& in_alt);
 
 }  // namespace pat
 }  // namespace shd

@@ -30,7 +30,7 @@ def split(sym, price, vol, ts, parts, call=1024):
             if b > a]
 
 
-UNPART = [(k, wl.S4_APPS[k]) for k in ("seq", "seqplus", "or", "and", "not", "bare")]
+UNPART = [(k, wl.S4_APPS[k]) for k in ("seq", "seq14", "seqplus", "or", "and", "not", "bare")]
 PART = [("P" + k, wl.S4_PART_APPS[k]) for k in ("seq", "seqplus", "or", "and", "not")]
 
 
