@@ -810,13 +810,18 @@ def main():
                     push_halo(halo)
             routed_iter = None
             if seqs is not None and not os.environ.get("SHD_ROUTE_TORCH") and not os.environ.get("SHD_ROUTE_SYNC"):
-                # micro-batch k+1 routed on a side stream while k is pushed (exchange.RoutePipeline)
+                # micro-batch k+1 routed on a side stream while k is pushed
+                # (exchange.RoutePipeline.run_staged: bucket + counts exchange of
+                # k+2 before the data exchange + merge of k+1, host copies one
+                # micro-batch ahead -- no blocking device-to-host read)
                 def job(a, b):
                     lo = (a * world) // 1024 * 1024
                     nb = -(-(b * world - lo) // 1024)
-                    return lambda: ex.route_device([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b], seqs[a:b],
-                                                   world, lo, 1024, nb, device=local)
-                routed_iter = pipe.run([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])])
+                    return (lambda: ex.route_stage_a([sym[a:b], price[a:b], vol[a:b], ts[a:b]], sym[a:b], seqs[a:b],
+                                                     world, lo, device=local),
+                            lambda st: ex.route_stage_b(st, 1024, nb))
+                routed_iter = pipe.run_staged([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])])
+                engine_stream = torch.cuda.ExternalStream(dq.stream_handle(), device=dev)
             held = None   # the previous micro-batch's routed tensors (RoutePipeline: lifetime)
             for a, b in zip(cuts[:-1], cuts[1:]):
                 if routed_iter is not None:
@@ -825,8 +830,9 @@ def main():
                     m = rs.numel()
                     routed_total[0] += m
                     if m > 0:
+                        engine_stream.wait_event(co.event)   # the merge done before the engine reads its rows
                         dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
-                                    he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+                                    he.SHD_MEM_DEVICE, co.get().astype(np.int64), True)
                     held = routed   # released after the next push has returned
                 elif seqs is None:
                     # InputHandler calls of 1024 events inside the micro-batch

@@ -219,12 +219,54 @@ def bucket(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world
     return send[:n * words.value], counts, words.value
 
 
+class HostCopy:
+    """A device -> pinned-host copy enqueued on the current stream, with an
+    event behind it: get() waits only for that event, and a pipelined caller
+    asks one micro-batch later, when the copy has long landed -- no
+    synchronous device-to-host read on the route's critical path."""
+
+    def __init__(self, t: torch.Tensor):
+        self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        self.host.copy_(t, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+
+    def get(self) -> torch.Tensor:
+        self.event.synchronize()
+        return self.host
+
+
+class CallOffsets:
+    """The merged micro-batch's InputHandler-call offsets, read from the
+    merge's tail (block offsets + error flag) once its HostCopy landed;
+    `event`: recorded after the merge on the route's stream (a consumer on
+    another stream waits on it instead of synchronising the host)."""
+
+    def __init__(self, tail: HostCopy, nblocks: int):
+        self._tail, self._nb, self._co = tail, nblocks, None
+        self.event = tail.event
+
+    def get(self):
+        import numpy as np
+        if self._co is None:
+            th = self._tail.get().numpy()
+            nb = self._nb
+            if int(th[nb + 1:].view(np.int32)[0]) != 0:
+                raise ValueError("route_device: received rows outside the micro-batch's calls (seq_lo / nblocks)")
+            co = np.unique(th[:nb + 1])
+            if len(co) == 0 or co[0] != 0:
+                co = np.concatenate([[0], co])
+            self._co = co.astype(np.int64)
+        return self._co
+
+
 def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtype], world: int, seq_lo: int,
-          call_size: int, nblocks: int, device: int = 0, m: Optional[int] = None):
+          call_size: int, nblocks: int, device: int = 0, m: Optional[int] = None, lazy: bool = False):
     """shd_route_merge on torch's current stream: the received rows of `world`
     senders (sender s's recv_counts[s] rows in turn) in global sequence order.
     m: total rows when the caller knows it (saves a device read).
-    Returns (columns, seq, call offsets as a host int64 array)."""
+    Returns (columns, seq, call offsets as a host int64 array; lazy: a
+    CallOffsets whose copy is still in flight)."""
     import ctypes
     import numpy as np
     from siddhi_amd import hip_engine as he
@@ -247,14 +289,57 @@ def merge(recv: torch.Tensor, recv_counts: torch.Tensor, dtypes: List[torch.dtyp
     he._check(lib.shd_route_merge(ctx, stream, world, recv.data_ptr(), seg_off.data_ptr(), m, int(seq_lo),
                                   int(call_size), int(nblocks), len(outs), ptrs, wa, out_seq.data_ptr(),
                                   start.data_ptr(), block_off.data_ptr(), err.data_ptr()))
-    th = tail.cpu().numpy()
-    bo = th[:nblocks + 1]
-    if int(th[nblocks + 1:].view(np.int32)[0]) != 0:
-        raise ValueError("route_device: received rows outside the micro-batch's calls (seq_lo / nblocks)")
-    co = np.unique(bo)
-    if len(co) == 0 or co[0] != 0:
-        co = np.concatenate([[0], co])
-    return outs, out_seq, co.astype(np.int64)
+    co = CallOffsets(HostCopy(tail), nblocks)
+    return outs, out_seq, (co if lazy else co.get())
+
+
+def route_stage_a(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int, seq_lo: int,
+                  group: Optional[dist.ProcessGroup] = None, device: int = 0, stage_host: bool = False) -> dict:
+    """Route, first half: HIP bucket by owner + the all-to-all of the
+    per-owner counts; both counts vectors go to pinned host memory without
+    waiting (HostCopy) -- stage B of the same micro-batch, issued one
+    micro-batch later in a pipeline, sizes the data exchange from them."""
+    st = {"dtypes": [c.dtype for c in cols], "n": seq.numel(), "world": world, "seq_lo": seq_lo,
+          "group": group, "device": device, "stage_host": stage_host}
+    send, counts, words = bucket(cols, key, seq, world, seq_lo, device)
+    st.update(send=send, counts=counts, words=words)
+    if world > 1:
+        recv_counts = torch.empty_like(counts)
+        _a2a(recv_counts, counts, group=group, stage_host=stage_host)
+        st["recv_counts"] = recv_counts
+        st["host_counts"] = HostCopy(torch.cat([counts, recv_counts]))
+    return st
+
+
+def _a2a(out, inp, out_splits=None, in_splits=None, group=None, stage_host=False):
+    if not stage_host:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        return
+    ho = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
+    out.copy_(ho)
+
+
+def route_stage_b(st: dict, call_size: int, nblocks: int, lazy: bool = True):
+    """Route, second half: the data all-to-all (split sizes from stage A's
+    host counts), then the HIP merge into global sequence order.  lazy: the
+    call offsets come back as a CallOffsets (copy in flight)."""
+    world, group, device = st["world"], st["group"], st["device"]
+    send, counts, words = st["send"], st["counts"], st["words"]
+    if world > 1:
+        hc = st["host_counts"].get().tolist()
+        cs, rcs = hc[:world], hc[world:]
+        recv = torch.empty(sum(rcs) * words, dtype=torch.int64, device=send.device)
+        _a2a(recv, send, [c * words for c in rcs], [c * words for c in cs], group=group,
+             stage_host=st["stage_host"])
+        rank = dist.get_rank(group)
+        stats = {"sent": sum(cs) - cs[rank], "received": sum(rcs) - rcs[rank]}
+        recv_counts, m = st["recv_counts"], sum(rcs)
+    else:
+        recv, recv_counts, stats, m = send, counts, {"sent": 0, "received": 0}, st["n"]
+    outs, rseq, co = merge(recv, recv_counts, st["dtypes"], world, st["seq_lo"], call_size, nblocks, device, m=m,
+                           lazy=lazy)
+    return outs, rseq, co, stats
 
 
 def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor, world: int, seq_lo: int,
@@ -265,30 +350,13 @@ def route_device(cols: List[torch.Tensor], key: torch.Tensor, seq: torch.Tensor,
     sizes the exchange).  The micro-batch's events hold sequence numbers in
     [seq_lo, seq_lo + nblocks * call_size) with seq_lo a multiple of call_size
     (the global stream's InputHandler calls).  Returns (columns, seq, host call
-    offsets, stats) in increasing sequence order.
+    offsets, stats) in increasing sequence order.  The two stages
+    (route_stage_a / route_stage_b) run back to back here; RoutePipeline.run_staged
+    interleaves them across micro-batches so nothing waits on the device.
     stage_host: the two all-to-alls run on host copies (a gloo group, e.g. ranks
     sharing one GPU in tests; RCCL needs one GPU per rank)."""
-    dtypes = [c.dtype for c in cols]
-    send, counts, words = bucket(cols, key, seq, world, seq_lo, device)
-    if world > 1:
-        def a2a(out, inp, out_splits=None, in_splits=None):
-            if not stage_host:
-                dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
-                return
-            ho = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
-            out.copy_(ho)
-        recv_counts = torch.empty_like(counts)
-        a2a(recv_counts, counts)
-        cs, rcs = counts.tolist(), recv_counts.tolist()
-        recv = torch.empty(sum(rcs) * words, dtype=torch.int64, device=send.device)
-        a2a(recv, send, [c * words for c in rcs], [c * words for c in cs])
-        rank = dist.get_rank(group)
-        stats = {"sent": sum(cs) - cs[rank], "received": sum(rcs) - rcs[rank]}
-    else:
-        recv, recv_counts, stats = send, counts, {"sent": 0, "received": 0}
-    outs, rseq, co = merge(recv, recv_counts, dtypes, world, seq_lo, call_size, nblocks, device,
-                           m=recv.numel() // words if world > 1 else seq.numel())
+    st = route_stage_a(cols, key, seq, world, seq_lo, group, device, stage_host)
+    outs, rseq, co, stats = route_stage_b(st, call_size, nblocks, lazy=False)
     return outs, rseq, co, stats
 
 
@@ -321,6 +389,35 @@ class RoutePipeline:
             r = job()
         self.stream.synchronize()   # routed columns complete before another stream reads them
         return r
+
+    def _staged(self, jobs, i):
+        """Worker step i: stage A of micro-batch i + 1, then stage B of i (whose
+        host counts were copied during step i - 1).  The routed columns are
+        fenced with an event on the side stream, not a host sync."""
+        torch.cuda.set_device(self.device)
+        with torch.cuda.stream(self.stream):
+            if i == 0:
+                self._st[0] = jobs[0][0]()
+            if i + 1 < len(jobs):
+                self._st[i + 1] = jobs[i + 1][0]()
+            r = jobs[i][1](self._st.pop(i))
+        return r
+
+    def run_staged(self, jobs):
+        """jobs: (stage_a, stage_b) pairs -- stage_a() -> state (route_stage_a),
+        stage_b(state) -> route result with lazy CallOffsets (route_stage_b).
+        The collectives keep micro-batch order on every rank: counts of i + 1
+        before the data of i.  The caller makes its engine stream wait on
+        result[2].event and reads result[2].get() when it pushes."""
+        self._st = {}
+        pending = None
+        for i in range(len(jobs)):
+            nxt = self.pool.submit(self._staged, jobs, i)
+            if pending is not None:
+                yield pending.result()
+            pending = nxt
+        if pending is not None:
+            yield pending.result()
 
     def run(self, jobs):
         pending = None

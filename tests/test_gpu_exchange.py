@@ -86,7 +86,7 @@ def test_in_seq_equals_oracle(hip_available, name, app, n, keys, delta):
 N_RR, KEYS_RR, DELTA_RR, BATCH_RR = 200_000, 4000, 0.02, 30_720
 
 
-def _rr_rank(rank, world, path, outdir):
+def _rr_rank(rank, world, path, outdir, staged):
     """One rank of the N > 1 bench path on a shared GPU: its round-robin share
     of the global stream resident in HBM, each micro-batch re-routed by key
     owner with the HIP bucket / merge passes (the all-to-all staged through host
@@ -116,17 +116,29 @@ def _rr_rank(rank, world, path, outdir):
     def job(a, b):
         lo = (a * world) // 1024 * 1024
         nb = -(-(b * world - lo) // 1024)
-        return lambda: ex2.route_device([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo, 1024, nb,
-                                        stage_host=True)
+        if not staged:
+            return lambda: ex2.route_device([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo, 1024, nb,
+                                            stage_host=True)
+        return (lambda: ex2.route_stage_a([c[a:b] for c in cols], cols[0][a:b], seq[a:b], world, lo,
+                                          stage_host=True),
+                lambda st: ex2.route_stage_b(st, 1024, nb))
 
     cuts = list(range(0, len(idx), BATCH_RR)) + [len(idx)]   # BATCH_RR * world: whole 1024-event calls
     pipe = ex2.RoutePipeline(0)   # micro-batch k+1 routed while k is pushed (bench.py's N > 1 path)
-    for (rs, rp, rv, rt), rseq, co, _ in pipe.run([job(a, b) for a, b in zip(cuts[:-1], cuts[1:])]):
+    jobs = [job(a, b) for a, b in zip(cuts[:-1], cuts[1:])]
+    engine_stream = torch.cuda.ExternalStream(dq.stream_handle(), device=dev)
+    held = None
+    for res in (pipe.run_staged(jobs) if staged else pipe.run(jobs)):
+        (rs, rp, rv, rt), rseq, co, _ = res
         m = rs.numel()
         if m == 0:
             continue
+        if staged:
+            engine_stream.wait_event(co.event)   # the merge done before the engine reads its rows
+            co = co.get()
         dq.push_raw(0, m, rt.data_ptr(), [rs.data_ptr(), rp.data_ptr(), rv.data_ptr()], [0, 0, 0],
                     he.SHD_MEM_DEVICE, co.astype(np.int64), True)
+        held = res   # RoutePipeline lifetime: kept until the next push has returned
         routed.append(rseq.cpu().numpy())
         r = dq.poll(with_seq=True)
         if r is not None:
@@ -142,17 +154,19 @@ def _rr_rank(rank, world, path, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_roundrobin_route_device_merges_to_single_engine(hip_available, tmp_path, world):
+@pytest.mark.parametrize("world,staged", [(2, False), (4, False), (2, True), (4, True)])
+def test_roundrobin_route_device_merges_to_single_engine(hip_available, tmp_path, world, staged):
     """The N > 1 bench path end to end (bench.py --input roundrobin): 2 or 4
     ranks on one GPU, HIP bucket -> all-to-all -> HIP merge -> P3 query per rank,
     the next micro-batch routed while the current one is pushed
-    (exchange.RoutePipeline), rows mapped to global sequence numbers and k-way
-    merged (exchange.merge_outputs): equal to one device query over the whole
-    stream and to the CPU oracle."""
+    (exchange.RoutePipeline; staged: run_staged -- counts exchanged one
+    micro-batch ahead through pinned host copies, the merge fenced by an
+    event on the engine's stream), rows mapped to global sequence numbers and
+    k-way merged (exchange.merge_outputs): equal to one device query over the
+    whole stream and to the CPU oracle."""
     import tempfile
     import torch.multiprocessing as mp
-    mp.spawn(_rr_rank, args=(world, tempfile.mktemp(dir=str(tmp_path)), str(tmp_path)), nprocs=world)
+    mp.spawn(_rr_rank, args=(world, tempfile.mktemp(dir=str(tmp_path)), str(tmp_path), staged), nprocs=world)
     parts = []
     for r in range(world):
         z = np.load(os.path.join(str(tmp_path), "r%d.npz" % r))
