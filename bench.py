@@ -408,12 +408,18 @@ def run_multi(args, torch, dist, rank, world, local, dev):
         # time of a step; device_*: / the HIP-event time of every push
         ach = bytes_step / (elapsed / args.steps) / 1e9
         dev_ach = bytes_step / (sum(stages.values()) * 1e-9) / 1e9
+        # HBM bytes of the whole fan-out (every unit's kernels per stream
+        # micro-batch, PMC summary of this build) x micro-batches per step
+        pmc, psrc = pmc_summary("M5")
+        traffic = round(pmc["push"]["hbm_bytes_per_event"] * n) if pmc else None
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_ratio": round(traffic / bytes_step, 3) if traffic else None,
                 "alg_bytes_per_event": round(bytes_step / n, 2),
                 "scope": "whole fan-out per step (wall clock), rank 0",
                 "device_achieved": round(dev_ach, 1), "device_frac": round(dev_ach / HBM_PEAK_GBS, 4),
-                "stage_top": max(stages, key=stages.get)}
+                "stage_top": max(stages, key=stages.get),
+                "pmc_source": psrc if pmc else None, "pmc_note": None if pmc else psrc}
     if rank == 0:
         line = {
             "metric": "events/sec ingested + matches/sec (partitioned pattern, 1–8 GPU); % HBM peak",

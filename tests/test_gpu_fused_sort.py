@@ -146,3 +146,26 @@ def test_fused_sort_f1_resolved_and_generic(hip_available, monkeypatch, f1):
     check(qp, batches, monkeypatch, min_rows=0)
     monkeypatch.setenv("SHD_KS_GENERIC_F1", "1")
     check(qp, batches, monkeypatch, min_rows=0)
+
+
+@pytest.mark.parametrize("app,keys", [("P3", 1_500_000), ("and", 1_500_000), ("or", 4_000_000)])
+def test_resume_list_equals_tile_pass(hip_available, monkeypatch, app, keys):
+    """Sparse keys: the deferred walks run from a compacted list, one lane each
+    (k_resume_list), instead of the per-tile outcome-byte pass (MODE 0,
+    SHD_NO_RESUME_LIST): same rows as the oracle, same walk counters."""
+    text = wl.P3_APP if app == "P3" else wl.S4_PART_APPS[app]
+    qp, _ = compile_single_query(text)
+    # E = events of a partial's key inside `within` < 0.25: the sparse layout
+    sym, price, vol, ts = wl.stock_stream(400_000, keys, 0.01, seed_offset=29)
+    batches = split((sym, price, vol, ts), 3)
+    ora = run_oracle(qp, batches)
+    assert len(ora[2]) > 0
+    monkeypatch.delenv("SHD_NO_RESUME_LIST", raising=False)
+    dev, c_list, kind = run_device(qp, batches)
+    assert kind == 1
+    assert_same_rows(dev, ora)
+    monkeypatch.setenv("SHD_NO_RESUME_LIST", "1")
+    dev2, c_tile, _ = run_device(qp, batches)
+    assert_same_rows(dev2, ora)
+    for k in COUNTERS:
+        assert c_list[k] == c_tile[k], k

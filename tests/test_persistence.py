@@ -275,3 +275,65 @@ def test_snapshot_restore_sparse_key_carry(hip_available):
     assert len(ora[2]) > 0
     for cut in range(1, len(batches)):
         assert_same_rows(_run_with_restore(qp, batches, cut), ora)
+
+
+# ---- output rate limiters across persist() / restoreRevision()
+# The limiters' RateLimiterState maps (counter, held rows, per-group maps,
+# scheduled time) ride in the snapshot head: an uninterrupted run and a run
+# restored into a fresh runtime mid-stream emit the same callback chunks.
+RATE_APPS = {
+    "every-3-events": "output every 3 events",
+    "last-every-4-events-grouped": "output last every 4 events",
+    "first-every-5-events-grouped": "output first every 5 events",
+    "all-every-time": "output all every 100 milliseconds",
+    "last-every-time-grouped": "output last every 50 milliseconds",
+}
+
+
+def _rate_app(rate, grouped):
+    return ("@app:name('R') @app:playback define stream S (symbol string, price double, volume long); "
+            "@info(name = 'q') from S select symbol, price, volume %s %s insert into O;"
+            % ("group by symbol" if grouped else "", rate))
+
+
+def _rate_run(app, events, cut=None):
+    """Callback chunks of `app` over `events` (ts, data); with `cut`, persist
+    after event cut - 1 and continue in a restored fresh runtime."""
+    m = SiddhiManager(engine_factory=OracleQueryEngine)
+    m.setPersistenceStore(InMemoryPersistenceStore())
+    chunks = []
+
+    class C(QueryCallback):
+        def receive(self, timestamp, inEvents, removeEvents):
+            chunks.append([(e.getTimestamp(), list(e.getData())) for e in inEvents or []])
+
+    rt = m.createSiddhiAppRuntime(app)
+    rt.clock = lambda: 1000   # the timed limiters schedule from the wall clock (partitionCreated)
+    rt.addCallback("q", C())
+    rt.start()
+    ih = rt.getInputHandler("S")
+    for k, (ts, d) in enumerate(events):
+        if cut is not None and k == cut:
+            rev = rt.persist().getRevision()
+            rt.shutdown()
+            rt = m.createSiddhiAppRuntime(app)
+            rt.clock = lambda: 5000   # a later wall clock: the restored schedule must win
+            rt.addCallback("q", C())
+            rt.start()
+            rt.restoreRevision(rev)
+            ih = rt.getInputHandler("S")
+        ih.send(ts, d)
+    rt.shutdown()
+    return chunks
+
+
+@pytest.mark.parametrize("name", list(RATE_APPS))
+def test_rate_limiter_state_survives_restore(name):
+    grouped = name.endswith("grouped")
+    app = _rate_app(RATE_APPS[name], grouped)
+    rng = np.random.default_rng(7)
+    events = [(1000 + 7 * k, ["S%d" % int(rng.integers(0, 4)), float(rng.integers(50, 100)), k]) for k in range(60)]
+    whole = _rate_run(app, events)
+    assert sum(len(c) for c in whole) > 0
+    for cut in (1, 7, 23, 41):
+        assert _rate_run(app, events, cut) == whole, cut
