@@ -436,10 +436,10 @@ class Parser:
             qs.append(self.query(pend))
             pend = []
         self.expect("end")
-        return Partition(withs, qs, anns)
+        return _inner_streams(Partition(withs, qs, anns))
 
     # -- query
-    def query(self, anns) -> Query:
+    def query(self, anns) -> Query:  # noqa: C901
         self.expect("from")
         inp = self.query_input()
         if self.at_kw("select"):
@@ -533,7 +533,7 @@ class Parser:
 
     def standard_stream(self) -> SingleInput:
         inner = self.accept("#")
-        sid = self.name()
+        sid = ("#" if inner else "") + self.name()
         handlers = []
         while True:
             if self.at("["):
@@ -642,9 +642,8 @@ class Parser:
         return StreamSE(sid, ref, filters)
 
     def basic_source(self):
-        if self.accept("#"):
-            raise OutOfScopeSyntax("partition-inner streams (#stream) are outside the hot path")
-        sid = self.name()
+        # `#Name`: a partition-inner stream (rewritten by _inner_streams)
+        sid = ("#" + self.name()) if self.accept("#") else self.name()
         filters = []
         while self.at("[") or (self.at("#") and self.peek(1).text == "["):
             self.accept("#")
@@ -863,3 +862,77 @@ class Parser:
 def parse(app_text: str) -> SiddhiApp:
     """SiddhiCompiler.parse equivalent (QC/java/io/siddhi/query/compiler/SiddhiCompiler.java)."""
     return Parser(app_text).parse_app()
+
+
+# ---------------------------------------------------------------- partition-inner streams
+def _qualify(expr, ref):
+    """A partition key expression over a stream's attributes, read through
+    the pattern state `ref` (e1.quantity)."""
+    if isinstance(expr, Var):
+        return Var(expr.attr, ref if expr.stream is None else expr.stream, expr.index)
+    if isinstance(expr, BinOp):
+        return BinOp(expr.op, _qualify(expr.left, ref), _qualify(expr.right, ref))
+    if isinstance(expr, Not):
+        return Not(_qualify(expr.expr, ref))
+    return expr
+
+
+def _state_streams(el):
+    """StreamSE leaves of a pattern / sequence element in text order."""
+    if isinstance(el, StreamSE):
+        return [el]
+    if isinstance(el, NextSE):
+        return _state_streams(el.a) + _state_streams(el.b)
+    if isinstance(el, EverySE):
+        return _state_streams(el.inner)
+    if isinstance(el, LogicalSE):
+        return [el.a, el.b]
+    if isinstance(el, CountSE):
+        return [el.stream]
+    if isinstance(el, (list, tuple)):
+        return [x for e in el for x in _state_streams(e)]
+    return []
+
+
+PKEY = "__pkey"
+
+
+def _inner_streams(p: Partition) -> Partition:
+    """`insert into #S` / `from #S` inside a partition (PartitionRuntimeImpl:
+    an inner stream is per partition instance, C/partition/
+    PartitionRuntimeImpl.java:346-402): the producer's rows carry the key of
+    the instance that emitted them as a hidden attribute `__pkey` (its input
+    stream's partition key, read through the first keyed pattern state), and
+    the inner stream joins the partition keyed by it -- so a consumer's
+    per-key state sees exactly the rows its own instance produced."""
+    keys = {sid: e for e, sid in p.with_}
+    inner = {q.target for q in p.queries if q.inner_target}
+    if not inner:
+        return p
+    for q in p.queries:
+        if not q.inner_target:
+            continue
+        if q.selector.select_all:
+            raise OutOfScopeSyntax("select * into a partition-inner stream is outside the hot path")
+        inp = q.input
+        if isinstance(inp, SingleInput):
+            k = keys.get(inp.stream)
+            kexpr = None if k is None else (_qualify(k, inp.ref) if inp.ref else k)
+        elif isinstance(inp, StateInput):
+            kexpr = None
+            for se in _state_streams(inp.element):
+                if not se.absent and se.ref is not None and se.stream in keys:
+                    kexpr = _qualify(keys[se.stream], se.ref)
+                    break
+        else:
+            kexpr = None
+        if kexpr is None:
+            raise OutOfScopeSyntax("partition-inner stream '%s' from a query without a keyed input" % q.target)
+        q.selector.attrs.append(OutAttr(kexpr, PKEY))
+        q.target = "#" + q.target
+        q.inner_target = False
+    for q in p.queries:
+        if isinstance(q.input, SingleInput) and q.input.inner:
+            q.input.inner = False
+    p.with_ = list(p.with_) + [(Var(PKEY), "#" + n) for n in sorted(inner)]
+    return p

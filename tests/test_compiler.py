@@ -65,3 +65,28 @@ def test_unsupported_reports_reason():
 def test_time_units():
     app = qc.parse("define stream A (x int); from every e1=A -> e2=A within 1 min 30 sec select e1.x as a insert into O;")
     assert app.queries[0].input.within_ms == 90_000
+
+
+def test_partition_inner_stream_rewrite():
+    """`insert into #S` / `from #S` inside a partition: the producer's rows
+    carry its instance's key as the hidden `__pkey`, read through the first
+    keyed pattern state (or the single input stream), and #S joins the
+    partition keyed by it (PatternPartitionTestCase 32/33 shapes)."""
+    app = qc.parse(
+        "define stream S1 (symbol string, price float, volume int, q int); "
+        "define stream S2 (symbol string, price float, volume int, q int); "
+        "partition with (q of S1, q of S2) begin "
+        "from every e1 = S1 -> e2 = S2[price > e1.price] select e1.symbol as s, e2.price as p insert into #Mid; "
+        "from #Mid[p > 1.0] select s, p insert into Out; "
+        "from S1 select symbol, volume insert into #Raw; "
+        "from #Raw select symbol insert into Out2; end;")
+    p = app.partitions[0]
+    keys = {sid: e for e, sid in p.with_}
+    assert keys["#Mid"] == qc.Var("__pkey") and keys["#Raw"] == qc.Var("__pkey")
+    prod, cons, prod2, cons2 = p.queries
+    assert prod.target == "#Mid" and not prod.inner_target
+    assert prod.selector.attrs[-1].name == "__pkey"
+    assert prod.selector.attrs[-1].expr == qc.Var("q", "e1")
+    assert prod2.selector.attrs[-1].expr == qc.Var("q")
+    assert cons.input.stream == "#Mid" and cons2.input.stream == "#Raw"
+    assert [o.name for o in cons.selector.attrs] == ["s", "p"]
