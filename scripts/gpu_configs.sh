@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
-for c in ${CONFIGS:-P1 P3-dense W2-length W2-time S4-seq S4-seqplus S4-or S4-and S4-not S4P-seqplus}; do
+for c in ${CONFIGS:-P1 P3-dense W2-length W2-time S4-seq S4-seq14 S4-seqplus S4-or S4-and S4-not S4P-seqplus}; do
   case $c in
     P3-dense) CPU=1000000 ;;
     W2-*) CPU=1000000 ;;

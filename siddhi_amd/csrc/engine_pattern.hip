@@ -30,7 +30,6 @@
 #include <cstdlib>
 
 #include "engine.h"
-#include "radix_tile.h"
 #include "pattern_common.h"
 
 namespace shd {
@@ -131,39 +130,43 @@ static_assert(sizeof(PrepAgg) <= 64 && sizeof(ScanOut) <= 64, "d_agg layout");
 // the tile's match / open counts (plain store, or added for the resume pass).
 __device__ __forceinline__ void scan_block_reduce(uint64_t steps, uint64_t pruned, uint32_t viol, uint32_t nm,
                                                   uint32_t no, ScanOut* blk, int slot, uint32_t* bcnt, int tile,
-                                                  int ntile, bool add) {
+                                                  int ntile, bool add, uint32_t nd = 0) {
   for (int o2 = 32; o2 > 0; o2 >>= 1) {
     steps += __shfl_xor(steps, o2, 64);
     pruned += __shfl_xor(pruned, o2, 64);
     viol |= __shfl_xor(viol, o2, 64);
     nm += __shfl_xor(nm, o2, 64);
     no += __shfl_xor(no, o2, 64);
+    nd += __shfl_xor(nd, o2, 64);
   }
   __shared__ ScanOut wpart[kBlock / 64];
-  __shared__ uint32_t wcnt[2][kBlock / 64];
+  __shared__ uint32_t wcnt[3][kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
     wpart[threadIdx.x >> 6] = ScanOut{steps, pruned, viol};
     wcnt[0][threadIdx.x >> 6] = nm;
     wcnt[1][threadIdx.x >> 6] = no;
+    wcnt[2][threadIdx.x >> 6] = nd;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     ScanOut r = wpart[0];
-    uint32_t tm = wcnt[0][0], to = wcnt[1][0];
+    uint32_t tm = wcnt[0][0], to = wcnt[1][0], td = wcnt[2][0];
     for (int w = 1; w < kBlock / 64; w++) {
       r.steps += wpart[w].steps;
       r.pruned += wpart[w].pruned;
       r.violation |= wpart[w].violation;
       tm += wcnt[0][w];
       to += wcnt[1][w];
+      td += wcnt[2][w];
     }
     blk[slot] = r;
     if (add) {
       if (tm) atomicAdd(&bcnt[tile], tm);
       if (to) atomicAdd(&bcnt[ntile + tile], to);
     } else {
-      bcnt[tile] = tm;           // matches of this tile
-      bcnt[ntile + tile] = to;   // still-open partials of this tile
+      bcnt[tile] = tm;                // matches of this tile
+      bcnt[ntile + tile] = to;        // still-open partials of this tile
+      bcnt[2 * ntile + tile] = td;    // deferred walks of this tile (k_forward_scan)
     }
   }
 }
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   const ScanArgs& a = *ap;
   const DExprSet es{};
   uint64_t steps = 0, pruned = 0;
-  uint32_t viol = 0, nm = 0, no = 0;
+  uint32_t viol = 0, nm = 0, no = 0, nd = 0;
   // this block's contiguous tile of positions (compaction offsets are per block)
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n_ext ? t0 + tile : n_ext;
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
       if (st == ST_DEFER) {
         out = PS_DEFER;
         match_row[p] = (int32_t)q;   // resume position (< 2^28)
+        nd++;
       } else if (st == ST_OPEN) {
         out = PS_OPEN;
         no++;
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_scan(const ScanArgs* __restr
   };
   const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
   for (int64_t p = t0 + threadIdx.x; p < t1; p += kBlock) visit(p, ld);
-  scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false);
+  scan_block_reduce(steps, pruned, viol, nm, no, blk, blockIdx.x, bcnt, blockIdx.x, gridDim.x, false, nd);
 }
 
 // Position-major copy of the e2-side attributes the filters read (ExtRows::bpos):
@@ -754,6 +758,65 @@ __global__ __launch_bounds__(kBlock) void k_forward_resume(const ScanArgs* __res
   scan_block_reduce(steps, pruned, viol, nm, no, blk, slot0 + blockIdx.x, bcnt, blockIdx.x, gridDim.x, true);
 }
 
+// Deferred walks from a list (sparse keys): the deferred positions, compacted
+// in position order by k_open_list (val PS_DEFER), one lane each -- every
+// lane of a wave walks, where the per-tile MODE 0 pass leaves a wave with a
+// few walking lanes among outcome-byte scans.  Same walk as MODE 0/1
+// (walk_partial from the deferred B event); a position's match / open counts
+// go to its own tile's slots, the walk counters to ScanOut partials
+// [slot0, slot0 + gridDim.x).  The list length is read on the device.
+template <bool K64, bool FAST, bool TS64>
+__global__ __launch_bounds__(kBlock) void k_resume_list(const ScanArgs* __restrict__ ap, int64_t n_ext, int64_t tile,
+                                                        int ntile, const uint32_t* __restrict__ skey32,
+                                                        const uint64_t* __restrict__ skey64,
+                                                        const uint32_t* __restrict__ spv,
+                                                        const int32_t* __restrict__ sts32,
+                                                        const int64_t* __restrict__ sts64,
+                                                        int32_t* __restrict__ match_row,
+                                                        int32_t* __restrict__ match_other, uint8_t* __restrict__ pst,
+                                                        uint32_t* __restrict__ bcnt, ScanOut* __restrict__ blk,
+                                                        int slot0, const uint32_t* __restrict__ dlist,
+                                                        const uint32_t* __restrict__ dcount) {
+  const ScanArgs& a = *ap;
+  const DExprSet es = a.es;
+  uint64_t steps = 0, pruned = 0;
+  uint32_t viol = 0;
+  const int64_t tbase = TS64 ? 0 : a.x.batch.ts[0];
+  const GlobalPos<K64, TS64> ld{skey32, skey64, spv, sts32, sts64, tbase, a.partitioned};
+  const int64_t cnt = *dcount;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t p = dlist[i];
+    int64_t q = match_row[p];
+    uint32_t pvp, pq;
+    int64_t tsi, tq;
+    uint64_t k = 0, kq = 0;
+    ld(p, pvp, tsi, k);
+    ld(q, pq, tq, kq);
+    int32_t j = -1;
+    uint32_t fm = 0;
+    int64_t ra = -1, rb = -1;
+    if (a.logical == 2) and_carried(a, pv_row(pvp), fm, ra, rb);
+    const uint8_t st = walk_partial<false, FAST, 1, GlobalPos<K64, TS64>, 0, false>(
+        a, es, n_ext, ld, pv_row(pvp), k, tsi, q, pq, tq, kq, tq, true, j, steps, viol, fm, ra, rb, p);
+    uint8_t out = PS_NONE;
+    const int t = (int)(p / tile);
+    if (st == ST_MATCH) {
+      out = PS_MATCH;
+      match_row[p] = j;
+      if (a.logical == 2) match_other[p] = (int32_t)((j >> kRowBits) ? ra : rb);
+      atomicAdd(&bcnt[t], 1u);
+    } else if (st == ST_OPEN) {
+      out = PS_OPEN | PS_PEND;   // it met a B event of its key: in the pending list now
+      if (a.logical == 2) match_row[p] = and_code(fm, ra, rb);
+      atomicAdd(&bcnt[ntile + t], 1u);
+    } else if (st == ST_PRUNED) {
+      pruned++;
+    }
+    pst[p] = out;
+  }
+  scan_block_reduce(steps, pruned, viol, 0u, 0u, blk, slot0 + blockIdx.x, bcnt, 0, ntile, true);
+}
+
 // Lockstep walks (plain `e1 -> e2` form, full-key sort, pre-decoded f2): one
 // lane per position as in k_forward_scan, but f2 is evaluated in the walk
 // itself, so every candidate of a wave starts at its successor and all of
@@ -1228,12 +1291,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_carry(const GatherArgs* __res
 // once.  Only the e1 columns read again after the carry (amask) are copied.
 __global__ __launch_bounds__(kBlock) void k_open_list(const uint8_t* __restrict__ pst, const uint32_t* __restrict__ boff,
                                                       int64_t n, int64_t tile, uint32_t* __restrict__ olist,
-                                                      uint32_t val) {
+                                                      uint32_t val, int which) {
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n ? t0 + tile : n;
   __shared__ uint32_t wsum[kBlock / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t base = boff[gridDim.x + blockIdx.x];
+  uint32_t base = boff[which * gridDim.x + blockIdx.x];   // offsets of count `which` (1: open, 2: deferred)
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
     const int64_t p = c0 + threadIdx.x;
@@ -1477,7 +1540,7 @@ struct PatternEngine : Engine {
   const int64_t* fin_sts64 = nullptr;
   // scratch
   DevBuf d_k32, d_k32_alt, d_k64, d_k64_alt, d_pv, d_pv_alt, d_ts, d_ts_alt, d_ts64, d_match, d_pst, d_bcnt, d_boff, d_pj,
-      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_olist;
+      d_pi, d_pj_alt, d_pi_alt, d_agg, d_sort, d_scan, d_blk, d_mother, d_se1, d_sot, d_olist, d_dlist;
   // stream-A attributes read again after a partial is carried (state-0 loads
   // of f2 / f3 / the selector): only these columns are copied into the carry
   uint32_t carry_mask = ~0u;
@@ -2007,6 +2070,10 @@ struct PatternEngine : Engine {
       sa.bsum = d_bsum.as<BlockSum>();
     }
     const ScanArgs* d_sa = dev_args(sa);
+    // sparse keys (MODE 0): the deferred walks from a compacted list
+    // (k_resume_list) unless SHD_NO_RESUME_LIST
+    const bool rlist = rmode == 0 && !lockstep && !sa.bsum && !sorted64 && !getenv("SHD_NO_RESUME_LIST");
+    const int nlb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n_ext, (int64_t)64 * kBlock)));
     if (sa.bsum) {
       hipLaunchKernelGGL(k_block_sum, dim3(grid_for(ceil_div(n_ext, 64) * 64, 1, 4096)), dim3(kBlock), 0, s, d_sa,
                          n_ext, skey32, spv, sts32, d_bsum.as<BlockSum>());
@@ -2071,6 +2138,28 @@ struct PatternEngine : Engine {
           SHD_LAUNCH_SKIP(2, 2 * ntile);
         } else if (rmode == 2) SHD_LAUNCH_SKIP(2, ntile);
         else SHD_LAUNCH_SKIP(1, ntile);
+      } else if (rlist) {
+        // sparse keys: the deferred positions compacted into a list (per-tile
+        // counts from k_forward_scan), then one lane per deferred walk
+        uint32_t* d_ndef = reinterpret_cast<uint32_t*>(d_agg.as<char>() + 240);
+        scan_exclusive_u32(d_bcnt.as<uint32_t>() + 2 * ntile, d_boff.as<uint32_t>() + 2 * ntile, ntile, d_ndef, d_scan,
+                           s);
+        d_dlist.reserve((size_t)n_ext * 4);
+        hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
+                           (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_dlist.as<uint32_t>(),
+                           (uint32_t)PS_DEFER, 2);
+        SHD_CHECK_LAUNCH();
+#define SHD_LAUNCH_RLIST(FAST, TS64)                                                                               \
+  hipLaunchKernelGGL((k_resume_list<false, FAST, TS64>), dim3(nlb), dim3(kBlock), 0, s, d_sa, n_ext, tile, ntile,     \
+                     skey32, skey64, spv, sts32, sts64, d_match.as<int32_t>(), d_mother.as<int32_t>(),              \
+                     d_pst.as<uint8_t>(), d_bcnt.as<uint32_t>(), d_blk.as<ScanOut>(), ntile,                        \
+                     (const uint32_t*)d_dlist.as<uint32_t>(), (const uint32_t*)d_ndef)
+        if (fast2) {
+          if (ts64) SHD_LAUNCH_RLIST(true, true); else SHD_LAUNCH_RLIST(true, false);
+        } else {
+          if (ts64) SHD_LAUNCH_RLIST(false, true); else SHD_LAUNCH_RLIST(false, false);
+        }
+#undef SHD_LAUNCH_RLIST
       } else if (fast2) { SHD_LAUNCH_RESUME2(false, true); }
       else { SHD_LAUNCH_RESUME2(false, false); }
     }
@@ -2082,7 +2171,7 @@ struct PatternEngine : Engine {
     SHD_CHECK_LAUNCH();
     // partials: [0, ntile) hot walk, [ntile, 2 ntile) deferred walks, [2 ntile, 3 ntile) continued walks
     hipLaunchKernelGGL(k_finish_scan, dim3(1), dim3(kBlock), 0, s, (const ScanOut*)d_blk.as<ScanOut>(),
-                       (rmode == 3 && !lockstep ? 3 : 2) * ntile,
+                       rlist ? ntile + nlb : (rmode == 3 && !lockstep ? 3 : 2) * ntile,
                        d_so);
     SHD_CHECK_LAUNCH();
     mark("forward_scan");
@@ -2231,7 +2320,7 @@ struct PatternEngine : Engine {
         d_olist.reserve((size_t)n_open * 4);
         hipLaunchKernelGGL(k_open_list, dim3(ntile), dim3(kBlock), 0, s, (const uint8_t*)d_pst.as<uint8_t>(),
                            (const uint32_t*)d_boff.as<uint32_t>(), n_ext, tile, d_olist.as<uint32_t>(),
-                           (uint32_t)PS_OPEN);
+                           (uint32_t)PS_OPEN, 1);
         SHD_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_gather_list, dim3(grid_cover((int64_t)n_open)), dim3(kBlock), 0, s, dev_args(ga),
                            (const uint32_t*)d_olist.as<uint32_t>(), (int64_t)n_open,
