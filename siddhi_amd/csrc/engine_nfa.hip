@@ -1893,20 +1893,52 @@ __global__ void k_nfa_calls(const int64_t* offs, int ncalls, const int64_t* ts, 
 // TimestampGeneratorImpl.setCurrentTimestamp per call: only moves forward, and
 // Scheduler.onTimeChange runs when t >= now.  Sequential over calls (one
 // thread; calls are ~1/1000 of the events).
-__global__ void k_nfa_now(const int64_t* last_ts, const int64_t* offs, int ncalls, int64_t now_prev, int64_t seq0,
-                          int advance, int64_t* now, uint8_t* changed, int64_t* first) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  int64_t cur = now_prev;
-  for (int c = 0; c < ncalls; c++) {
-    int64_t t = last_ts[c];
-    uint8_t ch = 0;
-    if (advance && offs[c + 1] > offs[c] && t >= cur) {
-      cur = t;
-      ch = 1;
+// Playback time per call (one workgroup): now[c] = the running max of the
+// non-empty calls' last timestamps (InputHandler.send -> setCurrentTimestamp,
+// time never goes back), changed[c] = call c moved (or met) the clock.  A
+// block-wide max scan over 1024-call chunks (the one-thread loop it replaces
+// took ~270 us per 1 M-event push).
+__global__ __launch_bounds__(1024) void k_nfa_now(const int64_t* last_ts, const int64_t* offs, int ncalls,
+                                                 int64_t now_prev, int64_t seq0, int advance, int64_t* now,
+                                                 uint8_t* changed, int64_t* first) {
+  __shared__ int64_t wmax[16];
+  __shared__ int64_t carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) carry_s = now_prev;
+  __syncthreads();
+  for (int c0 = 0; c0 < ncalls; c0 += 1024) {
+    const int c = c0 + tid;
+    const bool in = c < ncalls;
+    const bool live = in && advance && offs[c + 1] > offs[c];
+    const int64_t t = live ? last_ts[c] : INT64_MIN;
+    // inclusive max over the wave, then over the waves
+    int64_t inc = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc = u > inc ? u : inc;
     }
-    now[c] = cur;
-    changed[c] = ch;
-    first[c] = seq0 + offs[c];
+    if (lane == 63) wmax[w] = inc;
+    __syncthreads();
+    const int64_t carry = carry_s;
+    int64_t before = carry;   // max of now_prev and every earlier call's time
+    for (int i = 0; i < w; i++) before = wmax[i] > before ? wmax[i] : before;
+    int64_t excl = __shfl_up(inc, 1, 64);
+    if (lane == 0) excl = INT64_MIN;
+    excl = excl > before ? excl : before;
+    if (in) {
+      const bool ch = live && t >= excl;
+      now[c] = ch ? t : excl;
+      changed[c] = ch ? 1 : 0;
+      first[c] = seq0 + offs[c];
+    }
+    __syncthreads();
+    if (tid == 1023) {
+      int64_t m = carry;
+      for (int i = 0; i < 16; i++) m = wmax[i] > m ? wmax[i] : m;
+      carry_s = m;
+    }
+    __syncthreads();
   }
 }
 
@@ -2743,7 +2775,7 @@ struct NfaEngine : Engine {
     } else {
       upload(d_last.p, &t_only, 8);
     }
-    hipLaunchKernelGGL(k_nfa_now, dim3(1), dim3(64), 0, s, (const int64_t*)d_last.as<int64_t>(),
+    hipLaunchKernelGGL(k_nfa_now, dim3(1), dim3(1024), 0, s, (const int64_t*)d_last.as<int64_t>(),
                        (const int64_t*)d_offs.as<int64_t>(), ncalls, now, seq, (b ? (int)b->advance_time : 1),
                        d_now.as<int64_t>(), d_changed.as<uint8_t>(), d_first.as<int64_t>());
     SHD_CHECK_LAUNCH();
