@@ -654,9 +654,9 @@ def run_e2e(args):
                 offs = np.append(np.arange(0, b - a, 1024, dtype=np.int64), np.int64(b - a))
                 ih.send_batch(ColumnBatch(ts[a:b], [sym[a:b], price[a:b], vol[a:b]], [None, None, None], offs))
         t1 = time.perf_counter()
-        eng = rt.queries[0].engine
+        name = rt.queries[0].engine.engine_name
         rt.shutdown()
-        return (t1 - t0), cb, eng.engine_name
+        return (t1 - t0), cb, name
     he.load_library()
     run(min(n, 2_000_000))   # warm-up (library, device context, first allocations)
     el, cb, engine = run(n)
