@@ -27,9 +27,11 @@ from siddhi_amd.buildinfo import source_hash  # noqa: E402
 
 PEAK_GBS = 8000.0
 # kernels whose reads are dominated by row gathers (FETCH_SIZE x1); every other
-# kernel streams (x2)
+# kernel streams (x2).  k_resume_list: one lane per deferred walk, each from a
+# random sorted position, with the walk's f2 operands gathered by row (its
+# only streamed read is the list, 4 B per deferred walk)
 GATHER = ("k_gather_list", "k_project", "k_emit_pairs", "k_gather_bpos", "k_xw_gather_u64", "k_xw_gather_u32",
-          "k_bucket_resume")
+          "k_resume_list")
 
 
 def fetch_factor(kernel):

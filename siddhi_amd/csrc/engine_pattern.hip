@@ -1294,25 +1294,59 @@ __global__ __launch_bounds__(kBlock) void k_open_list(const uint8_t* __restrict_
                                                       uint32_t val, int which) {
   const int64_t t0 = (int64_t)blockIdx.x * tile;
   const int64_t t1 = t0 + tile < n ? t0 + tile : n;
-  __shared__ uint32_t wsum[kBlock / 64];
+  // Each lane reads four outcome bytes as one word (positions c0 + 4 lane ..
+  // + 3 of a 4 kBlock-position chunk; tiles start on 256-position boundaries
+  // and pst is padded, so the word loads are aligned and in bounds), kOlU
+  // chunks per round sharing one pair of barriers; a lane's hits are placed
+  // by a wave prefix sum of the per-lane hit counts.
+  constexpr int kOlU = 4;
+  constexpr int kW = kBlock / 64;
+  constexpr int kChunk = 4 * kBlock;
+  __shared__ uint32_t wsum[kOlU][kW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t base = boff[which * gridDim.x + blockIdx.x];   // offsets of count `which` (1: open, 2: deferred)
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int64_t c0 = t0; c0 < t1; c0 += kBlock) {
-    const int64_t p = c0 + threadIdx.x;
-    const uint8_t ps = p < t1 ? pst[p] : (uint8_t)PS_NONE;
-    const bool hit = (ps & 0x7Fu) == val;
-    const uint64_t m = __ballot(hit);
-    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
+  for (int64_t c0 = t0; c0 < t1; c0 += kOlU * kChunk) {
+    uint32_t word[kOlU];
 #pragma unroll
-    for (int k = 0; k < kBlock / 64; k++) {
-      pre += k < w ? wsum[k] : 0u;
-      tot += wsum[k];
+    for (int u = 0; u < kOlU; u++) {
+      const int64_t p = c0 + u * kChunk + 4 * threadIdx.x;
+      word[u] = p < t1 ? *reinterpret_cast<const uint32_t*>(pst + p) : 0u;
     }
-    if (hit) olist[base + pre + (uint32_t)__popcll(m & lt)] = (uint32_t)p;
-    base += tot;
+    uint32_t hm[kOlU], ex[kOlU];   // hit mask over the lane's 4 bytes, exclusive prefix in the wave
+#pragma unroll
+    for (int u = 0; u < kOlU; u++) {
+      const int64_t p = c0 + u * kChunk + 4 * threadIdx.x;
+      uint32_t m = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        m |= ((((word[u] >> (8 * b)) & 0x7Fu) == val) && p + b < t1 ? 1u : 0u) << b;
+      hm[u] = m;
+      const uint32_t c = (uint32_t)__popc(m);
+      uint32_t inc = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      ex[u] = inc - c;
+      if (lane == 63) wsum[u][w] = inc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kOlU; u++) {
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < kW; k++) {
+        pre += k < w ? wsum[u][k] : 0u;
+        tot += wsum[u][k];
+      }
+      uint32_t o = base + pre + ex[u];
+      const uint32_t p = (uint32_t)(c0 + u * kChunk + 4 * threadIdx.x);
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if ((hm[u] >> b) & 1u) olist[o++] = p + (uint32_t)b;
+      base += tot;
+    }
     __syncthreads();
   }
 }
@@ -1534,7 +1568,7 @@ struct PatternEngine : Engine {
   // fused prepare + first key-sort pass (keyed_sort.hip): the host reads the
   // push aggregates while the first pass runs
   DevBuf d_kps;
-  hipEvent_t ev_pg = nullptr;
+  hipEvent_t ev_pg = nullptr, ev_pt = nullptr;
   // sorted times of this push's positions (finish: carried partials' times)
   const int32_t* fin_sts32 = nullptr;
   const int64_t* fin_sts64 = nullptr;
@@ -1773,6 +1807,7 @@ struct PatternEngine : Engine {
 
   ~PatternEngine() override {
     if (ev_pg) (void)hipEventDestroy(ev_pg);
+    if (ev_pt) (void)hipEventDestroy(ev_pt);
   }
 
   void push(const Staged& b) override {
@@ -1804,7 +1839,7 @@ struct PatternEngine : Engine {
     d_match.reserve(n_ext * 4);
     d_pst.reserve(n_ext + kCompactPad);
     d_agg.reserve(256);
-    h_agg.reserve(256);
+    h_agg.reserve(320);
 
     ExtRows x{};
     x.carry = carry_cs();
@@ -1857,15 +1892,20 @@ struct PatternEngine : Engine {
     const bool fused = partitioned && !key64 && pa.key_col >= 0 && fattr >= -1 &&
                        (key_type[slot] == SHD_T_STRING || key_type[slot] == SHD_T_INT) && n_ext >= 2 &&
                        (fs_env ? atoi(fs_env) != 0 : n_ext >= ((int64_t)1 << 20));
-    unsigned long long* d_ncand = reinterpret_cast<unsigned long long*>(d_agg.as<char>() + 224);
     KsInfo* d_ksi = reinterpret_cast<KsInfo*>(d_agg.as<char>() + 232);
     if (fused) {
+      // the key range (ev_pg) is all the remaining passes need; the pushed
+      // rows' time aggregates and the candidate count arrive with the first
+      // pass (ev_pt, into h_agg + 256), read while the remaining passes run
       if (!ev_pg) SHD_HIP(hipEventCreateWithFlags(&ev_pg, hipEventDisableTiming));
-      keyed_sort_front(s, d_pa_args, pa, n_ext, d_kps, d_pa, d_ksi, d_ncand);
+      if (!ev_pt) SHD_HIP(hipEventCreateWithFlags(&ev_pt, hipEventDisableTiming));
+      keyed_sort_front(s, d_pa_args, pa, n_ext, d_kps, d_pa, d_ksi);
       SHD_HIP(hipMemcpyAsync(h_agg.p, d_agg.p, 64, hipMemcpyDeviceToHost, s));
       SHD_HIP(hipEventRecord(ev_pg, s));
       keyed_sort_pass0(s, d_pa_args, pa, fattr, n_ext, d_kps, d_ksi, d_k32.as<uint32_t>(), d_pv.as<uint32_t>(),
-                       d_ts.as<uint32_t>(), d_ncand);
+                       d_ts.as<uint32_t>(), d_pa);
+      SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 256, d_agg.p, 64, hipMemcpyDeviceToHost, s));
+      SHD_HIP(hipEventRecord(ev_pt, s));
       SHD_HIP(hipEventSynchronize(ev_pg));
     } else if (fast1)
       hipLaunchKernelGGL(k_prepare<true>, dim3(nblk), dim3(kBlock), 0, s, d_pa_args, n_ext, (int64_t)nblk * kBlock,
@@ -1888,7 +1928,8 @@ struct PatternEngine : Engine {
     // an unpartitioned plan retired partials that the last event of an earlier
     // push expired (global expiry: they are gone in the reference too); a push
     // going back before that time continues on the generic NFA engine with the
-    // remaining open partials (partitioned plans never retire: see `prune`)
+    // remaining open partials (partitioned plans never retire: see `prune`;
+    // the fused path is partitioned, so its ts_min, not read yet, is not needed)
     if (have_horizon && (int64_t)pg.ts_min < horizon)
       throw NeedNfa("pattern engine: an event precedes the retirement horizon of an earlier push");
 
@@ -1971,6 +2012,10 @@ struct PatternEngine : Engine {
       sts32 = in_alt ? d_ts_alt.as<int32_t>() : d_ts.as<int32_t>();
       mark("key_sort");
       counters.group_bits = bits;
+    }
+    if (fused) {   // the complete PrepAgg (k_ks_tfold after the first pass)
+      SHD_HIP(hipEventSynchronize(ev_pt));
+      std::memcpy(&pg, h_agg.as<char>() + 256, sizeof(pg));
     }
     if (pg.ovf || getenv("SHD_TS64")) {   // SHD_TS64: force the 64-bit path (tests)
       // some timestamp is more than 2^31 ms away from the batch's first event
@@ -2184,9 +2229,7 @@ struct PatternEngine : Engine {
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 64, d_agg.as<char>() + 64, 80, hipMemcpyDeviceToHost, s));
     // time of the push's last event in arrival order (NeedNfa hand-over: global expiry of unpartitioned plans)
     SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 192, b.cs.ts + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    if (fused) SHD_HIP(hipMemcpyAsync(h_agg.as<char>() + 224, d_ncand, 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    if (fused) pg.n_cand = *reinterpret_cast<const unsigned long long*>(h_agg.as<char>() + 224);
     ScanOut so;
     std::memcpy(&so, h_agg.as<char>() + 64, sizeof(so));
     const uint32_t m = h_agg.as<uint32_t>()[32];

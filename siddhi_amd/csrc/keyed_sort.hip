@@ -7,9 +7,10 @@
 // key / (flags, row) / 32-bit ts offset (12 B), and the first LSD pass reads
 // the keys again for its histogram (4 B) and the 12 B for its scatter: 48 B
 // per row before the first pass has written anything.  Here:
-//   k_ks_hist      reads key + ts (12 B): tile-major histogram of the key's raw
-//                  low byte + the push aggregates (PrepAgg: key range, time
-//                  range, order, offset overflow, latest carried partial);
+//   k_ks_hist      reads the key (4 B; carried partials also their time):
+//                  tile-major histogram of the key's raw low byte + the key
+//                  range and the carried partials' aggregates (latest time,
+//                  offset overflow);
 //   k_ks_finish    folds the aggregates and derives the sort's key base and
 //                  width exactly as the host does (engine_pattern.hip
 //                  sort_push), so the first pass needs no host round trip;
@@ -22,8 +23,14 @@
 //                  flags (prep_row's rules), ranks the tile by the first
 //                  digit and writes key / (flags, row) / ts offset sorted by
 //                  it (12 B) -- the input of the remaining passes
-//                  (radix_sort_triples_u32 from shift 8).
-// 32 + 12 B per row instead of 48 + 12, and the first pass's histogram comes
+//                  (radix_sort_triples_u32 from shift 8) -- and per tile the
+//                  pushed rows' time aggregates (range, order, offset
+//                  overflow) and the candidates created;
+//   k_ks_tfold     folds those into the push's PrepAgg: the host reads the
+//                  key range after k_ks_finish (the remaining passes need
+//                  only that) and the times after this fold, while the
+//                  remaining passes run.
+// 24 + 12 B per row instead of 48 + 12, and the first pass's histogram comes
 // with the aggregates.  The sorted arrays are bit-identical to the unfused
 // path's (same digits, same stable order), so everything downstream is
 // unchanged.  Reference semantics of the row flags: PartitionStreamReceiver
@@ -93,24 +100,30 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
   const uint32_t* kcol = (const uint32_t*)a.x.batch.col[a.key_col];
   const uint8_t* knul = a.x.batch.nul[a.key_col];
   const int64_t tbase = a.x.batch.ts[0];
+  const int64_t C = a.x.C;
   uint32_t kk[kKsRounds];
   int64_t tt[kKsRounds];
   uint8_t kn[kKsRounds];
-  // time of the row before the wave's slice (lane 0, round 0); the others come by shuffle
-  int64_t t_before = 0;
-  {
-    const int64_t li = wb < n_ext ? wb : n_ext - 1;
-    const int64_t pb = li - a.x.C - 1;
-    if (lane == 0 && pb >= 0) t_before = gld(a.x.batch.ts, pb);
-  }
-  if ((int64_t)tile * kKsTile >= a.x.C) {
-    const int64_t* bts = a.x.batch.ts;
+  // pushed rows: the key only (their time aggregates come from k_ks_scatter0,
+  // which loads the time anyway); carried partials: key + time
+  const bool pushed = (int64_t)tile * kKsTile >= C;
+  const bool carried = (int64_t)(tile + 1) * kKsTile <= C;   // every row a carried partial
+  if (carried) {
+    const uint32_t* ck = reinterpret_cast<const uint32_t*>(a.carry_key);
 #pragma unroll
     for (int r = 0; r < kKsRounds; r++) {
       const int64_t idx = wb + r * 64 + lane;
-      const int64_t b0 = (idx < n_ext ? idx : n_ext - 1) - a.x.C;
+      kk[r] = gld(ck, 2 * idx);   // low word of the u64 carry key
+      tt[r] = gld(a.x.carry.ts, idx);
+      kn[r] = 0;
+    }
+  } else if (pushed) {
+#pragma unroll
+    for (int r = 0; r < kKsRounds; r++) {
+      const int64_t idx = wb + r * 64 + lane;
+      const int64_t b0 = (idx < n_ext ? idx : n_ext - 1) - C;
       kk[r] = gld(kcol, b0);
-      tt[r] = gld(bts, b0);
+      tt[r] = 0;
       kn[r] = KNUL ? gld(knul, b0) : (uint8_t)0;
     }
   } else {
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
       const int64_t li = idx < n_ext ? idx : n_ext - 1;
       const KsRow x = ks_row(a, kcol, li);
       kk[r] = gld(x.kp, 0);
-      tt[r] = gld(x.tp, 0);
+      tt[r] = x.br < 0 ? gld(x.tp, 0) : 0;
       kn[r] = KNUL ? gld(knul, x.br >= 0 ? x.br : 0) : (uint8_t)0;
     }
   }
@@ -129,35 +142,24 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
 #pragma unroll
   for (int r = 0; r < kKsRounds; r++) {
     const int64_t idx = wb + r * 64 + lane;
-    // predecessor row idx - 1: lane - 1 of this round, lane 63 of the last
-    // (shuffles with every lane active)
-    const int64_t up = __shfl_up(tt[r], 1, 64);
-    const int64_t prev63 = r > 0 ? __shfl(tt[r > 0 ? r - 1 : 0], 63, 64) : t_before;
     if (idx >= n_ext) continue;
-    const bool isc = idx < a.x.C;
-    const long long t = (long long)tt[r];
-    const long long tprev = (long long)(lane ? up : prev63);
     uint32_t k = kk[r];
     bool skip = false;
-    if (isc) {
+    if (!pushed && idx < C) {
+      const long long t = (long long)tt[r];
       acc.ctmax = t > acc.ctmax ? t : acc.ctmax;
-    } else {
-      acc.tmin = t < acc.tmin ? t : acc.tmin;
-      acc.tmax = t > acc.tmax ? t : acc.tmax;
-      acc.unmono |= (idx - a.x.C > 0) && tprev > t;
-      if (KNUL && kn[r] && a.null_skip) {
-        skip = true;
-        k = (uint32_t)idx;   // prep_row: a dropped row's key is its row index
-      } else if (KNUL && kn[r]) {
-        k = 0;
-      }
+      const int64_t dt = (int64_t)t - tbase;
+      acc.ovf |= dt != (int64_t)(int32_t)dt;
+    } else if (KNUL && kn[r] && a.null_skip) {
+      skip = true;
+      k = (uint32_t)idx;   // prep_row: a dropped row's key is its row index
+    } else if (KNUL && kn[r]) {
+      k = 0;
     }
     if (!skip) {
       acc.kmax = (unsigned long long)k > acc.kmax ? (unsigned long long)k : acc.kmax;
       acc.kmin = (unsigned long long)k < acc.kmin ? (unsigned long long)k : acc.kmin;
     }
-    const int64_t dt = (int64_t)t - tbase;
-    acc.ovf |= dt != (int64_t)(int32_t)dt;
     atomicAdd(&h[w][k & 255u], 1u);
   }
   __syncthreads();
@@ -167,7 +169,32 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
     for (int i = 0; i < kRsWaves; i++) c += h[i][tid];
     hraw[(int64_t)tile * 256 + tid] = c;
   }
-  prep_block_reduce<kRsBlock>(acc, blk, tile);
+  if (!pushed) {
+    prep_block_reduce<kRsBlock>(acc, blk, tile);
+    return;
+  }
+  // pushed rows only: the key range is the whole aggregate (32-bit keys)
+  uint32_t kmn = acc.kmin > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)acc.kmin, kmx = (uint32_t)acc.kmax;
+  const bool any = __ballot(acc.kmin <= acc.kmax) != 0;
+  kmn = wave_min(kmn);
+  kmx = wave_max(kmx);
+  __shared__ uint32_t wk[2][kRsWaves];
+  __shared__ uint32_t wany[kRsWaves];
+  if (lane == 0) {
+    wk[0][w] = kmn;
+    wk[1][w] = kmx;
+    wany[w] = any;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    PrepAgg r{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN, ULLONG_MAX};
+    for (int i = 0; i < kRsWaves; i++) {
+      if (!wany[i]) continue;
+      r.kmin = wk[0][i] < r.kmin ? wk[0][i] : r.kmin;
+      r.kmax = wk[1][i] > r.kmax ? wk[1][i] : r.kmax;
+    }
+    blk[tile] = r;
+  }
 }
 
 // Per chunk of kKsChunk tiles: each raw low byte's count over the chunk, and
@@ -199,8 +226,7 @@ __global__ __launch_bounds__(256) void k_ks_chunk_sum(const uint32_t* __restrict
 // Fold of the chunks' aggregates + the sort's key base / width
 // (engine_pattern.hip sort_push: offsets from kmin when that narrows the key).
 __global__ __launch_bounds__(256) void k_ks_finish(const PrepAgg* __restrict__ cblk, int nch,
-                                                   PrepAgg* __restrict__ out, KsInfo* __restrict__ info,
-                                                   unsigned long long* __restrict__ ncand) {
+                                                   PrepAgg* __restrict__ out, KsInfo* __restrict__ info) {
   PrepAcc acc;
   for (int b = threadIdx.x; b < nch; b += 256) {
     const PrepAgg& x = cblk[b];
@@ -229,7 +255,6 @@ __global__ __launch_bounds__(256) void k_ks_finish(const PrepAgg* __restrict__ c
       kb = (uint32_t)kmin;
     }
     *info = KsInfo{kb, bits};
-    *ncand = 0;
   }
 }
 
@@ -348,7 +373,7 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
                                                           const uint32_t* __restrict__ offs, int nb,
                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                           uint32_t* __restrict__ wout,
-                                                          unsigned long long* __restrict__ ncand) {
+                                                          PrepAgg* __restrict__ blk) {
   const PrepArgs& a = *ap;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = rs_tile_of(blockIdx.x, nb);
@@ -376,7 +401,19 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
     kn[r] = KNUL ? gld(knul, b0) : (uint8_t)0;
     fn[r] = FNUL ? gld(fnul, b0) : (uint8_t)0;
   };
-  if (t0 >= C) {
+  if (t0 + kKsTile <= C) {
+    // every row a carried partial (the first C rows): key + time, uniform bases
+    const uint32_t* ck = reinterpret_cast<const uint32_t*>(a.carry_key);
+#pragma unroll
+    for (int r = 0; r < kKsRounds; r++) {
+      const int64_t idx = wb + r * 64 + lane;
+      kk[r] = gld(ck, 2 * idx);   // low word of the u64 carry key
+      tt[r] = gld(a.x.carry.ts, idx);
+      if constexpr (FSZ != 0) fv[r] = 0;
+      kn[r] = 0;
+      fn[r] = 0;
+    }
+  } else if (t0 >= C) {
     // every row of the tile is a pushed event: uniform column bases (the
     // common case; carried partials fill only the first C rows)
     const int64_t* bts = a.x.batch.ts;
@@ -399,8 +436,17 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
       load_f(r, x.br >= 0 ? x.br : 0);
     }
   }
+  // time of the pushed row before the wave's slice (lane 0); the others by shuffle
+  int64_t t_before = 0;
+  {
+    const int64_t li = wb < n_ext ? wb : n_ext - 1;
+    const int64_t pb = li - C - 1;
+    if (lane == 0 && pb >= 0) t_before = gld(a.x.batch.ts, pb);
+  }
   uint32_t kv[kKsRounds], pv[kKsRounds], tv[kKsRounds];
-  uint32_t created = 0;
+  // pushed rows' time aggregates (range, order, offset overflow) and the
+  // candidates created; carried partials' come from k_ks_hist
+  PrepAcc acc;
   // FK 2: f1 = (double attribute) op threshold for every row at once, the
   // operator switch outside the row loop (Java double comparison:
   // d_compare's -1 / 0 / 1 / unordered classes)
@@ -445,12 +491,25 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
 #pragma unroll
   for (int r = 0; r < kKsRounds; r++) {
     const int64_t idx = wb + r * 64 + lane;
+    // predecessor row idx - 1: lane - 1 of this round, lane 63 of the last
+    // (shuffles with every lane active)
+    const int64_t up = __shfl_up(tt[r], 1, 64);
+    const int64_t prev63 = r > 0 ? __shfl(tt[r > 0 ? r - 1 : 0], 63, 64) : t_before;
     uint32_t k = kk[r];
     uint32_t f;
     if ((idx < n_ext ? idx : n_ext - 1) < a.x.C) {
       f = F_CAND;
     } else {
       f = F_NEW;
+      if (idx < n_ext) {
+        const long long t = (long long)tt[r];
+        const long long tprev = (long long)(lane ? up : prev63);
+        acc.tmin = t < acc.tmin ? t : acc.tmin;
+        acc.tmax = t > acc.tmax ? t : acc.tmax;
+        acc.unmono |= (idx - C > 0) && tprev > t;
+        const int64_t dt = (int64_t)t - tbase;
+        acc.ovf |= dt != (int64_t)(int32_t)dt;
+      }
       bool p1 = false;
       if constexpr (FK == 2) {
         p1 = a.is_a && pre1[r];
@@ -484,7 +543,7 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
         if (a.is_b) f |= F_B;
         if (p1) {
           f |= F_CAND;
-          created += idx < n_ext ? 1u : 0u;
+          acc.created += idx < n_ext ? 1u : 0u;
         }
         if (KNUL && kn[r]) k = 0;
       }
@@ -493,22 +552,59 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
     pv[r] = (f << kRowBits) | (uint32_t)idx;
     tv[r] = (uint32_t)(int32_t)((int64_t)tt[r] - tbase);
   }
-  // one candidate count per workgroup (the host reads the push total)
-  for (int o = 32; o > 0; o >>= 1) created += __shfl_xor(created, o, 64);
-  __shared__ uint32_t wc[kRsWaves];
-  if (lane == 0) wc[w] = created;
   const bool zero = in.bits == 0;
   const uint32_t kb = in.kb;
   rs_scatter_tile_fn<uint32_t, kKsRounds, true>(
       kv, pv, tv, n_ext, t0, wb, [zero, kb](uint32_t k) { return zero ? 0u : ((k - kb) & 255u); }, c, gr, 0u, kout,
       vout, wout);
-  if (tid == 0) {
-    unsigned long long s = 0;
-    for (int i = 0; i < kRsWaves; i++) s += wc[i];
-    if (s) atomicAdd(ncand, s);
-  }
+  prep_block_reduce<kRsBlock>(acc, blk, tile);
 }
 
+// Fold of k_ks_scatter0's per-tile partials into the push's PrepAgg (whose
+// key range and carried-partial fields k_ks_finish wrote; n_cand 0, pushed
+// rows' time range empty): candidates created, pushed rows' time range /
+// order / offset overflow.  kKsFoldBlocks workgroups each fold a strided
+// slice (one workgroup alone was bound by its own CU's load rate) and merge
+// it with one atomic per field.
+constexpr int kKsFoldBlocks = 64;
+__global__ __launch_bounds__(256) void k_ks_tfold(const PrepAgg* __restrict__ blk, int nb, PrepAgg* __restrict__ out) {
+  PrepAcc acc;
+  constexpr int U = 4;   // partials per thread per round, loaded together
+  const int stride = kKsFoldBlocks * 256;
+  for (int b0 = blockIdx.x * 256 + threadIdx.x; b0 < nb; b0 += U * stride) {
+    unsigned long long c[U], o[U], u[U];
+    long long lo[U], hi[U];
+#pragma unroll
+    for (int i = 0; i < U; i++) {
+      const bool in = b0 + i * stride < nb;
+      const PrepAgg& x = blk[in ? b0 + i * stride : b0];
+      c[i] = in ? x.n_cand : 0ull;
+      o[i] = x.ovf;
+      u[i] = x.unmono;
+      lo[i] = x.ts_min;
+      hi[i] = x.ts_max;
+    }
+#pragma unroll
+    for (int i = 0; i < U; i++) {
+      acc.created += c[i];
+      acc.ovf |= o[i];
+      acc.unmono |= u[i];
+      acc.tmin = lo[i] < acc.tmin ? lo[i] : acc.tmin;
+      acc.tmax = hi[i] > acc.tmax ? hi[i] : acc.tmax;
+    }
+  }
+  __shared__ PrepAgg r1[1];
+  prep_block_reduce<256>(acc, r1, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const PrepAgg r = r1[0];
+    if (r.n_cand) atomicAdd(&out->n_cand, r.n_cand);
+    if (r.ovf) atomicOr(&out->ovf, r.ovf);
+    if (r.unmono) atomicOr(&out->unmono, r.unmono);
+    if (r.ts_min != LLONG_MAX) atomicMin(&out->ts_min, r.ts_min);
+    if (r.ts_max != LLONG_MIN) atomicMax(&out->ts_max, r.ts_max);
+  }
+}
 
 }  // namespace
 
@@ -556,7 +652,7 @@ static KsScratch ks_scratch(DevBuf& scratch, int64_t n_ext, bool reserve) {
 }
 
 void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int64_t n_ext, DevBuf& scratch,
-                      PrepAgg* d_pg, KsInfo* d_info, unsigned long long* d_ncand) {
+                      PrepAgg* d_pg, KsInfo* d_info) {
   const KsScratch k = ks_scratch(scratch, n_ext, true);
   const bool knul = pa.x.batch.nul[pa.key_col] != nullptr;
   if (knul)
@@ -567,7 +663,7 @@ void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, i
   hipLaunchKernelGGL(k_ks_chunk_sum, dim3(k.nch), dim3(256), 0, s, (const uint32_t*)k.hraw, k.nb,
                      (const PrepAgg*)k.blk, k.csum, k.cblk);
   SHD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_ks_finish, dim3(1), dim3(256), 0, s, (const PrepAgg*)k.cblk, k.nch, d_pg, d_info, d_ncand);
+  hipLaunchKernelGGL(k_ks_finish, dim3(1), dim3(256), 0, s, (const PrepAgg*)k.cblk, k.nch, d_pg, d_info);
   SHD_CHECK_LAUNCH();
 }
 
@@ -618,7 +714,7 @@ static KsF1 ks_f1(const DFilters& f1, int fattr, const ColSet& cs) {
 
 void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int fattr, int64_t n_ext,
                       DevBuf& scratch, const KsInfo* d_info, uint32_t* k32, uint32_t* pv, uint32_t* ts,
-                      unsigned long long* d_ncand) {
+                      PrepAgg* d_pg) {
   const KsScratch k = ks_scratch(scratch, n_ext, false);
   hipLaunchKernelGGL(k_ks_chunk_scan, dim3(256), dim3(256), 0, s, (const uint32_t*)k.csum, k.nch, k.nb, d_info, n_ext,
                      k.cpre, k.dtot);
@@ -633,9 +729,10 @@ void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, i
   const int nb = k.nb;
   const uint32_t* hraw = k.hraw;
   const uint32_t* offs = k.offs;
+  PrepAgg* blk = k.blk;   // k_ks_hist's partials were folded by k_ks_chunk_sum already
 #define SHD_KS_LAUNCH(FSZ, KN, FN, FK)                                                                               \
   hipLaunchKernelGGL((k_ks_scatter0<FSZ, KN, FN, FK>), dim3(nb), dim3(kRsBlock), 0, s, d_pa, n_ext, fattr, f1,      \
-                     d_info, hraw, offs, nb, k32, pv, ts, d_ncand)
+                     d_info, hraw, offs, nb, k32, pv, ts, blk)
 #define SHD_KS_LAUNCH_N(FSZ, FK)                             \
   do {                                                       \
     if (knul) {                                              \
@@ -658,6 +755,8 @@ void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, i
   }
 #undef SHD_KS_LAUNCH_N
 #undef SHD_KS_LAUNCH
+  SHD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ks_tfold, dim3(kKsFoldBlocks), dim3(256), 0, s, (const PrepAgg*)blk, nb, d_pg);
   SHD_CHECK_LAUNCH();
 }
 

@@ -368,13 +368,16 @@ struct KsInfo {
 // The one attribute f1's loads read (-1: none or the pushed stream is not A;
 // -2: f1 is not a pre-decoded chain over one attribute -- not fusable).
 int keyed_sort_f1_attr(const DFilters& f1, bool is_a);
-// hist + aggregates (d_pg: the push's PrepAgg with n_cand 0, d_info, *d_ncand = 0)
+// hist + key aggregates (d_pg: the push's PrepAgg -- key range, carried
+// partials' latest time and offset overflow; n_cand 0, pushed rows' time
+// fields unset -- and d_info)
 void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int64_t n_ext, DevBuf& scratch,
-                      PrepAgg* d_pg, KsInfo* d_info, unsigned long long* d_ncand);
-// first pass: rows sorted by the first digit into (k32, pv, ts); *d_ncand += candidates created
+                      PrepAgg* d_pg, KsInfo* d_info);
+// first pass: rows sorted by the first digit into (k32, pv, ts); completes
+// d_pg (candidates created, pushed rows' time range / order / overflow)
 void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int fattr, int64_t n_ext,
                       DevBuf& scratch, const KsInfo* d_info, uint32_t* k32, uint32_t* pv, uint32_t* ts,
-                      unsigned long long* d_ncand);
+                      PrepAgg* d_pg);
 // the remaining passes (digits from shift 8 to bits) of a fused sort
 void keyed_sort_rest(hipStream_t s, int64_t n_ext, int bits, uint32_t kb, uint32_t* k32, uint32_t* pv, uint32_t* ts,
                      uint32_t* k32_alt, uint32_t* pv_alt, uint32_t* ts_alt, DevBuf& scratch, DevBuf& sort_scratch,
