@@ -7,10 +7,9 @@
 // key / (flags, row) / 32-bit ts offset (12 B), and the first LSD pass reads
 // the keys again for its histogram (4 B) and the 12 B for its scatter: 48 B
 // per row before the first pass has written anything.  Here:
-//   k_ks_hist      reads the key (4 B; carried partials also their time):
-//                  tile-major histogram of the key's raw low byte + the key
-//                  range and the carried partials' aggregates (latest time,
-//                  offset overflow);
+//   k_ks_hist      reads the key (4 B; carried partials: the low word of
+//                  their 8-byte key): tile-major histogram of the key's raw
+//                  low byte + the key range;
 //   k_ks_finish    folds the aggregates and derives the sort's key base and
 //                  width exactly as the host does (engine_pattern.hip
 //                  sort_push), so the first pass needs no host round trip;
@@ -24,8 +23,9 @@
 //                  digit and writes key / (flags, row) / ts offset sorted by
 //                  it (12 B) -- the input of the remaining passes
 //                  (radix_sort_triples_u32 from shift 8) -- and per tile the
-//                  pushed rows' time aggregates (range, order, offset
-//                  overflow) and the candidates created;
+//                  time aggregates (pushed rows: range, order, offset
+//                  overflow; carried partials: latest time, overflow) and the
+//                  candidates created;
 //   k_ks_tfold     folds those into the push's PrepAgg: the host reads the
 //                  key range after k_ks_finish (the remaining passes need
 //                  only that) and the times after this fold, while the
@@ -99,22 +99,18 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
   const int64_t wb = (int64_t)tile * kKsTile + (int64_t)w * 64 * kKsRounds;
   const uint32_t* kcol = (const uint32_t*)a.x.batch.col[a.key_col];
   const uint8_t* knul = a.x.batch.nul[a.key_col];
-  const int64_t tbase = a.x.batch.ts[0];
   const int64_t C = a.x.C;
   uint32_t kk[kKsRounds];
-  int64_t tt[kKsRounds];
   uint8_t kn[kKsRounds];
-  // pushed rows: the key only (their time aggregates come from k_ks_scatter0,
-  // which loads the time anyway); carried partials: key + time
+  // the key only (every time aggregate comes from k_ks_scatter0, which loads
+  // the times anyway)
   const bool pushed = (int64_t)tile * kKsTile >= C;
   const bool carried = (int64_t)(tile + 1) * kKsTile <= C;   // every row a carried partial
   if (carried) {
     const uint32_t* ck = reinterpret_cast<const uint32_t*>(a.carry_key);
 #pragma unroll
     for (int r = 0; r < kKsRounds; r++) {
-      const int64_t idx = wb + r * 64 + lane;
-      kk[r] = gld(ck, 2 * idx);   // low word of the u64 carry key
-      tt[r] = gld(a.x.carry.ts, idx);
+      kk[r] = gld(ck, 2 * (wb + r * 64 + lane));   // low word of the u64 carry key
       kn[r] = 0;
     }
   } else if (pushed) {
@@ -123,7 +119,6 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
       const int64_t idx = wb + r * 64 + lane;
       const int64_t b0 = (idx < n_ext ? idx : n_ext - 1) - C;
       kk[r] = gld(kcol, b0);
-      tt[r] = 0;
       kn[r] = KNUL ? gld(knul, b0) : (uint8_t)0;
     }
   } else {
@@ -133,32 +128,31 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
       const int64_t li = idx < n_ext ? idx : n_ext - 1;
       const KsRow x = ks_row(a, kcol, li);
       kk[r] = gld(x.kp, 0);
-      tt[r] = x.br < 0 ? gld(x.tp, 0) : 0;
       kn[r] = KNUL ? gld(knul, x.br >= 0 ? x.br : 0) : (uint8_t)0;
     }
   }
   __syncthreads();
-  PrepAcc acc;
+  // key range as 32-bit keys (kmx < kmn: no keyed row in this lane)
+  uint32_t kmn = 0xFFFFFFFFu, kmx = 0;
+  bool any = false;
 #pragma unroll
   for (int r = 0; r < kKsRounds; r++) {
     const int64_t idx = wb + r * 64 + lane;
     if (idx >= n_ext) continue;
     uint32_t k = kk[r];
     bool skip = false;
-    if (!pushed && idx < C) {
-      const long long t = (long long)tt[r];
-      acc.ctmax = t > acc.ctmax ? t : acc.ctmax;
-      const int64_t dt = (int64_t)t - tbase;
-      acc.ovf |= dt != (int64_t)(int32_t)dt;
-    } else if (KNUL && kn[r] && a.null_skip) {
-      skip = true;
-      k = (uint32_t)idx;   // prep_row: a dropped row's key is its row index
-    } else if (KNUL && kn[r]) {
-      k = 0;
+    if (idx >= C && KNUL && kn[r]) {
+      if (a.null_skip) {
+        skip = true;
+        k = (uint32_t)idx;   // prep_row: a dropped row's key is its row index
+      } else {
+        k = 0;
+      }
     }
     if (!skip) {
-      acc.kmax = (unsigned long long)k > acc.kmax ? (unsigned long long)k : acc.kmax;
-      acc.kmin = (unsigned long long)k < acc.kmin ? (unsigned long long)k : acc.kmin;
+      kmx = k > kmx ? k : kmx;
+      kmn = k < kmn ? k : kmn;
+      any = true;
     }
     atomicAdd(&h[w][k & 255u], 1u);
   }
@@ -169,27 +163,21 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_hist(const PrepArgs* __restrict
     for (int i = 0; i < kRsWaves; i++) c += h[i][tid];
     hraw[(int64_t)tile * 256 + tid] = c;
   }
-  if (!pushed) {
-    prep_block_reduce<kRsBlock>(acc, blk, tile);
-    return;
-  }
-  // pushed rows only: the key range is the whole aggregate (32-bit keys)
-  uint32_t kmn = acc.kmin > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)acc.kmin, kmx = (uint32_t)acc.kmax;
-  const bool any = __ballot(acc.kmin <= acc.kmax) != 0;
+  const bool wany = __ballot(any) != 0;
   kmn = wave_min(kmn);
   kmx = wave_max(kmx);
   __shared__ uint32_t wk[2][kRsWaves];
-  __shared__ uint32_t wany[kRsWaves];
+  __shared__ uint32_t wa[kRsWaves];
   if (lane == 0) {
     wk[0][w] = kmn;
     wk[1][w] = kmx;
-    wany[w] = any;
+    wa[w] = wany;
   }
   __syncthreads();
   if (tid == 0) {
     PrepAgg r{0, 0, LLONG_MAX, LLONG_MIN, 0, 0, LLONG_MIN, ULLONG_MAX};
     for (int i = 0; i < kRsWaves; i++) {
-      if (!wany[i]) continue;
+      if (!wa[i]) continue;
       r.kmin = wk[0][i] < r.kmin ? wk[0][i] : r.kmin;
       r.kmax = wk[1][i] > r.kmax ? wk[1][i] : r.kmax;
     }
@@ -444,8 +432,8 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
     if (lane == 0 && pb >= 0) t_before = gld(a.x.batch.ts, pb);
   }
   uint32_t kv[kKsRounds], pv[kKsRounds], tv[kKsRounds];
-  // pushed rows' time aggregates (range, order, offset overflow) and the
-  // candidates created; carried partials' come from k_ks_hist
+  // time aggregates (pushed rows: range, order, offset overflow; carried
+  // partials: latest time, offset overflow) and the candidates created
   PrepAcc acc;
   // FK 2: f1 = (double attribute) op threshold for every row at once, the
   // operator switch outside the row loop (Java double comparison:
@@ -499,6 +487,12 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
     uint32_t f;
     if ((idx < n_ext ? idx : n_ext - 1) < a.x.C) {
       f = F_CAND;
+      if (idx < n_ext) {   // carried partial: the latest one's time, offset overflow
+        const long long t = (long long)tt[r];
+        acc.ctmax = t > acc.ctmax ? t : acc.ctmax;
+        const int64_t dt = (int64_t)t - tbase;
+        acc.ovf |= dt != (int64_t)(int32_t)dt;
+      }
     } else {
       f = F_NEW;
       if (idx < n_ext) {
@@ -561,9 +555,9 @@ __global__ __launch_bounds__(kRsBlock) void k_ks_scatter0(const PrepArgs* __rest
 }
 
 // Fold of k_ks_scatter0's per-tile partials into the push's PrepAgg (whose
-// key range and carried-partial fields k_ks_finish wrote; n_cand 0, pushed
-// rows' time range empty): candidates created, pushed rows' time range /
-// order / offset overflow.  kKsFoldBlocks workgroups each fold a strided
+// key range k_ks_finish wrote; n_cand 0, time fields empty): candidates
+// created, pushed rows' time range / order, offset overflow, latest carried
+// partial.  kKsFoldBlocks workgroups each fold a strided
 // slice (one workgroup alone was bound by its own CU's load rate) and merge
 // it with one atomic per field.
 constexpr int kKsFoldBlocks = 64;
@@ -573,7 +567,7 @@ __global__ __launch_bounds__(256) void k_ks_tfold(const PrepAgg* __restrict__ bl
   const int stride = kKsFoldBlocks * 256;
   for (int b0 = blockIdx.x * 256 + threadIdx.x; b0 < nb; b0 += U * stride) {
     unsigned long long c[U], o[U], u[U];
-    long long lo[U], hi[U];
+    long long lo[U], hi[U], ch[U];
 #pragma unroll
     for (int i = 0; i < U; i++) {
       const bool in = b0 + i * stride < nb;
@@ -583,6 +577,7 @@ __global__ __launch_bounds__(256) void k_ks_tfold(const PrepAgg* __restrict__ bl
       u[i] = x.unmono;
       lo[i] = x.ts_min;
       hi[i] = x.ts_max;
+      ch[i] = x.carry_tmax;
     }
 #pragma unroll
     for (int i = 0; i < U; i++) {
@@ -591,6 +586,7 @@ __global__ __launch_bounds__(256) void k_ks_tfold(const PrepAgg* __restrict__ bl
       acc.unmono |= u[i];
       acc.tmin = lo[i] < acc.tmin ? lo[i] : acc.tmin;
       acc.tmax = hi[i] > acc.tmax ? hi[i] : acc.tmax;
+      acc.ctmax = ch[i] > acc.ctmax ? ch[i] : acc.ctmax;
     }
   }
   __shared__ PrepAgg r1[1];
@@ -603,6 +599,7 @@ __global__ __launch_bounds__(256) void k_ks_tfold(const PrepAgg* __restrict__ bl
     if (r.unmono) atomicOr(&out->unmono, r.unmono);
     if (r.ts_min != LLONG_MAX) atomicMin(&out->ts_min, r.ts_min);
     if (r.ts_max != LLONG_MIN) atomicMax(&out->ts_max, r.ts_max);
+    if (r.carry_tmax != LLONG_MIN) atomicMax(&out->carry_tmax, r.carry_tmax);
   }
 }
 

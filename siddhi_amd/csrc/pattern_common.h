@@ -368,13 +368,13 @@ struct KsInfo {
 // The one attribute f1's loads read (-1: none or the pushed stream is not A;
 // -2: f1 is not a pre-decoded chain over one attribute -- not fusable).
 int keyed_sort_f1_attr(const DFilters& f1, bool is_a);
-// hist + key aggregates (d_pg: the push's PrepAgg -- key range, carried
-// partials' latest time and offset overflow; n_cand 0, pushed rows' time
-// fields unset -- and d_info)
+// hist + key range (d_pg: the push's PrepAgg with the key range only -- n_cand
+// 0, time fields unset: keyed_sort_pass0 completes them -- and d_info, the
+// sort's key base / width)
 void keyed_sort_front(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int64_t n_ext, DevBuf& scratch,
                       PrepAgg* d_pg, KsInfo* d_info);
 // first pass: rows sorted by the first digit into (k32, pv, ts); completes
-// d_pg (candidates created, pushed rows' time range / order / overflow)
+// d_pg (candidates created, time range / order / overflow, latest carried)
 void keyed_sort_pass0(hipStream_t s, const PrepArgs* d_pa, const PrepArgs& pa, int fattr, int64_t n_ext,
                       DevBuf& scratch, const KsInfo* d_info, uint32_t* k32, uint32_t* pv, uint32_t* ts,
                       PrepAgg* d_pg);
