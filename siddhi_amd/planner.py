@@ -534,9 +534,24 @@ def _plan_output_rate(qp: QueryPlan, q: qc.Query, partition):
     rate = q.output_rate
     if rate.value <= 0:
         raise SiddhiAppValidationException("output rate should be positive")
+    if rate.kind == "snapshot":
+        # WrappedSnapshotOutputRateLimiter.init (C/query/output/ratelimit/
+        # snapshot/WrappedSnapshotOutputRateLimiter.java:67-115): a windowed
+        # input picks the window-content limiters (they track what the window
+        # holds), the rest PerSnapshot / GroupByPerSnapshot.  QueryParser
+        # disables the selector's batching for all of them (QueryParser.java:
+        # 217-223): an aggregating selector then emits one row per event where
+        # this runtime's engines emit one per call and group, so only
+        # non-windowed, non-aggregating queries are exact here.
+        if isinstance(q.input, qc.SingleInput) and any(isinstance(h, qc.Window) for h in q.input.handlers):
+            raise UnsupportedPlanException("output snapshot on a windowed input (the windowed snapshot limiters) "
+                                           "is outside the hot path")
+        if q.selector and any(_has_agg(oa.expr) for oa in q.selector.attrs):
+            raise UnsupportedPlanException("output snapshot with aggregations (per-event selector output) is "
+                                           "outside the hot path")
     qp.output_rate = rate
     gb = q.selector.group_by if q.selector else []
-    if gb and rate.kind in ("first", "last"):
+    if gb and rate.kind in ("first", "last", "snapshot"):
         cols = []
         for g in gb:
             hit = None

@@ -172,7 +172,7 @@ class Selector:
 @dataclass
 class OutputRate:
     unit: str       # events | time
-    kind: str       # all | first | last
+    kind: str       # all | first | last | snapshot (time only)
     value: int      # events, or ms
 
 
@@ -449,16 +449,19 @@ class Parser:
         rate = None
         if self.accept("output"):
             # output_rate (SiddhiQL.g4): output [all|first|last] every <n> events | <time>
-            if self.at_kw("snapshot"):
-                raise OutOfScopeSyntax("output snapshot rate limiting is outside the hot path")
-            kind = self.name().lower() if self.at_kw("all", "first", "last") else "all"
-            self.expect("every")
-            if self.peek().kind == "num" and self.at_kw("events", "event", k=1):
-                n = int(self.next().text)
-                self.next()
-                rate = OutputRate("events", kind, n)
-            else:
-                rate = OutputRate("time", kind, self.time_value())
+            # | output snapshot every <time>
+            if self.accept("snapshot"):
+                self.expect("every")
+                rate = OutputRate("time", "snapshot", self.time_value())
+            kind = self.name().lower() if rate is None and self.at_kw("all", "first", "last") else "all"
+            if rate is None:
+                self.expect("every")
+                if self.peek().kind == "num" and self.at_kw("events", "event", k=1):
+                    n = int(self.next().text)
+                    self.next()
+                    rate = OutputRate("events", kind, n)
+                else:
+                    rate = OutputRate("time", kind, self.time_value())
         self.expect("insert")
         et = "current"
         if self.at_kw("all", "expired", "current", "events"):

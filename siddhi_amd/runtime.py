@@ -790,7 +790,7 @@ class OutputRateLimiter:
         self.notify = []                 # the Scheduler's toNotifyQueue (FIFO)
 
     def timed(self):
-        return self.unit == "time" and self.kind in ("all", "last")
+        return self.unit == "time" and self.kind in ("all", "last", "snapshot")
 
     # -- snapshot / restore: the limiters' RateLimiterState maps
     # (e.g. AllPerTimeOutputRateLimiter.RateLimiterState: the held chunk and
@@ -807,7 +807,7 @@ class OutputRateLimiter:
 
     def _group_vals(self):
         # first: count (per event) / output time (per time); last: the row
-        return "row" if self.kind == "last" else "int"
+        return "row" if self.kind in ("last", "snapshot") else "int"
 
     def state(self) -> dict:
         gv = self._group_vals()
@@ -877,6 +877,8 @@ class OutputRateLimiter:
                         out += list(self.groups.values())
                         self.groups = {}
             return out
+        if self.kind == "snapshot":
+            return self._snapshot_rows(rows)
         if self.kind == "all":                           # AllPerTimeOutputRateLimiter
             self.buf += rows
         elif self.kind == "last" and not self.grouped:   # LastPerTimeOutputRateLimiter
@@ -897,12 +899,46 @@ class OutputRateLimiter:
                     out.append(r)
         return out
 
+    # `output snapshot every <time>` on a non-windowed, non-aggregating query
+    # (the planner refuses the rest): PerSnapshotOutputRateLimiter /
+    # GroupByPerSnapshotOutputRateLimiter (C/query/output/ratelimit/snapshot/
+    # PerSnapshotOutputRateLimiter.java:62-100, GroupByPerSnapshotOutputRateLimiter
+    # .java:66-103).  Every event (and TIMER) at or past scheduledTime first
+    # flushes a copy of what is held -- the last event, or each group's last
+    # event in first-arrival order -- and moves scheduledTime on by one period;
+    # a CURRENT event is then held.  The snapshot does not consume what it sends.
+    def _snapshot_flush(self):
+        out = list(self.groups.values()) if self.grouped else ([self.last] if self.last is not None else [])
+        self.scheduled += self.value
+        self.notify.append(self.scheduled)
+        return out
+
+    def _snapshot_rows(self, rows):
+        out = []   # the flushes of one selector chunk go out as one chunk (SnapshotOutputRateLimiter.sendToCallBacks)
+        for r in rows:
+            if r[0].is_expired:
+                # PerSnapshot tries a flush on any other event type; the
+                # group-by limiter ignores them
+                if not self.grouped and r[0].timestamp >= self.scheduled:
+                    out += self._snapshot_flush()
+                continue
+            if r[0].timestamp >= self.scheduled:
+                out += self._snapshot_flush()
+            if self.grouped:
+                self.groups[r[1]] = r   # LinkedHashMap.put: a known group keeps its place
+            else:
+                self.last = r
+        return out
+
     def on_time(self, t: int):
         """Due TIMERs up to clock t: the flushed chunks, in order."""
         chunks = []
         while self.notify and self.notify[0] <= t:
             ts = self.notify.pop(0)
             if ts < self.scheduled:
+                continue
+            if self.kind == "snapshot":   # tryFlushEvents on the TIMER: a copy, nothing consumed
+                chunks += [c for c in [self._snapshot_flush()] if c]
                 continue
             if self.kind == "all":
                 out, self.buf = self.buf, []
