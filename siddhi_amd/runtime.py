@@ -135,6 +135,11 @@ def rows_to_batch(types: List[int], events: List[Event], dictionary) -> ColumnBa
                                                     dictionary.id(str(x))) for x in raw), np.uint32, n)
         elif t == pl.T_DOUBLE and not has_null and all(type(x) is float for x in raw):
             col = np.array(raw, np.float64)
+        elif t in (pl.T_LONG, pl.T_INT) and not has_null and all(type(x) is int for x in raw):
+            try:   # in range: the values as they are (no Java int wrap needed)
+                col = np.array(raw, dtype=_NP[t])
+            except OverflowError:
+                col = np.array([_java_value(x, t, dictionary) for x in raw], dtype=_NP[t])
         else:
             col = np.array([0 if x is None else _java_value(x, t, dictionary) for x in raw], dtype=_NP[t])
         cols.append(col)
